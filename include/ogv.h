@@ -1,0 +1,119 @@
+/*
+ * ogv.h — C-ABI of libogv_hip.so, the MI355X (gfx950) kernels behind the OutGridBlock hot path.
+ *
+ * The reference (pablo-reyes8/outlook-grid-vision-transformer) has no FFI: its hot path is a
+ * set of nn.Modules whose arithmetic runs in ATen.  Each entry point below replaces the ATen op
+ * chain named in its comment (reference file:line); the Python drop-in modules under
+ * outlook-grid-vision-transformer_amd/src/model bind these through ctypes.
+ *
+ * Conventions
+ *   - Activations are row-major [M, C] matrices with M = B*H*W in NHWC order (a channels_last
+ *     NCHW tensor is exactly this layout), element type `ogv_dtype` (fp32 or bf16), fp32 math.
+ *   - Weights/bias/affine parameters are fp32 (the AMP master copy); bf16 kernels round them
+ *     to bf16 when staging.  Weight gradients are produced in fp32.
+ *   - The library never allocates, frees or synchronises.  Scratch is passed in by the caller
+ *     (sizes from the *_ws_bytes queries).  Every call enqueues on `stream` (a hipStream_t).
+ *   - Return 0 on success; otherwise a non-zero code and ogv_last_error() (thread-local) says why.
+ *     Shapes are validated on the host before any launch.
+ */
+#ifndef OGV_H
+#define OGV_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum { OGV_F32 = 0, OGV_BF16 = 1 } ogv_dtype;
+typedef enum { OGV_ACT_NONE = 0, OGV_ACT_GELU = 1, OGV_ACT_SILU = 2, OGV_ACT_RELU = 3 } ogv_act;
+
+enum {
+  OGV_OK = 0,
+  OGV_ERR_ARG = 1,       /* bad shape / pointer / enum */
+  OGV_ERR_UNSUPPORTED = 2,
+  OGV_ERR_LAUNCH = 3     /* hipGetLastError after the launch */
+};
+
+const char* ogv_version(void);
+const char* ogv_last_error(void);
+
+/* ---------------------------------------------------------------------------------------------
+ * Outlook aggregation.  Replaces, for stride 1:
+ *   softmax over the k*k logits per (pixel, head)   src/model/outlook_attention.py:106-107
+ *   F.unfold(v, k, padding=k//2) + mul + sum(-1)    src/model/outlook_attention.py:111-120
+ * logits: [M, heads*k*k] (channel = head*k*k + ki*k + kj, unscaled), v/y: [M, C], M = B*H*W.
+ * Zero-padded neighbours keep their softmax mass (reference semantics).
+ * bwd writes dv [M, C] and dlogits [M, heads*k*k]; probs_ws is fp32 [M, heads*k*k] scratch.
+ * ld_logits is the row stride of logits/dlogits in elements (>= heads*k*k).
+ * ------------------------------------------------------------------------------------------- */
+int ogv_outlook_agg_fwd(const void* v, const void* logits, void* y, int B, int H, int W, int C,
+                        int heads, int k, int ld_logits, ogv_dtype dt, void* stream);
+int ogv_outlook_agg_bwd(const void* dy, const void* v, const void* logits, void* dv, void* dlogits,
+                        float* probs_ws, int B, int H, int W, int C, int heads, int k, int ld_logits,
+                        ogv_dtype dt, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Grid multi-head self-attention core.  Replaces
+ *   grid_partition (strided regroup)                 src/model/grid_partition.py:3-17
+ *   qkv reshape/permute, (q@k^T)*scale, softmax, @v  src/model/grid_attention.py:70-86
+ *   grid_unpartition                                  src/model/grid_partition.py:20-32
+ * The partition is folded into the addressing: group (b, gi, gj) holds the N = (H/g)*(W/g)
+ * pixels (ty*g+gi, tx*g+gj), token index ty*(W/g)+tx.
+ * qkv: [M, 3C] (channel = s*C + head*hd + d, s in {q,k,v}); out: [M, C]; lse: fp32 [M, heads]
+ * (log-sum-exp of the scaled scores, saved for bwd).  probs (nullable) receives the
+ * post-softmax matrix fp32 [B*g*g, heads, N, N] for the capture_attn hook (:77-83).
+ * bwd: dqkv [M, 3C]; delta_ws fp32 [M, heads] scratch.
+ * ------------------------------------------------------------------------------------------- */
+int ogv_grid_attn_fwd(const void* qkv, void* out, float* lse, float* probs, int B, int H, int W, int C,
+                      int heads, int g, float scale, ogv_dtype dt, void* stream);
+int ogv_grid_attn_bwd(const void* dout, const void* qkv, const void* out, const float* lse, void* dqkv,
+                      float* delta_ws, int B, int H, int W, int C, int heads, int g, float scale,
+                      ogv_dtype dt, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * LayerNorm over the contiguous channel dim of [M, C] rows.  Replaces nn.LayerNorm inside
+ * LayerNorm2d (src/model/outlook_attention.py:26-31, eps 1e-6) and OutGridBlock.norm2/norm3
+ * (src/model/Out_Grid_Block.py:69,84, eps 1e-5).  mean/rstd: fp32 [M] (saved for bwd).
+ * bwd: dx [M, C]; dgamma/dbeta fp32 [C] (overwritten); ws >= ogv_layernorm_bwd_ws_bytes(M, C).
+ * ------------------------------------------------------------------------------------------- */
+int ogv_layernorm_fwd(const void* x, const float* gamma, const float* beta, void* y, float* mean,
+                      float* rstd, int M, int C, float eps, ogv_dtype dt, void* stream);
+size_t ogv_layernorm_bwd_ws_bytes(int M, int C);
+int ogv_layernorm_bwd(const void* dy, const void* x, const float* gamma, const float* mean,
+                      const float* rstd, void* dx, float* dgamma, float* dbeta, void* ws, int M, int C,
+                      ogv_dtype dt, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Dense projection GEMMs on MFMA (1x1 Conv2d / nn.Linear of the hot path:
+ * outlook_attention.py:83-88,37-40; grid_attention.py:57-59; Out_Grid_Block.py:18-21).
+ *
+ * fwd:   out[m,n] = res[m,n] + rs[m/rps] * ( sum_k act_in(A[m,k]) * W[n,k] + bias[n] )
+ *        A: [M, K] (row stride lda), W: fp32 [N, K], out/res: [M, N] (row stride ldo).
+ *        act_in is applied to A on load (the producer stored the pre-activation).
+ *        res / rs / bias nullable; rps = rows per sample (H*W) for the per-sample DropPath scale.
+ * dgrad: dA[m,k] = act_in'(Z[m,k]) * sum_n (rs[m/rps]*dOut[m,n]) * W[n,k]
+ *        (Z = the pre-activation input of fwd, nullable when act_in = NONE).
+ * wgrad: dW[n,k] = sum_m rs*dOut[m,n] * act_in(A[m,k]);  dbias[n] = sum_m rs*dOut[m,n]
+ *        (dbias nullable).  dW/dbias are fp32 and overwritten; ws >= ogv_gemm_wgrad_ws_bytes.
+ * ------------------------------------------------------------------------------------------- */
+int ogv_gemm_fwd(const void* A, int lda, const float* W, const float* bias, const void* res,
+                 const float* rs, int rps, void* out, int ldo, int M, int N, int K, ogv_act act_in,
+                 ogv_dtype dt, void* stream);
+size_t ogv_gemm_dgrad_ws_bytes(int N, int K);
+int ogv_gemm_dgrad(const void* dout, int ldd, const float* W, const void* Z, int ldz, const float* rs,
+                   int rps, void* dA, int lda, int M, int N, int K, ogv_act act_in, void* ws,
+                   ogv_dtype dt, void* stream);
+size_t ogv_gemm_wgrad_ws_bytes(int M, int N, int K);
+int ogv_gemm_wgrad(const void* dout, int ldd, const void* A, int lda, const float* rs, int rps,
+                   float* dW, float* dbias, int M, int N, int K, ogv_act act_in, void* ws,
+                   ogv_dtype dt, void* stream);
+
+/* Elementwise helpers used by the autograd glue. */
+int ogv_cast(const void* src, ogv_dtype src_dt, void* dst, ogv_dtype dst_dt, size_t n, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OGV_H */

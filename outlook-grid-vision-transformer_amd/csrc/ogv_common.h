@@ -1,0 +1,133 @@
+// Shared device/host helpers for libogv_hip.so (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+#include <stdarg.h>
+
+#include "../../include/ogv.h"
+
+typedef __bf16 bf16;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+
+namespace ogv {
+
+// ---------------------------------------------------------------- host-side error plumbing
+void set_error(const char* fmt, ...);
+int check_launch(const char* what);
+
+#define OGV_REQUIRE(cond, ...)                 \
+  do {                                         \
+    if (!(cond)) {                             \
+      ::ogv::set_error(__VA_ARGS__);           \
+      return OGV_ERR_ARG;                      \
+    }                                          \
+  } while (0)
+
+static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+static inline unsigned cdiv(long a, long b) { return (unsigned)((a + b - 1) / b); }
+
+// ---------------------------------------------------------------- element conversion
+__device__ __forceinline__ float to_f(float x) { return x; }
+__device__ __forceinline__ float to_f(bf16 x) { return (float)x; }
+template <typename T> __device__ __forceinline__ T from_f(float x);
+template <> __device__ __forceinline__ float from_f<float>(float x) { return x; }
+template <> __device__ __forceinline__ bf16 from_f<bf16>(float x) { return (bf16)x; }
+
+// Vector load/store of V consecutive elements (V*sizeof(T) must be 4, 8 or 16 bytes aligned).
+template <typename T, int V> struct VecT;
+template <> struct VecT<float, 1> { typedef float type; };
+template <> struct VecT<float, 2> { typedef float2 type; };
+template <> struct VecT<float, 4> { typedef float4 type; };
+template <> struct VecT<float, 8> { typedef float4 type; };  // two loads
+template <> struct VecT<bf16, 1> { typedef bf16 type; };
+template <> struct VecT<bf16, 2> { typedef uint32_t type; };
+template <> struct VecT<bf16, 4> { typedef uint2 type; };
+template <> struct VecT<bf16, 8> { typedef uint4 type; };
+
+template <typename T, int V>
+__device__ __forceinline__ void load_vec(const T* __restrict__ p, float* out) {
+  if constexpr (sizeof(T) == 4 && V == 8) {
+    float4 a = *reinterpret_cast<const float4*>(p);
+    float4 b = *reinterpret_cast<const float4*>(p + 4);
+    out[0] = a.x; out[1] = a.y; out[2] = a.z; out[3] = a.w;
+    out[4] = b.x; out[5] = b.y; out[6] = b.z; out[7] = b.w;
+  } else if constexpr (V == 1) {
+    out[0] = to_f(p[0]);
+  } else {
+    typedef typename VecT<T, V>::type VT;
+    VT v = *reinterpret_cast<const VT*>(p);
+    const T* e = reinterpret_cast<const T*>(&v);
+#pragma unroll
+    for (int i = 0; i < V; ++i) out[i] = to_f(e[i]);
+  }
+}
+
+template <typename T, int V>
+__device__ __forceinline__ void store_vec(T* __restrict__ p, const float* in) {
+  if constexpr (sizeof(T) == 4 && V == 8) {
+    *reinterpret_cast<float4*>(p) = make_float4(in[0], in[1], in[2], in[3]);
+    *reinterpret_cast<float4*>(p + 4) = make_float4(in[4], in[5], in[6], in[7]);
+  } else if constexpr (V == 1) {
+    p[0] = from_f<T>(in[0]);
+  } else {
+    typedef typename VecT<T, V>::type VT;
+    VT v;
+    T* e = reinterpret_cast<T*>(&v);
+#pragma unroll
+    for (int i = 0; i < V; ++i) e[i] = from_f<T>(in[i]);
+    *reinterpret_cast<VT*>(p) = v;
+  }
+}
+
+// ---------------------------------------------------------------- activations (exact erf GELU)
+__device__ __forceinline__ float act_fwd(int act, float x) {
+  switch (act) {
+    case OGV_ACT_GELU: return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+    case OGV_ACT_SILU: return x / (1.0f + __expf(-x));
+    case OGV_ACT_RELU: return x > 0.f ? x : 0.f;
+    default: return x;
+  }
+}
+// d act / dx evaluated at the pre-activation x
+__device__ __forceinline__ float act_grad(int act, float x) {
+  switch (act) {
+    case OGV_ACT_GELU: {
+      const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+      const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
+      return cdf + x * pdf;
+    }
+    case OGV_ACT_SILU: {
+      const float s = 1.0f / (1.0f + __expf(-x));
+      return s * (1.0f + x * (1.0f - s));
+    }
+    case OGV_ACT_RELU: return x > 0.f ? 1.f : 0.f;
+    default: return 1.f;
+  }
+}
+
+// ---------------------------------------------------------------- wave reductions (wave64)
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+template <int G>
+__device__ __forceinline__ float group_sum(float v) {  // sum within aligned groups of G lanes
+#pragma unroll
+  for (int o = G / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+template <int G>
+__device__ __forceinline__ float group_max(float v) {
+#pragma unroll
+  for (int o = G / 2; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+}  // namespace ogv

@@ -1,0 +1,275 @@
+// LayerNorm over the contiguous channel dim of [M, C] rows (NHWC activations).
+// Replaces nn.LayerNorm in LayerNorm2d (src/model/outlook_attention.py:24-31; the two permute+
+// contiguous copies disappear because the activation is already channel-last) and
+// OutGridBlock.norm2/norm3 (src/model/Out_Grid_Block.py:69,84,98,102).
+// A row is owned by G lanes of one wave (G = pow2 >= C/VEC); two-pass mean/variance in registers.
+#include "ogv_common.h"
+
+namespace ogv {
+
+template <typename T, int G, int NV, int VEC>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, const float* __restrict__ gamma,
+                                                     const float* __restrict__ beta, T* __restrict__ y,
+                                                     float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                     long M, int C, float eps) {
+  constexpr int E = NV * VEC;
+  const int lane_g = threadIdx.x % G;
+  const long rows_per_block = blockDim.x / G;
+  float gw[E], bw[E];
+  bool valid[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int c = (v * G + lane_g) * VEC;
+    valid[v] = c < C;
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      gw[v * VEC + i] = valid[v] && gamma ? gamma[c + i] : 1.f;
+      bw[v * VEC + i] = valid[v] && beta ? beta[c + i] : 0.f;
+    }
+  }
+  const float invC = 1.f / (float)C;
+  for (long row = blockIdx.x * rows_per_block + threadIdx.x / G; row < M; row += (long)gridDim.x * rows_per_block) {
+    const T* xr = x + row * C;
+    float xv[E];
+    float s = 0.f;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int c = (v * G + lane_g) * VEC;
+      if (valid[v]) {
+        load_vec<T, VEC>(xr + c, xv + v * VEC);
+      } else {
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) xv[v * VEC + i] = 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) s += xv[v * VEC + i];
+    }
+    const float mu = group_sum<G>(s) * invC;
+    float ss = 0.f;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      if (valid[v]) {
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) {
+          const float d = xv[v * VEC + i] - mu;
+          ss = fmaf(d, d, ss);
+        }
+      }
+    }
+    const float rs = rsqrtf(group_sum<G>(ss) * invC + eps);
+    T* yr = y + row * C;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int c = (v * G + lane_g) * VEC;
+      if (valid[v]) {
+        float o[VEC];
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) o[i] = (xv[v * VEC + i] - mu) * rs * gw[v * VEC + i] + bw[v * VEC + i];
+        store_vec<T, VEC>(yr + c, o);
+      }
+    }
+    if (lane_g == 0) {
+      if (mean_out) mean_out[row] = mu;
+      if (rstd_out) rstd_out[row] = rs;
+    }
+  }
+}
+
+// dx = rstd * (g - mean(g) - xhat * mean(g * xhat)),  g = dy * gamma
+// per-block partial dgamma = sum dy*xhat, dbeta = sum dy  -> part[block][2][C]
+template <typename T, int G, int NV, int VEC>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                     const float* __restrict__ gamma, const float* __restrict__ mean,
+                                                     const float* __restrict__ rstd, T* __restrict__ dx,
+                                                     float* __restrict__ part, long M, int C) {
+  constexpr int E = NV * VEC;
+  const int lane_g = threadIdx.x % G;
+  const long rows_per_block = blockDim.x / G;
+  float gw[E], dgam[E], dbet[E];
+  bool valid[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int c = (v * G + lane_g) * VEC;
+    valid[v] = c < C;
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      gw[v * VEC + i] = valid[v] && gamma ? gamma[c + i] : 1.f;
+      dgam[v * VEC + i] = 0.f;
+      dbet[v * VEC + i] = 0.f;
+    }
+  }
+  const float invC = 1.f / (float)C;
+  for (long row = blockIdx.x * rows_per_block + threadIdx.x / G; row < M; row += (long)gridDim.x * rows_per_block) {
+    const float mu = mean[row], rs = rstd[row];
+    float xh[E], gv[E];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int c = (v * G + lane_g) * VEC;
+      if (valid[v]) {
+        float xv[VEC], dv[VEC];
+        load_vec<T, VEC>(x + row * C + c, xv);
+        load_vec<T, VEC>(dy + row * C + c, dv);
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) {
+          const int e = v * VEC + i;
+          xh[e] = (xv[i] - mu) * rs;
+          gv[e] = dv[i] * gw[e];
+          s1 += gv[e];
+          s2 = fmaf(gv[e], xh[e], s2);
+          dgam[e] = fmaf(dv[i], xh[e], dgam[e]);
+          dbet[e] += dv[i];
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) { xh[v * VEC + i] = 0.f; gv[v * VEC + i] = 0.f; }
+      }
+    }
+    const float m1 = group_sum<G>(s1) * invC;
+    const float m2 = group_sum<G>(s2) * invC;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int c = (v * G + lane_g) * VEC;
+      if (valid[v]) {
+        float o[VEC];
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) o[i] = rs * (gv[v * VEC + i] - m1 - xh[v * VEC + i] * m2);
+        store_vec<T, VEC>(dx + row * C + c, o);
+      }
+    }
+  }
+  // reduce the per-lane partials of the (256/G) row slots of this block through LDS
+  __shared__ float red[256];
+  float* out = part + (long)blockIdx.x * 2 * C;
+  for (int which = 0; which < 2; ++which) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) {
+        red[threadIdx.x] = which == 0 ? dgam[v * VEC + i] : dbet[v * VEC + i];
+        __syncthreads();
+        if (threadIdx.x < G) {
+          float acc = 0.f;
+          for (int r = threadIdx.x; r < (int)blockDim.x; r += G) acc += red[r];
+          const int c = (v * G + threadIdx.x) * VEC + i;
+          if (c < C) out[which * C + c] = acc;
+        }
+        __syncthreads();
+      }
+    }
+  }
+}
+
+// out[j] = sum_r part[r * ld + j] for j < n   (column sums of a [R, n] fp32 slab)
+__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ part, float* __restrict__ out0,
+                                                     float* __restrict__ out1, int R, int n0, int ld) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= ld) return;
+  float acc = 0.f;
+  for (int r = 0; r < R; ++r) acc += part[(long)r * ld + j];
+  if (j < n0) {
+    if (out0) out0[j] = acc;
+  } else if (out1) {
+    out1[j - n0] = acc;
+  }
+}
+
+struct LnPlan {
+  int G, NV, VEC;
+};
+
+static int ln_plan(int C, LnPlan& p) {
+  if (C % 8 == 0) p.VEC = 8;
+  else if (C % 4 == 0) p.VEC = 4;
+  else return OGV_ERR_UNSUPPORTED;
+  const int nvec = C / p.VEC;
+  int G = 1;
+  while (G < nvec && G < 64) G <<= 1;
+  p.G = G < 2 ? 2 : G;
+  p.NV = (nvec + p.G - 1) / p.G;
+  if (p.NV > 4) return OGV_ERR_UNSUPPORTED;
+  if (p.NV == 3) p.NV = 4;
+  return OGV_OK;
+}
+
+static long ln_blocks(long M, int G) {
+  const long rows_per_block = 256 / G;
+  long nb = (M + rows_per_block - 1) / rows_per_block;
+  return nb < 2048 ? nb : 2048;
+}
+
+#define OGV_LN_CASE_NV(T, G, VEC, FN, ...)                 \
+  switch (p.NV) {                                          \
+    case 1: FN<T, G, 1, VEC>(__VA_ARGS__); break;          \
+    case 2: FN<T, G, 2, VEC>(__VA_ARGS__); break;          \
+    default: FN<T, G, 4, VEC>(__VA_ARGS__); break;         \
+  }
+#define OGV_LN_CASE_G(T, VEC, FN, ...)                     \
+  switch (p.G) {                                           \
+    case 2: OGV_LN_CASE_NV(T, 2, VEC, FN, __VA_ARGS__) break;   \
+    case 4: OGV_LN_CASE_NV(T, 4, VEC, FN, __VA_ARGS__) break;   \
+    case 8: OGV_LN_CASE_NV(T, 8, VEC, FN, __VA_ARGS__) break;   \
+    case 16: OGV_LN_CASE_NV(T, 16, VEC, FN, __VA_ARGS__) break; \
+    case 32: OGV_LN_CASE_NV(T, 32, VEC, FN, __VA_ARGS__) break; \
+    default: OGV_LN_CASE_NV(T, 64, VEC, FN, __VA_ARGS__) break; \
+  }
+#define OGV_LN_DISPATCH(FN, ...)                                               \
+  do {                                                                         \
+    if (dt == OGV_BF16) {                                                      \
+      if (p.VEC == 8) { OGV_LN_CASE_G(bf16, 8, FN, __VA_ARGS__) }              \
+      else { OGV_LN_CASE_G(bf16, 4, FN, __VA_ARGS__) }                         \
+    } else {                                                                   \
+      if (p.VEC == 8) { OGV_LN_CASE_G(float, 8, FN, __VA_ARGS__) }             \
+      else { OGV_LN_CASE_G(float, 4, FN, __VA_ARGS__) }                        \
+    }                                                                          \
+  } while (0)
+
+template <typename T, int G, int NV, int VEC>
+static void ln_fwd_launch(const void* x, const float* gamma, const float* beta, void* y, float* mean, float* rstd,
+                          long M, int C, float eps, hipStream_t s) {
+  ln_fwd_kernel<T, G, NV, VEC><<<(unsigned)ln_blocks(M, G), 256, 0, s>>>((const T*)x, gamma, beta, (T*)y, mean, rstd,
+                                                                         M, C, eps);
+}
+
+template <typename T, int G, int NV, int VEC>
+static void ln_bwd_launch(const void* dy, const void* x, const float* gamma, const float* mean, const float* rstd,
+                          void* dx, float* part, long nb, long M, int C, hipStream_t s) {
+  ln_bwd_kernel<T, G, NV, VEC><<<(unsigned)nb, 256, 0, s>>>((const T*)dy, (const T*)x, gamma, mean, rstd, (T*)dx,
+                                                            part, M, C);
+}
+
+}  // namespace ogv
+
+using namespace ogv;
+
+extern "C" int ogv_layernorm_fwd(const void* x, const float* gamma, const float* beta, void* y, float* mean,
+                                 float* rstd, int M, int C, float eps, ogv_dtype dt, void* stream) {
+  OGV_REQUIRE(x && y, "ogv_layernorm_fwd: null pointer");
+  OGV_REQUIRE(M >= 0 && C > 0, "ogv_layernorm_fwd: bad shape M=%d C=%d", M, C);
+  LnPlan p;
+  OGV_REQUIRE(ln_plan(C, p) == OGV_OK, "ogv_layernorm_fwd: C=%d unsupported (need C%%4==0, C<=2048)", C);
+  if (M == 0) return OGV_OK;
+  OGV_LN_DISPATCH(ln_fwd_launch, x, gamma, beta, y, mean, rstd, (long)M, C, eps, as_stream(stream));
+  return check_launch("ogv_layernorm_fwd");
+}
+
+extern "C" size_t ogv_layernorm_bwd_ws_bytes(int M, int C) {
+  LnPlan p;
+  if (ln_plan(C, p) != OGV_OK) return 0;
+  return (size_t)ln_blocks(M > 0 ? M : 1, p.G) * 2 * C * sizeof(float);
+}
+
+extern "C" int ogv_layernorm_bwd(const void* dy, const void* x, const float* gamma, const float* mean,
+                                 const float* rstd, void* dx, float* dgamma, float* dbeta, void* ws, int M, int C,
+                                 ogv_dtype dt, void* stream) {
+  OGV_REQUIRE(dy && x && mean && rstd && dx && ws, "ogv_layernorm_bwd: null pointer");
+  OGV_REQUIRE(M > 0 && C > 0, "ogv_layernorm_bwd: bad shape M=%d C=%d", M, C);
+  LnPlan p;
+  OGV_REQUIRE(ln_plan(C, p) == OGV_OK, "ogv_layernorm_bwd: C=%d unsupported", C);
+  const long nb = ln_blocks(M, p.G);
+  hipStream_t s = as_stream(stream);
+  float* part = (float*)ws;
+  OGV_LN_DISPATCH(ln_bwd_launch, dy, x, gamma, mean, rstd, dx, part, nb, (long)M, C, s);
+  if (dgamma || dbeta) colsum_kernel<<<cdiv(2 * C, 256), 256, 0, s>>>(part, dgamma, dbeta, (int)nb, C, 2 * C);
+  return check_launch("ogv_layernorm_bwd");
+}

@@ -1,0 +1,76 @@
+"""ctypes binding of libogv_hip.so (the C-ABI declared in include/ogv.h).
+
+The library is loaded AFTER ``import torch`` so that its ``libamdhip64.so.7`` dependency resolves
+to the HIP runtime torch already mapped (same SONAME); device pointers and streams are then
+shared with PyTorch's caching allocator and stream pool.  There is no fallback: if the shared
+object is missing or a symbol is absent, the import raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the CDLL: binds to torch's HIP runtime)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("OGV_LIB", os.path.join(_HERE, "libogv_hip.so"))
+
+_p = ctypes.c_void_p
+_i = ctypes.c_int
+_f = ctypes.c_float
+_sz = ctypes.c_size_t
+
+# name -> (restype, argtypes); must match include/ogv.h exactly
+SIGNATURES = {
+    "ogv_version": (ctypes.c_char_p, []),
+    "ogv_last_error": (ctypes.c_char_p, []),
+    "ogv_outlook_agg_fwd": (_i, [_p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _p]),
+    "ogv_outlook_agg_bwd": (_i, [_p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _p]),
+    "ogv_grid_attn_fwd": (_i, [_p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _f, _i, _p]),
+    "ogv_grid_attn_bwd": (_i, [_p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _f, _i, _p]),
+    "ogv_layernorm_fwd": (_i, [_p, _p, _p, _p, _p, _p, _i, _i, _f, _i, _p]),
+    "ogv_layernorm_bwd_ws_bytes": (_sz, [_i, _i]),
+    "ogv_layernorm_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _p]),
+    "ogv_gemm_fwd": (_i, [_p, _i, _p, _p, _p, _p, _i, _p, _i, _i, _i, _i, _i, _i, _p]),
+    "ogv_gemm_dgrad_ws_bytes": (_sz, [_i, _i]),
+    "ogv_gemm_dgrad": (_i, [_p, _i, _p, _p, _i, _p, _i, _p, _i, _i, _i, _i, _i, _p, _i, _p]),
+    "ogv_gemm_wgrad_ws_bytes": (_sz, [_i, _i, _i]),
+    "ogv_gemm_wgrad": (_i, [_p, _i, _p, _i, _p, _i, _p, _p, _i, _i, _i, _i, _p, _i, _p]),
+    "ogv_cast": (_i, [_p, _i, _p, _i, _sz, _p]),
+}
+
+OGV_F32, OGV_BF16 = 0, 1
+ACT = {None: 0, "none": 0, "gelu": 1, "silu": 2, "relu": 3}
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load (once) and return the library; raises OSError / AttributeError loudly on failure."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise OSError(f"libogv_hip.so not found at {LIB_PATH}: build it with "
+                      f"`python -c 'import __graft_entry__ as g; g.build()'` (or make -C .../csrc)")
+    lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)  # AttributeError if the symbol is missing
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+class OgvError(RuntimeError):
+    pass
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load().ogv_last_error().decode(errors="replace")
+        raise OgvError(f"{what} failed (code {rc}): {msg}")
+
+
+def version() -> str:
+    return load().ogv_version().decode()

@@ -1,0 +1,277 @@
+"""Autograd glue between the drop-in nn.Modules and the C-ABI of libogv_hip.so.
+
+Every function here takes/returns device tensors and calls the HIP kernels through ctypes on
+torch's current stream.  There is NO CPU path: a CPU tensor raises, so a test that passes can
+only have passed through the native kernels.
+
+Activations are handled as row-major [M, C] matrices, M = B*H*W: a channels_last NCHW tensor is
+exactly that layout, so the reference's `.permute(...).contiguous()` copies
+(src/model/outlook_attention.py:28-30, src/model/Out_Grid_Block.py:96,107) become free views.
+"""
+from __future__ import annotations
+
+import ctypes
+import warnings
+
+import torch
+
+from . import _lib
+from ._lib import ACT, OGV_BF16, OGV_F32, check
+
+_vp = ctypes.c_void_p
+
+
+def _ptr(t):
+    return None if t is None else _vp(t.data_ptr())
+
+
+def _stream():
+    return _vp(torch.cuda.current_stream().cuda_stream)
+
+
+def _dt(t: torch.Tensor) -> int:
+    if t.dtype == torch.bfloat16:
+        return OGV_BF16
+    if t.dtype == torch.float32:
+        return OGV_F32
+    raise TypeError(f"ogv kernels support float32 and bfloat16 activations, got {t.dtype}")
+
+
+def require_device(*tensors, what="ogv"):
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError(f"{what}: the MI355X kernels need HIP device tensors (got {t.device}); "
+                               f"this framework has no CPU execution path")
+
+
+def _ws(nbytes: int, device) -> torch.Tensor:
+    return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
+
+
+_warned_fp16 = False
+
+
+def compute_dtype(x: torch.Tensor) -> torch.dtype:
+    """Activation dtype for the kernels: the autocast dtype inside an autocast region (fp16 is
+    computed as bf16 on MI355X), else the input dtype (fp32 or bf16)."""
+    global _warned_fp16
+    if x.is_cuda and torch.is_autocast_enabled("cuda"):
+        d = torch.get_autocast_dtype("cuda")
+    else:
+        d = x.dtype
+    if d == torch.float16:
+        if not _warned_fp16:
+            warnings.warn("ogv: fp16 autocast requested; the MI355X kernels compute in bf16 instead")
+            _warned_fp16 = True
+        d = torch.bfloat16
+    if d not in (torch.float32, torch.bfloat16):
+        raise TypeError(f"ogv: unsupported activation dtype {d}")
+    return d
+
+
+def f32(p):
+    """Parameters go to the kernels as fp32 (the AMP master copy); differentiable cast if needed."""
+    if p is None:
+        return None
+    return p if p.dtype == torch.float32 else p.float()
+
+
+# ------------------------------------------------------------------------------------------------
+# layout helpers
+# ------------------------------------------------------------------------------------------------
+def nchw_to_rows(x: torch.Tensor) -> torch.Tensor:
+    """[B,C,H,W] -> [B*H*W, C] view (copies once into channels_last if the input is not)."""
+    B, C, H, W = x.shape
+    if not x.is_contiguous(memory_format=torch.channels_last):
+        x = x.contiguous(memory_format=torch.channels_last)
+    return x.permute(0, 2, 3, 1).reshape(B * H * W, C)
+
+
+def rows_to_nchw(y: torch.Tensor, B: int, H: int, W: int) -> torch.Tensor:
+    """[B*H*W, C] -> [B,C,H,W] channels_last view (no copy)."""
+    return y.view(B, H, W, y.shape[-1]).permute(0, 3, 1, 2)
+
+
+def _rows_contig(t: torch.Tensor) -> torch.Tensor:
+    if t.stride(-1) != 1 or t.stride(0) < t.shape[-1] or t.data_ptr() % 16:
+        t = t.contiguous()
+    return t
+
+
+# ------------------------------------------------------------------------------------------------
+# Linear / 1x1 conv on rows:  out = res + rs[b] * (act_in(x) @ W^T + b)
+# ------------------------------------------------------------------------------------------------
+class _Linear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x2d, w2d, bias, residual, row_scale, rps, act_in):
+        lib = _lib.load()
+        M, K = x2d.shape
+        N = w2d.shape[0]
+        out = torch.empty((M, N), dtype=x2d.dtype, device=x2d.device)
+        check(lib.ogv_gemm_fwd(_ptr(x2d), x2d.stride(0), _ptr(w2d), _ptr(bias), _ptr(residual), _ptr(row_scale),
+                               int(rps), _ptr(out), N, M, N, K, ACT[act_in], _dt(x2d), _stream()), "ogv_gemm_fwd")
+        ctx.save_for_backward(x2d, w2d, row_scale)
+        ctx.meta = (M, N, K, int(rps), ACT[act_in], bias is not None, residual is not None)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        lib = _lib.load()
+        x2d, w2d, rs = ctx.saved_tensors
+        M, N, K, rps, act, has_bias, has_res = ctx.meta
+        dout = dout.to(x2d.dtype).contiguous()
+        dt, st = _dt(x2d), _stream()
+        dx = dw = db = dres = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty((M, K), dtype=x2d.dtype, device=x2d.device)
+            ws = _ws(lib.ogv_gemm_dgrad_ws_bytes(N, K), x2d.device)
+            check(lib.ogv_gemm_dgrad(_ptr(dout), N, _ptr(w2d), _ptr(x2d) if act else None, x2d.stride(0), _ptr(rs),
+                                     rps, _ptr(dx), K, M, N, K, act, _ptr(ws), dt, st), "ogv_gemm_dgrad")
+        if ctx.needs_input_grad[1] or (has_bias and ctx.needs_input_grad[2]):
+            dw = torch.empty((N, K), dtype=torch.float32, device=x2d.device)
+            db = torch.empty((N,), dtype=torch.float32, device=x2d.device) if has_bias else None
+            ws = _ws(lib.ogv_gemm_wgrad_ws_bytes(M, N, K), x2d.device)
+            check(lib.ogv_gemm_wgrad(_ptr(dout), N, _ptr(x2d), x2d.stride(0), _ptr(rs), rps, _ptr(dw), _ptr(db), M, N,
+                                     K, act, _ptr(ws), dt, st), "ogv_gemm_wgrad")
+        if has_res and ctx.needs_input_grad[3]:
+            dres = dout
+        return dx, dw, db, dres, None, None, None
+
+
+def linear_rows(x2d, weight, bias=None, residual=None, row_scale=None, rps=1, act_in=None):
+    """x2d [M,K] (row stride >= K), weight [N,K] (or [N,K,1,1]), residual [M,N]."""
+    require_device(x2d, weight, bias, residual, row_scale, what="ogv.linear")
+    x2d = _rows_contig(x2d)
+    w2d = f32(weight).reshape(weight.shape[0], -1)
+    if w2d.shape[1] != x2d.shape[1]:
+        raise ValueError(f"ogv.linear: weight in_features {w2d.shape[1]} != input features {x2d.shape[1]}")
+    if residual is not None:
+        residual = residual.to(x2d.dtype).contiguous()
+        if residual.shape != (x2d.shape[0], w2d.shape[0]):
+            raise ValueError("ogv.linear: residual shape mismatch")
+    if row_scale is not None:
+        row_scale = row_scale.float().contiguous()
+    return _Linear.apply(x2d, w2d, f32(bias), residual, row_scale, int(rps), act_in)
+
+
+# ------------------------------------------------------------------------------------------------
+# LayerNorm over the last (contiguous) dim
+# ------------------------------------------------------------------------------------------------
+class _LayerNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x2d, gamma, beta, eps):
+        lib = _lib.load()
+        M, C = x2d.shape
+        y = torch.empty_like(x2d)
+        mean = torch.empty((M,), dtype=torch.float32, device=x2d.device)
+        rstd = torch.empty((M,), dtype=torch.float32, device=x2d.device)
+        check(lib.ogv_layernorm_fwd(_ptr(x2d), _ptr(gamma), _ptr(beta), _ptr(y), _ptr(mean), _ptr(rstd), M, C,
+                                    float(eps), _dt(x2d), _stream()), "ogv_layernorm_fwd")
+        ctx.save_for_backward(x2d, gamma, mean, rstd)
+        ctx.affine = (gamma is not None, beta is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        lib = _lib.load()
+        x2d, gamma, mean, rstd = ctx.saved_tensors
+        M, C = x2d.shape
+        dy = dy.to(x2d.dtype).contiguous()
+        dx = torch.empty_like(x2d)
+        dgamma = torch.empty((C,), dtype=torch.float32, device=x2d.device) if ctx.affine[0] else None
+        dbeta = torch.empty((C,), dtype=torch.float32, device=x2d.device) if ctx.affine[1] else None
+        ws = _ws(lib.ogv_layernorm_bwd_ws_bytes(M, C), x2d.device)
+        check(lib.ogv_layernorm_bwd(_ptr(dy), _ptr(x2d), _ptr(gamma), _ptr(mean), _ptr(rstd), _ptr(dx), _ptr(dgamma),
+                                    _ptr(dbeta), _ptr(ws), M, C, _dt(x2d), _stream()), "ogv_layernorm_bwd")
+        return dx, dgamma, dbeta, None
+
+
+def layer_norm_rows(x2d, gamma, beta, eps):
+    require_device(x2d, gamma, beta, what="ogv.layer_norm")
+    x2d = x2d.contiguous()
+    return _LayerNorm.apply(x2d, f32(gamma), f32(beta), float(eps))
+
+
+# ------------------------------------------------------------------------------------------------
+# Outlook aggregation (softmax over k*k + zero-padded neighbourhood gather)
+# ------------------------------------------------------------------------------------------------
+class _OutlookAgg(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, v2d, logits2d, B, H, W, heads, k):
+        lib = _lib.load()
+        M, C = v2d.shape
+        y = torch.empty_like(v2d)
+        check(lib.ogv_outlook_agg_fwd(_ptr(v2d), _ptr(logits2d), _ptr(y), B, H, W, C, heads, k, logits2d.stride(0),
+                                      _dt(v2d), _stream()), "ogv_outlook_agg_fwd")
+        ctx.save_for_backward(v2d, logits2d)
+        ctx.meta = (B, H, W, C, heads, k)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        lib = _lib.load()
+        v2d, logits2d = ctx.saved_tensors
+        B, H, W, C, heads, k = ctx.meta
+        kk = k * k
+        dy = dy.to(v2d.dtype).contiguous()
+        dv = torch.empty_like(v2d)
+        M = v2d.shape[0]
+        ld = logits2d.stride(0)
+        dlogits = torch.empty((M, ld), dtype=v2d.dtype, device=v2d.device)[:, : heads * kk]
+        probs = torch.empty((M, heads * kk), dtype=torch.float32, device=v2d.device)
+        check(lib.ogv_outlook_agg_bwd(_ptr(dy), _ptr(v2d), _ptr(logits2d), _ptr(dv), _ptr(dlogits), _ptr(probs), B, H,
+                                      W, C, heads, k, ld, _dt(v2d), _stream()), "ogv_outlook_agg_bwd")
+        return dv, dlogits, None, None, None, None, None
+
+
+def outlook_aggregate_rows(v2d, logits2d, B, H, W, heads, k):
+    require_device(v2d, logits2d, what="ogv.outlook_aggregate")
+    v2d = _rows_contig(v2d)
+    if logits2d.stride(-1) != 1 or logits2d.data_ptr() % 4:
+        logits2d = logits2d.contiguous()
+    if logits2d.dtype != v2d.dtype:
+        logits2d = logits2d.to(v2d.dtype)
+    return _OutlookAgg.apply(v2d, logits2d, int(B), int(H), int(W), int(heads), int(k))
+
+
+# ------------------------------------------------------------------------------------------------
+# Grid attention core (partition folded into addressing)
+# ------------------------------------------------------------------------------------------------
+class _GridAttn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv2d, B, H, W, heads, g, scale, want_probs):
+        lib = _lib.load()
+        M = qkv2d.shape[0]
+        C = qkv2d.shape[1] // 3
+        out = torch.empty((M, C), dtype=qkv2d.dtype, device=qkv2d.device)
+        lse = torch.empty((M, heads), dtype=torch.float32, device=qkv2d.device)
+        N = (H // g) * (W // g)
+        probs = (torch.empty((B * g * g, heads, N, N), dtype=torch.float32, device=qkv2d.device)
+                 if want_probs else None)
+        check(lib.ogv_grid_attn_fwd(_ptr(qkv2d), _ptr(out), _ptr(lse), _ptr(probs), B, H, W, C, heads, g,
+                                    float(scale), _dt(qkv2d), _stream()), "ogv_grid_attn_fwd")
+        ctx.save_for_backward(qkv2d, out, lse)
+        ctx.meta = (B, H, W, C, heads, g, float(scale))
+        if probs is None:
+            probs = torch.empty(0, device=qkv2d.device)
+        ctx.mark_non_differentiable(probs)
+        return out, probs
+
+    @staticmethod
+    def backward(ctx, dout, _dprobs):
+        lib = _lib.load()
+        qkv2d, out, lse = ctx.saved_tensors
+        B, H, W, C, heads, g, scale = ctx.meta
+        dout = dout.to(qkv2d.dtype).contiguous()
+        dqkv = torch.empty_like(qkv2d)
+        delta = torch.empty((qkv2d.shape[0], heads), dtype=torch.float32, device=qkv2d.device)
+        check(lib.ogv_grid_attn_bwd(_ptr(dout), _ptr(qkv2d), _ptr(out), _ptr(lse), _ptr(dqkv), _ptr(delta), B, H, W, C,
+                                    heads, g, scale, _dt(qkv2d), _stream()), "ogv_grid_attn_bwd")
+        return dqkv, None, None, None, None, None, None, None
+
+
+def grid_attention_rows(qkv2d, B, H, W, heads, g, scale, want_probs=False):
+    """qkv2d [B*H*W, 3C] -> (out [B*H*W, C], probs [B*g*g, heads, N, N] or empty)."""
+    require_device(qkv2d, what="ogv.grid_attention")
+    qkv2d = qkv2d.contiguous()
+    return _GridAttn.apply(qkv2d, int(B), int(H), int(W), int(heads), int(g), float(scale), bool(want_probs))

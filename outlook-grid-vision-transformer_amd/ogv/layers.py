@@ -1,0 +1,81 @@
+"""Parameter-compatible replacements for the dense layers of the hot path.
+
+They subclass the stock modules (so state_dict keys/shapes, isinstance checks and forward hooks
+are exactly those of the reference) and override ``forward`` to run the MFMA GEMM / LayerNorm
+kernels on channels-last rows.  Extra keyword arguments carry the fusions the blocks ask for:
+``residual`` (+ ``row_scale`` for DropPath) in the epilogue and ``act_in`` in the prologue.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from . import functional as OF
+
+
+def act_name(mod: nn.Module):
+    """Map an activation module to the kernels' prologue/epilogue activation."""
+    if isinstance(mod, nn.GELU):
+        if getattr(mod, "approximate", "none") != "none":
+            return None
+        return "gelu"
+    if isinstance(mod, nn.SiLU):
+        return "silu"
+    if isinstance(mod, nn.ReLU):
+        return "relu"
+    return None
+
+
+class Conv1x1(nn.Conv2d):
+    """nn.Conv2d(in, out, kernel_size=1) on NCHW tensors, computed as a GEMM over B*H*W rows.
+    The output is a channels_last NCHW tensor (physically [B*H*W, out])."""
+
+    def __init__(self, in_channels: int, out_channels: int, bias: bool = True):
+        super().__init__(in_channels, out_channels, kernel_size=1, bias=bias)
+
+    def forward(self, x, residual=None, row_scale=None, act_in=None):
+        B, C, H, W = x.shape
+        dt = OF.compute_dtype(x)
+        x2d = OF.nchw_to_rows(x.to(dt))
+        r2d = OF.nchw_to_rows(residual.to(dt)) if residual is not None else None
+        y = OF.linear_rows(x2d, self.weight, self.bias, r2d, row_scale, H * W, act_in)
+        return OF.rows_to_nchw(y, B, H, W)
+
+
+class Linear(nn.Linear):
+    """nn.Linear over the last dim of a contiguous [..., in] tensor (BHWC or [B, N, C]).
+    ``rps`` = rows per sample for the DropPath row scale."""
+
+    def forward(self, x, residual=None, row_scale=None, rps=None, act_in=None):
+        lead = x.shape[:-1]
+        dt = OF.compute_dtype(x)
+        x2d = x.to(dt).reshape(-1, x.shape[-1])
+        r2d = residual.to(dt).reshape(-1, self.out_features) if residual is not None else None
+        if rps is None:
+            rps = max(1, x2d.shape[0] // max(1, lead[0] if len(lead) else 1))
+        y = OF.linear_rows(x2d, self.weight, self.bias, r2d, row_scale, rps, act_in)
+        return y.view(*lead, self.out_features)
+
+
+class LayerNorm(nn.LayerNorm):
+    """nn.LayerNorm over the last dim (normalized_shape must be 1-D)."""
+
+    def forward(self, x):
+        if len(self.normalized_shape) != 1:
+            raise NotImplementedError("ogv LayerNorm supports a 1-D normalized_shape")
+        dt = OF.compute_dtype(x)
+        x2d = x.to(dt).reshape(-1, x.shape[-1])
+        y = OF.layer_norm_rows(x2d, self.weight, self.bias, self.eps)
+        return y.view(x.shape)
+
+
+def drop_path_scale(dp: nn.Module, x: torch.Tensor):
+    """Per-sample DropPath factor mask/keep as an fp32 [B] tensor, or None when the module is an
+    identity (eval, p == 0, nn.Identity).  Same Bernoulli(keep) draw as the reference
+    DropPath (src/model/Outlook_Block.py:15-22), applied inside the GEMM epilogue."""
+    p = float(getattr(dp, "drop_prob", 0.0))
+    if p <= 0.0 or not dp.training:
+        return None
+    keep = 1.0 - p
+    mask = torch.empty((x.shape[0],), device=x.device, dtype=torch.float32).bernoulli_(keep)
+    return mask / keep

@@ -1,0 +1,46 @@
+"""Model A (MaxOutNet): stem -> [OutGridBlock x depth (+ Downsample)] per stage -> BN/GAP/Linear.
+
+Drop-in for src/Model_A_OutGridNet.py:9-67 — the same constructor, module names
+(stem, proj_in, stages.<s>.<b>, downs.<s>, head_norm, classifier) and state_dict.  The blocks
+come from our src.model (HIP kernels); stem/downsample/head stay stock PyTorch-ROCm ops.
+"""
+from src.model.Out_Grid_Block import *  # noqa: F401,F403
+from src.model.downsampling import *  # noqa: F401,F403
+from src.model.stem_head import *  # noqa: F401,F403
+from src.stage_config import *  # noqa: F401,F403
+from src.model.Out_Grid_Block import OutGridBlock
+from src.model.downsampling import Downsample, DownsampleConfig
+from src.model.stem_head import ConvStem, List, make_dpr
+from src.stage_config import StageCfg
+import torch.nn as nn
+
+
+class MaxOutNet(nn.Module):
+    def __init__(self, num_classes: int, stages: List[StageCfg], in_ch: int = 3, stem_dim: int = 64,
+                 dpr_max: float = 0.1,
+                 down_cfg: DownsampleConfig = DownsampleConfig(kind="conv", act="silu", use_bn=True)):
+        super().__init__()
+        assert len(stages) >= 1
+        self.stem = ConvStem(in_ch, stem_dim, act="silu", use_bn=True)
+        first = stages[0].dim
+        self.proj_in = nn.Conv2d(stem_dim, first, kernel_size=1, bias=True) if stem_dim != first else nn.Identity()
+        rates = iter(make_dpr(sum(s.depth for s in stages), dpr_max))
+        self.stages = nn.ModuleList()
+        self.downs = nn.ModuleList()
+        for si, scfg in enumerate(stages):
+            self.stages.append(nn.ModuleList(
+                OutGridBlock(StageCfg(**{**scfg.__dict__, "drop_path": next(rates)})) for _ in range(scfg.depth)))
+            if si + 1 < len(stages):
+                self.downs.append(Downsample(scfg.dim, stages[si + 1].dim, cfg=down_cfg))
+        self.head_norm = nn.BatchNorm2d(stages[-1].dim)
+        self.classifier = nn.Linear(stages[-1].dim, num_classes)
+
+    def forward(self, x):
+        x = self.proj_in(self.stem(x))
+        for si, blocks in enumerate(self.stages):
+            for blk in blocks:
+                x = blk(x)
+            if si < len(self.downs):
+                x = self.downs[si](x)
+        pooled = self.head_norm(x).mean(dim=(2, 3))
+        return self.classifier(pooled)

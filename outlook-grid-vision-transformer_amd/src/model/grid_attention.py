@@ -1,0 +1,126 @@
+"""Grid multi-head self-attention — drop-in for src/model/grid_attention.py.
+
+  AttentionConfig / GridAttention2DConfig   :12-30
+  MultiHeadSelfAttention                    :33-89   qkv / proj Linear -> MFMA GEMMs;
+        reshape/permute + (q@k^T)*scale + softmax + @v (:70-86) -> ogv_grid_attn_{fwd,bwd}
+        capture_attn (:77-83) -> the kernel also writes the softmax matrix (last_attn)
+  GridAttention2D                           :93-131  partition/unpartition folded into the
+        kernel's addressing; _last_meta / _last_grid_hw / _last_g kept for the analysis hooks
+"""
+from dataclasses import dataclass
+from typing import Literal
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from src.model.grid_partition import *  # noqa: F401,F403
+from ogv import functional as OF
+from ogv.layers import Linear
+
+AttnMode = Literal["grid"]
+
+
+@dataclass(frozen=True)
+class AttentionConfig:
+    dim: int
+    num_heads: int
+    qkv_bias: bool = True
+    attn_drop: float = 0.0
+    proj_drop: float = 0.0
+
+
+@dataclass(frozen=True)
+class GridAttention2DConfig:
+    mode: AttnMode
+    dim: int
+    num_heads: int
+    grid_size: int
+    window_size: int = 1
+    qkv_bias: bool = True
+    attn_drop: float = 0.0
+    proj_drop: float = 0.0
+
+
+class MultiHeadSelfAttention(nn.Module):
+    """MHSA over token sets: [B, N, C] -> [B, N, C] (grid groups are token sets too)."""
+
+    def __init__(self, cfg: AttentionConfig):
+        super().__init__()
+        if cfg.dim <= 0:
+            raise ValueError("cfg.dim must be > 0")
+        if cfg.num_heads <= 0:
+            raise ValueError("cfg.num_heads must be > 0")
+        if cfg.dim % cfg.num_heads != 0:
+            raise ValueError(f"dim ({cfg.dim}) must be divisible by num_heads ({cfg.num_heads})")
+        self.dim = cfg.dim
+        self.num_heads = cfg.num_heads
+        self.head_dim = cfg.dim // cfg.num_heads
+        self.scale = self.head_dim ** -0.5
+        self.qkv = Linear(cfg.dim, 3 * cfg.dim, bias=cfg.qkv_bias)
+        self.attn_drop = nn.Dropout(cfg.attn_drop)
+        self.proj = Linear(cfg.dim, cfg.dim, bias=True)
+        self.proj_drop = nn.Dropout(cfg.proj_drop)
+
+    def attend_rows(self, x2d, B, H, W, g, residual=None, row_scale=None):
+        """Rows of a [B, H, W, C] image (or [B, 1, N, C] token set) -> attended rows (+ residual)."""
+        if self.training and self.attn_drop.p > 0:
+            raise NotImplementedError("ogv grid attention: attn_drop > 0 in training is not implemented")
+        capture = bool(getattr(self, "capture_attn", False))
+        qkv = self.qkv(x2d, rps=H * W)
+        out, probs = OF.grid_attention_rows(qkv, B, H, W, self.num_heads, g, self.scale, want_probs=capture)
+        if capture:
+            self.last_attn = probs.detach()
+            self.last_attn_postdrop = self.last_attn
+        if self.training and self.proj_drop.p > 0:
+            y = self.proj_drop(self.proj(out, rps=H * W))
+            if residual is None:
+                return y
+            if row_scale is not None:
+                y = y * row_scale.repeat_interleave(H * W).view(-1, 1).to(y.dtype)
+            return residual + y
+        return self.proj(out, residual=residual, row_scale=row_scale, rps=H * W)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if x.ndim != 3:
+            raise ValueError(f"Expected x.ndim==3 with shape [B, N, C]. Got {tuple(x.shape)}")
+        B, N, C = x.shape
+        if C != self.dim:
+            raise ValueError(f"Expected last dim C={self.dim}. Got C={C}")
+        x2d = x.to(OF.compute_dtype(x)).reshape(B * N, C)
+        return self.attend_rows(x2d, B, 1, N, 1).view(B, N, C)
+
+
+class GridAttention2D(nn.Module):
+    """BHWC [B, H, W, C] -> [B, H, W, C] attention inside each strided grid group."""
+
+    def __init__(self, cfg: GridAttention2DConfig):
+        super().__init__()
+        if cfg.mode != "grid":
+            raise ValueError("This minimal version only supports mode='grid'")
+        self.cfg = cfg
+        self.mhsa = MultiHeadSelfAttention(AttentionConfig(dim=cfg.dim, num_heads=cfg.num_heads,
+                                                           qkv_bias=cfg.qkv_bias, attn_drop=cfg.attn_drop,
+                                                           proj_drop=cfg.proj_drop))
+
+    def forward(self, x: torch.Tensor, residual=None, row_scale=None) -> torch.Tensor:
+        if x.ndim != 4:
+            raise ValueError(f"Expected x.ndim==4 (BHWC). Got {tuple(x.shape)}")
+        B, H, W, C = x.shape
+        if C != self.cfg.dim:
+            raise ValueError(f"Expected C=={self.cfg.dim}. Got C={C}")
+        g = self.cfg.grid_size
+        if g <= 0:
+            raise ValueError("grid_size must be > 0")
+        if H % g or W % g:
+            raise ValueError(f"H and W must be divisible by grid_size. Got H={H}, W={W}, g={g}")
+        self._last_meta = (B, H, W, C, g)
+        self._last_grid_hw = (H // g, W // g)
+        self._last_g = g
+        dt = OF.compute_dtype(x)
+        x2d = x.to(dt).reshape(B * H * W, C)
+        r2d = residual.to(dt).reshape(B * H * W, C) if residual is not None else None
+        return self.mhsa.attend_rows(x2d, B, H, W, g, residual=r2d, row_scale=row_scale).view(B, H, W, C)
+
+
+LocalAttention2D = GridAttention2D  # older name used by the reference notebooks

@@ -1,0 +1,112 @@
+"""Outlooker attention, channel LayerNorm and the 1x1-conv MLP — MI355X kernels.
+
+Drop-in for src/model/outlook_attention.py of the reference:
+  make_activation            :6-14     (same names / errors)
+  LayerNorm2d                :17-31    (LN over C of NCHW; eps 1e-6) -> ogv_layernorm_* on rows
+  MLP2d                      :33-49    (1x1 C->hidden, act, 1x1 hidden->C) -> two MFMA GEMMs,
+                                        the activation applied in the second GEMM's prologue
+  OutlookAttention2d         :52-124   logits/v/proj 1x1 convs -> MFMA GEMMs; softmax over k*k +
+                                        unfold-gather (:100-120) -> ogv_outlook_agg_{fwd,bwd}
+Parameters and their names/shapes are unchanged (attn.weight [heads*k*k, C, 1, 1], v.*, proj.*).
+Tensors are NCHW logically and channels_last physically.
+"""
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ogv import functional as OF
+from ogv.layers import Conv1x1, act_name
+
+
+def make_activation(act: str) -> nn.Module:
+    name = act.lower()
+    table = {"silu": lambda: nn.SiLU(inplace=True), "relu": lambda: nn.ReLU(inplace=True), "gelu": nn.GELU}
+    if name not in table:
+        raise ValueError(f"Unknown activation '{act}'. Use one of: silu|gelu|relu")
+    return table[name]()
+
+
+class LayerNorm2d(nn.Module):
+    """LayerNorm across channels at every (h, w) of an NCHW tensor."""
+
+    def __init__(self, num_channels: int, eps: float = 1e-6, affine: bool = True):
+        super().__init__()
+        self.ln = nn.LayerNorm(num_channels, eps=eps, elementwise_affine=affine)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        B, C, H, W = x.shape
+        rows = OF.nchw_to_rows(x.to(OF.compute_dtype(x)))
+        y = OF.layer_norm_rows(rows, self.ln.weight, self.ln.bias, self.ln.eps)
+        return OF.rows_to_nchw(y, B, H, W)
+
+
+class MLP2d(nn.Module):
+    """fc1 (1x1) -> act -> drop -> fc2 (1x1) -> drop.  fc1 stores the pre-activation; fc2 applies
+    the activation while loading it and fuses the block's residual + DropPath into its epilogue."""
+
+    def __init__(self, dim, mlp_ratio=4.0, drop=0.0, act="gelu"):
+        super().__init__()
+        hidden = max(1, int(dim * mlp_ratio))
+        self.fc1 = Conv1x1(dim, hidden)
+        self.act = make_activation(act)
+        self.drop1 = nn.Dropout(drop)
+        self.fc2 = Conv1x1(hidden, dim)
+        self.drop2 = nn.Dropout(drop)
+
+    def forward(self, x, residual=None, row_scale=None):
+        a = act_name(self.act)
+        dropping = self.training and (self.drop1.p > 0 or self.drop2.p > 0)
+        if a is None or dropping:
+            h = self.drop1(self.act(self.fc1(x)))
+            y = self.drop2(self.fc2(h))
+            if residual is None:
+                return y
+            if row_scale is not None:
+                y = y * row_scale.view(-1, 1, 1, 1).to(y.dtype)
+            return residual + y
+        return self.fc2(self.fc1(x), residual=residual, row_scale=row_scale, act_in=a)
+
+
+class OutlookAttention2d(nn.Module):
+    """Dynamic local aggregation on NCHW: per pixel and head, a softmax over the k*k logits
+    weights the zero-padded k*k neighbourhood of v (padded neighbours keep their mass)."""
+
+    def __init__(self, dim: int, num_heads: int = 6, kernel_size: int = 3, stride: int = 1,
+                 attn_drop: float = 0.0, proj_drop: float = 0.0, qkv_bias: bool = True):
+        super().__init__()
+        assert dim % num_heads == 0, "dim must be divisible by num_heads"
+        if kernel_size <= 0 or kernel_size % 2 == 0:
+            raise ValueError("kernel_size must be odd and >0 (e.g., 3,5,7)")
+        if stride <= 0:
+            raise ValueError("stride must be > 0")
+        self.dim = dim
+        self.num_heads = num_heads
+        self.head_dim = dim // num_heads
+        self.kernel_size = kernel_size
+        self.stride = stride
+        kk = kernel_size * kernel_size
+        self.attn = Conv1x1(dim, num_heads * kk, bias=bool(qkv_bias))   # logits (hooks read this)
+        self.v = Conv1x1(dim, dim, bias=bool(qkv_bias))
+        self.attn_drop = nn.Dropout(attn_drop)
+        self.proj = Conv1x1(dim, dim, bias=True)
+        self.proj_drop = nn.Dropout(proj_drop)
+
+    def forward(self, x: torch.Tensor, residual=None, row_scale=None) -> torch.Tensor:
+        if self.stride != 1:
+            raise NotImplementedError("ogv OutlookAttention2d implements stride=1 (the OutGridBlock path)")
+        if self.training and self.attn_drop.p > 0:
+            raise NotImplementedError("ogv OutlookAttention2d: attn_drop > 0 in training is not implemented")
+        B, C, H, W = x.shape
+        a = self.attn(x)                     # [B, heads*k*k, H, W]
+        v = self.v(x)                        # [B, C, H, W]
+        y = OF.outlook_aggregate_rows(OF.nchw_to_rows(v), OF.nchw_to_rows(a), B, H, W,
+                                      self.num_heads, self.kernel_size)
+        y = OF.rows_to_nchw(y, B, H, W)
+        if self.training and self.proj_drop.p > 0:
+            y = self.proj_drop(self.proj(y))
+            if residual is None:
+                return y
+            if row_scale is not None:
+                y = y * row_scale.view(-1, 1, 1, 1).to(y.dtype)
+            return residual + y
+        return self.proj(y, residual=residual, row_scale=row_scale)

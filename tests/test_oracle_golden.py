@@ -1,0 +1,99 @@
+"""Pin the CPU oracle (oracle/ogv_oracle.py) to the golden vectors recorded from the reference
+implementation itself (tests/golden/make_golden.py).  CPU only, fp32."""
+import numpy as np
+import pytest
+import torch
+
+import _fixtures as fx
+import gen_params as gp
+import ogv_oracle as orc
+
+torch.set_num_threads(4)
+RTOL, ATOL = 2e-5, 2e-5
+
+
+def _run(meta, fwd):
+    x, dy = fx.inputs(meta)
+    p = fx.oracle_params(meta)
+    xt = torch.from_numpy(x).requires_grad_(True)
+    y = fwd(xt, p, meta)
+    y.backward(torch.from_numpy(dy))
+    grads = {k: t.grad for k, t in p.items() if isinstance(t, torch.Tensor) and t.requires_grad}
+    return y, xt.grad, grads, p
+
+
+def _check(name, fwd):
+    meta, arr = fx.load(name)
+    y, dx, grads, p = _run(meta, fwd)
+    assert fx.maxabs(y.detach(), arr["y"]) <= ATOL + RTOL * np.abs(arr["y"]).max(), name
+    assert fx.maxabs(dx, arr["dx"]) <= ATOL + RTOL * np.abs(arr["dx"]).max(), name
+    n = fx.compare_grads(grads, arr, 1e-4, 1e-5, name)
+    assert n > 0
+    for k in arr:
+        if k.startswith("buf_after."):
+            key = k[len("buf_after."):]
+            assert fx.maxabs(p[key], arr[k]) <= 1e-5 * max(1.0, np.abs(arr[k]).max()), (name, key)
+
+
+@pytest.mark.parametrize("name", fx.fixture_names("outlook_attn_"))
+def test_outlook_attention(name):
+    _check(name, lambda x, p, m: orc.outlook_attention(x, p, "", m["heads"], m["k"]))
+
+
+@pytest.mark.parametrize("name", [n for n in fx.fixture_names("grid_attn_") if "capture" not in n])
+def test_grid_attention(name):
+    _check(name, lambda x, p, m: orc.grid_attention(x, p, "", m["heads"], m["g"]))
+
+
+def test_layernorm2d():
+    _check("layernorm2d_s0", lambda x, p, m: orc.ln2d(x, p["ln.weight"], p["ln.bias"], m["eps"]))
+
+
+def test_outlooker_block():
+    _check("outlooker_block_s1", lambda x, p, m: orc.outlooker_block(x, p, "", m["heads"]))
+
+
+@pytest.mark.parametrize("name", fx.fixture_names("mbconv_"))
+def test_mbconv(name):
+    _check(name, lambda x, p, m: orc.mbconv(x, p, "", m["train"]))
+
+
+@pytest.mark.parametrize("name", fx.fixture_names("outgrid_block_"))
+def test_outgrid_block(name):
+    _check(name, lambda x, p, m: orc.outgrid_block(x, p, "", m["stage"], m["train"]))
+
+
+def test_grid_partition_golden():
+    meta, arr = fx.load("grid_partition_g2")
+    x = torch.from_numpy(gp.input_from_spec(meta["x"]))
+    g = orc.grid_partition(x, meta["g"])
+    assert torch.equal(g, torch.from_numpy(arr["grids"]))
+    assert torch.equal(orc.grid_unpartition(g, *x.shape[:3], meta["g"]), x)
+
+
+def test_grid_capture_golden():
+    meta, arr = fx.load("grid_attn_capture_s1")
+    p = fx.oracle_params(meta, requires_grad=False)
+    x = torch.from_numpy(gp.input_from_spec(meta["x"]))
+    y, att = orc.grid_attention(x, p, "", meta["heads"], meta["g"], want_probs=True)
+    assert fx.maxabs(y, arr["y"]) < 1e-5
+    assert fx.maxabs(att, arr["last_attn"]) < 1e-6
+
+
+@pytest.mark.parametrize("mode", ["eval", "train"])
+def test_model_a(mode):
+    meta, arr = fx.load(f"model_a_7m_{mode}_b2")
+    p = fx.oracle_params(meta)
+    assert list(p.keys()) == list(fx.shapes_for(meta).keys())
+    names = [k for k in p if p[k].requires_grad]
+    assert names == meta["param_names"], "state_dict parameter order differs from the reference"
+    x = torch.from_numpy(gp.input_from_spec(meta["x"]))
+    logits = orc.model_a(x, p, meta["stages"], train=(mode == "train"))
+    assert fx.maxabs(logits.detach(), arr["logits"]) < 2e-5
+    loss = torch.nn.functional.cross_entropy(logits, torch.from_numpy(arr["targets"]), label_smoothing=0.1)
+    assert abs(loss.item() - arr["loss"][0]) < 2e-6
+    loss.backward()
+    gn = np.array([p[k].grad.norm().item() if p[k].grad is not None else 0.0 for k in names])
+    np.testing.assert_allclose(gn, arr["grad_norms"], rtol=2e-4, atol=1e-7)
+    n_params = sum(p[k].numel() for k in names)
+    assert n_params == meta["n_params"] == 7518102

@@ -1,0 +1,188 @@
+"""Benchmark: Model-A-7M CIFAR-100 32x32 training throughput on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+A step = one full training iteration on a synthetic batch already resident in HBM:
+autocast(bf16) forward through the HIP OutGridBlock kernels, CE(label smoothing 0.1), backward,
+clip_grad_norm(1.0), fused AdamW, WarmupCosine — bs=512 per GPU (weak scaling), DDP/RCCL for N>1.
+Prints ONE JSON line on rank 0 with `roofline` (dominant kernel, HIP events around its launches
+inside the timed region) and `cpu_baseline` (the CPU oracle's train step on the host cores,
+bounded sample, rank 0 at N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import pathlib
+import sys
+import time
+
+ROOT = pathlib.Path(__file__).resolve().parent
+PKG = ROOT / "outlook-grid-vision-transformer_amd"
+sys.path.insert(0, str(PKG))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=512, help="per-GPU batch")
+    ap.add_argument("--model", default="model_a_7m")
+    ap.add_argument("--probe", default="outlook_fwd", help="kernel whose launches feed `roofline`")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-parity", action="store_true")
+    return ap.parse_args()
+
+
+def roofline_bytes(name, u):
+    """Algorithmic HBM bytes of one launch."""
+    if name == "outlook_fwd":   # read v [M,C] + logits [M,9h], write y [M,C]
+        return u["elem"] * u["M"] * (2 * u["C"] + u["k"] * u["k"] * u["heads"])
+    if name == "grid_fwd":      # read qkv [M,3C], write out [M,C] (+ fp32 lse [M,h])
+        return u["elem"] * u["M"] * 4 * u["C"] + 4 * u["M"] * u["heads"]
+    raise KeyError(name)
+
+
+def fwd_parity(device):
+    """max|logits - reference logits| on the golden Model-A-7M B=2 case (reference output
+    recorded from pablo-reyes8/outlook-grid-vision-transformer), fp32 and bf16-autocast."""
+    sys.path.insert(0, str(ROOT / "tests" / "golden"))
+    import numpy as np
+    import gen_params as gp
+    from ogv.train import MODEL_CONFIGS, build_model
+    z = np.load(ROOT / "tests" / "golden" / "model_a_7m_eval_b2.npz", allow_pickle=False)
+    meta = json.loads(bytes(z["meta"]).decode())
+    m = build_model(dict(type="model_a", num_classes=100, stem_dim=64, dpr_max=meta["dpr_max"],
+                         stages=meta["stages"]))
+    gp.fill_module(m, meta["seed"])
+    m = m.to(device).eval()
+    x = torch.from_numpy(gp.input_from_spec(meta["x"])).to(device).contiguous(memory_format=torch.channels_last)
+    ref = torch.from_numpy(z["logits"]).double()
+    out = {}
+    with torch.no_grad():
+        out["fp32"] = (m(x).double().cpu() - ref).abs().max().item()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out["bf16"] = (m(x).double().cpu() - ref).abs().max().item()
+    return out
+
+
+def cpu_baseline(seconds):
+    """The oracle's fwd+CE+bwd+clip+AdamW at bs=8, fp32, NCHW on the host cores (bounded)."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    sys.path.insert(0, str(ROOT / "tests" / "golden"))
+    import gen_params as gp
+    import ogv_oracle as orc
+    from ogv.train import MODEL_CONFIGS
+    cfg = MODEL_CONFIGS["model_a_7m"]
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    p = orc.make_params(orc.model_a_shapes(cfg["stages"], cfg["num_classes"], 3, cfg["stem_dim"]),
+                        lambda k, s: gp.param_value(k, s, 7))
+    opt = orc.make_optimizer(p)
+    bs = 8
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(bs, 3, 32, 32, generator=g)
+    y = torch.randint(0, 100, (bs,), generator=g)
+    for _ in range(2):
+        orc.train_step(x, y, p, cfg["stages"], opt)
+    n, t0 = 0, time.perf_counter()
+    while True:
+        orc.train_step(x, y, p, cfg["stages"], opt)
+        n += 1
+        if time.perf_counter() - t0 > seconds:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(n * bs / dt, 2), "unit": "imgs/s", "cores": threads, "kind": "port",
+            "sample": f"{n} steps x bs={bs} Model-A-7M 32x32 fp32 fwd+CE+bwd+clip+AdamW (oracle restatement, "
+                      f"{dt:.1f}s after 2 warmup steps)"}
+
+
+def main():
+    args = parse()
+    from ogv import functional as OF
+    from ogv.train import MODEL_CONFIGS, Trainer, build_model, setup_distributed, wrap_ddp
+    import ogv
+
+    rank, world, local, device = setup_distributed()
+    torch.backends.cudnn.benchmark = True   # as the reference (src/training/autocast.py:8-17)
+    assert device.type == "cuda", "bench.py needs a HIP device"
+    ogv.load()
+    cfg = MODEL_CONFIGS[args.model]
+    torch.manual_seed(7)
+    model = build_model(dict(type="model_a", num_classes=cfg["num_classes"], stem_dim=cfg["stem_dim"],
+                             dpr_max=cfg["dpr_max"], stages=cfg["stages"]))
+    model = model.to(device).to(memory_format=torch.channels_last)
+    model = wrap_ddp(model, device)
+    trainer = Trainer(model, total_steps=max(100, args.steps + args.warmup))
+
+    B, S = args.batch, cfg["img"]
+    g = torch.Generator(device=device).manual_seed(7 + rank)
+    x = torch.randn(B, 3, S, S, device=device, generator=g).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, cfg["num_classes"], (B,), device=device, generator=g)
+
+    for _ in range(args.warmup):
+        trainer.step(x, y)
+    OF.probe_reset()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        OF.probe_arm(args.probe)
+        loss = trainer.step(x, y)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    OF.probe_disarm()
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    ms_probe, units, nprobe = OF.probe_results()
+    assert torch.isfinite(loss).item(), "non-finite loss"
+
+    if rank == 0:
+        value = world * B * args.steps / elapsed
+        roof = None
+        if ms_probe:
+            ach = roofline_bytes(args.probe, units) / (ms_probe * 1e-3) / 1e9
+            traffic = None
+            tf = ROOT / "profiles" / "pmc_traffic.json"
+            if tf.exists():
+                traffic = json.loads(tf.read_text()).get(args.probe, {}).get("hbm_bytes_per_launch")
+            roof = {"kernel": args.probe, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "algorithmic_bytes": roofline_bytes(args.probe, units), "avg_launch_ms": round(ms_probe, 5),
+                    "launches": nprobe}
+        out = {
+            "metric": "training imgs/s Model-A-7M CIFAR-100 32x32 (bf16, bs=512/GPU)",
+            "value": round(value, 1), "unit": "imgs/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "bf16", "data": "synthetic (randn images, randint labels; random init)",
+            "config": {"workload": f"{args.model} train step: fwd+CE(ls=0.1)+bwd+clip(1.0)+AdamW", "img_size": S,
+                       "per_gpu_batch": B, "global_batch": B * world, "parallelism": f"dp{world}"},
+            "roofline": roof,
+        }
+        if world == 1 and not args.no_parity:
+            out["fwd_max_abs_diff"] = fwd_parity(device)
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+            out["gpu_over_cpu"] = round(value / out["cpu_baseline"]["value"], 1)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -110,6 +110,19 @@ int ogv_gemm_wgrad(const void* dout, int ldd, const void* A, int lda, const floa
                    float* dW, float* dbias, int M, int N, int K, ogv_act act_in, void* ws,
                    ogv_dtype dt, void* stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * Depthwise 3x3 convolution, padding 1, stride 1|2, on NHWC rows.  Replaces MBConv.depthwise's
+ * Conv2d(mid, mid, 3, stride, padding=1, groups=mid) (src/model/mbc_conv.py:75-79).
+ * w: fp32 [C, 1, 3, 3]; bias nullable.  x: [B*H*W, C] -> y: [B*Ho*Wo, C].
+ * bwd: dx (nullable) [B*H*W, C]; dw fp32 [C,1,3,3] and dbias fp32 [C] (nullable, overwritten).
+ * ------------------------------------------------------------------------------------------- */
+size_t ogv_dwconv_fwd_ws_bytes(int C);
+int ogv_dwconv3x3_fwd(const void* x, const float* w, const float* bias, void* y, int B, int H, int W, int C,
+                      int stride, void* ws, ogv_dtype dt, void* stream);
+size_t ogv_dwconv_bwd_ws_bytes(int B, int H, int W, int C, int stride);
+int ogv_dwconv3x3_bwd(const void* dy, const void* x, const float* w, void* dx, float* dw, float* dbias, int B,
+                      int H, int W, int C, int stride, void* ws, ogv_dtype dt, void* stream);
+
 /* Elementwise helpers used by the autograd glue. */
 int ogv_cast(const void* src, ogv_dtype src_dt, void* dst, ogv_dtype dst_dt, size_t n, void* stream);
 

@@ -270,3 +270,29 @@ def train_step(x, y, p, stages, opt, clip=1.0, label_smoothing=0.1):
     torch.nn.utils.clip_grad_norm_(params, clip)
     opt.step()
     return loss.detach()
+
+
+# ---------------------------------------------------------------------------- kernel-level oracles
+def outlook_aggregate(v, logits, heads: int, k: int):
+    """softmax over k*k + unfold-gather only (outlook_attention.py:106-120), NCHW in/out."""
+    B, C, H, W = v.shape
+    kk, hd, L = k * k, C // heads, H * W
+    prob = logits.reshape(B, heads, kk, L).permute(0, 3, 1, 2).softmax(dim=-1)
+    cols = F.unfold(v, kernel_size=k, padding=k // 2).view(B, heads, hd, kk, L).permute(0, 4, 1, 2, 3)
+    y = (cols * prob.unsqueeze(3)).sum(dim=-1)
+    return y.permute(0, 2, 3, 1).reshape(B, C, H, W)
+
+
+def grid_core(qkv, heads: int, g: int, want_probs=False):
+    """q@k^T*scale, softmax, @v inside strided grid groups (grid_attention.py:70-86 with the
+    partition of grid_partition.py:13-15); qkv BHWC [B,H,W,3C] -> out BHWC [B,H,W,C]."""
+    B, H, W, C3 = qkv.shape
+    C = C3 // 3
+    hd = C // heads
+    t = grid_partition(qkv, g)
+    Bg, N = t.shape[0], t.shape[1] * t.shape[2]
+    q, k, v = t.reshape(Bg, N, 3, heads, hd).permute(2, 0, 3, 1, 4)
+    att = ((q @ k.transpose(-2, -1)) * (hd ** -0.5)).softmax(dim=-1)
+    o = (att @ v).transpose(1, 2).reshape(Bg, H // g, W // g, C)
+    y = grid_unpartition(o, B, H, W, g)
+    return (y, att) if want_probs else y

@@ -29,6 +29,10 @@ int check_launch(const char* what);
     }                                          \
   } while (0)
 
+// deterministic "sum the rows of an fp32 slab" (ogv_dwconv.hip)
+size_t colreduce_tmp_floats(long R, long n);
+void colreduce(const float* src, float* dst, long R, long n, long ld, float* tmp, hipStream_t s);
+
 static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 static inline unsigned cdiv(long a, long b) { return (unsigned)((a + b - 1) / b); }
 

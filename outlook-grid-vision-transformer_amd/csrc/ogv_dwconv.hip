@@ -1,0 +1,340 @@
+// Depthwise 3x3 convolution on NHWC rows (MBConv.depthwise, src/model/mbc_conv.py:75-79:
+// Conv2d(mid, mid, 3, stride, padding=1, groups=mid)), plus the deterministic column reducer
+// shared by every "sum over the M rows" gradient (LN gamma/beta, conv weights, GEMM slabs).
+//
+// fwd  : out[b,oy,ox,c] = sum_{ki,kj} w[c,ki,kj] * in[b, oy*s+ki-1, ox*s+kj-1, c]   (+ bias[c])
+// dgrad: din[b,y,x,c]   = sum_{ki,kj: (y+1-ki)%s==0 ...} w[c,ki,kj] * dout[b,(y+1-ki)/s,(x+1-kj)/s,c]
+// wgrad: dw[c,ki,kj]    = sum_{b,oy,ox} dout[b,oy,ox,c] * in[b, oy*s+ki-1, ox*s+kj-1, c]
+//        (per-block partials [S][9][C] -> column reducer; dbias = sum dout)
+// Channels are vectorised V-wide per thread (16-B loads for bf16 at V=8); weights are staged as
+// wt[tap][C] fp32 so a thread's 9 taps x V channels are contiguous.
+#include "ogv_common.h"
+
+namespace ogv {
+
+// ------------------------------------------------------------------ column reducer
+// dst[j] (+)= sum_r src[r*ld + j], j < n.  Block = 64 columns x 4 row lanes; grid.y splits rows.
+__global__ __launch_bounds__(256) void colreduce_kernel(const float* __restrict__ src, float* __restrict__ dst, long R,
+                                                        long n, long ld, long rows_per_chunk) {
+  __shared__ float red[4][64];
+  const int cx = threadIdx.x & 63, ry = threadIdx.x >> 6;
+  const long j = (long)blockIdx.x * 64 + cx;
+  const long r0 = (long)blockIdx.y * rows_per_chunk;
+  const long r1 = r0 + rows_per_chunk < R ? r0 + rows_per_chunk : R;
+  float acc = 0.f;
+  if (j < n) {
+    long r = r0 + ry;
+    for (; r + 12 < r1; r += 16) {
+      const float a = src[r * ld + j], b = src[(r + 4) * ld + j], c = src[(r + 8) * ld + j],
+                  d = src[(r + 12) * ld + j];
+      acc += (a + b) + (c + d);
+    }
+    for (; r < r1; r += 4) acc += src[r * ld + j];
+  }
+  red[ry][cx] = acc;
+  __syncthreads();
+  if (ry == 0 && j < n) {
+    const float s = (red[0][cx] + red[1][cx]) + (red[2][cx] + red[3][cx]);
+    dst[(long)blockIdx.y * n + j] = s;
+  }
+}
+
+// Sum R rows of a [R, ld] fp32 slab into dst[n].  Two passes when R is large; tmp needs
+// colreduce_tmp_floats(R, n) floats (may be null when that is 0).  Deterministic.
+size_t colreduce_tmp_floats(long R, long n) {
+  if (R <= 256) return 0;
+  const long chunks = (R + 255) / 256;
+  return (size_t)(chunks < 64 ? chunks : 64) * n;
+}
+
+void colreduce(const float* src, float* dst, long R, long n, long ld, float* tmp, hipStream_t s) {
+  const unsigned gx = (unsigned)((n + 63) / 64);
+  if (R <= 256) {
+    colreduce_kernel<<<dim3(gx, 1), 256, 0, s>>>(src, dst, R, n, ld, R);
+    return;
+  }
+  long chunks = (R + 255) / 256;
+  if (chunks > 64) chunks = 64;
+  const long per = (R + chunks - 1) / chunks;
+  chunks = (R + per - 1) / per;
+  colreduce_kernel<<<dim3(gx, (unsigned)chunks), 256, 0, s>>>(src, tmp, R, n, ld, per);
+  colreduce_kernel<<<dim3(gx, 1), 256, 0, s>>>(tmp, dst, chunks, n, n, chunks);
+}
+
+// ------------------------------------------------------------------ depthwise conv kernels
+struct DwGeom {
+  int B, H, W, C, Ho, Wo, stride;
+};
+
+// wt[tap*C + c] = w[c*9 + tap]
+__global__ void dw_weight_t_kernel(const float* __restrict__ w, float* __restrict__ wt, int C) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 9 * C) return;
+  const int tap = i / C, c = i - tap * C;
+  wt[i] = w[c * 9 + tap];
+}
+
+template <typename T, int V>
+__global__ __launch_bounds__(256) void dw_fwd_kernel(const T* __restrict__ in, const float* __restrict__ wt,
+                                                     const float* __restrict__ bias, T* __restrict__ out, DwGeom g) {
+  const int nch = g.C / V;
+  const long total = (long)g.B * g.Ho * g.Wo * nch;
+  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid >= total) return;
+  const int c0 = (int)(tid % nch) * V;
+  const long p = tid / nch;
+  const int ox = (int)(p % g.Wo);
+  const long t = p / g.Wo;
+  const int oy = (int)(t % g.Ho);
+  const long b = t / g.Ho;
+  float acc[V];
+#pragma unroll
+  for (int i = 0; i < V; ++i) acc[i] = bias ? bias[c0 + i] : 0.f;
+#pragma unroll
+  for (int ki = 0; ki < 3; ++ki) {
+    const int y = oy * g.stride + ki - 1;
+    if (y < 0 || y >= g.H) continue;
+#pragma unroll
+    for (int kj = 0; kj < 3; ++kj) {
+      const int x = ox * g.stride + kj - 1;
+      if (x < 0 || x >= g.W) continue;
+      float v[V], w[V];
+      load_vec<T, V>(in + ((b * g.H + y) * g.W + x) * g.C + c0, v);
+      load_vec<float, V>(wt + (ki * 3 + kj) * g.C + c0, w);
+#pragma unroll
+      for (int i = 0; i < V; ++i) acc[i] = fmaf(w[i], v[i], acc[i]);
+    }
+  }
+  store_vec<T, V>(out + p * g.C + c0, acc);
+}
+
+template <typename T, int V>
+__global__ __launch_bounds__(256) void dw_dgrad_kernel(const T* __restrict__ dout, const float* __restrict__ wt,
+                                                       T* __restrict__ din, DwGeom g) {
+  const int nch = g.C / V;
+  const long total = (long)g.B * g.H * g.W * nch;
+  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid >= total) return;
+  const int c0 = (int)(tid % nch) * V;
+  const long p = tid / nch;
+  const int x = (int)(p % g.W);
+  const long t = p / g.W;
+  const int y = (int)(t % g.H);
+  const long b = t / g.H;
+  float acc[V];
+#pragma unroll
+  for (int i = 0; i < V; ++i) acc[i] = 0.f;
+#pragma unroll
+  for (int ki = 0; ki < 3; ++ki) {
+    const int ny = y + 1 - ki;
+    if (ny < 0 || ny % g.stride) continue;
+    const int oy = ny / g.stride;
+    if (oy >= g.Ho) continue;
+#pragma unroll
+    for (int kj = 0; kj < 3; ++kj) {
+      const int nx = x + 1 - kj;
+      if (nx < 0 || nx % g.stride) continue;
+      const int ox = nx / g.stride;
+      if (ox >= g.Wo) continue;
+      float d[V], w[V];
+      load_vec<T, V>(dout + ((b * g.Ho + oy) * g.Wo + ox) * g.C + c0, d);
+      load_vec<float, V>(wt + (ki * 3 + kj) * g.C + c0, w);
+#pragma unroll
+      for (int i = 0; i < V; ++i) acc[i] = fmaf(w[i], d[i], acc[i]);
+    }
+  }
+  store_vec<T, V>(din + p * g.C + c0, acc);
+}
+
+// Block: 256 threads = LANES pixel lanes x NCHB channel chunks (V channels each) of one channel
+// tile; grid = (channel tiles, S pixel slices).  part[s][tap*C + c] (+ part[s][9C + c] = dbias).
+template <typename T, int V>
+__global__ __launch_bounds__(256) void dw_wgrad_kernel(const T* __restrict__ dout, const T* __restrict__ in,
+                                                       float* __restrict__ part, DwGeom g, int nchb,
+                                                       long pix_per_slice, int with_bias) {
+  __shared__ float red[256 * (V <= 4 ? 10 : 5)];
+  const int lanes = 256 / nchb;
+  const int cl = threadIdx.x % nchb, pl = threadIdx.x / nchb;
+  const int c0 = (blockIdx.x * nchb + cl) * V;
+  const bool active = pl < lanes && c0 < g.C;
+  const long P = (long)g.B * g.Ho * g.Wo;
+  const long p0 = (long)blockIdx.y * pix_per_slice;
+  const long p1 = p0 + pix_per_slice < P ? p0 + pix_per_slice : P;
+  float acc[10][V];
+#pragma unroll
+  for (int k = 0; k < 10; ++k)
+#pragma unroll
+    for (int i = 0; i < V; ++i) acc[k][i] = 0.f;
+  if (active) {
+    for (long p = p0 + pl; p < p1; p += lanes) {
+      const int ox = (int)(p % g.Wo);
+      const long t = p / g.Wo;
+      const int oy = (int)(t % g.Ho);
+      const long b = t / g.Ho;
+      float d[V];
+      load_vec<T, V>(dout + p * g.C + c0, d);
+#pragma unroll
+      for (int i = 0; i < V; ++i) acc[9][i] += d[i];
+#pragma unroll
+      for (int ki = 0; ki < 3; ++ki) {
+        const int y = oy * g.stride + ki - 1;
+        if (y < 0 || y >= g.H) continue;
+#pragma unroll
+        for (int kj = 0; kj < 3; ++kj) {
+          const int x = ox * g.stride + kj - 1;
+          if (x < 0 || x >= g.W) continue;
+          float v[V];
+          load_vec<T, V>(in + ((b * g.H + y) * g.W + x) * g.C + c0, v);
+#pragma unroll
+          for (int i = 0; i < V; ++i) acc[ki * 3 + kj][i] = fmaf(d[i], v[i], acc[ki * 3 + kj][i]);
+        }
+      }
+    }
+  }
+  // reduce across the pixel lanes of each channel chunk: 10 taps (9 + bias) in LDS passes
+  constexpr int TPP = V <= 4 ? 10 : 5;  // taps per pass
+  float* out = part + (long)blockIdx.y * 10 * g.C;
+#pragma unroll
+  for (int k0 = 0; k0 < 10; k0 += TPP) {
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+#pragma unroll
+      for (int k = 0; k < TPP; ++k) red[k * 256 + threadIdx.x] = acc[k0 + k][i];
+      __syncthreads();
+      for (int idx = threadIdx.x; idx < nchb * TPP; idx += 256) {   // nchb*TPP can exceed 256
+        const int k = idx / nchb, ch = idx % nchb;
+        const int c = (blockIdx.x * nchb + ch) * V + i;
+        float s = 0.f;
+        for (int l = 0; l < lanes; ++l) s += red[k * 256 + l * nchb + ch];
+        const int tap = k0 + k;
+        if (c < g.C && (tap < 9 || with_bias)) out[(long)tap * g.C + c] = s;
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// dw[c*9 + tap] = sum9[tap*C + c]
+__global__ void dw_weight_untranspose_kernel(const float* __restrict__ s, float* __restrict__ dw, int C) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 9 * C) return;
+  const int c = i / 9, tap = i - c * 9;
+  dw[i] = s[tap * C + c];
+}
+
+static int dw_vec(int C) { return C % 8 == 0 ? 8 : (C % 4 == 0 ? 4 : 1); }
+
+static int dw_check(int B, int H, int W, int C, int stride, ogv_dtype dt, DwGeom& g, const char* who) {
+  OGV_REQUIRE(B > 0 && H > 0 && W > 0 && C > 0, "%s: bad shape", who);
+  OGV_REQUIRE(stride == 1 || stride == 2, "%s: stride %d unsupported", who, stride);
+  OGV_REQUIRE(dt == OGV_F32 || dt == OGV_BF16, "%s: bad dtype", who);
+  g.B = B; g.H = H; g.W = W; g.C = C; g.stride = stride;
+  g.Ho = (H - 1) / stride + 1;
+  g.Wo = (W - 1) / stride + 1;
+  return OGV_OK;
+}
+
+struct DwWgradPlan {
+  int nchb, ctiles, S;
+  long per;
+};
+static DwWgradPlan dw_wgrad_plan(const DwGeom& g, int V) {
+  DwWgradPlan p;
+  const int nch = g.C / V;
+  p.nchb = nch < 64 ? nch : 64;
+  p.ctiles = (nch + p.nchb - 1) / p.nchb;
+  const long P = (long)g.B * g.Ho * g.Wo;
+  long S = (2048 + p.ctiles - 1) / p.ctiles;
+  const long lanes = 256 / p.nchb;
+  const long maxS = (P + lanes * 16 - 1) / (lanes * 16);  // >= 16 pixels per lane
+  if (S > maxS) S = maxS;
+  if (S < 1) S = 1;
+  p.per = (P + S - 1) / S;
+  p.S = (int)((P + p.per - 1) / p.per);
+  return p;
+}
+
+}  // namespace ogv
+
+using namespace ogv;
+
+#define OGV_DW_DISPATCH(FN, ...)                                            \
+  do {                                                                      \
+    const int vv = dw_vec(C);                                               \
+    if (dt == OGV_BF16) {                                                   \
+      if (vv == 8) FN<bf16, 8>(__VA_ARGS__);                                \
+      else if (vv == 4) FN<bf16, 4>(__VA_ARGS__);                           \
+      else FN<bf16, 1>(__VA_ARGS__);                                        \
+    } else {                                                                \
+      if (vv == 8) FN<float, 8>(__VA_ARGS__);                               \
+      else if (vv == 4) FN<float, 4>(__VA_ARGS__);                          \
+      else FN<float, 1>(__VA_ARGS__);                                       \
+    }                                                                       \
+  } while (0)
+
+template <typename T, int V>
+static void dw_fwd_launch(const void* in, const float* wt, const float* bias, void* out, const DwGeom& g,
+                          hipStream_t s) {
+  const long total = (long)g.B * g.Ho * g.Wo * (g.C / V);
+  dw_fwd_kernel<T, V><<<cdiv(total, 256), 256, 0, s>>>((const T*)in, wt, bias, (T*)out, g);
+}
+template <typename T, int V>
+static void dw_dgrad_launch(const void* dout, const float* wt, void* din, const DwGeom& g, hipStream_t s) {
+  const long total = (long)g.B * g.H * g.W * (g.C / V);
+  dw_dgrad_kernel<T, V><<<cdiv(total, 256), 256, 0, s>>>((const T*)dout, wt, (T*)din, g);
+}
+template <typename T, int V>
+static void dw_wgrad_launch(const void* dout, const void* in, float* part, const DwGeom& g, int with_bias,
+                            hipStream_t s) {
+  DwWgradPlan p = dw_wgrad_plan(g, V);
+  dw_wgrad_kernel<T, V><<<dim3(p.ctiles, p.S), 256, 0, s>>>((const T*)dout, (const T*)in, part, g, p.nchb, p.per,
+                                                             with_bias);
+}
+
+extern "C" size_t ogv_dwconv_fwd_ws_bytes(int C) { return (size_t)9 * C * sizeof(float); }
+
+extern "C" int ogv_dwconv3x3_fwd(const void* x, const float* w, const float* bias, void* y, int B, int H, int W, int C,
+                                 int stride, void* ws, ogv_dtype dt, void* stream) {
+  OGV_REQUIRE(x && w && y && ws, "ogv_dwconv3x3_fwd: null pointer");
+  DwGeom g;
+  int rc = dw_check(B, H, W, C, stride, dt, g, "ogv_dwconv3x3_fwd");
+  if (rc) return rc;
+  hipStream_t s = as_stream(stream);
+  float* wt = (float*)ws;
+  dw_weight_t_kernel<<<cdiv(9 * C, 256), 256, 0, s>>>(w, wt, C);
+  OGV_DW_DISPATCH(dw_fwd_launch, x, wt, bias, y, g, s);
+  return check_launch("ogv_dwconv3x3_fwd");
+}
+
+extern "C" size_t ogv_dwconv_bwd_ws_bytes(int B, int H, int W, int C, int stride) {
+  DwGeom g;
+  if (dw_check(B, H, W, C, stride, OGV_F32, g, "ws") != OGV_OK) return 0;
+  DwWgradPlan p = dw_wgrad_plan(g, dw_vec(C));
+  const size_t part = (size_t)p.S * 10 * C;
+  return (9 * (size_t)C + part + colreduce_tmp_floats(p.S, 10L * C) + 10 * (size_t)C) * sizeof(float);
+}
+
+extern "C" int ogv_dwconv3x3_bwd(const void* dy, const void* x, const float* w, void* dx, float* dw, float* dbias,
+                                 int B, int H, int W, int C, int stride, void* ws, ogv_dtype dt, void* stream) {
+  OGV_REQUIRE(dy && x && w && ws, "ogv_dwconv3x3_bwd: null pointer");
+  DwGeom g;
+  int rc = dw_check(B, H, W, C, stride, dt, g, "ogv_dwconv3x3_bwd");
+  if (rc) return rc;
+  hipStream_t s = as_stream(stream);
+  DwWgradPlan p = dw_wgrad_plan(g, dw_vec(C));
+  float* wt = (float*)ws;
+  float* part = wt + 9 * (size_t)C;
+  float* tmp = part + (size_t)p.S * 10 * C;
+  float* sum10 = tmp + colreduce_tmp_floats(p.S, 10L * C);
+  if (dx) {
+    dw_weight_t_kernel<<<cdiv(9 * C, 256), 256, 0, s>>>(w, wt, C);
+    OGV_DW_DISPATCH(dw_dgrad_launch, dy, wt, dx, g, s);
+  }
+  if (dw || dbias) {
+    OGV_DW_DISPATCH(dw_wgrad_launch, dy, x, part, g, dbias ? 1 : 0, s);
+    colreduce(part, sum10, p.S, dbias ? 10L * C : 9L * C, 10L * C, tmp, s);
+    if (dw) dw_weight_untranspose_kernel<<<cdiv(9 * C, 256), 256, 0, s>>>(sum10, dw, C);
+    if (dbias) (void)hipMemcpyAsync(dbias, sum10 + 9 * (size_t)C, C * sizeof(float), hipMemcpyDeviceToDevice, s);
+  }
+  return check_launch("ogv_dwconv3x3_bwd");
+}

@@ -470,16 +470,6 @@ __global__ __launch_bounds__(256) void wgrad_f32_kernel(const float* __restrict_
   if (do_bias && tid < BN && n0 + tid < N) dbias_part[(long)s * N + n0 + tid] = bsum;
 }
 
-// dst[j] = sum_s src[s*len + j]
-__global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ src, float* __restrict__ dst,
-                                                          int S, long len) {
-  const long j = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= len) return;
-  float acc = 0.f;
-  for (int s = 0; s < S; ++s) acc += src[(long)s * len + j];
-  dst[j] = acc;
-}
-
 // WT[k][n] = W[n][k]  (fp32, 32x32 tiles through LDS)
 __global__ __launch_bounds__(256) void transpose_f32_kernel(const float* __restrict__ W, float* __restrict__ WT, int N,
                                                             int K, int ldt) {
@@ -624,7 +614,8 @@ extern "C" int ogv_gemm_dgrad(const void* dout, int ldd, const float* W, const v
 
 extern "C" size_t ogv_gemm_wgrad_ws_bytes(int M, int N, int K) {
   WgradPlan p = wgrad_plan(M > 0 ? M : 1, N, K, 32);
-  return (size_t)p.S * ((size_t)N * K + N) * sizeof(float);
+  const size_t t1 = colreduce_tmp_floats(p.S, (long)N * K), t2 = colreduce_tmp_floats(p.S, N);
+  return ((size_t)p.S * ((size_t)N * K + N) + (t1 > t2 ? t1 : t2)) * sizeof(float);
 }
 
 extern "C" int ogv_gemm_wgrad(const void* dout, int ldd, const void* A, int lda, const float* rs, int rps, float* dW,
@@ -684,7 +675,8 @@ extern "C" int ogv_gemm_wgrad(const void* dout, int ldd, const void* A, int lda,
     }
   }
   const long len = (long)N * K;
-  slab_reduce_kernel<<<cdiv(len, 256), 256, 0, s>>>(part, dW, p.S, len);
-  if (dbias) slab_reduce_kernel<<<cdiv(N, 256), 256, 0, s>>>(bpart, dbias, p.S, N);
+  float* tmp = bpart + (size_t)p.S * N;
+  colreduce(part, dW, p.S, len, len, tmp, s);
+  if (dbias) colreduce(bpart, dbias, p.S, N, N, tmp, s);
   return check_launch("ogv_gemm_wgrad");
 }

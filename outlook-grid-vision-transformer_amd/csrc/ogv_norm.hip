@@ -160,20 +160,6 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
   }
 }
 
-// out[j] = sum_r part[r * ld + j] for j < n   (column sums of a [R, n] fp32 slab)
-__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ part, float* __restrict__ out0,
-                                                     float* __restrict__ out1, int R, int n0, int ld) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= ld) return;
-  float acc = 0.f;
-  for (int r = 0; r < R; ++r) acc += part[(long)r * ld + j];
-  if (j < n0) {
-    if (out0) out0[j] = acc;
-  } else if (out1) {
-    out1[j - n0] = acc;
-  }
-}
-
 struct LnPlan {
   int G, NV, VEC;
 };
@@ -253,10 +239,18 @@ extern "C" int ogv_layernorm_fwd(const void* x, const float* gamma, const float*
   return check_launch("ogv_layernorm_fwd");
 }
 
+static long ln_bwd_blocks(long M, int G) {
+  // fewer, fatter blocks than the forward: each block's dgamma/dbeta partial is a row of the slab
+  const long rows_per_block = 256 / G;
+  long nb = (M + rows_per_block - 1) / rows_per_block;
+  return nb < 512 ? nb : 512;
+}
+
 extern "C" size_t ogv_layernorm_bwd_ws_bytes(int M, int C) {
   LnPlan p;
   if (ln_plan(C, p) != OGV_OK) return 0;
-  return (size_t)ln_blocks(M > 0 ? M : 1, p.G) * 2 * C * sizeof(float);
+  const long nb = ln_bwd_blocks(M > 0 ? M : 1, p.G);
+  return ((size_t)nb * 2 * C + colreduce_tmp_floats(nb, 2L * C) + 2 * (size_t)C) * sizeof(float);
 }
 
 extern "C" int ogv_layernorm_bwd(const void* dy, const void* x, const float* gamma, const float* mean,
@@ -266,10 +260,16 @@ extern "C" int ogv_layernorm_bwd(const void* dy, const void* x, const float* gam
   OGV_REQUIRE(M > 0 && C > 0, "ogv_layernorm_bwd: bad shape M=%d C=%d", M, C);
   LnPlan p;
   OGV_REQUIRE(ln_plan(C, p) == OGV_OK, "ogv_layernorm_bwd: C=%d unsupported", C);
-  const long nb = ln_blocks(M, p.G);
+  const long nb = ln_bwd_blocks(M, p.G);
   hipStream_t s = as_stream(stream);
   float* part = (float*)ws;
+  float* tmp = part + (size_t)nb * 2 * C;
+  float* sums = tmp + colreduce_tmp_floats(nb, 2L * C);
   OGV_LN_DISPATCH(ln_bwd_launch, dy, x, gamma, mean, rstd, dx, part, nb, (long)M, C, s);
-  if (dgamma || dbeta) colsum_kernel<<<cdiv(2 * C, 256), 256, 0, s>>>(part, dgamma, dbeta, (int)nb, C, 2 * C);
+  if (dgamma || dbeta) {
+    colreduce(part, sums, nb, 2L * C, 2L * C, tmp, s);
+    if (dgamma) (void)hipMemcpyAsync(dgamma, sums, C * sizeof(float), hipMemcpyDeviceToDevice, s);
+    if (dbeta) (void)hipMemcpyAsync(dbeta, sums + C, C * sizeof(float), hipMemcpyDeviceToDevice, s);
+  }
   return check_launch("ogv_layernorm_bwd");
 }

@@ -36,6 +36,10 @@ SIGNATURES = {
     "ogv_gemm_dgrad": (_i, [_p, _i, _p, _p, _i, _p, _i, _p, _i, _i, _i, _i, _i, _p, _i, _p]),
     "ogv_gemm_wgrad_ws_bytes": (_sz, [_i, _i, _i]),
     "ogv_gemm_wgrad": (_i, [_p, _i, _p, _i, _p, _i, _p, _p, _i, _i, _i, _i, _p, _i, _p]),
+    "ogv_dwconv_fwd_ws_bytes": (_sz, [_i]),
+    "ogv_dwconv3x3_fwd": (_i, [_p, _p, _p, _p, _i, _i, _i, _i, _i, _p, _i, _p]),
+    "ogv_dwconv_bwd_ws_bytes": (_sz, [_i, _i, _i, _i, _i]),
+    "ogv_dwconv3x3_bwd": (_i, [_p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p, _i, _p]),
     "ogv_cast": (_i, [_p, _i, _p, _i, _sz, _p]),
 }
 

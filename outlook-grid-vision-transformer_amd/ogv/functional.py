@@ -50,6 +50,55 @@ def _ws(nbytes: int, device) -> torch.Tensor:
 
 _warned_fp16 = False
 
+# ------------------------------------------------------------------------------------------------
+# live kernel probe (bench.py): HIP events on the launching stream around the FIRST launch of a
+# named kernel per step, so its average duration inside the timed region can be reported.
+# ------------------------------------------------------------------------------------------------
+_PROBE = {"target": None, "armed": False, "pairs": [], "units": None}
+
+
+def probe_arm(target: str):
+    _PROBE["target"], _PROBE["armed"] = target, True
+
+
+def probe_disarm():
+    _PROBE["armed"] = False
+
+
+class _probe:
+    def __init__(self, name, units):
+        self.on = _PROBE["armed"] and _PROBE["target"] == name
+        if self.on:
+            _PROBE["armed"] = False           # first launch of the step only
+            _PROBE["units"] = units
+            self.e0 = torch.cuda.Event(enable_timing=True)
+            self.e1 = torch.cuda.Event(enable_timing=True)
+
+    def __enter__(self):
+        if self.on:
+            self.e0.record()
+        return self
+
+    def __exit__(self, *a):
+        if self.on:
+            self.e1.record()
+            _PROBE["pairs"].append((self.e0, self.e1))
+        return False
+
+
+def probe_results():
+    """(mean ms per probed launch, units of the last probed launch, n)."""
+    pairs = _PROBE["pairs"]
+    if not pairs:
+        return None, None, 0
+    torch.cuda.synchronize()
+    ms = [a.elapsed_time(b) for a, b in pairs]
+    return sum(ms) / len(ms), _PROBE["units"], len(ms)
+
+
+def probe_reset():
+    _PROBE["pairs"] = []
+
 
 def compute_dtype(x: torch.Tensor) -> torch.dtype:
     """Activation dtype for the kernels: the autocast dtype inside an autocast region (fp16 is
@@ -201,8 +250,9 @@ class _OutlookAgg(torch.autograd.Function):
         lib = _lib.load()
         M, C = v2d.shape
         y = torch.empty_like(v2d)
-        check(lib.ogv_outlook_agg_fwd(_ptr(v2d), _ptr(logits2d), _ptr(y), B, H, W, C, heads, k, logits2d.stride(0),
-                                      _dt(v2d), _stream()), "ogv_outlook_agg_fwd")
+        with _probe("outlook_fwd", dict(M=M, C=C, heads=heads, k=k, elem=v2d.element_size())):
+            check(lib.ogv_outlook_agg_fwd(_ptr(v2d), _ptr(logits2d), _ptr(y), B, H, W, C, heads, k,
+                                          logits2d.stride(0), _dt(v2d), _stream()), "ogv_outlook_agg_fwd")
         ctx.save_for_backward(v2d, logits2d)
         ctx.meta = (B, H, W, C, heads, k)
         return y
@@ -248,8 +298,9 @@ class _GridAttn(torch.autograd.Function):
         N = (H // g) * (W // g)
         probs = (torch.empty((B * g * g, heads, N, N), dtype=torch.float32, device=qkv2d.device)
                  if want_probs else None)
-        check(lib.ogv_grid_attn_fwd(_ptr(qkv2d), _ptr(out), _ptr(lse), _ptr(probs), B, H, W, C, heads, g,
-                                    float(scale), _dt(qkv2d), _stream()), "ogv_grid_attn_fwd")
+        with _probe("grid_fwd", dict(M=M, C=C, heads=heads, N=N, elem=qkv2d.element_size())):
+            check(lib.ogv_grid_attn_fwd(_ptr(qkv2d), _ptr(out), _ptr(lse), _ptr(probs), B, H, W, C, heads, g,
+                                        float(scale), _dt(qkv2d), _stream()), "ogv_grid_attn_fwd")
         ctx.save_for_backward(qkv2d, out, lse)
         ctx.meta = (B, H, W, C, heads, g, float(scale))
         if probs is None:
@@ -275,3 +326,44 @@ def grid_attention_rows(qkv2d, B, H, W, heads, g, scale, want_probs=False):
     require_device(qkv2d, what="ogv.grid_attention")
     qkv2d = qkv2d.contiguous()
     return _GridAttn.apply(qkv2d, int(B), int(H), int(W), int(heads), int(g), float(scale), bool(want_probs))
+
+
+# ------------------------------------------------------------------------------------------------
+# Depthwise 3x3 conv (MBConv.depthwise)
+# ------------------------------------------------------------------------------------------------
+class _DwConv3x3(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x2d, w, bias, B, H, W, stride):
+        lib = _lib.load()
+        C = x2d.shape[1]
+        Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
+        y = torch.empty((B * Ho * Wo, C), dtype=x2d.dtype, device=x2d.device)
+        ws = _ws(lib.ogv_dwconv_fwd_ws_bytes(C), x2d.device)
+        check(lib.ogv_dwconv3x3_fwd(_ptr(x2d), _ptr(w), _ptr(bias), _ptr(y), B, H, W, C, stride, _ptr(ws), _dt(x2d),
+                                    _stream()), "ogv_dwconv3x3_fwd")
+        ctx.save_for_backward(x2d, w)
+        ctx.meta = (B, H, W, C, stride, bias is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        lib = _lib.load()
+        x2d, w = ctx.saved_tensors
+        B, H, W, C, stride, has_bias = ctx.meta
+        dy = dy.to(x2d.dtype).contiguous()
+        dx = torch.empty_like(x2d) if ctx.needs_input_grad[0] else None
+        dw = torch.empty_like(w) if ctx.needs_input_grad[1] else None
+        db = torch.empty((C,), dtype=torch.float32, device=x2d.device) if (has_bias and ctx.needs_input_grad[2]) else None
+        ws = _ws(lib.ogv_dwconv_bwd_ws_bytes(B, H, W, C, stride), x2d.device)
+        check(lib.ogv_dwconv3x3_bwd(_ptr(dy), _ptr(x2d), _ptr(w), _ptr(dx), _ptr(dw), _ptr(db), B, H, W, C, stride,
+                                    _ptr(ws), _dt(x2d), _stream()), "ogv_dwconv3x3_bwd")
+        return dx, dw, db, None, None, None, None
+
+
+def dwconv3x3_nchw(x, weight, bias=None, stride=1):
+    """Depthwise 3x3 conv (padding 1) on an NCHW (channels_last) tensor -> channels_last NCHW."""
+    require_device(x, weight, bias, what="ogv.dwconv3x3")
+    B, C, H, W = x.shape
+    x2d = _rows_contig(nchw_to_rows(x))
+    y = _DwConv3x3.apply(x2d, f32(weight).contiguous(), f32(bias), B, H, W, int(stride))
+    return rows_to_nchw(y, B, (H - 1) // stride + 1, (W - 1) // stride + 1)

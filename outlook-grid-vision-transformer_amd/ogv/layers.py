@@ -42,6 +42,16 @@ class Conv1x1(nn.Conv2d):
         return OF.rows_to_nchw(y, B, H, W)
 
 
+class DepthwiseConv3x3(nn.Conv2d):
+    """nn.Conv2d(C, C, 3, stride, padding=1, groups=C) on the ogv depthwise kernels (NHWC)."""
+
+    def __init__(self, channels: int, stride: int = 1, bias: bool = True):
+        super().__init__(channels, channels, kernel_size=3, stride=stride, padding=1, groups=channels, bias=bias)
+
+    def forward(self, x):
+        return OF.dwconv3x3_nchw(x.to(OF.compute_dtype(x)), self.weight, self.bias, self.stride[0])
+
+
 class Linear(nn.Linear):
     """nn.Linear over the last dim of a contiguous [..., in] tensor (BHWC or [B, N, C]).
     ``rps`` = rows per sample for the DropPath row scale."""

@@ -5,8 +5,9 @@
   MBConv         :44-98  expand 1x1 (+BN+act) -> dw3x3 (+BN+act) -> SE -> project 1x1 (+BN) (+x)
 
 Round-1 status: the two 1x1 convolutions (expand / project: the GEMM-shaped >90% of the FLOPs)
-run on the ogv MFMA GEMM; BatchNorm, the depthwise 3x3 and the SE gate run on PyTorch-ROCm
-ops over channels_last tensors.  Fusing those is SURVEY.md §8(f) rank 1 ("next").
+run on the ogv MFMA GEMM and the depthwise 3x3 on the ogv NHWC depthwise kernels; BatchNorm and
+the SE gate still run on PyTorch-ROCm ops over channels_last tensors.  Fusing BN/SiLU/SE into the
+kernels is SURVEY.md §8(f) rank 1 ("next").
 """
 from typing import Literal
 from dataclasses import dataclass
@@ -17,7 +18,8 @@ import torch.nn.functional as F
 from src.model.Outlook_Block import *  # noqa: F401,F403
 from src.model.Outlook_Block import DropPath
 from src.model.outlook_attention import make_activation
-from ogv.layers import Conv1x1
+from ogv import functional as OF
+from ogv.layers import Conv1x1, DepthwiseConv3x3
 
 
 class SqueezeExcite(nn.Module):
@@ -69,14 +71,17 @@ class MBConv(nn.Module):
                                         make_activation(cfg.act))
         else:
             self.expand = nn.Identity()
-        self.depthwise = nn.Sequential(
-            nn.Conv2d(mid, mid, kernel_size=3, stride=stride, padding=1, groups=mid, bias=not cfg.use_bn),
-            norm(mid), make_activation(cfg.act))
+        self.depthwise = nn.Sequential(DepthwiseConv3x3(mid, stride=stride, bias=not cfg.use_bn),
+                                       norm(mid), make_activation(cfg.act))
         self.se = SqueezeExcite(mid, se_ratio=cfg.se_ratio, act=cfg.act) if cfg.se_ratio > 0 else nn.Identity()
         self.project = nn.Sequential(Conv1x1(mid, out_ch, bias=not cfg.use_bn), norm(out_ch))
         self.use_res = stride == 1 and in_ch == out_ch
         self.drop_path = DropPath(cfg.drop_path) if (cfg.drop_path and cfg.drop_path > 0) else nn.Identity()
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        h = self.project(self.se(self.depthwise(self.expand(x))))
+        dt = OF.compute_dtype(x)
+        x = x.to(dt)
+        # the stock-op parts (BN, depthwise, SE) follow the activation dtype even outside autocast
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=(dt == torch.bfloat16 and x.is_cuda)):
+            h = self.project(self.se(self.depthwise(self.expand(x))))
         return x + self.drop_path(h) if self.use_res else h

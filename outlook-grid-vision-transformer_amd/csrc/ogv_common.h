@@ -90,10 +90,13 @@ __device__ __forceinline__ void store_vec(T* __restrict__ p, const float* in) {
 }
 
 // ---------------------------------------------------------------- activations (exact erf GELU)
+// logistic sigmoid with the hardware reciprocal (v_rcp_f32, 1 ulp) instead of an IEEE division
+__device__ __forceinline__ float fast_sigmoid(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
+
 __device__ __forceinline__ float act_fwd(int act, float x) {
   switch (act) {
     case OGV_ACT_GELU: return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
-    case OGV_ACT_SILU: return x / (1.0f + __expf(-x));
+    case OGV_ACT_SILU: return x * fast_sigmoid(x);
     case OGV_ACT_RELU: return x > 0.f ? x : 0.f;
     default: return x;
   }
@@ -107,7 +110,7 @@ __device__ __forceinline__ float act_grad(int act, float x) {
       return cdf + x * pdf;
     }
     case OGV_ACT_SILU: {
-      const float s = 1.0f / (1.0f + __expf(-x));
+      const float s = fast_sigmoid(x);
       return s * (1.0f + x * (1.0f - s));
     }
     case OGV_ACT_RELU: return x > 0.f ? 1.f : 0.f;

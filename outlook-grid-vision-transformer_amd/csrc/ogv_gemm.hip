@@ -3,33 +3,106 @@
 // Every 1x1 Conv2d / nn.Linear on the OutGridBlock path is out = A[M,K] . W[N,K]^T with M = B*H*W
 // (hundreds of thousands of rows) and K, N <= 1024: tall-skinny and HBM-bound, so the kernel's
 // job is to stream A once with full-width loads and to fuse what the reference does in separate
-// ATen passes (bias, DropPath scale, residual add, activation of the producer's output, and the
-// activation derivative in backward).
+// ATen passes: bias, DropPath scale and residual add in the epilogue; the activation of the
+// producer's output (and, for MBConv, BatchNorm-apply + SiLU + the SE gate) in the A prologue;
+// the activation derivative in the backward epilogue; BatchNorm batch statistics of the output.
 //
-//   fwd   : out = res + rs[m/rps] * (act_in(A) . W^T + bias)
-//   dgrad : dA  = act_in'(Z) * rs[m/rps] * (dOut . W)      (W^T staged once into the workspace)
-//   wgrad : dW  = (rs*dOut)^T . act_in(A),  dbias = colsum(rs*dOut)   (split over M, fp32 slabs)
+//   fwd   : out = res + rs[m/rps] * (pro(A) . W^T + bias)      [+ per-column stats of out]
+//   dgrad : dA  = act'(Z) * rs[m/rps] * (dOut . W) (+ res)     (W^T staged once into the workspace)
+//   wgrad : dW  = (rs*dOut)^T . pro(X),  dbias = colsum(rs*dOut)  (split over M, fp32 slabs)
 //
 // bf16 operands use v_mfma_f32_16x16x32_bf16, fp32 operands the exact-f32 v_mfma_f32_16x16x4_f32.
-// Block = 256 threads (4 waves in 2x2), tile BM x BN, BK = 32 (bf16) / 16 (fp32); the tile -> block
-// map keeps all N-tiles of an M-panel on one XCD (blocks b and b+8 share an XCD) so the A panel is
-// fetched from HBM once and re-read from that XCD's L2.
-#include "ogv_common.h"
+// Block = 256 threads (4 waves in 2x2), tile 128 x BN, BK = 32 (bf16) / 16 (fp32); the tile ->
+// block map keeps all N-tiles of an M-panel on one XCD (blocks b and b+8 share an XCD) so the A
+// panel is fetched from HBM once and re-read from that XCD's L2.
+#include "ogv_gemm.h"
 
 namespace ogv {
+
+__device__ __forceinline__ float pro_apply(const Pro& p, float v, int m, int k) {
+  if (p.sc) v *= p.sc[k];
+  if (p.sh) v += p.sh[k];
+  v = act_fwd(p.act, v);
+  if (p.gate) v *= p.gate[(long)(m / p.rps) * p.gld + k];
+  return v;
+}
+
+// E consecutive columns k..k+E-1 of row m; per-column parameters fetched as vectors when the
+// run is full and 16-B aligned (k % 4 == 0, gld % 4 == 0), element-wise otherwise.
+template <int E>
+__device__ __forceinline__ void pro_apply_run(const Pro& p, float (&v)[E], int m, int k, int Ka) {
+  if (k + E <= Ka && (k & 3) == 0 && (p.gld & 3) == 0) {
+    if (p.sc) {
+      float t[E];
+      load_vec<float, E>(p.sc + k, t);
+#pragma unroll
+      for (int i = 0; i < E; ++i) v[i] *= t[i];
+    }
+    if (p.sh) {
+      float t[E];
+      load_vec<float, E>(p.sh + k, t);
+#pragma unroll
+      for (int i = 0; i < E; ++i) v[i] += t[i];
+    }
+#pragma unroll
+    for (int i = 0; i < E; ++i) v[i] = act_fwd(p.act, v[i]);
+    if (p.gate) {
+      float t[E];
+      load_vec<float, E>(p.gate + (long)(m / p.rps) * p.gld + k, t);
+#pragma unroll
+      for (int i = 0; i < E; ++i) v[i] *= t[i];
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < E; ++i)
+      if (k + i < Ka) v[i] = pro_apply(p, v[i], m, k + i);
+  }
+}
+
+// Column statistics of a wave's accumulator tile -> per-panel partials (deterministic).
+// Each thread holds rows 4*(lane>>4)+r (+16*i) of columns (lane&15) (+16*j); sums over its rows,
+// then across the 4 lane groups (xor 16, 32), then across the two M-waves through LDS.
+template <int TN, int WN, int BN>
+__device__ __forceinline__ void stats_store(float (&s1)[TN], float (&s2)[TN], float* lds, int wm, int wn, int lane,
+                                            float* stat, int mt, int n0, int N) {
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    s1[j] += __shfl_xor(s1[j], 16, 64);
+    s1[j] += __shfl_xor(s1[j], 32, 64);
+    s2[j] += __shfl_xor(s2[j], 16, 64);
+    s2[j] += __shfl_xor(s2[j], 32, 64);
+  }
+  __syncthreads();  // LDS tiles are dead: reuse them
+  if (lane < 16) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int c = wn * WN + j * 16 + lane;
+      lds[(wm * 2 + 0) * BN + c] = s1[j];
+      lds[(wm * 2 + 1) * BN + c] = s2[j];
+    }
+  }
+  __syncthreads();
+  if (wm == 0 && lane < 16) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int c = wn * WN + j * 16 + lane;
+      const int n = n0 + c;
+      if (n < N) {
+        stat[((long)mt * 2 + 0) * N + n] = lds[0 * BN + c] + lds[2 * BN + c];
+        stat[((long)mt * 2 + 1) * N + n] = lds[1 * BN + c] + lds[3 * BN + c];
+      }
+    }
+  }
+}
 
 // ------------------------------------------------------------------------------------------------
 // fwd / dgrad kernel, bf16
 // ------------------------------------------------------------------------------------------------
-template <int BM, int BN, int ACT>
-__global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__ A, int lda,
-                                                        const float* __restrict__ Wt, int ldw,
-                                                        const float* __restrict__ bias, const bf16* __restrict__ res,
-                                                        const float* __restrict__ rs, int rps,
-                                                        const bf16* __restrict__ Z, int ldz, int zact,
-                                                        bf16* __restrict__ out, int ldo, int M, int N, int K,
-                                                        int Ka, int Kb, int nMt, int nNt) {
-  // K: reduction length; Ka / Kb: valid reduction columns of A / W (zero beyond)
+template <int BM, int BN, bool PRO, bool STATS>
+__global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__ A, int lda, Pro pro,
+                                                        const float* __restrict__ Wt, int ldw, Epi epi,
+                                                        bf16* __restrict__ out, int ldo, int M, int N, int K, int Ka,
+                                                        int Kb, int nMt, int nNt) {
   constexpr int BK = 32;
   constexpr int PITCH = BK + 8;  // 80-byte rows: 16-B aligned fragment reads
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
@@ -91,15 +164,22 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
       }
     }
   };
-  auto store_tile = [&]() {
+  auto store_tile = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < A_VECS; ++i) {
       const int idx = tid + i * 256, row = idx / (BK / 8), kv = idx % (BK / 8);
       uint4 v = ra[i];
-      if constexpr (ACT != OGV_ACT_NONE) {
+      if constexpr (PRO) {
+        const int gm = m0 + row, gk = k0 + kv * 8;
         bf16* e = reinterpret_cast<bf16*>(&v);
+        if (gm < M) {
+          float f[8];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) e[q] = (bf16)act_fwd(ACT, (float)e[q]);
+          for (int q = 0; q < 8; ++q) f[q] = (float)e[q];
+          pro_apply_run<8>(pro, f, gm, gk, Ka);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) e[q] = gk + q < Ka ? (bf16)f[q] : (bf16)0.f;
+        }
       }
       *reinterpret_cast<uint4*>(As + row * PITCH + kv * 8) = v;
     }
@@ -113,7 +193,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
 
   load_tile(0);
   for (int k0 = 0; k0 < K; k0 += BK) {
-    store_tile();
+    store_tile(k0);
     __syncthreads();
     if (k0 + BK < K) load_tile(k0 + BK);  // next tile's HBM latency hides under this tile's MFMAs
     bf16x8 af[TM], bfg[TN];
@@ -131,39 +211,49 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
     __syncthreads();
   }
 
+  const bf16* res = static_cast<const bf16*>(epi.res);
+  const bf16* Z = static_cast<const bf16*>(epi.Z);
+  float s1[TN], s2[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int m = m0 + wm * WM + i * 16 + 4 * (lane >> 4) + r;
       if (m >= M) continue;
-      const float sc = rs ? rs[m / rps] : 1.f;
+      const float sc = epi.rs ? epi.rs[m / epi.rps] : 1.f;
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int n = n0 + wn * WN + j * 16 + (lane & 15);
         if (n >= N) continue;
         float v = acc[i][j][r];
-        if (bias) v += bias[n];
+        if (epi.bias) v += epi.bias[n];
         v *= sc;
         if (res) v += (float)res[(long)m * ldo + n];
-        if (zact) v *= act_grad(zact, (float)Z[(long)m * ldz + n]);
-        out[(long)m * ldo + n] = (bf16)v;
+        if (epi.zact) v *= act_grad(epi.zact, (float)Z[(long)m * epi.ldz + n]);
+        const bf16 o = (bf16)v;
+        out[(long)m * ldo + n] = o;
+        if constexpr (STATS) {
+          const float d = (float)o - (epi.stat_shift ? epi.stat_shift[n] : 0.f);
+          s1[j] += d;
+          s2[j] = fmaf(d, d, s2[j]);
+        }
       }
     }
   }
+  if constexpr (STATS)
+    stats_store<TN, WN, BN>(s1, s2, reinterpret_cast<float*>(As), wm, wn, lane, epi.stat, mt, n0, N);
 }
 
 // ------------------------------------------------------------------------------------------------
 // fwd / dgrad kernel, fp32 (exact-f32 MFMA 16x16x4)
 // ------------------------------------------------------------------------------------------------
-template <int BM, int BN, int ACT>
-__global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__ A, int lda,
-                                                       const float* __restrict__ Wt, int ldw,
-                                                       const float* __restrict__ bias, const float* __restrict__ res,
-                                                       const float* __restrict__ rs, int rps,
-                                                       const float* __restrict__ Z, int ldz, int zact,
-                                                       float* __restrict__ out, int ldo, int M, int N, int K,
-                                                       int Ka, int Kb, int nMt, int nNt) {
+template <int BM, int BN, bool PRO, bool STATS>
+__global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__ A, int lda, Pro pro,
+                                                       const float* __restrict__ Wt, int ldw, Epi epi,
+                                                       float* __restrict__ out, int ldo, int M, int N, int K, int Ka,
+                                                       int Kb, int nMt, int nNt) {
   constexpr int BK = 16;
   constexpr int PITCH = BK + 1;
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
@@ -214,13 +304,21 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
       if (gn < N) rb[i] = ld4(Wt + (long)gn * ldw + gk, gk, Kb, b_vec);
     }
   };
-  auto store_tile = [&]() {
+  auto store_tile = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < A_F4; ++i) {
       const int idx = tid + i * 256, row = idx / (BK / 4), kq = idx % (BK / 4);
+      float v[4] = {ra[i].x, ra[i].y, ra[i].z, ra[i].w};
+      if constexpr (PRO) {
+        const int gm = m0 + row, gk = k0 + kq * 4;
+        if (gm < M) {
+          pro_apply_run<4>(pro, v, gm, gk, Ka);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] = gk + q < Ka ? v[q] : 0.f;
+        }
+      }
       float* d = As + row * PITCH + kq * 4;
-      d[0] = act_fwd(ACT, ra[i].x); d[1] = act_fwd(ACT, ra[i].y);
-      d[2] = act_fwd(ACT, ra[i].z); d[3] = act_fwd(ACT, ra[i].w);
+      d[0] = v[0]; d[1] = v[1]; d[2] = v[2]; d[3] = v[3];
     }
 #pragma unroll
     for (int i = 0; i < B_F4; ++i) {
@@ -232,7 +330,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
 
   load_tile(0);
   for (int k0 = 0; k0 < K; k0 += BK) {
-    store_tile();
+    store_tile(k0);
     __syncthreads();
     if (k0 + BK < K) load_tile(k0 + BK);
 #pragma unroll
@@ -250,38 +348,49 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
     __syncthreads();
   }
 
+  const float* res = static_cast<const float*>(epi.res);
+  const float* Z = static_cast<const float*>(epi.Z);
+  float s1[TN], s2[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int m = m0 + wm * WM + i * 16 + 4 * (lane >> 4) + r;
       if (m >= M) continue;
-      const float sc = rs ? rs[m / rps] : 1.f;
+      const float sc = epi.rs ? epi.rs[m / epi.rps] : 1.f;
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int n = n0 + wn * WN + j * 16 + (lane & 15);
         if (n >= N) continue;
         float v = acc[i][j][r];
-        if (bias) v += bias[n];
+        if (epi.bias) v += epi.bias[n];
         v *= sc;
         if (res) v += res[(long)m * ldo + n];
-        if (zact) v *= act_grad(zact, Z[(long)m * ldz + n]);
+        if (epi.zact) v *= act_grad(epi.zact, Z[(long)m * epi.ldz + n]);
         out[(long)m * ldo + n] = v;
+        if constexpr (STATS) {
+          const float d = v - (epi.stat_shift ? epi.stat_shift[n] : 0.f);
+          s1[j] += d;
+          s2[j] = fmaf(d, d, s2[j]);
+        }
       }
     }
   }
+  if constexpr (STATS) stats_store<TN, WN, BN>(s1, s2, As, wm, wn, lane, epi.stat, mt, n0, N);
 }
 
 // ------------------------------------------------------------------------------------------------
-// wgrad, bf16: part[s][n][k] = sum_{m in chunk s} G[m,n] * act(X[m,k])   (G pre-scaled by rs)
+// wgrad, bf16: part[s][n][k] = sum_{m in chunk s} G[m,n] * pro(X)[m,k]   (G pre-scaled by rs)
 // Tiles staged [m][col] as loaded; MFMA fragments (reduction index = m) come from
 // ds_read_b64_tr_b16 transposed reads.  The m -> fragment-k map is permuted (j<4: m = 4g+j,
 // j>=4: m = 16+4g+j-4) identically for both operands, which makes each 32-lane half read 8
 // distinct rows: with an 80-element pitch the reads are bank-conflict free.
 // ------------------------------------------------------------------------------------------------
-template <int ACT>
+template <bool PRO>
 __global__ __launch_bounds__(256) void wgrad_bf16_kernel(const bf16* __restrict__ G, int ldg, const bf16* __restrict__ X,
-                                                         int ldx, const float* __restrict__ rs, int rps,
+                                                         int ldx, Pro pro, const float* __restrict__ rs, int rps,
                                                          float* __restrict__ part, float* __restrict__ dbias_part,
                                                          int M, int N, int K, int mchunk, int nNt) {
   constexpr int BN = 64, BKK = 64, MS = 32, PITCH = 80;
@@ -332,10 +441,14 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(const bf16* __restrict_
 #pragma unroll
           for (int t = 0; t < 8; ++t) e[t] = (bf16)((float)e[t] * sc);
         }
-        if constexpr (ACT != OGV_ACT_NONE) {
+        if constexpr (PRO) {
           bf16* e = reinterpret_cast<bf16*>(&xv);
+          float f[8];
 #pragma unroll
-          for (int t = 0; t < 8; ++t) e[t] = (bf16)act_fwd(ACT, (float)e[t]);
+          for (int t = 0; t < 8; ++t) f[t] = (float)e[t];
+          pro_apply_run<8>(pro, f, gm, k0 + scol, K);
+#pragma unroll
+          for (int t = 0; t < 8; ++t) e[t] = k0 + scol + t < K ? (bf16)f[t] : (bf16)0.f;
         }
       }
       *reinterpret_cast<uint4*>(Gs + srow * PITCH + scol) = gv;
@@ -383,9 +496,9 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(const bf16* __restrict_
 }
 
 // wgrad, fp32: f32 MFMA fragments read straight from the [m][col] tiles (k = lane>>4 layout).
-template <int ACT>
+template <bool PRO>
 __global__ __launch_bounds__(256) void wgrad_f32_kernel(const float* __restrict__ G, int ldg, const float* __restrict__ X,
-                                                        int ldx, const float* __restrict__ rs, int rps,
+                                                        int ldx, Pro pro, const float* __restrict__ rs, int rps,
                                                         float* __restrict__ part, float* __restrict__ dbias_part,
                                                         int M, int N, int K, int mchunk, int nNt) {
   constexpr int BN = 64, BKK = 64, MS = 16, PITCH = 68;
@@ -412,29 +525,37 @@ __global__ __launch_bounds__(256) void wgrad_f32_kernel(const float* __restrict_
   for (int m0 = mbeg; m0 < mend; m0 += MS) {
     {
       const int gm = m0 + srow;
-      float4 gv = float4{0.f, 0.f, 0.f, 0.f}, xv = float4{0.f, 0.f, 0.f, 0.f};
+      float gv[4] = {0.f, 0.f, 0.f, 0.f}, xv[4] = {0.f, 0.f, 0.f, 0.f};
       if (gm < mend) {
         const float* gsrc = G + (long)gm * ldg + n0 + scol;
         const float* xsrc = X + (long)gm * ldx + k0 + scol;
-        if (g_vec && n0 + scol + 4 <= N) gv = *reinterpret_cast<const float4*>(gsrc);
-        else {
-          gv.x = n0 + scol < N ? gsrc[0] : 0.f; gv.y = n0 + scol + 1 < N ? gsrc[1] : 0.f;
-          gv.z = n0 + scol + 2 < N ? gsrc[2] : 0.f; gv.w = n0 + scol + 3 < N ? gsrc[3] : 0.f;
+        if (g_vec && n0 + scol + 4 <= N) {
+          const float4 t = *reinterpret_cast<const float4*>(gsrc);
+          gv[0] = t.x; gv[1] = t.y; gv[2] = t.z; gv[3] = t.w;
+        } else {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) gv[t] = n0 + scol + t < N ? gsrc[t] : 0.f;
         }
-        if (x_vec && k0 + scol + 4 <= K) xv = *reinterpret_cast<const float4*>(xsrc);
-        else {
-          xv.x = k0 + scol < K ? xsrc[0] : 0.f; xv.y = k0 + scol + 1 < K ? xsrc[1] : 0.f;
-          xv.z = k0 + scol + 2 < K ? xsrc[2] : 0.f; xv.w = k0 + scol + 3 < K ? xsrc[3] : 0.f;
+        if (x_vec && k0 + scol + 4 <= K) {
+          const float4 t = *reinterpret_cast<const float4*>(xsrc);
+          xv[0] = t.x; xv[1] = t.y; xv[2] = t.z; xv[3] = t.w;
+        } else {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) xv[t] = k0 + scol + t < K ? xsrc[t] : 0.f;
         }
         if (rs) {
           const float sc = rs[gm / rps];
-          gv.x *= sc; gv.y *= sc; gv.z *= sc; gv.w *= sc;
+#pragma unroll
+          for (int t = 0; t < 4; ++t) gv[t] *= sc;
         }
-        xv.x = act_fwd(ACT, xv.x); xv.y = act_fwd(ACT, xv.y);
-        xv.z = act_fwd(ACT, xv.z); xv.w = act_fwd(ACT, xv.w);
+        if constexpr (PRO) {
+          pro_apply_run<4>(pro, xv, gm, k0 + scol, K);
+#pragma unroll
+          for (int t = 0; t < 4; ++t) xv[t] = k0 + scol + t < K ? xv[t] : 0.f;
+        }
       }
-      *reinterpret_cast<float4*>(Gs + srow * PITCH + scol) = gv;
-      *reinterpret_cast<float4*>(Xs + srow * PITCH + scol) = xv;
+      *reinterpret_cast<float4*>(Gs + srow * PITCH + scol) = make_float4(gv[0], gv[1], gv[2], gv[3]);
+      *reinterpret_cast<float4*>(Xs + srow * PITCH + scol) = make_float4(xv[0], xv[1], xv[2], xv[3]);
     }
     __syncthreads();
     if (do_bias && tid < BN) {
@@ -470,7 +591,60 @@ __global__ __launch_bounds__(256) void wgrad_f32_kernel(const float* __restrict_
   if (do_bias && tid < BN && n0 + tid < N) dbias_part[(long)s * N + n0 + tid] = bsum;
 }
 
-// WT[k][n] = W[n][k]  (fp32, 32x32 tiles through LDS)
+// ------------------------------------------------------------------------------------------------
+// Tiny GEMMs (the SE MLP: M = batch rows, fp32): one thread per output, K-loop dot products.
+// The MFMA kernels would launch a handful of 128-row blocks for these and run latency-bound.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void small_fwd_kernel(const float* __restrict__ A, int lda, Pro pro,
+                                                        const float* __restrict__ Wt, int ldw, Epi epi,
+                                                        float* __restrict__ out, int ldo, int M, int N, int Ka,
+                                                        int Kb) {
+  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid >= (long)M * N) return;
+  const int n = (int)(tid % N), m = (int)(tid / N);
+  const int K = Ka < Kb ? Ka : Kb;
+  const float* a = A + (long)m * lda;
+  const float* w = Wt + (long)n * ldw;
+  float acc = 0.f;
+  const bool p = pro.act != OGV_ACT_NONE || pro.sc || pro.sh || pro.gate;
+  for (int k = 0; k < K; ++k) acc = fmaf(p ? pro_apply(pro, a[k], m, k) : a[k], w[k], acc);
+  const float* res = static_cast<const float*>(epi.res);
+  const float* Z = static_cast<const float*>(epi.Z);
+  float v = acc;
+  if (epi.bias) v += epi.bias[n];
+  if (epi.rs) v *= epi.rs[m / epi.rps];
+  if (res) v += res[(long)m * ldo + n];
+  if (epi.zact) v *= act_grad(epi.zact, Z[(long)m * epi.ldz + n]);
+  out[(long)m * ldo + n] = v;
+}
+
+// dW[n][k] = sum_m rs*G[m,n] * pro(X)[m,k], dbias[n] = sum_m rs*G[m,n]   (thread per (n, k))
+__global__ __launch_bounds__(256) void small_wgrad_kernel(const float* __restrict__ G, int ldg,
+                                                          const float* __restrict__ X, int ldx, Pro pro,
+                                                          const float* __restrict__ rs, int rps, float* __restrict__ dW,
+                                                          float* __restrict__ dbias, int M, int N, int K) {
+  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long NK = (long)N * K;
+  if (tid >= NK + (dbias ? N : 0)) return;
+  const bool p = pro.act != OGV_ACT_NONE || pro.sc || pro.sh || pro.gate;
+  if (tid < NK) {
+    const int k = (int)(tid % K), n = (int)(tid / K);
+    float acc = 0.f;
+    for (int m = 0; m < M; ++m) {
+      const float x = X[(long)m * ldx + k];
+      const float g = G[(long)m * ldg + n] * (rs ? rs[m / rps] : 1.f);
+      acc = fmaf(g, p ? pro_apply(pro, x, m, k) : x, acc);
+    }
+    dW[tid] = acc;
+  } else {
+    const int n = (int)(tid - NK);
+    float acc = 0.f;
+    for (int m = 0; m < M; ++m) acc += G[(long)m * ldg + n] * (rs ? rs[m / rps] : 1.f);
+    dbias[n] = acc;
+  }
+}
+
+// WT[k][n] = W[n][k]  (fp32, 32x32 tiles through LDS), zero for n in [N, ldt)
 __global__ __launch_bounds__(256) void transpose_f32_kernel(const float* __restrict__ W, float* __restrict__ WT, int N,
                                                             int K, int ldt) {
   __shared__ float t[32][33];
@@ -488,57 +662,83 @@ __global__ __launch_bounds__(256) void transpose_f32_kernel(const float* __restr
 }
 
 // ------------------------------------------------------------------------------------------------
-// host dispatch
+// internal launchers
 // ------------------------------------------------------------------------------------------------
-template <typename T, int BM, int BN, int ACT>
-static void launch_mm(const void* A, int lda, const float* Wt, int ldw, const float* bias, const void* res,
-                      const float* rs, int rps, const void* Z, int ldz, int zact, void* out, int ldo, int M, int N,
-                      int K, int Ka, int Kb, hipStream_t s) {
+template <typename T, int BN, bool PRO, bool STATS>
+static void launch_mm(const void* A, int lda, const Pro& pro, const float* Wt, int ldw, void* out, int ldo, int M,
+                      int N, int K, int Ka, int Kb, const Epi& epi, hipStream_t s) {
+  constexpr int BM = GEMM_BM;
   const int nMt = (M + BM - 1) / BM, nNt = (N + BN - 1) / BN;
   const unsigned grid = (unsigned)(((nMt + 7) / 8) * 8 * nNt);
   if constexpr (sizeof(T) == 2)
-    gemm_bf16_kernel<BM, BN, ACT><<<grid, 256, 0, s>>>((const bf16*)A, lda, Wt, ldw, bias, (const bf16*)res, rs, rps,
-                                                       (const bf16*)Z, ldz, zact, (bf16*)out, ldo, M, N, K, Ka, Kb, nMt, nNt);
+    gemm_bf16_kernel<BM, BN, PRO, STATS><<<grid, 256, 0, s>>>((const bf16*)A, lda, pro, Wt, ldw, epi, (bf16*)out, ldo,
+                                                              M, N, K, Ka, Kb, nMt, nNt);
   else
-    gemm_f32_kernel<BM, BN, ACT><<<grid, 256, 0, s>>>((const float*)A, lda, Wt, ldw, bias, (const float*)res, rs, rps,
-                                                      (const float*)Z, ldz, zact, (float*)out, ldo, M, N, K, Ka, Kb, nMt, nNt);
+    gemm_f32_kernel<BM, BN, PRO, STATS><<<grid, 256, 0, s>>>((const float*)A, lda, pro, Wt, ldw, epi, (float*)out, ldo,
+                                                             M, N, K, Ka, Kb, nMt, nNt);
 }
 
-template <typename T, int ACT>
-static void launch_mm_tiles(const void* A, int lda, const float* Wt, int ldw, const float* bias, const void* res,
-                            const float* rs, int rps, const void* Z, int ldz, int zact, void* out, int ldo, int M,
-                            int N, int K, hipStream_t s, int Ka = -1, int Kb = -1) {
-  if (Ka < 0) Ka = K;
-  if (Kb < 0) Kb = K;
+template <typename T, bool PRO, bool STATS>
+static void launch_mm_bn(const void* A, int lda, const Pro& pro, const float* Wt, int ldw, void* out, int ldo, int M,
+                         int N, int K, int Ka, int Kb, const Epi& epi, hipStream_t s) {
   if (N > 64)
-    launch_mm<T, 128, 128, ACT>(A, lda, Wt, ldw, bias, res, rs, rps, Z, ldz, zact, out, ldo, M, N, K, Ka, Kb, s);
+    launch_mm<T, 128, PRO, STATS>(A, lda, pro, Wt, ldw, out, ldo, M, N, K, Ka, Kb, epi, s);
   else
-    launch_mm<T, 128, 64, ACT>(A, lda, Wt, ldw, bias, res, rs, rps, Z, ldz, zact, out, ldo, M, N, K, Ka, Kb, s);
+    launch_mm<T, 64, PRO, STATS>(A, lda, pro, Wt, ldw, out, ldo, M, N, K, Ka, Kb, epi, s);
 }
 
 template <typename T>
-static void launch_mm_act(int act, const void* A, int lda, const float* Wt, int ldw, const float* bias,
-                          const void* res, const float* rs, int rps, const void* Z, int ldz, int zact, void* out,
-                          int ldo, int M, int N, int K, hipStream_t s) {
-  switch (act) {
-    case OGV_ACT_GELU:
-      launch_mm_tiles<T, OGV_ACT_GELU>(A, lda, Wt, ldw, bias, res, rs, rps, Z, ldz, zact, out, ldo, M, N, K, s);
-      break;
-    case OGV_ACT_SILU:
-      launch_mm_tiles<T, OGV_ACT_SILU>(A, lda, Wt, ldw, bias, res, rs, rps, Z, ldz, zact, out, ldo, M, N, K, s);
-      break;
-    case OGV_ACT_RELU:
-      launch_mm_tiles<T, OGV_ACT_RELU>(A, lda, Wt, ldw, bias, res, rs, rps, Z, ldz, zact, out, ldo, M, N, K, s);
-      break;
-    default:
-      launch_mm_tiles<T, OGV_ACT_NONE>(A, lda, Wt, ldw, bias, res, rs, rps, Z, ldz, zact, out, ldo, M, N, K, s);
+static void launch_mm_any(const void* A, int lda, const Pro& pro, const float* Wt, int ldw, void* out, int ldo, int M,
+                          int N, int K, int Ka, int Kb, const Epi& epi, hipStream_t s) {
+  const bool p = pro.any(), st = epi.stat != nullptr;
+  if (p && st) launch_mm_bn<T, true, true>(A, lda, pro, Wt, ldw, out, ldo, M, N, K, Ka, Kb, epi, s);
+  else if (p) launch_mm_bn<T, true, false>(A, lda, pro, Wt, ldw, out, ldo, M, N, K, Ka, Kb, epi, s);
+  else if (st) launch_mm_bn<T, false, true>(A, lda, pro, Wt, ldw, out, ldo, M, N, K, Ka, Kb, epi, s);
+  else launch_mm_bn<T, false, false>(A, lda, pro, Wt, ldw, out, ldo, M, N, K, Ka, Kb, epi, s);
+}
+
+static bool tiny(int M, int N, ogv_dtype dt, const Epi& epi) {
+  return dt == OGV_F32 && epi.stat == nullptr && M <= 2048 && (long)M * N <= (1L << 20);
+}
+
+void gemm_fwd_launch(ogv_dtype dt, const void* A, int lda, const Pro& pro, const float* W, int ldw, void* out, int ldo,
+                     int M, int N, int K, int Ka, int Kb, const Epi& epi, hipStream_t s) {
+  if (M <= 0) return;
+  if (tiny(M, N, dt, epi)) {
+    small_fwd_kernel<<<cdiv((long)M * N, 256), 256, 0, s>>>((const float*)A, lda, pro, W, ldw, epi, (float*)out, ldo, M,
+                                                            N, Ka, Kb);
+    return;
   }
+  if (dt == OGV_BF16) launch_mm_any<bf16>(A, lda, pro, W, ldw, out, ldo, M, N, K, Ka, Kb, epi, s);
+  else launch_mm_any<float>(A, lda, pro, W, ldw, out, ldo, M, N, K, Ka, Kb, epi, s);
+}
+
+static inline int pad8(int n) { return (n + 7) / 8 * 8; }
+size_t dgrad_ws_bytes(int N, int K) { return (size_t)pad8(N) * K * sizeof(float); }
+
+void gemm_dgrad_launch(ogv_dtype dt, const void* dout, int ldd, const float* W, const void* Z, int ldz, int zact,
+                       const float* rs, int rps, const void* res, void* dA, int lda, int M, int N, int K, void* ws,
+                       hipStream_t s) {
+  if (M <= 0) return;
+  float* WT = (float*)ws;  // [K][Np], zero beyond N
+  const int Np = pad8(N);
+  dim3 tg(cdiv(K, 32), cdiv(Np, 32));
+  transpose_f32_kernel<<<tg, 256, 0, s>>>(W, WT, N, K, Np);
+  Epi e;
+  e.rs = rs;
+  e.rps = rps;
+  e.Z = Z;
+  e.ldz = ldz;
+  e.zact = zact;
+  e.res = res;
+  // dA[M,K] = dout[M,N] . WT[K,Np]^T
+  gemm_fwd_launch(dt, dout, ldd, Pro(), WT, Np, dA, lda, M, K, Np, N, Np, e, s);
 }
 
 struct WgradPlan {
   int nNt, nKt, S, mchunk;
 };
-static WgradPlan wgrad_plan(int M, int N, int K, int ms) {
+static WgradPlan wgrad_plan(int M, int N, int K) {
   WgradPlan p;
   p.nNt = (N + 63) / 64;
   p.nKt = (K + 63) / 64;
@@ -548,10 +748,51 @@ static WgradPlan wgrad_plan(int M, int N, int K, int ms) {
   if (S > max_s) S = max_s;
   if (S < 1) S = 1;
   int mchunk = (M + S - 1) / S;
-  mchunk = (mchunk + ms - 1) / ms * ms;
+  mchunk = (mchunk + 31) / 32 * 32;
   p.S = (M + mchunk - 1) / mchunk;
   p.mchunk = mchunk;
   return p;
+}
+
+size_t wgrad_ws_bytes(int M, int N, int K) {
+  WgradPlan p = wgrad_plan(M > 0 ? M : 1, N, K);
+  const size_t t1 = colreduce_tmp_floats(p.S, (long)N * K), t2 = colreduce_tmp_floats(p.S, N);
+  return ((size_t)p.S * ((size_t)N * K + N) + (t1 > t2 ? t1 : t2)) * sizeof(float);
+}
+
+void gemm_wgrad_launch(ogv_dtype dt, const void* G, int ldg, const void* X, int ldx, const Pro& pro, const float* rs,
+                       int rps, float* dW, float* dbias, int M, int N, int K, void* ws, hipStream_t s) {
+  if (M <= 0) {
+    (void)hipMemsetAsync(dW, 0, (size_t)N * K * sizeof(float), s);
+    if (dbias) (void)hipMemsetAsync(dbias, 0, (size_t)N * sizeof(float), s);
+    return;
+  }
+  if (dt == OGV_F32 && M <= 2048) {
+    small_wgrad_kernel<<<cdiv((long)N * K + (dbias ? N : 0), 256), 256, 0, s>>>(
+        (const float*)G, ldg, (const float*)X, ldx, pro, rs, rps, dW, dbias, M, N, K);
+    return;
+  }
+  WgradPlan p = wgrad_plan(M, N, K);
+  float* part = (float*)ws;
+  float* bpart = part + (size_t)p.S * N * K;
+  float* tmp = bpart + (size_t)p.S * N;
+  dim3 grid(p.nNt * p.nKt, p.S);
+  float* bp = dbias ? bpart : nullptr;
+  const bool pr = pro.any();
+  if (dt == OGV_BF16) {
+    if (pr) wgrad_bf16_kernel<true><<<grid, 256, 0, s>>>((const bf16*)G, ldg, (const bf16*)X, ldx, pro, rs, rps, part, bp,
+                                                         M, N, K, p.mchunk, p.nNt);
+    else wgrad_bf16_kernel<false><<<grid, 256, 0, s>>>((const bf16*)G, ldg, (const bf16*)X, ldx, pro, rs, rps, part, bp,
+                                                       M, N, K, p.mchunk, p.nNt);
+  } else {
+    if (pr) wgrad_f32_kernel<true><<<grid, 256, 0, s>>>((const float*)G, ldg, (const float*)X, ldx, pro, rs, rps, part,
+                                                        bp, M, N, K, p.mchunk, p.nNt);
+    else wgrad_f32_kernel<false><<<grid, 256, 0, s>>>((const float*)G, ldg, (const float*)X, ldx, pro, rs, rps, part, bp,
+                                                      M, N, K, p.mchunk, p.nNt);
+  }
+  const long len = (long)N * K;
+  colreduce(part, dW, p.S, len, len, tmp, s);
+  if (dbias) colreduce(bpart, dbias, p.S, N, N, tmp, s);
 }
 
 static int check_common(int M, int N, int K, ogv_act act, ogv_dtype dt, const char* who) {
@@ -574,17 +815,18 @@ extern "C" int ogv_gemm_fwd(const void* A, int lda, const float* W, const float*
   OGV_REQUIRE(lda >= K, "ogv_gemm_fwd: lda %d < K %d", lda, K);
   OGV_REQUIRE(ldo >= N, "ogv_gemm_fwd: ldo %d < N %d", ldo, N);
   OGV_REQUIRE(!rs || rps > 0, "ogv_gemm_fwd: rows-per-sample must be > 0 with a row scale");
-  if (M == 0) return OGV_OK;
-  hipStream_t s = as_stream(stream);
-  if (dt == OGV_BF16)
-    launch_mm_act<bf16>(act_in, A, lda, W, K, bias, res, rs, rps, nullptr, 0, 0, out, ldo, M, N, K, s);
-  else
-    launch_mm_act<float>(act_in, A, lda, W, K, bias, res, rs, rps, nullptr, 0, 0, out, ldo, M, N, K, s);
+  Pro pro;
+  pro.act = act_in;
+  Epi epi;
+  epi.bias = bias;
+  epi.res = res;
+  epi.rs = rs;
+  epi.rps = rps > 0 ? rps : 1;
+  gemm_fwd_launch(dt, A, lda, pro, W, K, out, ldo, M, N, K, K, K, epi, as_stream(stream));
   return check_launch("ogv_gemm_fwd");
 }
 
-static inline int pad8(int n) { return (n + 7) / 8 * 8; }
-extern "C" size_t ogv_gemm_dgrad_ws_bytes(int N, int K) { return (size_t)pad8(N) * K * sizeof(float); }
+extern "C" size_t ogv_gemm_dgrad_ws_bytes(int N, int K) { return dgrad_ws_bytes(N, K); }
 
 extern "C" int ogv_gemm_dgrad(const void* dout, int ldd, const float* W, const void* Z, int ldz, const float* rs,
                               int rps, void* dA, int lda, int M, int N, int K, ogv_act act_in, void* ws, ogv_dtype dt,
@@ -596,27 +838,12 @@ extern "C" int ogv_gemm_dgrad(const void* dout, int ldd, const float* W, const v
   OGV_REQUIRE(ldd >= N, "ogv_gemm_dgrad: ldd %d < N %d", ldd, N);
   OGV_REQUIRE(lda >= K, "ogv_gemm_dgrad: lda %d < K %d", lda, K);
   OGV_REQUIRE(!rs || rps > 0, "ogv_gemm_dgrad: rows-per-sample must be > 0 with a row scale");
-  if (M == 0) return OGV_OK;
-  hipStream_t s = as_stream(stream);
-  float* WT = (float*)ws;  // [K][Np], zero beyond N
-  const int Np = pad8(N);
-  dim3 tg(cdiv(K, 32), cdiv(Np, 32));
-  transpose_f32_kernel<<<tg, 256, 0, s>>>(W, WT, N, K, Np);
-  // dA[M,K] = dout[M,N] . WT[K,N]^T, epilogue: * rs, * act'(Z)
-  if (dt == OGV_BF16)
-    launch_mm_tiles<bf16, OGV_ACT_NONE>(dout, ldd, WT, Np, nullptr, nullptr, rs, rps, Z, ldz, (int)act_in, dA, lda, M,
-                                        K, Np, s, N, Np);
-  else
-    launch_mm_tiles<float, OGV_ACT_NONE>(dout, ldd, WT, Np, nullptr, nullptr, rs, rps, Z, ldz, (int)act_in, dA, lda,
-                                         M, K, Np, s, N, Np);
+  gemm_dgrad_launch(dt, dout, ldd, W, Z, ldz, (int)act_in, rs, rps > 0 ? rps : 1, nullptr, dA, lda, M, N, K, ws,
+                    as_stream(stream));
   return check_launch("ogv_gemm_dgrad");
 }
 
-extern "C" size_t ogv_gemm_wgrad_ws_bytes(int M, int N, int K) {
-  WgradPlan p = wgrad_plan(M > 0 ? M : 1, N, K, 32);
-  const size_t t1 = colreduce_tmp_floats(p.S, (long)N * K), t2 = colreduce_tmp_floats(p.S, N);
-  return ((size_t)p.S * ((size_t)N * K + N) + (t1 > t2 ? t1 : t2)) * sizeof(float);
-}
+extern "C" size_t ogv_gemm_wgrad_ws_bytes(int M, int N, int K) { return wgrad_ws_bytes(M, N, K); }
 
 extern "C" int ogv_gemm_wgrad(const void* dout, int ldd, const void* A, int lda, const float* rs, int rps, float* dW,
                               float* dbias, int M, int N, int K, ogv_act act_in, void* ws, ogv_dtype dt,
@@ -626,57 +853,8 @@ extern "C" int ogv_gemm_wgrad(const void* dout, int ldd, const void* A, int lda,
   OGV_REQUIRE(dout && A && dW && ws, "ogv_gemm_wgrad: null pointer");
   OGV_REQUIRE(ldd >= N && lda >= K, "ogv_gemm_wgrad: ldd/lda smaller than N/K");
   OGV_REQUIRE(!rs || rps > 0, "ogv_gemm_wgrad: rows-per-sample must be > 0 with a row scale");
-  hipStream_t s = as_stream(stream);
-  if (M == 0) {
-    (void)hipMemsetAsync(dW, 0, (size_t)N * K * sizeof(float), s);
-    if (dbias) (void)hipMemsetAsync(dbias, 0, (size_t)N * sizeof(float), s);
-    return check_launch("ogv_gemm_wgrad");
-  }
-  // plan with the same row granularity used by the size query (32)
-  WgradPlan p = wgrad_plan(M, N, K, 32);
-  float* part = (float*)ws;
-  float* bpart = part + (size_t)p.S * N * K;
-  dim3 grid(p.nNt * p.nKt, p.S);
-  if (dt == OGV_BF16) {
-    switch (act_in) {
-      case OGV_ACT_GELU:
-        wgrad_bf16_kernel<OGV_ACT_GELU><<<grid, 256, 0, s>>>((const bf16*)dout, ldd, (const bf16*)A, lda, rs, rps, part,
-                                                             dbias ? bpart : nullptr, M, N, K, p.mchunk, p.nNt);
-        break;
-      case OGV_ACT_SILU:
-        wgrad_bf16_kernel<OGV_ACT_SILU><<<grid, 256, 0, s>>>((const bf16*)dout, ldd, (const bf16*)A, lda, rs, rps, part,
-                                                             dbias ? bpart : nullptr, M, N, K, p.mchunk, p.nNt);
-        break;
-      case OGV_ACT_RELU:
-        wgrad_bf16_kernel<OGV_ACT_RELU><<<grid, 256, 0, s>>>((const bf16*)dout, ldd, (const bf16*)A, lda, rs, rps, part,
-                                                             dbias ? bpart : nullptr, M, N, K, p.mchunk, p.nNt);
-        break;
-      default:
-        wgrad_bf16_kernel<OGV_ACT_NONE><<<grid, 256, 0, s>>>((const bf16*)dout, ldd, (const bf16*)A, lda, rs, rps, part,
-                                                             dbias ? bpart : nullptr, M, N, K, p.mchunk, p.nNt);
-    }
-  } else {
-    switch (act_in) {
-      case OGV_ACT_GELU:
-        wgrad_f32_kernel<OGV_ACT_GELU><<<grid, 256, 0, s>>>((const float*)dout, ldd, (const float*)A, lda, rs, rps, part,
-                                                            dbias ? bpart : nullptr, M, N, K, p.mchunk, p.nNt);
-        break;
-      case OGV_ACT_SILU:
-        wgrad_f32_kernel<OGV_ACT_SILU><<<grid, 256, 0, s>>>((const float*)dout, ldd, (const float*)A, lda, rs, rps, part,
-                                                            dbias ? bpart : nullptr, M, N, K, p.mchunk, p.nNt);
-        break;
-      case OGV_ACT_RELU:
-        wgrad_f32_kernel<OGV_ACT_RELU><<<grid, 256, 0, s>>>((const float*)dout, ldd, (const float*)A, lda, rs, rps, part,
-                                                            dbias ? bpart : nullptr, M, N, K, p.mchunk, p.nNt);
-        break;
-      default:
-        wgrad_f32_kernel<OGV_ACT_NONE><<<grid, 256, 0, s>>>((const float*)dout, ldd, (const float*)A, lda, rs, rps, part,
-                                                            dbias ? bpart : nullptr, M, N, K, p.mchunk, p.nNt);
-    }
-  }
-  const long len = (long)N * K;
-  float* tmp = bpart + (size_t)p.S * N;
-  colreduce(part, dW, p.S, len, len, tmp, s);
-  if (dbias) colreduce(bpart, dbias, p.S, N, N, tmp, s);
+  Pro pro;
+  pro.act = act_in;
+  gemm_wgrad_launch(dt, dout, ldd, A, lda, pro, rs, rps > 0 ? rps : 1, dW, dbias, M, N, K, ws, as_stream(stream));
   return check_launch("ogv_gemm_wgrad");
 }

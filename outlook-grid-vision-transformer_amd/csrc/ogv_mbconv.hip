@@ -1,0 +1,968 @@
+// Fused MBConv (src/model/mbc_conv.py:44-98) for the OutGridBlock path:
+//   e  = x . We^T                      expand 1x1, no bias   (+ BN1 batch stats in the GEMM epilogue)
+//   a1 = act(BN1(e))                   applied on the fly by the depthwise conv's loads
+//   d  = dw3x3(a1)                     (+ BN2 batch stats in the conv epilogue)
+//   a2 = act(BN2(d))
+//   g  = sigmoid(W2 act(W1 mean_hw(a2) + b1) + b2)        SqueezeExcite (:22-27), B rows only
+//   p  = (a2 * g) . Wp^T               project 1x1: BN2-apply, act and the SE gate in the A prologue
+//                                      (+ BN3 batch stats in the epilogue)
+//   out = x + BN3(p)
+// BatchNorm2d semantics (train): normalise with the biased batch variance, update running_mean /
+// running_var (unbiased) with momentum 0.1; eval: running statistics.  Batch statistics are
+// accumulated as per-panel sums of (v - running_mean) and (v - running_mean)^2 (shifted sums: no
+// cancellation once the running mean tracks the batch mean) and reduced deterministically.
+//
+// Backward is hand-scheduled: the five per-(image, channel) reductions the SE and BN2 backward
+// need are taken in ONE pass over (dA3, d); BN1's reductions ride in the depthwise-dgrad epilogue.
+// HBM passes over the [M, mid] tensors: fwd 4 (e write, e read+d write, d read for the pool, d
+// read for project), bwd 9.
+#include "ogv_gemm.h"
+
+namespace ogv {
+
+struct RowPlan {
+  int V, nch, nchb, lanes, ctiles;
+};
+static RowPlan row_plan(int K) {
+  RowPlan p;
+  p.V = K % 8 == 0 ? 8 : (K % 4 == 0 ? 4 : 1);
+  p.nch = K / p.V;
+  p.nchb = p.nch < 64 ? p.nch : 64;
+  p.lanes = 256 / p.nchb;
+  p.ctiles = (p.nch + p.nchb - 1) / p.nchb;
+  return p;
+}
+
+// ------------------------------------------------------------------ BN finalize / coefficients
+// train: mean = shift + S1/n, var = S2/n - (S1/n)^2; running stats updated (unbiased var).
+// eval : mean/var = running stats.  Emits invstd, sc = gamma*invstd, sh = beta - mean*sc.
+__global__ void bn_finalize_kernel(const float* __restrict__ sums, int K, double n, const float* __restrict__ gamma,
+                                   const float* __restrict__ beta, float eps, float momentum, float* rm, float* rv,
+                                   float* __restrict__ mean_out, float* __restrict__ invstd_out, float* __restrict__ sc,
+                                   float* __restrict__ sh, int train) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= K) return;
+  float mean, var;
+  if (train) {
+    const double s1 = sums[c] / n, s2 = sums[K + c] / n;
+    const double shift = rm[c];
+    mean = (float)(shift + s1);
+    double v = s2 - s1 * s1;
+    var = (float)(v > 0.0 ? v : 0.0);
+    rm[c] = (1.f - momentum) * rm[c] + momentum * mean;
+    rv[c] = (1.f - momentum) * rv[c] + momentum * (float)(var * (n / (n > 1.0 ? n - 1.0 : 1.0)));
+  } else {
+    mean = rm[c];
+    var = rv[c];
+  }
+  const float is = rsqrtf(var + eps);
+  const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
+  mean_out[c] = mean;
+  invstd_out[c] = is;
+  sc[c] = g * is;
+  sh[c] = b - mean * g * is;
+}
+
+// From S = [sum dy, sum dy*xhat]: dgamma, dbeta and the apply coefficients
+// dx = ca*(dy - cb - xhat*cc),  ca = gamma*invstd, (cb, cc) = (S0, S1)/n in train, 0 in eval.
+__global__ void bn_coeffs_kernel(const float* __restrict__ S, int K, float n, const float* __restrict__ gamma,
+                                 const float* __restrict__ invstd, float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                 float* __restrict__ coef, int train) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= K) return;
+  const float sdy = S[c], sdyx = S[K + c];
+  if (dgamma) dgamma[c] = sdyx;
+  if (dbeta) dbeta[c] = sdy;
+  coef[c] = (gamma ? gamma[c] : 1.f) * invstd[c];
+  coef[K + c] = train ? sdy / n : 0.f;
+  coef[2 * K + c] = train ? sdyx / n : 0.f;
+}
+
+// ------------------------------------------------------------------ depthwise conv with BN fusion
+// ---- LDS-tiled depthwise kernels -------------------------------------------------------------
+// Block = (image b, band of TR rows, column tile of TW, channel tile of CT = 4*V channels).
+// The (TR+2) x (TW+2) x CT input tile (1-pixel halo, zero outside the image) is staged into LDS as
+// fp32 with the producer's BatchNorm + activation applied ONCE per element; 256 threads =
+// 64 pixel slots x 4 channel chunks then compute from LDS.  Per-block statistics partials go to
+// row rid = (b*nbands + band)*ncolt + colt of a [rows][Q][C] slab (Q quantities).
+struct DwTile {
+  int B, H, W, C, TR, TW, nbands, ncolt, nct, CT, PP;
+  __host__ __device__ long rows() const { return (long)B * nbands * ncolt; }
+  __host__ __device__ size_t lds_bytes() const { return (size_t)(TR + 2) * (TW + 2) * PP * sizeof(float); }
+};
+static DwTile dw_tile_plan(int B, int H, int W, int C, int V) {
+  DwTile t;
+  t.B = B; t.H = H; t.W = W; t.C = C;
+  t.TW = W < 32 ? W : 32;
+  int tr = 128 / t.TW;
+  const int hcap = H < 32 ? H : 32;
+  t.TR = tr < 1 ? 1 : (tr > hcap ? hcap : tr);
+  t.nbands = (H + t.TR - 1) / t.TR;
+  t.ncolt = (W + t.TW - 1) / t.TW;
+  t.CT = 4 * V;
+  t.PP = t.CT + 4;
+  t.nct = (C + t.CT - 1) / t.CT;
+  return t;
+}
+
+struct TileIdx {
+  int ct, colt, band;
+  long b, rid;
+};
+__device__ __forceinline__ TileIdx tile_idx(const DwTile& t) {
+  TileIdx i;
+  long id = blockIdx.x;
+  i.ct = (int)(id % t.nct); id /= t.nct;
+  i.colt = (int)(id % t.ncolt); id /= t.ncolt;
+  i.band = (int)(id % t.nbands);
+  i.b = id / t.nbands;
+  i.rid = (i.b * t.nbands + i.band) * t.ncolt + i.colt;
+  return i;
+}
+
+// stage tile[r][c][ch] = pro(src[b, y0-1+r, x0-1+c, c0+ch]) (0 outside image / channels)
+template <typename T, int V, bool PRO>
+__device__ __forceinline__ void stage_tile(float* tile, const T* __restrict__ src, const DwTile& t, const TileIdx& ti,
+                                           const float* __restrict__ sc, const float* __restrict__ sh, int act) {
+  const int y0 = ti.band * t.TR - 1, x0 = ti.colt * t.TW - 1, c0 = ti.ct * t.CT;
+  const int tw2 = t.TW + 2;
+  const int n = (t.TR + 2) * tw2 * 4;
+  for (int idx = threadIdx.x; idx < n; idx += 256) {
+    const int chunk = idx & 3, pix = idx >> 2;
+    const int r = pix / tw2, cc = pix - r * tw2;
+    const int y = y0 + r, x = x0 + cc, c = c0 + chunk * V;
+    float v[V];
+    if (y >= 0 && y < t.H && x >= 0 && x < t.W && c < t.C) {
+      load_vec<T, V>(src + ((ti.b * t.H + y) * t.W + x) * t.C + c, v);
+      if constexpr (PRO) {
+        float s[V], h[V];
+        load_vec<float, V>(sc + c, s);
+        load_vec<float, V>(sh + c, h);
+#pragma unroll
+        for (int i = 0; i < V; ++i) v[i] = act_fwd(act, fmaf(v[i], s[i], h[i]));
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < V; ++i) v[i] = 0.f;
+    }
+    float* d = tile + pix * t.PP + chunk * V;
+#pragma unroll
+    for (int i = 0; i < V; i += 4) *reinterpret_cast<float4*>(d + i) = make_float4(v[i], v[i + 1], v[i + 2], v[i + 3]);
+  }
+}
+
+// Sum q[NQ][V] over the 64 slots of each of the 4 channel chunks (chunk = tid & 3,
+// slot = tid >> 2): xor-shuffles over lane bits 2..5 inside each wave, then the 4 waves through
+// LDS (4*NQ*4*V floats; the LDS may be reused).  out[k*qstride + c], c = cbase + chunk*V + i < C.
+template <int NQ, int V>
+__device__ __forceinline__ void chunk_reduce_store(float (&q)[NQ][V], float* lds, float* out, long qstride, int C,
+                                                   int cbase) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < NQ; ++k)
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      float v = q[k][i];
+      v += __shfl_xor(v, 4, 64);
+      v += __shfl_xor(v, 8, 64);
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      q[k][i] = v;
+    }
+  __syncthreads();
+  if (lane < 4) {
+#pragma unroll
+    for (int k = 0; k < NQ; ++k)
+#pragma unroll
+      for (int i = 0; i < V; ++i) lds[((wave * NQ + k) * 4 + lane) * V + i] = q[k][i];
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < NQ * 4 * V; idx += 256) {
+    const int k = idx / (4 * V), r = idx - k * 4 * V;
+    const int ch = r / V, i = r - ch * V;
+    float sum = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) sum += lds[((w * NQ + k) * 4 + ch) * V + i];
+    const int c = cbase + ch * V + i;
+    if (c < C) out[(long)k * qstride + c] = sum;
+  }
+}
+
+// d = dw3x3(act(e*sc1 + sh1)) (+ stats of the rounded output minus shift)
+template <typename T, int V>
+__global__ __launch_bounds__(256) void dw_fwd_tile_kernel(const T* __restrict__ e, const float* __restrict__ wdw,
+                                                          const float* __restrict__ sc, const float* __restrict__ sh,
+                                                          int act, T* __restrict__ out, float* __restrict__ stat,
+                                                          const float* __restrict__ shift, DwTile t) {
+  extern __shared__ __attribute__((aligned(16))) float tile[];
+  const TileIdx ti = tile_idx(t);
+  stage_tile<T, V, true>(tile, e, t, ti, sc, sh, act);
+  __syncthreads();
+  const int chunk = threadIdx.x & 3, slot = threadIdx.x >> 2;
+  const int c = ti.ct * t.CT + chunk * V;
+  float q[2][V];
+#pragma unroll
+  for (int i = 0; i < V; ++i) { q[0][i] = 0.f; q[1][i] = 0.f; }
+  if (c < t.C) {
+    float w[9][V], sft[V];
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+#pragma unroll
+      for (int k = 0; k < 9; ++k) w[k][i] = wdw[(c + i) * 9 + k];
+      sft[i] = shift ? shift[c + i] : 0.f;
+    }
+    const int tw2 = t.TW + 2;
+    for (int o = slot; o < t.TR * t.TW; o += 64) {
+      const int ry = o / t.TW, cx = o - ry * t.TW;
+      const int y = ti.band * t.TR + ry, x = ti.colt * t.TW + cx;
+      if (y >= t.H || x >= t.W) continue;
+      float acc[V];
+#pragma unroll
+      for (int i = 0; i < V; ++i) acc[i] = 0.f;
+#pragma unroll
+      for (int ki = 0; ki < 3; ++ki)
+#pragma unroll
+        for (int kj = 0; kj < 3; ++kj) {
+          const float* src = tile + ((ry + ki) * tw2 + cx + kj) * t.PP + chunk * V;
+#pragma unroll
+          for (int i = 0; i < V; i += 4) {
+            const float4 a = *reinterpret_cast<const float4*>(src + i);
+            acc[i] = fmaf(w[ki * 3 + kj][i], a.x, acc[i]);
+            acc[i + 1] = fmaf(w[ki * 3 + kj][i + 1], a.y, acc[i + 1]);
+            acc[i + 2] = fmaf(w[ki * 3 + kj][i + 2], a.z, acc[i + 2]);
+            acc[i + 3] = fmaf(w[ki * 3 + kj][i + 3], a.w, acc[i + 3]);
+          }
+        }
+      float of[V];
+#pragma unroll
+      for (int i = 0; i < V; ++i) {
+        of[i] = to_f(from_f<T>(acc[i]));
+        const float dl = of[i] - sft[i];
+        q[0][i] += dl;
+        q[1][i] = fmaf(dl, dl, q[1][i]);
+      }
+      store_vec<T, V>(out + ((ti.b * t.H + y) * t.W + x) * t.C + c, of);
+    }
+  }
+  if (stat) chunk_reduce_store<2, V>(q, tile, stat + ti.rid * 2 * t.C, t.C, t.C, ti.ct * t.CT);
+}
+
+// dy1 = (dw3x3^T dd) * act'(e*sc1 + sh1) -> out; stats: sum dy1, sum dy1*(e - mean1)*invstd1
+template <typename T, int V>
+__global__ __launch_bounds__(256) void dw_dgrad_tile_kernel(const T* __restrict__ dd, const float* __restrict__ wdw,
+                                                            const T* __restrict__ e, const float* __restrict__ sc,
+                                                            const float* __restrict__ sh,
+                                                            const float* __restrict__ mean,
+                                                            const float* __restrict__ invstd, int act,
+                                                            T* __restrict__ out, float* __restrict__ stat, DwTile t) {
+  extern __shared__ __attribute__((aligned(16))) float tile[];
+  const TileIdx ti = tile_idx(t);
+  stage_tile<T, V, false>(tile, dd, t, ti, nullptr, nullptr, 0);
+  __syncthreads();
+  const int chunk = threadIdx.x & 3, slot = threadIdx.x >> 2;
+  const int c = ti.ct * t.CT + chunk * V;
+  float q[2][V];
+#pragma unroll
+  for (int i = 0; i < V; ++i) { q[0][i] = 0.f; q[1][i] = 0.f; }
+  if (c < t.C) {
+    float w[9][V], s[V], h[V], mu[V], is[V];
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+#pragma unroll
+      for (int k = 0; k < 9; ++k) w[k][i] = wdw[(c + i) * 9 + k];
+    }
+    load_vec<float, V>(sc + c, s);
+    load_vec<float, V>(sh + c, h);
+    load_vec<float, V>(mean + c, mu);
+    load_vec<float, V>(invstd + c, is);
+    const int tw2 = t.TW + 2;
+    for (int o = slot; o < t.TR * t.TW; o += 64) {
+      const int ry = o / t.TW, cx = o - ry * t.TW;
+      const int y = ti.band * t.TR + ry, x = ti.colt * t.TW + cx;
+      if (y >= t.H || x >= t.W) continue;
+      float acc[V];
+#pragma unroll
+      for (int i = 0; i < V; ++i) acc[i] = 0.f;
+#pragma unroll
+      for (int ki = 0; ki < 3; ++ki)
+#pragma unroll
+        for (int kj = 0; kj < 3; ++kj) {
+          const float* src = tile + ((ry + 2 - ki) * tw2 + cx + 2 - kj) * t.PP + chunk * V;
+#pragma unroll
+          for (int i = 0; i < V; i += 4) {
+            const float4 a = *reinterpret_cast<const float4*>(src + i);
+            acc[i] = fmaf(w[ki * 3 + kj][i], a.x, acc[i]);
+            acc[i + 1] = fmaf(w[ki * 3 + kj][i + 1], a.y, acc[i + 1]);
+            acc[i + 2] = fmaf(w[ki * 3 + kj][i + 2], a.z, acc[i + 2]);
+            acc[i + 3] = fmaf(w[ki * 3 + kj][i + 3], a.w, acc[i + 3]);
+          }
+        }
+      const long off = ((ti.b * t.H + y) * t.W + x) * t.C + c;
+      float ev[V], o2[V];
+      load_vec<T, V>(e + off, ev);
+#pragma unroll
+      for (int i = 0; i < V; ++i) {
+        o2[i] = to_f(from_f<T>(acc[i] * act_grad(act, fmaf(ev[i], s[i], h[i]))));
+        q[0][i] += o2[i];
+        q[1][i] = fmaf(o2[i], (ev[i] - mu[i]) * is[i], q[1][i]);
+      }
+      store_vec<T, V>(out + off, o2);
+    }
+  }
+  chunk_reduce_store<2, V>(q, tile, stat + ti.rid * 2 * t.C, t.C, t.C, ti.ct * t.CT);
+}
+
+// dWdw partials: part[rid][tap][c] = sum over the block's pixels dd[p,c] * act(e*sc1+sh1)[p+tap, c]
+template <typename T, int V>
+__global__ __launch_bounds__(256) void dw_wgrad_tile_kernel(const T* __restrict__ dd, const T* __restrict__ e,
+                                                            const float* __restrict__ sc, const float* __restrict__ sh,
+                                                            int act, float* __restrict__ part, DwTile t) {
+  extern __shared__ __attribute__((aligned(16))) float tile[];
+  const TileIdx ti = tile_idx(t);
+  stage_tile<T, V, true>(tile, e, t, ti, sc, sh, act);
+  __syncthreads();
+  const int chunk = threadIdx.x & 3, slot = threadIdx.x >> 2;
+  const int c = ti.ct * t.CT + chunk * V;
+  float q[9][V];
+#pragma unroll
+  for (int k = 0; k < 9; ++k)
+#pragma unroll
+    for (int i = 0; i < V; ++i) q[k][i] = 0.f;
+  if (c < t.C) {
+    const int tw2 = t.TW + 2;
+    for (int o = slot; o < t.TR * t.TW; o += 64) {
+      const int ry = o / t.TW, cx = o - ry * t.TW;
+      const int y = ti.band * t.TR + ry, x = ti.colt * t.TW + cx;
+      if (y >= t.H || x >= t.W) continue;
+      float g[V];
+      load_vec<T, V>(dd + ((ti.b * t.H + y) * t.W + x) * t.C + c, g);
+#pragma unroll
+      for (int ki = 0; ki < 3; ++ki)
+#pragma unroll
+        for (int kj = 0; kj < 3; ++kj) {
+          const float* src = tile + ((ry + ki) * tw2 + cx + kj) * t.PP + chunk * V;
+#pragma unroll
+          for (int i = 0; i < V; i += 4) {
+            const float4 a = *reinterpret_cast<const float4*>(src + i);
+            q[ki * 3 + kj][i] = fmaf(g[i], a.x, q[ki * 3 + kj][i]);
+            q[ki * 3 + kj][i + 1] = fmaf(g[i + 1], a.y, q[ki * 3 + kj][i + 1]);
+            q[ki * 3 + kj][i + 2] = fmaf(g[i + 2], a.z, q[ki * 3 + kj][i + 2]);
+            q[ki * 3 + kj][i + 3] = fmaf(g[i + 3], a.w, q[ki * 3 + kj][i + 3]);
+          }
+        }
+    }
+  }
+  chunk_reduce_store<9, V>(q, tile, part + ti.rid * 9 * t.C, t.C, t.C, ti.ct * t.CT);
+}
+
+// dw[c*9 + tap] = s[tap*C + c]
+__global__ void tapmajor_to_chan_kernel(const float* __restrict__ s, float* __restrict__ dw, int C) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 9 * C) return;
+  const int c = i / 9, tap = i - c * 9;
+  dw[i] = s[tap * C + c];
+}
+
+// ------------------------------------------------------------------ Squeeze-Excite
+// pooled[b, c] = mean over the image's pixels of act(d*sc + sh)   (grid = (channel tiles, image))
+template <typename T, int V>
+__global__ __launch_bounds__(256) void se_pool_kernel(const T* __restrict__ d, const float* __restrict__ sc,
+                                                      const float* __restrict__ sh, int act, float* __restrict__ pooled,
+                                                      int HW, int K) {
+  __shared__ float lds[4 * 1 * 4 * 8];
+  const int chunk = threadIdx.x & 3, slot = threadIdx.x >> 2;
+  const int c0 = (blockIdx.x * 4 + chunk) * V;
+  const long b = blockIdx.y;
+  float q[1][V];
+#pragma unroll
+  for (int i = 0; i < V; ++i) q[0][i] = 0.f;
+  if (c0 < K) {
+    float s[V], h[V];
+    load_vec<float, V>(sc + c0, s);
+    load_vec<float, V>(sh + c0, h);
+    for (int p = slot; p < HW; p += 64) {
+      float v[V];
+      load_vec<T, V>(d + (b * HW + p) * K + c0, v);
+#pragma unroll
+      for (int i = 0; i < V; ++i) q[0][i] += act_fwd(act, fmaf(v[i], s[i], h[i]));
+    }
+    const float inv = 1.f / (float)HW;
+#pragma unroll
+    for (int i = 0; i < V; ++i) q[0][i] *= inv;
+  }
+  chunk_reduce_store<1, V>(q, lds, pooled + b * K, K, K, blockIdx.x * 4 * V);
+}
+
+__global__ void sigmoid_kernel(const float* __restrict__ z, float* __restrict__ g, long n) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) g[i] = fast_sigmoid(z[i]);
+}
+
+// dz2 = dgate * g * (1 - g)
+__global__ void sigmoid_bwd_kernel(const float* __restrict__ dgate, const float* __restrict__ g, float* __restrict__ dz,
+                                   long n) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dz[i] = dgate[i] * g[i] * (1.f - g[i]);
+}
+
+// One pass over (dA3, d) per image: R[q][b][c] for
+//   q0 = sum dA3*a2 (-> dgate), q1 = sum dA3*s', q2 = sum s', q3 = sum dA3*s'*dh, q4 = sum s'*dh
+// with y2 = d*sc2+sh2, a2 = act(y2), s' = act'(y2), dh = (d-mean2)*invstd2.
+template <typename T, int V>
+__global__ __launch_bounds__(256) void se_bwd_reduce_kernel(const T* __restrict__ dA3, const T* __restrict__ d,
+                                                            const float* __restrict__ sc, const float* __restrict__ sh,
+                                                            const float* __restrict__ mean,
+                                                            const float* __restrict__ invstd, int act,
+                                                            float* __restrict__ R, int B, int HW, int K) {
+  __shared__ float lds[4 * 5 * 4 * 8];
+  const int chunk = threadIdx.x & 3, slot = threadIdx.x >> 2;
+  const int c0 = (blockIdx.x * 4 + chunk) * V;
+  const long b = blockIdx.y;
+  float q[5][V];
+#pragma unroll
+  for (int k = 0; k < 5; ++k)
+#pragma unroll
+    for (int i = 0; i < V; ++i) q[k][i] = 0.f;
+  if (c0 < K) {
+    float s[V], h[V], mu[V], is[V];
+    load_vec<float, V>(sc + c0, s);
+    load_vec<float, V>(sh + c0, h);
+    load_vec<float, V>(mean + c0, mu);
+    load_vec<float, V>(invstd + c0, is);
+    for (int p = slot; p < HW; p += 64) {
+      float ga[V], dv[V];
+      load_vec<T, V>(dA3 + (b * HW + p) * K + c0, ga);
+      load_vec<T, V>(d + (b * HW + p) * K + c0, dv);
+#pragma unroll
+      for (int i = 0; i < V; ++i) {
+        const float y = fmaf(dv[i], s[i], h[i]);
+        const float sg = fast_sigmoid(y);
+        float a, sp;
+        if (act == OGV_ACT_SILU) {
+          a = y * sg;
+          sp = sg * (1.0f + y * (1.0f - sg));
+        } else {
+          a = act_fwd(act, y);
+          sp = act_grad(act, y);
+        }
+        const float dh = (dv[i] - mu[i]) * is[i];
+        q[0][i] = fmaf(ga[i], a, q[0][i]);
+        q[1][i] = fmaf(ga[i], sp, q[1][i]);
+        q[2][i] += sp;
+        q[3][i] = fmaf(ga[i] * sp, dh, q[3][i]);
+        q[4][i] = fmaf(sp, dh, q[4][i]);
+      }
+    }
+  }
+  chunk_reduce_store<5, V>(q, lds, R + b * K, (long)B * K, K, blockIdx.x * 4 * V);
+}
+
+// BN2 reductions from the per-image sums: dy2 = (dA3*gate + dpool/HW) * s'
+//   sum dy2 = sum_b gate*R1 + dpool/HW*R2,  sum dy2*dh = sum_b gate*R3 + dpool/HW*R4
+// terms[b][0][c], terms[b][1][c] here; the sum over b is a column reduction (colreduce).
+__global__ void bn2_terms_kernel(const float* __restrict__ R, const float* __restrict__ gate,
+                                 const float* __restrict__ dpool, float* __restrict__ terms, int B, int HW, int K) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long BK = (long)B * K;
+  if (i >= BK) return;
+  const long b = i / K, c = i - b * K;
+  const float gg = gate[i], dp = dpool[i] * (1.f / (float)HW);
+  terms[b * 2 * K + c] = gg * R[1 * BK + i] + dp * R[2 * BK + i];
+  terms[b * 2 * K + K + c] = gg * R[3 * BK + i] + dp * R[4 * BK + i];
+}
+
+// dd = ca*(dy2 - cb - dh*cc), dy2 = (dA3*gate + dpool/HW) * act'(d*sc2+sh2)
+template <typename T, int V>
+__global__ __launch_bounds__(256) void bn2_apply_kernel(const T* __restrict__ dA3, const T* __restrict__ d,
+                                                        const float* __restrict__ sc, const float* __restrict__ sh,
+                                                        const float* __restrict__ mean, const float* __restrict__ invstd,
+                                                        const float* __restrict__ gate, const float* __restrict__ dpool,
+                                                        const float* __restrict__ coef, int act, T* __restrict__ out,
+                                                        long M, int HW, int K) {
+  const int nch = K / V;
+  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid >= M * nch) return;
+  const int c0 = (int)(tid % nch) * V;
+  const long m = tid / nch;
+  const long b = m / HW;
+  const float inv = 1.f / (float)HW;
+  float ga[V], dv[V], o[V], s[V], h[V], mu[V], is[V], gt[V], dp[V], ca[V], cb[V], cc[V];
+  load_vec<T, V>(dA3 + m * K + c0, ga);
+  load_vec<T, V>(d + m * K + c0, dv);
+  load_vec<float, V>(sc + c0, s);
+  load_vec<float, V>(sh + c0, h);
+  load_vec<float, V>(mean + c0, mu);
+  load_vec<float, V>(invstd + c0, is);
+  load_vec<float, V>(gate + b * K + c0, gt);
+  load_vec<float, V>(dpool + b * K + c0, dp);
+  load_vec<float, V>(coef + c0, ca);
+  load_vec<float, V>(coef + K + c0, cb);
+  load_vec<float, V>(coef + 2 * K + c0, cc);
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    const float y = fmaf(dv[i], s[i], h[i]);
+    const float dy2 = fmaf(ga[i], gt[i], dp[i] * inv) * act_grad(act, y);
+    const float dh = (dv[i] - mu[i]) * is[i];
+    o[i] = ca[i] * (dy2 - cb[i] - dh * cc[i]);
+  }
+  store_vec<T, V>(out + m * K + c0, o);
+}
+
+// generic BN backward reduction over rows: stat[slice] = [sum dy, sum dy*(x-mean)*invstd]
+template <typename T, int V>
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                            const float* __restrict__ mean,
+                                                            const float* __restrict__ invstd, float* __restrict__ stat,
+                                                            long M, int K, long rows_per_slice) {
+  __shared__ float lds[4 * 2 * 4 * 8];
+  const int chunk = threadIdx.x & 3, slot = threadIdx.x >> 2;
+  const int c0 = (blockIdx.x * 4 + chunk) * V;
+  const long r0 = (long)blockIdx.y * rows_per_slice;
+  const long r1 = r0 + rows_per_slice < M ? r0 + rows_per_slice : M;
+  float q[2][V];
+#pragma unroll
+  for (int i = 0; i < V; ++i) { q[0][i] = 0.f; q[1][i] = 0.f; }
+  if (c0 < K) {
+    float mu[V], is[V];
+    load_vec<float, V>(mean + c0, mu);
+    load_vec<float, V>(invstd + c0, is);
+    for (long r = r0 + slot; r < r1; r += 64) {
+      float g[V], xv[V];
+      load_vec<T, V>(dy + r * K + c0, g);
+      load_vec<T, V>(x + r * K + c0, xv);
+#pragma unroll
+      for (int i = 0; i < V; ++i) {
+        q[0][i] += g[i];
+        q[1][i] = fmaf(g[i], (xv[i] - mu[i]) * is[i], q[1][i]);
+      }
+    }
+  }
+  chunk_reduce_store<2, V>(q, lds, stat + (long)blockIdx.y * 2 * K, K, K, blockIdx.x * 4 * V);
+}
+
+// out = ca*(dy - cb - (x-mean)*invstd*cc)
+template <typename T, int V>
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                           const float* __restrict__ mean,
+                                                           const float* __restrict__ invstd,
+                                                           const float* __restrict__ coef, T* __restrict__ out, long M,
+                                                           int K) {
+  const int nch = K / V;
+  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid >= M * nch) return;
+  const int c0 = (int)(tid % nch) * V;
+  const long m = tid / nch;
+  float g[V], xv[V], o[V], mu[V], is[V], ca[V], cb[V], cc[V];
+  load_vec<T, V>(dy + m * K + c0, g);
+  load_vec<T, V>(x + m * K + c0, xv);
+  load_vec<float, V>(mean + c0, mu);
+  load_vec<float, V>(invstd + c0, is);
+  load_vec<float, V>(coef + c0, ca);
+  load_vec<float, V>(coef + K + c0, cb);
+  load_vec<float, V>(coef + 2 * K + c0, cc);
+#pragma unroll
+  for (int i = 0; i < V; ++i) o[i] = ca[i] * (g[i] - cb[i] - (xv[i] - mu[i]) * is[i] * cc[i]);
+  store_vec<T, V>(out + m * K + c0, o);
+}
+
+// out = res + p*sc + sh
+template <typename T, int V>
+__global__ __launch_bounds__(256) void affine_residual_kernel(const T* __restrict__ res, const T* __restrict__ p,
+                                                              const float* __restrict__ sc,
+                                                              const float* __restrict__ sh, T* __restrict__ out, long M,
+                                                              int K) {
+  const int nch = K / V;
+  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid >= M * nch) return;
+  const int c0 = (int)(tid % nch) * V;
+  const long m = tid / nch;
+  float a[V], b[V], s[V], h[V];
+  load_vec<T, V>(res + m * K + c0, a);
+  load_vec<T, V>(p + m * K + c0, b);
+  load_vec<float, V>(sc + c0, s);
+  load_vec<float, V>(sh + c0, h);
+#pragma unroll
+  for (int i = 0; i < V; ++i) a[i] += fmaf(b[i], s[i], h[i]);
+  store_vec<T, V>(out + m * K + c0, a);
+}
+
+// ------------------------------------------------------------------ orchestration
+struct Buf {
+  char* base;
+  size_t off = 0;
+  explicit Buf(void* b) : base((char*)b) {}
+  template <typename P>
+  P* take(size_t n) {
+    off = (off + 255) & ~(size_t)255;
+    P* r = reinterpret_cast<P*>(base ? base + off : nullptr);
+    off += n * sizeof(P);
+    return r;
+  }
+};
+
+// Saved-for-backward layout (lives in the caller's `saved` buffer).
+struct Saved {
+  void *e, *d, *p;                             // [M,mid], [M,mid], [M,C] activation dtype
+  float *mean1, *inv1, *sc1, *sh1;             // [mid]
+  float *mean2, *inv2, *sc2, *sh2;             // [mid]
+  float *mean3, *inv3, *sc3, *sh3;             // [C]
+  float *pooled, *z1, *z2, *gate;              // [B,mid], [B,se], [B,mid], [B,mid]
+};
+static Saved saved_layout(void* base, const ogv_mbconv_desc& s, size_t esz, size_t* total) {
+  Buf b(base);
+  const long M = (long)s.B * s.H * s.W;
+  Saved v;
+  v.e = b.take<char>(M * s.mid * esz);
+  v.d = b.take<char>(M * s.mid * esz);
+  v.p = b.take<char>(M * s.C * esz);
+  v.mean1 = b.take<float>(s.mid); v.inv1 = b.take<float>(s.mid); v.sc1 = b.take<float>(s.mid); v.sh1 = b.take<float>(s.mid);
+  v.mean2 = b.take<float>(s.mid); v.inv2 = b.take<float>(s.mid); v.sc2 = b.take<float>(s.mid); v.sh2 = b.take<float>(s.mid);
+  v.mean3 = b.take<float>(s.C); v.inv3 = b.take<float>(s.C); v.sc3 = b.take<float>(s.C); v.sh3 = b.take<float>(s.C);
+  v.pooled = b.take<float>((size_t)s.B * s.mid);
+  v.z1 = b.take<float>((size_t)s.B * s.se);
+  v.z2 = b.take<float>((size_t)s.B * s.mid);
+  v.gate = b.take<float>((size_t)s.B * s.mid);
+  if (total) *total = b.off + 256;
+  return v;
+}
+
+static long dw_slices(long P, const RowPlan& rp) {   // row slices for the global BN reductions
+  const long ct = (rp.nch + 3) / 4;
+  long S = (2048 + ct - 1) / ct;
+  const long maxS = (P + 511) / 512;                    // >= 8 rows per slot
+  if (S > maxS) S = maxS;
+  return S < 1 ? 1 : S;
+}
+
+struct FwdWs {
+  float *stat1, *stat2, *stat3, *sums, *tmp;
+  char* gemm;
+};
+static FwdWs fwd_ws_layout(void* base, const ogv_mbconv_desc& s, size_t* total) {
+  Buf b(base);
+  const long M = (long)s.B * s.H * s.W;
+  RowPlan rp = row_plan(s.mid);
+  const long S2 = dw_tile_plan(s.B, s.H, s.W, s.mid, 4).rows();
+  const long R1 = gemm_stat_rows((int)M);
+  FwdWs w;
+  w.stat1 = b.take<float>(R1 * 2 * s.mid);
+  w.stat2 = b.take<float>(S2 * 2 * s.mid);
+  w.stat3 = b.take<float>(R1 * 2 * s.C);
+  w.sums = b.take<float>(2 * (size_t)(s.mid > s.C ? s.mid : s.C));
+  long Rmax = R1 > S2 ? R1 : S2;
+  w.tmp = b.take<float>(colreduce_tmp_floats(Rmax, 2L * (s.mid > s.C ? s.mid : s.C)) + 16);
+  w.gemm = b.take<char>(64);
+  if (total) *total = b.off + 256;
+  return w;
+}
+
+struct BwdWs {
+  void *dp, *bufA, *bufB;
+  float *stat, *S, *coef, *R, *dgate, *dz2, *dh, *dz1, *dpool, *part9, *tmp, *sums9, *terms;
+  char* gemm;
+};
+static size_t max3(size_t a, size_t b, size_t c) { return a > b ? (a > c ? a : c) : (b > c ? b : c); }
+static BwdWs bwd_ws_layout(void* base, const ogv_mbconv_desc& s, size_t esz, size_t* total) {
+  Buf b(base);
+  const long M = (long)s.B * s.H * s.W;
+  RowPlan rp = row_plan(s.mid), rc = row_plan(s.C);
+  const long S2 = dw_tile_plan(s.B, s.H, s.W, s.mid, 4).rows(), S3 = dw_slices(M, rc);
+  const long K2 = s.mid > s.C ? s.mid : s.C;
+  BwdWs w;
+  w.dp = b.take<char>(M * s.C * esz);
+  w.bufA = b.take<char>(M * s.mid * esz);
+  w.bufB = b.take<char>(M * s.mid * esz);
+  const long Smax = S2 > S3 ? S2 : S3;
+  w.stat = b.take<float>(Smax * 2 * K2);
+  w.S = b.take<float>(2 * K2);
+  w.coef = b.take<float>(3 * K2);
+  w.R = b.take<float>((size_t)5 * s.B * s.mid);
+  w.dgate = b.take<float>((size_t)s.B * s.mid);
+  w.dz2 = b.take<float>((size_t)s.B * s.mid);
+  w.dh = b.take<float>((size_t)s.B * s.se);
+  w.dz1 = b.take<float>((size_t)s.B * s.se);
+  w.dpool = b.take<float>((size_t)s.B * s.mid);
+  w.part9 = b.take<float>(S2 * 9 * s.mid);
+  w.terms = b.take<float>((size_t)2 * s.B * s.mid);
+  w.tmp = b.take<float>(max3(max3(colreduce_tmp_floats(Smax, 2 * K2), colreduce_tmp_floats(S2, 9L * s.mid), 16),
+                             colreduce_tmp_floats(s.B, 2L * s.mid), 16));
+  w.sums9 = b.take<float>(9 * (size_t)s.mid);
+  const size_t g = max3(max3(dgrad_ws_bytes(s.C, s.mid), dgrad_ws_bytes(s.mid, s.C), wgrad_ws_bytes((int)M, s.C, s.mid)),
+                        max3(wgrad_ws_bytes((int)M, s.mid, s.C), wgrad_ws_bytes(s.B, s.mid, s.se),
+                             wgrad_ws_bytes(s.B, s.se, s.mid)),
+                        max3(dgrad_ws_bytes(s.mid, s.se), dgrad_ws_bytes(s.se, s.mid), 64));
+  w.gemm = b.take<char>(g);
+  if (total) *total = b.off + 256;
+  return w;
+}
+
+#define OGV_V_DISPATCH(V, FN, ...)      \
+  do {                                  \
+    if ((V) == 8) FN<8>(__VA_ARGS__);   \
+    else if ((V) == 4) FN<4>(__VA_ARGS__); \
+    else FN<1>(__VA_ARGS__);            \
+  } while (0)
+#define OGV_V84_DISPATCH(V, FN, ...)    \
+  do {                                  \
+    if ((V) == 8) FN<8>(__VA_ARGS__);   \
+    else FN<4>(__VA_ARGS__);            \
+  } while (0)
+
+template <typename T>
+struct Ops {
+  template <int V>
+  static void dw_fwd(const void* e, const float* w, const float* sc, const float* sh, int act, void* out, float* stat,
+                     const float* shift, const DwTile& t, hipStream_t st) {
+    const unsigned nb = (unsigned)(t.rows() * t.nct);
+    dw_fwd_tile_kernel<T, V><<<nb, 256, t.lds_bytes(), st>>>((const T*)e, w, sc, sh, act, (T*)out, stat, shift, t);
+  }
+  template <int V>
+  static void dw_dgrad(const void* dd, const float* w, const void* e, const float* sc, const float* sh,
+                       const float* mean, const float* inv, int act, void* out, float* stat, const DwTile& t,
+                       hipStream_t st) {
+    const unsigned nb = (unsigned)(t.rows() * t.nct);
+    dw_dgrad_tile_kernel<T, V><<<nb, 256, t.lds_bytes(), st>>>((const T*)dd, w, (const T*)e, sc, sh, mean, inv, act,
+                                                              (T*)out, stat, t);
+  }
+  template <int V>
+  static void dw_wgrad(const void* dd, const void* e, const float* sc, const float* sh, int act, float* part,
+                       const DwTile& t, hipStream_t st) {
+    const unsigned nb = (unsigned)(t.rows() * t.nct);
+    dw_wgrad_tile_kernel<T, V><<<nb, 256, t.lds_bytes(), st>>>((const T*)dd, (const T*)e, sc, sh, act, part, t);
+  }
+  template <int V>
+  static void pool(const void* d, const float* sc, const float* sh, int act, float* pooled, int B, int HW, int K,
+                   const RowPlan& rp, hipStream_t st) {
+    se_pool_kernel<T, V><<<dim3(cdiv(K, 4 * V), B), 256, 0, st>>>((const T*)d, sc, sh, act, pooled, HW, K);
+  }
+  template <int V>
+  static void se_reduce(const void* dA3, const void* d, const float* sc, const float* sh, const float* mean,
+                        const float* inv, int act, float* R, int B, int HW, int K, const RowPlan& rp, hipStream_t st) {
+    se_bwd_reduce_kernel<T, V><<<dim3(cdiv(K, 4 * V), B), 256, 0, st>>>((const T*)dA3, (const T*)d, sc, sh, mean, inv,
+                                                                        act, R, B, HW, K);
+  }
+  template <int V>
+  static void bn2_apply(const void* dA3, const void* d, const float* sc, const float* sh, const float* mean,
+                        const float* inv, const float* gate, const float* dpool, const float* coef, int act, void* out,
+                        long M, int HW, int K, hipStream_t st) {
+    bn2_apply_kernel<T, V><<<cdiv(M * (K / V), 256), 256, 0, st>>>((const T*)dA3, (const T*)d, sc, sh, mean, inv, gate,
+                                                                    dpool, coef, act, (T*)out, M, HW, K);
+  }
+  template <int V>
+  static void bn_reduce(const void* dy, const void* x, const float* mean, const float* inv, float* stat, long M, int K,
+                        const RowPlan& rp, long S, long per, hipStream_t st) {
+    bn_bwd_reduce_kernel<T, V><<<dim3(cdiv(K, 4 * V), S), 256, 0, st>>>((const T*)dy, (const T*)x, mean, inv, stat, M,
+                                                                        K, per);
+  }
+  template <int V>
+  static void bn_apply(const void* dy, const void* x, const float* mean, const float* inv, const float* coef, void* out,
+                       long M, int K, hipStream_t st) {
+    bn_bwd_apply_kernel<T, V><<<cdiv(M * (K / V), 256), 256, 0, st>>>((const T*)dy, (const T*)x, mean, inv, coef,
+                                                                       (T*)out, M, K);
+  }
+  template <int V>
+  static void affine_res(const void* res, const void* p, const float* sc, const float* sh, void* out, long M, int K,
+                         hipStream_t st) {
+    affine_residual_kernel<T, V><<<cdiv(M * (K / V), 256), 256, 0, st>>>((const T*)res, (const T*)p, sc, sh, (T*)out, M,
+                                                                          K);
+  }
+};
+
+template <typename T>
+static void mbconv_fwd_impl(const void* x, void* out, const Saved& sv, const FwdWs& w, const ogv_mbconv_desc& s,
+                            const ogv_mbconv_params& P, ogv_dtype dt, hipStream_t st) {
+  using O = Ops<T>;
+  const long M = (long)s.B * s.H * s.W;
+  const int HW = s.H * s.W;
+  const bool tr = s.train != 0;
+  RowPlan rp = row_plan(s.mid), rc = row_plan(s.C);
+  // 1) expand GEMM (+ BN1 stats)
+  {
+    Epi e;
+    if (tr) { e.stat = w.stat1; e.stat_shift = P.bn1_rm; }
+    gemm_fwd_launch(dt, x, s.C, Pro(), P.w_expand, s.C, sv.e, s.mid, (int)M, s.mid, s.C, s.C, s.C, e, st);
+    if (tr) colreduce(w.stat1, w.sums, gemm_stat_rows((int)M), 2L * s.mid, 2L * s.mid, w.tmp, st);
+    bn_finalize_kernel<<<cdiv(s.mid, 256), 256, 0, st>>>(w.sums, s.mid, (double)M, P.bn1_w, P.bn1_b, s.bn_eps,
+                                                         s.bn_momentum, P.bn1_rm, P.bn1_rv, sv.mean1, sv.inv1, sv.sc1,
+                                                         sv.sh1, s.train);
+  }
+  // 2) depthwise conv on act(BN1(e)) (+ BN2 stats)
+  {
+    const DwTile t = dw_tile_plan(s.B, s.H, s.W, s.mid, 4);
+    OGV_V84_DISPATCH(4, O::template dw_fwd, sv.e, P.w_dw, sv.sc1, sv.sh1, s.act, sv.d, tr ? w.stat2 : nullptr,
+                     tr ? P.bn2_rm : nullptr, t, st);
+    if (tr) colreduce(w.stat2, w.sums, t.rows(), 2L * s.mid, 2L * s.mid, w.tmp, st);
+    bn_finalize_kernel<<<cdiv(s.mid, 256), 256, 0, st>>>(w.sums, s.mid, (double)M, P.bn2_w, P.bn2_b, s.bn_eps,
+                                                         s.bn_momentum, P.bn2_rm, P.bn2_rv, sv.mean2, sv.inv2, sv.sc2,
+                                                         sv.sh2, s.train);
+  }
+  // 3) Squeeze-Excite gate (B rows)
+  {
+    OGV_V_DISPATCH(rp.V, O::template pool, sv.d, sv.sc2, sv.sh2, s.act, sv.pooled, s.B, HW, s.mid, rp, st);
+    Epi e1;
+    e1.bias = P.se_b1;
+    gemm_fwd_launch(OGV_F32, sv.pooled, s.mid, Pro(), P.se_w1, s.mid, sv.z1, s.se, s.B, s.se, s.mid, s.mid, s.mid, e1,
+                    st);
+    Pro p2;
+    p2.act = s.act;
+    Epi e2;
+    e2.bias = P.se_b2;
+    gemm_fwd_launch(OGV_F32, sv.z1, s.se, p2, P.se_w2, s.se, sv.z2, s.mid, s.B, s.mid, s.se, s.se, s.se, e2, st);
+    sigmoid_kernel<<<cdiv((long)s.B * s.mid, 256), 256, 0, st>>>(sv.z2, sv.gate, (long)s.B * s.mid);
+  }
+  // 4) project GEMM on act(BN2(d)) * gate (+ BN3 stats), then out = x + BN3(p)
+  {
+    Pro pr;
+    pr.act = s.act;
+    pr.sc = sv.sc2;
+    pr.sh = sv.sh2;
+    pr.gate = sv.gate;
+    pr.rps = HW;
+    pr.gld = s.mid;
+    Epi e;
+    if (tr) { e.stat = w.stat3; e.stat_shift = P.bn3_rm; }
+    gemm_fwd_launch(dt, sv.d, s.mid, pr, P.w_proj, s.mid, sv.p, s.C, (int)M, s.C, s.mid, s.mid, s.mid, e, st);
+    if (tr) colreduce(w.stat3, w.sums, gemm_stat_rows((int)M), 2L * s.C, 2L * s.C, w.tmp, st);
+    bn_finalize_kernel<<<cdiv(s.C, 256), 256, 0, st>>>(w.sums, s.C, (double)M, P.bn3_w, P.bn3_b, s.bn_eps,
+                                                       s.bn_momentum, P.bn3_rm, P.bn3_rv, sv.mean3, sv.inv3, sv.sc3,
+                                                       sv.sh3, s.train);
+    OGV_V_DISPATCH(rc.V, O::template affine_res, x, sv.p, sv.sc3, sv.sh3, out, M, s.C, st);
+  }
+}
+
+template <typename T>
+static void mbconv_bwd_impl(const void* dout, const void* x, const Saved& sv, void* dx, const ogv_mbconv_grads& G,
+                            const BwdWs& w, const ogv_mbconv_desc& s, const ogv_mbconv_params& P, ogv_dtype dt,
+                            hipStream_t st) {
+  using O = Ops<T>;
+  const long M = (long)s.B * s.H * s.W;
+  const int HW = s.H * s.W;
+  RowPlan rp = row_plan(s.mid), rc = row_plan(s.C);
+  // B1) BN3 backward: dp = ca*(dout - cb - phat*cc)
+  {
+    const long S = dw_slices(M, rc), per = (M + S - 1) / S;
+    OGV_V_DISPATCH(rc.V, O::template bn_reduce, dout, sv.p, sv.mean3, sv.inv3, w.stat, M, s.C, rc, S, per, st);
+    colreduce(w.stat, w.S, S, 2L * s.C, 2L * s.C, w.tmp, st);
+    bn_coeffs_kernel<<<cdiv(s.C, 256), 256, 0, st>>>(w.S, s.C, (float)M, P.bn3_w, sv.inv3, G.bn3_w, G.bn3_b, w.coef,
+                                                     s.train);
+    OGV_V_DISPATCH(rc.V, O::template bn_apply, dout, sv.p, sv.mean3, sv.inv3, w.coef, w.dp, M, s.C, st);
+  }
+  // B2) project: dA3 = dp . Wp ; dWp = dp^T . (act(BN2(d)) * gate)
+  {
+    gemm_dgrad_launch(dt, w.dp, s.C, P.w_proj, nullptr, 0, 0, nullptr, 1, nullptr, w.bufA, s.mid, (int)M, s.C, s.mid,
+                      w.gemm, st);
+    Pro pr;
+    pr.act = s.act;
+    pr.sc = sv.sc2;
+    pr.sh = sv.sh2;
+    pr.gate = sv.gate;
+    pr.rps = HW;
+    pr.gld = s.mid;
+    gemm_wgrad_launch(dt, w.dp, s.C, sv.d, s.mid, pr, nullptr, 1, G.w_proj, nullptr, (int)M, s.C, s.mid, w.gemm, st);
+  }
+  // B3) one pass over (dA3, d): SE gate grads + BN2 partial sums per image
+  OGV_V_DISPATCH(rp.V, O::template se_reduce, w.bufA, sv.d, sv.sc2, sv.sh2, sv.mean2, sv.inv2, s.act, w.R, s.B, HW,
+                 s.mid, rp, st);
+  // B4) SE MLP backward (fp32, B rows): dgate = R0 -> dz2 -> (W2, b2) -> dz1 (act') -> (W1, b1) -> dpooled
+  {
+    const long n2 = (long)s.B * s.mid;
+    sigmoid_bwd_kernel<<<cdiv(n2, 256), 256, 0, st>>>(w.R, sv.gate, w.dz2, n2);
+    Pro p2;
+    p2.act = s.act;
+    gemm_wgrad_launch(OGV_F32, w.dz2, s.mid, sv.z1, s.se, p2, nullptr, 1, G.se_w2, G.se_b2, s.B, s.mid, s.se, w.gemm, st);
+    gemm_dgrad_launch(OGV_F32, w.dz2, s.mid, P.se_w2, sv.z1, s.se, s.act, nullptr, 1, nullptr, w.dz1, s.se, s.B, s.mid,
+                      s.se, w.gemm, st);
+    gemm_wgrad_launch(OGV_F32, w.dz1, s.se, sv.pooled, s.mid, Pro(), nullptr, 1, G.se_w1, G.se_b1, s.B, s.se, s.mid,
+                      w.gemm, st);
+    gemm_dgrad_launch(OGV_F32, w.dz1, s.se, P.se_w1, nullptr, 0, 0, nullptr, 1, nullptr, w.dpool, s.mid, s.B, s.se,
+                      s.mid, w.gemm, st);
+  }
+  // B5) BN2 backward: dd = ca*(dy2 - cb - dhat*cc)  -> bufB
+  {
+    bn2_terms_kernel<<<cdiv((long)s.B * s.mid, 256), 256, 0, st>>>(w.R, sv.gate, w.dpool, w.terms, s.B, HW, s.mid);
+    colreduce(w.terms, w.S, s.B, 2L * s.mid, 2L * s.mid, w.tmp, st);
+    bn_coeffs_kernel<<<cdiv(s.mid, 256), 256, 0, st>>>(w.S, s.mid, (float)M, P.bn2_w, sv.inv2, G.bn2_w, G.bn2_b,
+                                                       w.coef, s.train);
+    OGV_V_DISPATCH(rp.V, O::template bn2_apply, w.bufA, sv.d, sv.sc2, sv.sh2, sv.mean2, sv.inv2, sv.gate, w.dpool,
+                   w.coef, s.act, w.bufB, M, HW, s.mid, st);
+  }
+  // B6) depthwise backward: dy1 = dgrad(dd) * act'(BN1(e)) -> bufA (+ BN1 sums); dWdw from (dd, act(BN1(e)))
+  {
+    const DwTile t = dw_tile_plan(s.B, s.H, s.W, s.mid, 4);
+    OGV_V84_DISPATCH(4, O::template dw_dgrad, w.bufB, P.w_dw, sv.e, sv.sc1, sv.sh1, sv.mean1, sv.inv1, s.act,
+                     w.bufA, w.stat, t, st);
+    colreduce(w.stat, w.S, t.rows(), 2L * s.mid, 2L * s.mid, w.tmp, st);
+    OGV_V84_DISPATCH(4, O::template dw_wgrad, w.bufB, sv.e, sv.sc1, sv.sh1, s.act, w.part9, t, st);
+    colreduce(w.part9, w.sums9, t.rows(), 9L * s.mid, 9L * s.mid, w.tmp, st);
+    tapmajor_to_chan_kernel<<<cdiv(9 * s.mid, 256), 256, 0, st>>>(w.sums9, G.w_dw, s.mid);
+  }
+  // B7) BN1 backward: de = ca*(dy1 - cb - ehat*cc) -> bufB
+  bn_coeffs_kernel<<<cdiv(s.mid, 256), 256, 0, st>>>(w.S, s.mid, (float)M, P.bn1_w, sv.inv1, G.bn1_w, G.bn1_b, w.coef,
+                                                     s.train);
+  OGV_V_DISPATCH(rp.V, O::template bn_apply, w.bufA, sv.e, sv.mean1, sv.inv1, w.coef, w.bufB, M, s.mid, st);
+  // B8) expand: dx = de . We + dout (residual) ; dWe = de^T . x
+  gemm_dgrad_launch(dt, w.bufB, s.mid, P.w_expand, nullptr, 0, 0, nullptr, 1, dout, dx, s.C, (int)M, s.mid, s.C,
+                    w.gemm, st);
+  gemm_wgrad_launch(dt, w.bufB, s.mid, x, s.C, Pro(), nullptr, 1, G.w_expand, nullptr, (int)M, s.mid, s.C, w.gemm, st);
+}
+
+static int mb_check(const ogv_mbconv_desc* s, ogv_dtype dt, const char* who) {
+  OGV_REQUIRE(s, "%s: null desc", who);
+  OGV_REQUIRE(s->B > 0 && s->H > 0 && s->W > 0 && s->C > 0 && s->mid > 0 && s->se > 0, "%s: bad shape", who);
+  OGV_REQUIRE(s->C % 4 == 0 && s->mid % 4 == 0, "%s: channels must be multiples of 4 (C=%d, mid=%d)", who, s->C,
+              s->mid);
+  OGV_REQUIRE(dt == OGV_F32 || dt == OGV_BF16, "%s: bad dtype", who);
+  OGV_REQUIRE(s->act >= OGV_ACT_NONE && s->act <= OGV_ACT_RELU, "%s: bad activation", who);
+  return OGV_OK;
+}
+
+}  // namespace ogv
+
+using namespace ogv;
+
+extern "C" size_t ogv_mbconv_saved_bytes(const ogv_mbconv_desc* s, ogv_dtype dt) {
+  if (!s) return 0;
+  size_t t = 0;
+  saved_layout(nullptr, *s, dt == OGV_BF16 ? 2 : 4, &t);
+  return t;
+}
+
+extern "C" size_t ogv_mbconv_ws_bytes(const ogv_mbconv_desc* s, ogv_dtype dt) {
+  if (!s) return 0;
+  size_t a = 0, b = 0;
+  fwd_ws_layout(nullptr, *s, &a);
+  bwd_ws_layout(nullptr, *s, dt == OGV_BF16 ? 2 : 4, &b);
+  return a > b ? a : b;
+}
+
+extern "C" int ogv_mbconv_fwd(const void* x, void* out, void* saved, void* ws, const ogv_mbconv_desc* s,
+                              const ogv_mbconv_params* P, ogv_dtype dt, void* stream) {
+  int rc = mb_check(s, dt, "ogv_mbconv_fwd");
+  if (rc) return rc;
+  OGV_REQUIRE(x && out && saved && ws && P, "ogv_mbconv_fwd: null pointer");
+  OGV_REQUIRE(P->w_expand && P->w_dw && P->se_w1 && P->se_b1 && P->se_w2 && P->se_b2 && P->w_proj,
+              "ogv_mbconv_fwd: missing weight");
+  OGV_REQUIRE(P->bn1_rm && P->bn1_rv && P->bn2_rm && P->bn2_rv && P->bn3_rm && P->bn3_rv,
+              "ogv_mbconv_fwd: missing BatchNorm running statistics");
+  Saved sv = saved_layout(saved, *s, dt == OGV_BF16 ? 2 : 4, nullptr);
+  FwdWs w = fwd_ws_layout(ws, *s, nullptr);
+  if (dt == OGV_BF16) mbconv_fwd_impl<bf16>(x, out, sv, w, *s, *P, dt, as_stream(stream));
+  else mbconv_fwd_impl<float>(x, out, sv, w, *s, *P, dt, as_stream(stream));
+  return check_launch("ogv_mbconv_fwd");
+}
+
+extern "C" int ogv_mbconv_bwd(const void* dout, const void* x, const void* saved, void* dx,
+                              const ogv_mbconv_grads* G, void* ws, const ogv_mbconv_desc* s,
+                              const ogv_mbconv_params* P, ogv_dtype dt, void* stream) {
+  int rc = mb_check(s, dt, "ogv_mbconv_bwd");
+  if (rc) return rc;
+  OGV_REQUIRE(dout && x && saved && dx && G && ws && P, "ogv_mbconv_bwd: null pointer");
+  OGV_REQUIRE(G->w_expand && G->bn1_w && G->bn1_b && G->w_dw && G->bn2_w && G->bn2_b && G->se_w1 && G->se_b1 &&
+                  G->se_w2 && G->se_b2 && G->w_proj && G->bn3_w && G->bn3_b,
+              "ogv_mbconv_bwd: every gradient output must be given");
+  Saved sv = saved_layout(const_cast<void*>(saved), *s, dt == OGV_BF16 ? 2 : 4, nullptr);
+  BwdWs w = bwd_ws_layout(ws, *s, dt == OGV_BF16 ? 2 : 4, nullptr);
+  if (dt == OGV_BF16) mbconv_bwd_impl<bf16>(dout, x, sv, dx, *G, w, *s, *P, dt, as_stream(stream));
+  else mbconv_bwd_impl<float>(dout, x, sv, dx, *G, w, *s, *P, dt, as_stream(stream));
+  return check_launch("ogv_mbconv_bwd");
+}

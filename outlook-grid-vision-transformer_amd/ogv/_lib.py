@@ -20,6 +20,29 @@ _i = ctypes.c_int
 _f = ctypes.c_float
 _sz = ctypes.c_size_t
 
+class MBConvDesc(ctypes.Structure):
+    _fields_ = [("B", _i), ("H", _i), ("W", _i), ("C", _i), ("mid", _i), ("se", _i), ("train", _i),
+                ("bn_eps", _f), ("bn_momentum", _f), ("act", _i)]
+
+
+MBCONV_PARAM_FIELDS = ["w_expand", "bn1_w", "bn1_b", "bn1_rm", "bn1_rv", "w_dw", "bn2_w", "bn2_b", "bn2_rm", "bn2_rv",
+                       "se_w1", "se_b1", "se_w2", "se_b2", "w_proj", "bn3_w", "bn3_b", "bn3_rm", "bn3_rv"]
+MBCONV_GRAD_FIELDS = ["w_expand", "bn1_w", "bn1_b", "w_dw", "bn2_w", "bn2_b", "se_w1", "se_b1", "se_w2", "se_b2",
+                      "w_proj", "bn3_w", "bn3_b"]
+
+
+class MBConvParams(ctypes.Structure):
+    _fields_ = [(n, _p) for n in MBCONV_PARAM_FIELDS]
+
+
+class MBConvGrads(ctypes.Structure):
+    _fields_ = [(n, _p) for n in MBCONV_GRAD_FIELDS]
+
+
+_PD = ctypes.POINTER(MBConvDesc)
+_PP = ctypes.POINTER(MBConvParams)
+_PG = ctypes.POINTER(MBConvGrads)
+
 # name -> (restype, argtypes); must match include/ogv.h exactly
 SIGNATURES = {
     "ogv_version": (ctypes.c_char_p, []),
@@ -40,6 +63,10 @@ SIGNATURES = {
     "ogv_dwconv3x3_fwd": (_i, [_p, _p, _p, _p, _i, _i, _i, _i, _i, _p, _i, _p]),
     "ogv_dwconv_bwd_ws_bytes": (_sz, [_i, _i, _i, _i, _i]),
     "ogv_dwconv3x3_bwd": (_i, [_p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p, _i, _p]),
+    "ogv_mbconv_saved_bytes": (_sz, [_PD, _i]),
+    "ogv_mbconv_ws_bytes": (_sz, [_PD, _i]),
+    "ogv_mbconv_fwd": (_i, [_p, _p, _p, _p, _PD, _PP, _i, _p]),
+    "ogv_mbconv_bwd": (_i, [_p, _p, _p, _p, _PG, _p, _PD, _PP, _i, _p]),
     "ogv_cast": (_i, [_p, _i, _p, _i, _sz, _p]),
 }
 

@@ -367,3 +367,55 @@ def dwconv3x3_nchw(x, weight, bias=None, stride=1):
     x2d = _rows_contig(nchw_to_rows(x))
     y = _DwConv3x3.apply(x2d, f32(weight).contiguous(), f32(bias), B, H, W, int(stride))
     return rows_to_nchw(y, B, (H - 1) // stride + 1, (W - 1) // stride + 1)
+
+
+# ------------------------------------------------------------------------------------------------
+# Fused MBConv (expand+BN1+act -> dw3x3+BN2+act -> SE -> project+BN3 -> +x)
+# ------------------------------------------------------------------------------------------------
+class _MBConv(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x2d, geom, buffers, *params):
+        lib = _lib.load()
+        desc = _lib.MBConvDesc(*geom)
+        w = dict(zip(_lib.MBCONV_GRAD_FIELDS, params))
+        w.update(buffers)
+        P = _lib.MBConvParams(*[_vp(w[n].data_ptr()) for n in _lib.MBCONV_PARAM_FIELDS])
+        dt = _dt(x2d)
+        saved = torch.empty(lib.ogv_mbconv_saved_bytes(ctypes.byref(desc), dt), dtype=torch.uint8, device=x2d.device)
+        ws = _ws(lib.ogv_mbconv_ws_bytes(ctypes.byref(desc), dt), x2d.device)
+        out = torch.empty_like(x2d)
+        check(lib.ogv_mbconv_fwd(_ptr(x2d), _ptr(out), _ptr(saved), _ptr(ws), ctypes.byref(desc), ctypes.byref(P), dt,
+                                 _stream()), "ogv_mbconv_fwd")
+        ctx.save_for_backward(x2d, saved, *params)
+        ctx.geom, ctx.buffers = geom, buffers
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        lib = _lib.load()
+        x2d, saved, *params = ctx.saved_tensors
+        desc = _lib.MBConvDesc(*ctx.geom)
+        w = dict(zip(_lib.MBCONV_GRAD_FIELDS, params))
+        w.update(ctx.buffers)
+        P = _lib.MBConvParams(*[_vp(w[n].data_ptr()) for n in _lib.MBCONV_PARAM_FIELDS])
+        grads = [torch.empty_like(t) for t in params]
+        G = _lib.MBConvGrads(*[_vp(g.data_ptr()) for g in grads])
+        dt = _dt(x2d)
+        dout = dout.to(x2d.dtype).contiguous()
+        dx = torch.empty_like(x2d)
+        ws = _ws(lib.ogv_mbconv_ws_bytes(ctypes.byref(desc), dt), x2d.device)
+        check(lib.ogv_mbconv_bwd(_ptr(dout), _ptr(x2d), _ptr(saved), _ptr(dx), ctypes.byref(G), _ptr(ws),
+                                 ctypes.byref(desc), ctypes.byref(P), dt, _stream()), "ogv_mbconv_bwd")
+        return (dx, None, None, *grads)
+
+
+def mbconv_fused(x, B, H, W, mid, se, train, eps, momentum, act, params, buffers):
+    """x: NCHW (channels_last); params: 13 fp32 tensors in MBCONV_GRAD_FIELDS order;
+    buffers: {'bn1_rm', 'bn1_rv', ...} running statistics (updated in place when train)."""
+    require_device(x, *params, what="ogv.mbconv")
+    C = x.shape[1]
+    x2d = _rows_contig(nchw_to_rows(x))
+    geom = (int(B), int(H), int(W), int(C), int(mid), int(se), int(bool(train)), float(eps), float(momentum),
+            ACT[act])
+    y = _MBConv.apply(x2d, geom, buffers, *[f32(t).contiguous() for t in params])
+    return rows_to_nchw(y, B, H, W)

@@ -4,10 +4,12 @@
   MBConvConfig   :32-38
   MBConv         :44-98  expand 1x1 (+BN+act) -> dw3x3 (+BN+act) -> SE -> project 1x1 (+BN) (+x)
 
-Round-1 status: the two 1x1 convolutions (expand / project: the GEMM-shaped >90% of the FLOPs)
-run on the ogv MFMA GEMM and the depthwise 3x3 on the ogv NHWC depthwise kernels; BatchNorm and
-the SE gate still run on PyTorch-ROCm ops over channels_last tensors.  Fusing BN/SiLU/SE into the
-kernels is SURVEY.md §8(f) rank 1 ("next").
+The OutGridBlock configuration (BN, expand, SE, stride 1, residual) runs as ONE fused HIP
+forward and ONE hand-scheduled HIP backward (ogv_mbconv_fwd/bwd): BatchNorm statistics in the
+GEMM / depthwise epilogues, BN-apply + activation (+ SE gate) in the consumers' prologues, the
+SE and BN2 backward reductions in a single pass.  Other configurations (no BN, stride 2, active
+DropPath, ...) run the same modules unfused (1x1 GEMMs and depthwise conv on the ogv kernels,
+BN/SE on PyTorch-ROCm ops).
 """
 from typing import Literal
 from dataclasses import dataclass
@@ -19,7 +21,7 @@ from src.model.Outlook_Block import *  # noqa: F401,F403
 from src.model.Outlook_Block import DropPath
 from src.model.outlook_attention import make_activation
 from ogv import functional as OF
-from ogv.layers import Conv1x1, DepthwiseConv3x3
+from ogv.layers import Conv1x1, DepthwiseConv3x3, act_name
 
 
 class SqueezeExcite(nn.Module):
@@ -78,9 +80,44 @@ class MBConv(nn.Module):
         self.use_res = stride == 1 and in_ch == out_ch
         self.drop_path = DropPath(cfg.drop_path) if (cfg.drop_path and cfg.drop_path > 0) else nn.Identity()
 
+    def _fusable(self):
+        """The fused HIP path covers the OutGridBlock configuration: BN everywhere, a real expand,
+        SE, stride 1, residual, no active DropPath, one BN eps/momentum."""
+        if getattr(self, "ogv_unfused", False):
+            return False
+        if not (isinstance(self.expand, nn.Sequential) and isinstance(self.se, SqueezeExcite)):
+            return False
+        if self.stride != 1 or not self.use_res:
+            return False
+        bns = [self.expand[1], self.depthwise[1], self.project[1]]
+        if not all(isinstance(b, nn.BatchNorm2d) and b.affine and b.track_running_stats and b.momentum is not None
+                   for b in bns):
+            return False
+        if len({(b.eps, b.momentum) for b in bns}) != 1 or len({b.training for b in bns}) != 1:
+            return False
+        acts = {act_name(self.expand[2]), act_name(self.depthwise[2]), act_name(self.se.act)}
+        if len(acts) != 1 or None in acts:
+            return False
+        dp = self.drop_path
+        return not (isinstance(dp, DropPath) and dp.training and dp.drop_prob > 0)
+
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         dt = OF.compute_dtype(x)
         x = x.to(dt)
+        if x.is_cuda and self._fusable():
+            B, C, H, W = x.shape
+            e, bn1, dw, bn2, pj, bn3 = self.expand[0], self.expand[1], self.depthwise[0], self.depthwise[1], \
+                self.project[0], self.project[1]
+            params = [e.weight, bn1.weight, bn1.bias, dw.weight, bn2.weight, bn2.bias, self.se.fc1.weight,
+                      self.se.fc1.bias, self.se.fc2.weight, self.se.fc2.bias, pj.weight, bn3.weight, bn3.bias]
+            buffers = {"bn1_rm": bn1.running_mean, "bn1_rv": bn1.running_var, "bn2_rm": bn2.running_mean,
+                       "bn2_rv": bn2.running_var, "bn3_rm": bn3.running_mean, "bn3_rv": bn3.running_var}
+            train = bn1.training
+            if train:
+                for b in (bn1, bn2, bn3):
+                    b.num_batches_tracked.add_(1)
+            return OF.mbconv_fused(x, B, H, W, e.out_channels, self.se.fc1.out_channels, train, bn1.eps,
+                                   bn1.momentum, act_name(self.expand[2]), params, buffers)
         # the stock-op parts (BN, depthwise, SE) follow the activation dtype even outside autocast
         with torch.autocast("cuda", dtype=torch.bfloat16, enabled=(dt == torch.bfloat16 and x.is_cuda)):
             h = self.project(self.se(self.depthwise(self.expand(x))))

@@ -393,3 +393,39 @@ def test_dwconv_vs_fp64(case, dtype):
     assert fx.maxrel(wd.grad, wr.grad) <= (1e-4 if dtype == torch.float32 else 1e-2)
     if has_b:
         assert fx.maxrel(bd.grad, br.grad) <= (1e-4 if dtype == torch.float32 else 1e-2)
+
+
+@pytest.mark.parametrize("C,H,B", [(48, 32, 4), (96, 16, 3), (192, 8, 2), (256, 4, 5), (20, 6, 2)])
+@pytest.mark.parametrize("train", [True, False])
+def test_mbconv_fused_vs_unfused(C, H, B, train):
+    """The fused ogv_mbconv_{fwd,bwd} path against the same module run unfused (1x1 GEMMs and the
+    depthwise conv on ogv kernels, BN/SE on torch), fp32: outputs, dx, every grad, running stats."""
+    from src.model.mbc_conv import MBConv, MBConvConfig
+    torch.manual_seed(C + H)
+    ref = MBConv(C, C, 1, MBConvConfig()).to(DEV)
+    with torch.no_grad():
+        for b in ref.modules():
+            if isinstance(b, torch.nn.BatchNorm2d):
+                b.running_mean.normal_(0, 0.2)
+                b.running_var.uniform_(0.5, 1.5)
+                b.weight.normal_(1, 0.1)
+                b.bias.normal_(0, 0.1)
+    fused = MBConv(C, C, 1, MBConvConfig()).to(DEV)
+    fused.load_state_dict(ref.state_dict())
+    ref.ogv_unfused = True
+    ref.train(train)
+    fused.train(train)
+    x = torch.randn(B, C, H, H, device=DEV).contiguous(memory_format=torch.channels_last)
+    dy = torch.randn_like(x)
+    xr, xf = x.clone().requires_grad_(), x.clone().requires_grad_()
+    yr, yf = ref(xr), fused(xf)
+    yr.backward(dy)
+    yf.backward(dy)
+    assert fx.maxabs(yf, yr) <= 1e-3 * max(1, yr.abs().max().item())
+    assert fx.maxabs(xf.grad, xr.grad) <= 2e-3 * max(1, xr.grad.abs().max().item())
+    pr, pf = dict(ref.named_parameters()), dict(fused.named_parameters())
+    for k in pr:
+        assert fx.maxabs(pf[k].grad, pr[k].grad) <= 2e-3 * max(1, pr[k].grad.abs().max().item()), k
+    br, bf = dict(ref.named_buffers()), dict(fused.named_buffers())
+    for k in br:
+        assert fx.maxabs(bf[k].float(), br[k].float()) <= 1e-4 * max(1, br[k].float().abs().max().item()), k

@@ -31,7 +31,9 @@ int check_launch(const char* what);
 
 // deterministic "sum the rows of an fp32 slab" (ogv_dwconv.hip)
 size_t colreduce_tmp_floats(long R, long n);
-void colreduce(const float* src, float* dst, long R, long n, long ld, float* tmp, hipStream_t s);
+// dst[j] = sum_r src[r*ld + j] for j < n; with dst2, columns j >= n1 go to dst2[j - n1] instead.
+void colreduce(const float* src, float* dst, long R, long n, long ld, float* tmp, hipStream_t s,
+               float* dst2 = nullptr, long n1 = 0);
 
 static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 static inline unsigned cdiv(long a, long b) { return (unsigned)((a + b - 1) / b); }
@@ -93,9 +95,28 @@ __device__ __forceinline__ void store_vec(T* __restrict__ p, const float* in) {
 // logistic sigmoid with the hardware reciprocal (v_rcp_f32, 1 ulp) instead of an IEEE division
 __device__ __forceinline__ float fast_sigmoid(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
 
+// Phi(x) = 0.5 (1 + erf(x / sqrt 2)) for the exact (erf) GELU of nn.GELU().  erf from
+// Abramowitz & Stegun 7.1.26 (|abs err| <= 1.5e-7, i.e. fp32-level): branch-free, one v_rcp and
+// one v_exp, where the library erff evaluates two divergent polynomial branches.  Also returns
+// e = exp(-x^2 / 2), which the derivative's pdf term reuses.
+__device__ __forceinline__ float gelu_cdf(float x, float& e) {
+  const float u = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, u, 1.0f));
+  float p = fmaf(t, 1.061405429f, -1.453152027f);
+  p = fmaf(t, p, 1.421413741f);
+  p = fmaf(t, p, -0.284496736f);
+  p = fmaf(t, p, 0.254829592f);
+  e = __expf(-u * u);
+  const float h = 0.5f * (p * t) * e;  // 0.5 * erfc(u)
+  return x >= 0.f ? 1.0f - h : h;
+}
+
 __device__ __forceinline__ float act_fwd(int act, float x) {
   switch (act) {
-    case OGV_ACT_GELU: return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+    case OGV_ACT_GELU: {
+      float e;
+      return x * gelu_cdf(x, e);
+    }
     case OGV_ACT_SILU: return x * fast_sigmoid(x);
     case OGV_ACT_RELU: return x > 0.f ? x : 0.f;
     default: return x;
@@ -105,9 +126,9 @@ __device__ __forceinline__ float act_fwd(int act, float x) {
 __device__ __forceinline__ float act_grad(int act, float x) {
   switch (act) {
     case OGV_ACT_GELU: {
-      const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
-      const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
-      return cdf + x * pdf;
+      float e;
+      const float cdf = gelu_cdf(x, e);
+      return fmaf(x * 0.39894228040143268f, e, cdf);
     }
     case OGV_ACT_SILU: {
       const float s = fast_sigmoid(x);

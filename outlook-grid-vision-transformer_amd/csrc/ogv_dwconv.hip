@@ -15,7 +15,8 @@ namespace ogv {
 // ------------------------------------------------------------------ column reducer
 // dst[j] (+)= sum_r src[r*ld + j], j < n.  Block = 64 columns x 4 row lanes; grid.y splits rows.
 __global__ __launch_bounds__(256) void colreduce_kernel(const float* __restrict__ src, float* __restrict__ dst, long R,
-                                                        long n, long ld, long rows_per_chunk) {
+                                                        long n, long ld, long rows_per_chunk, float* __restrict__ dst2,
+                                                        long n1) {
   __shared__ float red[4][64];
   const int cx = threadIdx.x & 63, ry = threadIdx.x >> 6;
   const long j = (long)blockIdx.x * 64 + cx;
@@ -35,7 +36,8 @@ __global__ __launch_bounds__(256) void colreduce_kernel(const float* __restrict_
   __syncthreads();
   if (ry == 0 && j < n) {
     const float s = (red[0][cx] + red[1][cx]) + (red[2][cx] + red[3][cx]);
-    dst[(long)blockIdx.y * n + j] = s;
+    if (dst2 && j >= n1) dst2[j - n1] = s;  // single-pass split destination (gridDim.y == 1)
+    else dst[(long)blockIdx.y * n + j] = s;
   }
 }
 
@@ -47,18 +49,20 @@ size_t colreduce_tmp_floats(long R, long n) {
   return (size_t)(chunks < 64 ? chunks : 64) * n;
 }
 
-void colreduce(const float* src, float* dst, long R, long n, long ld, float* tmp, hipStream_t s) {
+void colreduce(const float* src, float* dst, long R, long n, long ld, float* tmp, hipStream_t s, float* dst2,
+               long n1) {
   const unsigned gx = (unsigned)((n + 63) / 64);
+  if (!dst2) n1 = n;
   if (R <= 256) {
-    colreduce_kernel<<<dim3(gx, 1), 256, 0, s>>>(src, dst, R, n, ld, R);
+    colreduce_kernel<<<dim3(gx, 1), 256, 0, s>>>(src, dst, R, n, ld, R, dst2, n1);
     return;
   }
   long chunks = (R + 255) / 256;
   if (chunks > 64) chunks = 64;
   const long per = (R + chunks - 1) / chunks;
   chunks = (R + per - 1) / per;
-  colreduce_kernel<<<dim3(gx, (unsigned)chunks), 256, 0, s>>>(src, tmp, R, n, ld, per);
-  colreduce_kernel<<<dim3(gx, 1), 256, 0, s>>>(tmp, dst, chunks, n, n, chunks);
+  colreduce_kernel<<<dim3(gx, (unsigned)chunks), 256, 0, s>>>(src, tmp, R, n, ld, per, nullptr, n);
+  colreduce_kernel<<<dim3(gx, 1), 256, 0, s>>>(tmp, dst, chunks, n, n, chunks, dst2, n1);
 }
 
 // ------------------------------------------------------------------ depthwise conv kernels

@@ -95,6 +95,136 @@ __device__ __forceinline__ void stats_store(float (&s1)[TN], float (&s2)[TN], fl
   }
 }
 
+// Row-contiguous epilogue for the bf16 kernels.  The MFMA C fragment gives each lane one column
+// of 4 rows, so storing straight from registers means 2-byte scattered stores (and 2-byte
+// residual / Z loads).  Instead each wave stages its accumulator 16 rows at a time through LDS
+// (fp32, pitch WN+4) and re-reads it as 8-column runs: LPR = WN/8 lanes per row, 16-byte loads of
+// res / Z and 16-byte stores of out.  Per-column batch statistics follow the same mapping
+// (8 columns per lane), reduced over lanes sharing columns, then over the two M-waves.
+template <int TM, int TN, int WM, int WN, bool STATS>
+__device__ __forceinline__ void gemm_epilogue_bf16(f32x4 (&acc)[TM][TN], float* stage_all, const Epi& epi,
+                                                   bf16* __restrict__ out, int ldo, int M, int N, int m0, int n0,
+                                                   int mt, int wm, int wn, int wave, int lane) {
+  constexpr int SP = WN + 4, LPR = WN / 8, RPP = 64 / LPR, PASSES = 16 / RPP;
+  float* stage = stage_all + wave * 16 * SP;
+  const bf16* res = static_cast<const bf16*>(epi.res);
+  const bf16* Z = static_cast<const bf16*>(epi.Z);
+  const int c8 = (lane % LPR) * 8, rr0 = lane / LPR;
+  const int n = n0 + wn * WN + c8;
+  const bool full = n + 8 <= N;
+  const bool vec = full && (ldo & 7) == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0 &&
+                   (!res || (reinterpret_cast<uintptr_t>(res) & 15) == 0) &&
+                   (!epi.zact || ((epi.ldz & 7) == 0 && (reinterpret_cast<uintptr_t>(Z) & 15) == 0));
+  float bias[8], shift[8], s1[8], s2[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    bias[q] = (epi.bias && n + q < N) ? epi.bias[n + q] : 0.f;
+    shift[q] = (STATS && epi.stat_shift && n + q < N) ? epi.stat_shift[n + q] : 0.f;
+    s1[q] = 0.f;
+    s2[q] = 0.f;
+  }
+  __syncthreads();  // main-loop LDS tiles are dead
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) stage[(4 * (lane >> 4) + r) * SP + j * 16 + (lane & 15)] = acc[i][j][r];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int ps = 0; ps < PASSES; ++ps) {
+      const int rr = rr0 + ps * RPP;
+      const int m = m0 + wm * (TM * 16) + i * 16 + rr;
+      if (m < M && n < N) {
+        float v[8];
+        const float4 lo = *reinterpret_cast<const float4*>(stage + rr * SP + c8);
+        const float4 hi = *reinterpret_cast<const float4*>(stage + rr * SP + c8 + 4);
+        v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w;
+        v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
+        const float sc = epi.rs ? epi.rs[m / epi.rps] : 1.f;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = (v[q] + bias[q]) * sc;
+        const long o = (long)m * ldo + n;
+        bf16 ob[8];
+        if (vec) {
+          if (res) {
+            float t[8];
+            load_vec<bf16, 8>(res + o, t);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) v[q] += t[q];
+          }
+          if (epi.zact) {
+            float t[8];
+            load_vec<bf16, 8>(Z + (long)m * epi.ldz + n, t);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) v[q] *= act_grad(epi.zact, t[q]);
+          }
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            ob[q] = (bf16)v[q];
+            v[q] = (float)ob[q];
+          }
+          store_vec<bf16, 8>(out + o, v);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            if (n + q >= N) { ob[q] = (bf16)0.f; continue; }
+            if (res) v[q] += (float)res[o + q];
+            if (epi.zact) v[q] *= act_grad(epi.zact, (float)Z[(long)m * epi.ldz + n + q]);
+            ob[q] = (bf16)v[q];
+            out[o + q] = ob[q];
+          }
+        }
+        if constexpr (STATS) {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const float d = n + q < N ? (float)ob[q] - shift[q] : 0.f;
+            s1[q] += d;
+            s2[q] = fmaf(d, d, s2[q]);
+          }
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  if constexpr (STATS) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+#pragma unroll
+      for (int o = LPR; o < 64; o <<= 1) {
+        s1[q] += __shfl_xor(s1[q], o, 64);
+        s2[q] += __shfl_xor(s2[q], o, 64);
+      }
+    }
+    __syncthreads();
+    // [wm][2][BN] partials; lanes < LPR hold their wave's column sums
+    constexpr int BN = 2 * WN;
+    float* red = stage_all;
+    if (lane < LPR) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        red[(wm * 2 + 0) * BN + wn * WN + c8 + q] = s1[q];
+        red[(wm * 2 + 1) * BN + wn * WN + c8 + q] = s2[q];
+      }
+    }
+    __syncthreads();
+    if (wm == 0 && lane < LPR) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int c = wn * WN + c8 + q;
+        if (n + q < N) {
+          epi.stat[((long)mt * 2 + 0) * N + n + q] = red[0 * BN + c] + red[2 * BN + c];
+          epi.stat[((long)mt * 2 + 1) * N + n + q] = red[1 * BN + c] + red[3 * BN + c];
+        }
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------------
 // fwd / dgrad kernel, bf16
 // ------------------------------------------------------------------------------------------------
@@ -108,8 +238,11 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
   constexpr int A_VECS = BM * BK / 8 / 256;
   constexpr int B_F4 = BN * BK / 4 / 256;
-  __shared__ __attribute__((aligned(16))) bf16 As[BM * PITCH];
-  __shared__ __attribute__((aligned(16))) bf16 Bs[BN * PITCH];
+  constexpr int SP = WN + 4;  // epilogue staging pitch (floats)
+  constexpr int MAIN_BYTES = (BM + BN) * PITCH * 2, EPI_BYTES = 4 * 16 * SP * 4;
+  __shared__ __attribute__((aligned(16))) char smem[MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES];
+  bf16* As = reinterpret_cast<bf16*>(smem);
+  bf16* Bs = As + BM * PITCH;
 
   const int bid = blockIdx.x;
   const int xcd = bid & 7, local = bid >> 3;
@@ -211,39 +344,8 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
     __syncthreads();
   }
 
-  const bf16* res = static_cast<const bf16*>(epi.res);
-  const bf16* Z = static_cast<const bf16*>(epi.Z);
-  float s1[TN], s2[TN];
-#pragma unroll
-  for (int j = 0; j < TN; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int m = m0 + wm * WM + i * 16 + 4 * (lane >> 4) + r;
-      if (m >= M) continue;
-      const float sc = epi.rs ? epi.rs[m / epi.rps] : 1.f;
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int n = n0 + wn * WN + j * 16 + (lane & 15);
-        if (n >= N) continue;
-        float v = acc[i][j][r];
-        if (epi.bias) v += epi.bias[n];
-        v *= sc;
-        if (res) v += (float)res[(long)m * ldo + n];
-        if (epi.zact) v *= act_grad(epi.zact, (float)Z[(long)m * epi.ldz + n]);
-        const bf16 o = (bf16)v;
-        out[(long)m * ldo + n] = o;
-        if constexpr (STATS) {
-          const float d = (float)o - (epi.stat_shift ? epi.stat_shift[n] : 0.f);
-          s1[j] += d;
-          s2[j] = fmaf(d, d, s2[j]);
-        }
-      }
-    }
-  }
-  if constexpr (STATS)
-    stats_store<TN, WN, BN>(s1, s2, reinterpret_cast<float*>(As), wm, wn, lane, epi.stat, mt, n0, N);
+  gemm_epilogue_bf16<TM, TN, WM, WN, STATS>(acc, reinterpret_cast<float*>(smem), epi, out, ldo, M, N, m0, n0, mt, wm,
+                                             wn, wave, lane);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -388,119 +490,177 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
 // j>=4: m = 16+4g+j-4) identically for both operands, which makes each 32-lane half read 8
 // distinct rows: with an 80-element pitch the reads are bank-conflict free.
 // ------------------------------------------------------------------------------------------------
-template <bool PRO>
+template <int BN, int BK, bool PRO>
 __global__ __launch_bounds__(256) void wgrad_bf16_kernel(const bf16* __restrict__ G, int ldg, const bf16* __restrict__ X,
                                                          int ldx, Pro pro, const float* __restrict__ rs, int rps,
-                                                         float* __restrict__ part, float* __restrict__ dbias_part,
-                                                         int M, int N, int K, int mchunk, int nNt) {
-  constexpr int BN = 64, BKK = 64, MS = 32, PITCH = 80;
-  __shared__ __attribute__((aligned(16))) bf16 Gs[MS * PITCH];
-  __shared__ __attribute__((aligned(16))) bf16 Xs[MS * PITCH];
-  const int nt = blockIdx.x % nNt, kt = blockIdx.x / nNt;
-  const int s = blockIdx.y;
-  const int n0 = nt * BN, k0 = kt * BKK;
+                                                         float* __restrict__ part, long ldp, int want_bias, int M, int N,
+                                                         int K, int mchunk, int nNt, int tiles, int S) {
+  constexpr int MS = 32;
+  constexpr int GP = BN + 16, XP = BK + 16;  // 16 * odd elements: conflict-free transposed reads
+  constexpr int GV = MS * BN / 8 / 256, XV = MS * BK / 8 / 256;
+  constexpr int GC = BN / 8, XC = BK / 8;  // 8-element chunks per staged row
+  constexpr int TN = BN / 32, TK = BK / 32;
+  __shared__ __attribute__((aligned(16))) bf16 Gs[MS * GP];
+  __shared__ __attribute__((aligned(16))) bf16 Xs[MS * XP];
+  // slab-major XCD map: all tiles of slab s run on XCD s % 8, so their re-reads of the slab's
+  // G / X rows come from that XCD's L2
+  const int b = blockIdx.x, xcd = b & 7, local = b >> 3;
+  const int tile = local % tiles, s = (local / tiles) * 8 + xcd;
+  if (s >= S) return;
+  const int nt = tile % nNt, kt = tile / nNt;
+  const int n0 = nt * BN, k0 = kt * BK;
   const int mbeg = s * mchunk;
   const int mend = min(M, mbeg + mchunk);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wn = wave >> 1, wk = wave & 1;
-  const bool do_bias = dbias_part != nullptr && kt == 0;
+  const bool do_bias = want_bias && kt == 0;
 
-  f32x4 acc[2][2];
+  f32x4 acc[TN][TK];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < TN; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float bsum = 0.f;
+    for (int j = 0; j < TK; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bacc[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) bacc[t] = 0.f;
 
-  const int srow = tid >> 3, scol = (tid & 7) * 8;
-  const int g = lane >> 4, c16 = lane & 15, q = c16 >> 2, p4 = (c16 & 3) * 4;
-  const bool g_vec = ((ldg & 7) == 0) && ((reinterpret_cast<uintptr_t>(G) & 15) == 0);
-  const bool x_vec = ((ldx & 7) == 0) && ((reinterpret_cast<uintptr_t>(X) & 15) == 0);
-  for (int m0 = mbeg; m0 < mend; m0 += MS) {
-    {
-      const int gm = m0 + srow;
-      uint4 gv = uint4{0u, 0u, 0u, 0u}, xv = uint4{0u, 0u, 0u, 0u};
+  const int gc8 = (tid % GC) * 8, grow = tid / GC;
+  const int xc8 = (tid % XC) * 8, xrow = tid / XC;
+  const bool g_vec = ((ldg & 7) == 0) && ((reinterpret_cast<uintptr_t>(G) & 15) == 0) && n0 + gc8 + 8 <= N;
+  const bool x_vec = ((ldx & 7) == 0) && ((reinterpret_cast<uintptr_t>(X) & 15) == 0) && k0 + xc8 + 8 <= K;
+  uint4 gr[GV], xr[XV];
+  auto load = [&](int m0) {
+#pragma unroll
+    for (int i = 0; i < GV; ++i) {
+      const int gm = m0 + grow + i * (256 / GC);
+      gr[i] = uint4{0u, 0u, 0u, 0u};
       if (gm < mend) {
-        const bf16* gsrc = G + (long)gm * ldg + n0 + scol;
-        const bf16* xsrc = X + (long)gm * ldx + k0 + scol;
-        if (g_vec && n0 + scol + 8 <= N) gv = *reinterpret_cast<const uint4*>(gsrc);
+        const bf16* src = G + (long)gm * ldg + n0 + gc8;
+        if (g_vec) gr[i] = *reinterpret_cast<const uint4*>(src);
         else {
-          bf16* e = reinterpret_cast<bf16*>(&gv);
+          bf16* e = reinterpret_cast<bf16*>(&gr[i]);
 #pragma unroll
-          for (int t = 0; t < 8; ++t) e[t] = (n0 + scol + t < N) ? gsrc[t] : (bf16)0.f;
+          for (int t = 0; t < 8; ++t) e[t] = (n0 + gc8 + t < N) ? src[t] : (bf16)0.f;
         }
-        if (x_vec && k0 + scol + 8 <= K) xv = *reinterpret_cast<const uint4*>(xsrc);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < XV; ++i) {
+      const int gm = m0 + xrow + i * (256 / XC);
+      xr[i] = uint4{0u, 0u, 0u, 0u};
+      if (gm < mend) {
+        const bf16* src = X + (long)gm * ldx + k0 + xc8;
+        if (x_vec) xr[i] = *reinterpret_cast<const uint4*>(src);
         else {
-          bf16* e = reinterpret_cast<bf16*>(&xv);
+          bf16* e = reinterpret_cast<bf16*>(&xr[i]);
 #pragma unroll
-          for (int t = 0; t < 8; ++t) e[t] = (k0 + scol + t < K) ? xsrc[t] : (bf16)0.f;
+          for (int t = 0; t < 8; ++t) e[t] = (k0 + xc8 + t < K) ? src[t] : (bf16)0.f;
         }
-        if (rs) {
-          const float sc = rs[gm / rps];
-          bf16* e = reinterpret_cast<bf16*>(&gv);
+      }
+    }
+  };
+  auto stage = [&](int m0) {
 #pragma unroll
-          for (int t = 0; t < 8; ++t) e[t] = (bf16)((float)e[t] * sc);
-        }
-        if constexpr (PRO) {
-          bf16* e = reinterpret_cast<bf16*>(&xv);
+    for (int i = 0; i < GV; ++i) {
+      const int r = grow + i * (256 / GC);
+      uint4 v = gr[i];
+      bf16* e = reinterpret_cast<bf16*>(&v);
+      if (rs && m0 + r < mend) {
+        const float sc = rs[(m0 + r) / rps];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) e[t] = (bf16)((float)e[t] * sc);
+      }
+      if (do_bias) {
+#pragma unroll
+        for (int t = 0; t < 8; ++t) bacc[t] += (float)e[t];
+      }
+      *reinterpret_cast<uint4*>(Gs + r * GP + gc8) = v;
+    }
+#pragma unroll
+    for (int i = 0; i < XV; ++i) {
+      const int r = xrow + i * (256 / XC);
+      uint4 v = xr[i];
+      if constexpr (PRO) {
+        const int gm = m0 + r;
+        if (gm < mend) {
+          bf16* e = reinterpret_cast<bf16*>(&v);
           float f[8];
 #pragma unroll
           for (int t = 0; t < 8; ++t) f[t] = (float)e[t];
-          pro_apply_run<8>(pro, f, gm, k0 + scol, K);
+          pro_apply_run<8>(pro, f, gm, k0 + xc8, K);
 #pragma unroll
-          for (int t = 0; t < 8; ++t) e[t] = k0 + scol + t < K ? (bf16)f[t] : (bf16)0.f;
+          for (int t = 0; t < 8; ++t) e[t] = k0 + xc8 + t < K ? (bf16)f[t] : (bf16)0.f;
         }
       }
-      *reinterpret_cast<uint4*>(Gs + srow * PITCH + scol) = gv;
-      *reinterpret_cast<uint4*>(Xs + srow * PITCH + scol) = xv;
+      *reinterpret_cast<uint4*>(Xs + r * XP + xc8) = v;
     }
+  };
+
+  const int g = lane >> 4, c16 = lane & 15, q = c16 >> 2, p4 = (c16 & 3) * 4;
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  typedef __attribute__((ext_vector_type(8))) short s16x8;
+  load(mbeg);
+  for (int m0 = mbeg; m0 < mend; m0 += MS) {
+    stage(m0);
     __syncthreads();
-    if (do_bias && tid < BN) {
-#pragma unroll 8
-      for (int r = 0; r < MS; ++r) bsum += (float)Gs[r * PITCH + tid];
-    }
-    bf16x8 af[2], xf[2];
+    if (m0 + MS < mend) load(m0 + MS);  // next rows' HBM latency hides under this step's MFMAs
+    bf16x8 af[TN], xf[TK];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int col = wn * 32 + i * 16 + p4;
-      typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-      s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Gs + (4 * g + q) * PITCH + col));
-      s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Gs + (16 + 4 * g + q) * PITCH + col));
-      const int colx = wk * 32 + i * 16 + p4;
-      s16x4 xlo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Xs + (4 * g + q) * PITCH + colx));
-      s16x4 xhi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Xs + (16 + 4 * g + q) * PITCH + colx));
-      typedef __attribute__((ext_vector_type(8))) short s16x8;
+    for (int i = 0; i < TN; ++i) {
+      const int col = wn * (BN / 2) + i * 16 + p4;
+      s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Gs + (4 * g + q) * GP + col));
+      s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Gs + (16 + 4 * g + q) * GP + col));
       s16x8 a8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      s16x8 x8 = {xlo[0], xlo[1], xlo[2], xlo[3], xhi[0], xhi[1], xhi[2], xhi[3]};
       af[i] = __builtin_bit_cast(bf16x8, a8);
-      xf[i] = __builtin_bit_cast(bf16x8, x8);
     }
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int j = 0; j < TK; ++j) {
+      const int col = wk * (BK / 2) + j * 16 + p4;
+      s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Xs + (4 * g + q) * XP + col));
+      s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Xs + (16 + 4 * g + q) * XP + col));
+      s16x8 x8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      xf[j] = __builtin_bit_cast(bf16x8, x8);
+    }
 #pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], xf[j], acc[i][j], 0, 0, 0);
+    for (int i = 0; i < TN; ++i)
+#pragma unroll
+      for (int j = 0; j < TK; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], xf[j], acc[i][j], 0, 0, 0);
     __syncthreads();
   }
-  float* dst = part + (long)s * N * K;
+  float* dst = part + (long)s * ldp;
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < TN; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < TK; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int n = n0 + wn * 32 + i * 16 + 4 * g + r;
-        const int k = k0 + wk * 32 + j * 16 + c16;
+        const int n = n0 + wn * (BN / 2) + i * 16 + 4 * g + r;
+        const int k = k0 + wk * (BK / 2) + j * 16 + c16;
         if (n < N && k < K) dst[(long)n * K + k] = acc[i][j][r];
       }
-  if (do_bias && tid < BN && n0 + tid < N) dbias_part[(long)s * N + n0 + tid] = bsum;
+  if (do_bias) {
+    // lanes sharing gc8 within the wave, then the 4 waves through LDS (Gs is free after the loop)
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+#pragma unroll
+      for (int o = GC; o < 64; o <<= 1) bacc[t] += __shfl_xor(bacc[t], o, 64);
+    float* red = reinterpret_cast<float*>(Gs);  // 4 x BN floats <= MS * GP * 2 bytes
+    if (lane < GC) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t) red[wave * BN + gc8 + t] = bacc[t];
+    }
+    __syncthreads();
+    if (tid < BN && n0 + tid < N)
+      dst[(long)N * K + n0 + tid] = (red[tid] + red[BN + tid]) + (red[2 * BN + tid] + red[3 * BN + tid]);
+  }
 }
 
 // wgrad, fp32: f32 MFMA fragments read straight from the [m][col] tiles (k = lane>>4 layout).
 template <bool PRO>
 __global__ __launch_bounds__(256) void wgrad_f32_kernel(const float* __restrict__ G, int ldg, const float* __restrict__ X,
                                                         int ldx, Pro pro, const float* __restrict__ rs, int rps,
-                                                        float* __restrict__ part, float* __restrict__ dbias_part,
-                                                        int M, int N, int K, int mchunk, int nNt) {
+                                                        float* __restrict__ part, long ldp, int want_bias, int M,
+                                                        int N, int K, int mchunk, int nNt) {
   constexpr int BN = 64, BKK = 64, MS = 16, PITCH = 68;
   __shared__ __attribute__((aligned(16))) float Gs[MS * PITCH];
   __shared__ __attribute__((aligned(16))) float Xs[MS * PITCH];
@@ -511,7 +671,7 @@ __global__ __launch_bounds__(256) void wgrad_f32_kernel(const float* __restrict_
   const int mend = min(M, mbeg + mchunk);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wn = wave >> 1, wk = wave & 1;
-  const bool do_bias = dbias_part != nullptr && kt == 0;
+  const bool do_bias = want_bias && kt == 0;
 
   f32x4 acc[2][2];
 #pragma unroll
@@ -577,7 +737,7 @@ __global__ __launch_bounds__(256) void wgrad_f32_kernel(const float* __restrict_
     }
     __syncthreads();
   }
-  float* dst = part + (long)s * N * K;
+  float* dst = part + (long)s * ldp;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -588,29 +748,42 @@ __global__ __launch_bounds__(256) void wgrad_f32_kernel(const float* __restrict_
         const int k = k0 + wk * 32 + j * 16 + (lane & 15);
         if (n < N && k < K) dst[(long)n * K + k] = acc[i][j][r];
       }
-  if (do_bias && tid < BN && n0 + tid < N) dbias_part[(long)s * N + n0 + tid] = bsum;
+  if (do_bias && tid < BN && n0 + tid < N) dst[(long)N * K + n0 + tid] = bsum;
 }
 
 // ------------------------------------------------------------------------------------------------
-// Tiny GEMMs (the SE MLP: M = batch rows, fp32): one thread per output, K-loop dot products.
-// The MFMA kernels would launch a handful of 128-row blocks for these and run latency-bound.
+// Tiny GEMMs (the SE MLP: M = batch rows, fp32).  The MFMA kernels would launch a handful of
+// 128-row blocks for these and run latency-bound.
 // ------------------------------------------------------------------------------------------------
+// Groups of G lanes per output (G = 4 / 16 / 64 chosen from K): the group reads one A row and
+// one W row with coalesced loads, reduces with shuffles; lane 0 of the group runs the epilogue.
+template <int G>
 __global__ __launch_bounds__(256) void small_fwd_kernel(const float* __restrict__ A, int lda, Pro pro,
                                                         const float* __restrict__ Wt, int ldw, Epi epi,
                                                         float* __restrict__ out, int ldo, int M, int N, int Ka,
                                                         int Kb) {
-  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (tid >= (long)M * N) return;
-  const int n = (int)(tid % N), m = (int)(tid / N);
+  const long gid = ((long)blockIdx.x * blockDim.x + threadIdx.x) / G;
+  const int j = threadIdx.x & (G - 1);
+  const bool live = gid < (long)M * N;
+  const int n = live ? (int)(gid % N) : 0, m = live ? (int)(gid / N) : 0;
   const int K = Ka < Kb ? Ka : Kb;
   const float* a = A + (long)m * lda;
   const float* w = Wt + (long)n * ldw;
-  float acc = 0.f;
   const bool p = pro.act != OGV_ACT_NONE || pro.sc || pro.sh || pro.gate;
-  for (int k = 0; k < K; ++k) acc = fmaf(p ? pro_apply(pro, a[k], m, k) : a[k], w[k], acc);
+  float acc0 = 0.f, acc1 = 0.f;
+  int k = j;
+  if (live) {
+    for (; k + G < K; k += 2 * G) {
+      const float x0 = a[k], x1 = a[k + G];
+      acc0 = fmaf(p ? pro_apply(pro, x0, m, k) : x0, w[k], acc0);
+      acc1 = fmaf(p ? pro_apply(pro, x1, m, k + G) : x1, w[k + G], acc1);
+    }
+    if (k < K) acc0 = fmaf(p ? pro_apply(pro, a[k], m, k) : a[k], w[k], acc0);
+  }
+  float v = group_sum<G>(acc0 + acc1);
+  if (!live || j != 0) return;
   const float* res = static_cast<const float*>(epi.res);
   const float* Z = static_cast<const float*>(epi.Z);
-  float v = acc;
   if (epi.bias) v += epi.bias[n];
   if (epi.rs) v *= epi.rs[m / epi.rps];
   if (res) v += res[(long)m * ldo + n];
@@ -618,29 +791,47 @@ __global__ __launch_bounds__(256) void small_fwd_kernel(const float* __restrict_
   out[(long)m * ldo + n] = v;
 }
 
-// dW[n][k] = sum_m rs*G[m,n] * pro(X)[m,k], dbias[n] = sum_m rs*G[m,n]   (thread per (n, k))
+// dW[n][k] = sum_m rs*G[m,n] * pro(X)[m,k], dbias[n] = sum_m rs*G[m,n].
+// Block = 64 k-columns of one n; its 4 waves take interleaved quarters of M (coalesced X rows),
+// partials combined through LDS in a fixed order.  Column block kb == nKb carries dbias.
 __global__ __launch_bounds__(256) void small_wgrad_kernel(const float* __restrict__ G, int ldg,
                                                           const float* __restrict__ X, int ldx, Pro pro,
                                                           const float* __restrict__ rs, int rps, float* __restrict__ dW,
                                                           float* __restrict__ dbias, int M, int N, int K) {
-  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long NK = (long)N * K;
-  if (tid >= NK + (dbias ? N : 0)) return;
+  __shared__ float part[4][64];
+  const int nKb = (K + 63) / 64;
+  const int n = blockIdx.y, kb = blockIdx.x;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const bool bias_blk = kb == nKb;
+  const int k = kb * 64 + lane;
   const bool p = pro.act != OGV_ACT_NONE || pro.sc || pro.sh || pro.gate;
-  if (tid < NK) {
-    const int k = (int)(tid % K), n = (int)(tid / K);
-    float acc = 0.f;
-    for (int m = 0; m < M; ++m) {
-      const float x = X[(long)m * ldx + k];
-      const float g = G[(long)m * ldg + n] * (rs ? rs[m / rps] : 1.f);
-      acc = fmaf(g, p ? pro_apply(pro, x, m, k) : x, acc);
+  float acc0 = 0.f, acc1 = 0.f;
+  if (bias_blk) {
+    if (lane == 0)
+      for (int m = wv; m < M; m += 4) acc0 += G[(long)m * ldg + n] * (rs ? rs[m / rps] : 1.f);
+  } else if (k < K) {
+    int m = wv;
+    for (; m + 4 < M; m += 8) {
+      const float x0 = X[(long)m * ldx + k], x1 = X[(long)(m + 4) * ldx + k];
+      const float g0 = G[(long)m * ldg + n] * (rs ? rs[m / rps] : 1.f);
+      const float g1 = G[(long)(m + 4) * ldg + n] * (rs ? rs[(m + 4) / rps] : 1.f);
+      acc0 = fmaf(g0, p ? pro_apply(pro, x0, m, k) : x0, acc0);
+      acc1 = fmaf(g1, p ? pro_apply(pro, x1, m + 4, k) : x1, acc1);
     }
-    dW[tid] = acc;
-  } else {
-    const int n = (int)(tid - NK);
-    float acc = 0.f;
-    for (int m = 0; m < M; ++m) acc += G[(long)m * ldg + n] * (rs ? rs[m / rps] : 1.f);
-    dbias[n] = acc;
+    if (m < M) {
+      const float x0 = X[(long)m * ldx + k];
+      acc0 = fmaf(G[(long)m * ldg + n] * (rs ? rs[m / rps] : 1.f), p ? pro_apply(pro, x0, m, k) : x0, acc0);
+    }
+  }
+  part[wv][lane] = acc0 + acc1;
+  __syncthreads();
+  if (wv == 0) {
+    const float v = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
+    if (bias_blk) {
+      if (lane == 0) dbias[n] = v;
+    } else if (k < K) {
+      dW[(long)n * K + k] = v;
+    }
   }
 }
 
@@ -705,8 +896,17 @@ void gemm_fwd_launch(ogv_dtype dt, const void* A, int lda, const Pro& pro, const
                      int M, int N, int K, int Ka, int Kb, const Epi& epi, hipStream_t s) {
   if (M <= 0) return;
   if (tiny(M, N, dt, epi)) {
-    small_fwd_kernel<<<cdiv((long)M * N, 256), 256, 0, s>>>((const float*)A, lda, pro, W, ldw, epi, (float*)out, ldo, M,
-                                                            N, Ka, Kb);
+    const int K0 = Ka < Kb ? Ka : Kb;
+    const long outs = (long)M * N;
+    if (K0 >= 256)
+      small_fwd_kernel<64><<<cdiv(outs * 64, 256), 256, 0, s>>>((const float*)A, lda, pro, W, ldw, epi, (float*)out,
+                                                                 ldo, M, N, Ka, Kb);
+    else if (K0 >= 48)
+      small_fwd_kernel<16><<<cdiv(outs * 16, 256), 256, 0, s>>>((const float*)A, lda, pro, W, ldw, epi, (float*)out,
+                                                                 ldo, M, N, Ka, Kb);
+    else
+      small_fwd_kernel<4><<<cdiv(outs * 4, 256), 256, 0, s>>>((const float*)A, lda, pro, W, ldw, epi, (float*)out, ldo,
+                                                               M, N, Ka, Kb);
     return;
   }
   if (dt == OGV_BF16) launch_mm_any<bf16>(A, lda, pro, W, ldw, out, ldo, M, N, K, Ka, Kb, epi, s);
@@ -735,19 +935,25 @@ void gemm_dgrad_launch(ogv_dtype dt, const void* dout, int ldd, const float* W, 
   gemm_fwd_launch(dt, dout, ldd, Pro(), WT, Np, dA, lda, M, K, Np, N, Np, e, s);
 }
 
+// Split-M plan.  bf16: tiles of BN x BK in {64,128}^2, slab partials [S][N*K + N] (dW then
+// dbias) summed by one colreduce.  S is sized to put ~1024 blocks on the chip with >= 256 rows per
+// slab, while keeping the partial traffic under max(data / 4, 16 MB).
 struct WgradPlan {
-  int nNt, nKt, S, mchunk;
+  int BN, BK, nNt, nKt, S, mchunk;
 };
-static WgradPlan wgrad_plan(int M, int N, int K) {
+static WgradPlan wgrad_plan(ogv_dtype dt, int M, int N, int K) {
   WgradPlan p;
-  p.nNt = (N + 63) / 64;
-  p.nKt = (K + 63) / 64;
-  const int tiles = p.nNt * p.nKt;
-  int S = (1024 + tiles - 1) / tiles;
-  const int max_s = (M + 1023) / 1024;  // keep >= ~1024 rows per chunk so the slab pass stays small
-  if (S > max_s) S = max_s;
-  if (S < 1) S = 1;
-  int mchunk = (M + S - 1) / S;
+  p.BN = (dt == OGV_BF16 && N > 64) ? 128 : 64;
+  p.BK = (dt == OGV_BF16 && K > 64) ? 128 : 64;
+  p.nNt = (N + p.BN - 1) / p.BN;
+  p.nKt = (K + p.BK - 1) / p.BK;
+  const long tiles = (long)p.nNt * p.nKt;
+  long S = (1024 + tiles - 1) / tiles;
+  S = std::min(S, ((long)M + 255) / 256);
+  const double data = 2.0 * M * (N + K) * (dt == OGV_BF16 ? 2 : 4);
+  const long cap = (long)(std::max(data / 4, 16.0 * (1 << 20)) / (4.0 * ((double)N * K + N)));
+  S = std::max(1L, std::min(S, cap));
+  int mchunk = (int)((M + S - 1) / S);
   mchunk = (mchunk + 31) / 32 * 32;
   p.S = (M + mchunk - 1) / mchunk;
   p.mchunk = mchunk;
@@ -755,9 +961,28 @@ static WgradPlan wgrad_plan(int M, int N, int K) {
 }
 
 size_t wgrad_ws_bytes(int M, int N, int K) {
-  WgradPlan p = wgrad_plan(M > 0 ? M : 1, N, K);
-  const size_t t1 = colreduce_tmp_floats(p.S, (long)N * K), t2 = colreduce_tmp_floats(p.S, N);
-  return ((size_t)p.S * ((size_t)N * K + N) + (t1 > t2 ? t1 : t2)) * sizeof(float);
+  // the larger of the bf16 and fp32 plans (the C ABI sizes the workspace without the dtype)
+  size_t best = 0;
+  for (ogv_dtype dt : {OGV_BF16, OGV_F32}) {
+    WgradPlan p = wgrad_plan(dt, M > 0 ? M : 1, N, K);
+    const long ld = (long)N * K + N;
+    best = std::max(best, ((size_t)p.S * ld + colreduce_tmp_floats(p.S, ld)) * sizeof(float));
+  }
+  return best;
+}
+
+template <int BN, int BK>
+static void launch_wgrad_bf16(const WgradPlan& p, const void* G, int ldg, const void* X, int ldx, const Pro& pro,
+                              const float* rs, int rps, float* part, long ldp, bool bias, int M, int N, int K,
+                              hipStream_t s) {
+  const int tiles = p.nNt * p.nKt;
+  const unsigned grid = (unsigned)(((p.S + 7) / 8) * 8 * tiles);
+  if (pro.any())
+    wgrad_bf16_kernel<BN, BK, true><<<grid, 256, 0, s>>>((const bf16*)G, ldg, (const bf16*)X, ldx, pro, rs, rps, part,
+                                                         ldp, bias, M, N, K, p.mchunk, p.nNt, tiles, p.S);
+  else
+    wgrad_bf16_kernel<BN, BK, false><<<grid, 256, 0, s>>>((const bf16*)G, ldg, (const bf16*)X, ldx, pro, rs, rps, part,
+                                                          ldp, bias, M, N, K, p.mchunk, p.nNt, tiles, p.S);
 }
 
 void gemm_wgrad_launch(ogv_dtype dt, const void* G, int ldg, const void* X, int ldx, const Pro& pro, const float* rs,
@@ -768,31 +993,31 @@ void gemm_wgrad_launch(ogv_dtype dt, const void* G, int ldg, const void* X, int 
     return;
   }
   if (dt == OGV_F32 && M <= 2048) {
-    small_wgrad_kernel<<<cdiv((long)N * K + (dbias ? N : 0), 256), 256, 0, s>>>(
-        (const float*)G, ldg, (const float*)X, ldx, pro, rs, rps, dW, dbias, M, N, K);
+    dim3 grid(cdiv(K, 64) + (dbias ? 1 : 0), N);
+    small_wgrad_kernel<<<grid, 256, 0, s>>>((const float*)G, ldg, (const float*)X, ldx, pro, rs, rps, dW, dbias, M, N,
+                                            K);
     return;
   }
-  WgradPlan p = wgrad_plan(M, N, K);
+  const WgradPlan p = wgrad_plan(dt, M, N, K);
+  const long ldp = (long)N * K + N;
   float* part = (float*)ws;
-  float* bpart = part + (size_t)p.S * N * K;
-  float* tmp = bpart + (size_t)p.S * N;
-  dim3 grid(p.nNt * p.nKt, p.S);
-  float* bp = dbias ? bpart : nullptr;
-  const bool pr = pro.any();
+  float* tmp = part + (size_t)p.S * ldp;
   if (dt == OGV_BF16) {
-    if (pr) wgrad_bf16_kernel<true><<<grid, 256, 0, s>>>((const bf16*)G, ldg, (const bf16*)X, ldx, pro, rs, rps, part, bp,
-                                                         M, N, K, p.mchunk, p.nNt);
-    else wgrad_bf16_kernel<false><<<grid, 256, 0, s>>>((const bf16*)G, ldg, (const bf16*)X, ldx, pro, rs, rps, part, bp,
-                                                       M, N, K, p.mchunk, p.nNt);
+    const bool b = dbias != nullptr;
+    if (p.BN == 128 && p.BK == 128) launch_wgrad_bf16<128, 128>(p, G, ldg, X, ldx, pro, rs, rps, part, ldp, b, M, N, K, s);
+    else if (p.BN == 128) launch_wgrad_bf16<128, 64>(p, G, ldg, X, ldx, pro, rs, rps, part, ldp, b, M, N, K, s);
+    else if (p.BK == 128) launch_wgrad_bf16<64, 128>(p, G, ldg, X, ldx, pro, rs, rps, part, ldp, b, M, N, K, s);
+    else launch_wgrad_bf16<64, 64>(p, G, ldg, X, ldx, pro, rs, rps, part, ldp, b, M, N, K, s);
   } else {
-    if (pr) wgrad_f32_kernel<true><<<grid, 256, 0, s>>>((const float*)G, ldg, (const float*)X, ldx, pro, rs, rps, part,
-                                                        bp, M, N, K, p.mchunk, p.nNt);
-    else wgrad_f32_kernel<false><<<grid, 256, 0, s>>>((const float*)G, ldg, (const float*)X, ldx, pro, rs, rps, part, bp,
-                                                      M, N, K, p.mchunk, p.nNt);
+    dim3 grid(p.nNt * p.nKt, p.S);
+    if (pro.any())
+      wgrad_f32_kernel<true><<<grid, 256, 0, s>>>((const float*)G, ldg, (const float*)X, ldx, pro, rs, rps, part, ldp,
+                                                  dbias != nullptr, M, N, K, p.mchunk, p.nNt);
+    else
+      wgrad_f32_kernel<false><<<grid, 256, 0, s>>>((const float*)G, ldg, (const float*)X, ldx, pro, rs, rps, part, ldp,
+                                                   dbias != nullptr, M, N, K, p.mchunk, p.nNt);
   }
-  const long len = (long)N * K;
-  colreduce(part, dW, p.S, len, len, tmp, s);
-  if (dbias) colreduce(bpart, dbias, p.S, N, N, tmp, s);
+  colreduce(part, dW, p.S, dbias ? ldp : (long)N * K, ldp, tmp, s, dbias, (long)N * K);
 }
 
 static int check_common(int M, int N, int K, ogv_act act, ogv_dtype dt, const char* who) {

@@ -6,10 +6,13 @@
 
 A step = one full training iteration on a synthetic batch already resident in HBM:
 autocast(bf16) forward through the HIP OutGridBlock kernels, CE(label smoothing 0.1), backward,
-clip_grad_norm(1.0), fused AdamW, WarmupCosine — bs=512 per GPU (weak scaling), DDP/RCCL for N>1.
-Prints ONE JSON line on rank 0 with `roofline` (dominant kernel, HIP events around its launches
-inside the timed region) and `cpu_baseline` (the CPU oracle's train step on the host cores,
-bounded sample, rank 0 at N=1 only).
+clip_grad_norm(1.0), fused AdamW, WarmupCosine — bs=512 per GPU (weak scaling).  The step runs
+as a replayed hipGraph (ogv.train.Trainer, graphs=True; --eager for plain launches); for N>1 the
+gradients are averaged by one RCCL all_reduce of a flat bucket between two graphs.
+Prints ONE JSON line on rank 0 with `roofline` (dominant kernel: HIP events around every launch
+of it in one step — in graph mode an eager step right after the timed replays, since ROCm graphs
+cannot hold timing events) and `cpu_baseline`
+(the CPU oracle's train step on the host cores, bounded sample, rank 0 at N=1 only).
 """
 from __future__ import annotations
 
@@ -37,20 +40,20 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=512, help="per-GPU batch")
     ap.add_argument("--model", default="model_a_7m")
-    ap.add_argument("--probe", default="outlook_fwd", help="kernel whose launches feed `roofline`")
+    ap.add_argument("--probe", default="gemm_fwd", choices=["gemm_fwd", "outlook_fwd", "grid_fwd"],
+                    help="kernel whose launches feed `roofline`")
+    ap.add_argument("--eager", action="store_true", help="launch kernels one by one instead of graph replay")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-parity", action="store_true")
     return ap.parse_args()
 
 
-def roofline_bytes(name, u):
-    """Algorithmic HBM bytes of one launch."""
-    if name == "outlook_fwd":   # read v [M,C] + logits [M,9h], write y [M,C]
-        return u["elem"] * u["M"] * (2 * u["C"] + u["k"] * u["k"] * u["heads"])
-    if name == "grid_fwd":      # read qkv [M,3C], write out [M,C] (+ fp32 lse [M,h])
-        return u["elem"] * u["M"] * 4 * u["C"] + 4 * u["M"] * u["heads"]
-    raise KeyError(name)
+PROBE_KERNEL = {  # probe name -> kernel symbol(s) it times (rocprofv3 names)
+    "gemm_fwd": "ogv::gemm_bf16_kernel<128,{128|64},*,false> (Linear / 1x1-conv forward launches)",
+    "outlook_fwd": "ogv::outlook_fwd_kernel",
+    "grid_fwd": "ogv::grid_fwd_kernel",
+}
 
 
 def fwd_parity(device):
@@ -110,7 +113,7 @@ def cpu_baseline(seconds):
 def main():
     args = parse()
     from ogv import functional as OF
-    from ogv.train import MODEL_CONFIGS, Trainer, build_model, setup_distributed, wrap_ddp
+    from ogv.train import MODEL_CONFIGS, Trainer, build_model, setup_distributed
     import ogv
 
     rank, world, local, device = setup_distributed()
@@ -122,23 +125,25 @@ def main():
     model = build_model(dict(type="model_a", num_classes=cfg["num_classes"], stem_dim=cfg["stem_dim"],
                              dpr_max=cfg["dpr_max"], stages=cfg["stages"]))
     model = model.to(device).to(memory_format=torch.channels_last)
-    model = wrap_ddp(model, device)
-    trainer = Trainer(model, total_steps=max(100, args.steps + args.warmup))
+    trainer = Trainer(model, total_steps=max(100, args.steps + args.warmup + 1), graphs=not args.eager,
+                      capture_warmup=max(0, args.warmup - 1))
 
     B, S = args.batch, cfg["img"]
     g = torch.Generator(device=device).manual_seed(7 + rank)
     x = torch.randn(B, 3, S, S, device=device, generator=g).contiguous(memory_format=torch.channels_last)
     y = torch.randint(0, cfg["num_classes"], (B,), device=device, generator=g)
 
-    for _ in range(args.warmup):
+    for _ in range(max(0, args.warmup - 1)):
         trainer.step(x, y)
+    trainer.step(x, y)       # last warmup step (graph mode: eager step on a side stream + capture)
     OF.probe_reset()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        OF.probe_arm(args.probe)
+        if not trainer.graphs:
+            OF.probe_arm(args.probe)
         loss = trainer.step(x, y)
     torch.cuda.synchronize()
     if world > 1:
@@ -149,29 +154,40 @@ def main():
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
-    ms_probe, units, nprobe = OF.probe_results()
     assert torch.isfinite(loss).item(), "non-finite loss"
+    if trainer.graphs:
+        # ROCm graphs cannot carry timing events (torch: "External events are disallowed in rocm"), so
+        # the probed kernel's launches are timed with HIP events in one eager step right after the
+        # timed replays: same kernels, shapes and stream.
+        OF.probe_reset()
+        OF.probe_arm(args.probe)
+        trainer._eager(x, y)
+        OF.probe_disarm()
+    probe = OF.probe_results()
 
     if rank == 0:
         value = world * B * args.steps / elapsed
         roof = None
-        if ms_probe:
-            ach = roofline_bytes(args.probe, units) / (ms_probe * 1e-3) / 1e9
+        if probe and probe["achieved_GBs"]:
             traffic = None
             tf = ROOT / "profiles" / "pmc_traffic.json"
             if tf.exists():
                 traffic = json.loads(tf.read_text()).get(args.probe, {}).get("hbm_bytes_per_launch")
-            roof = {"kernel": args.probe, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
-                    "algorithmic_bytes": roofline_bytes(args.probe, units), "avg_launch_ms": round(ms_probe, 5),
-                    "launches": nprobe}
+            ach = probe["achieved_GBs"]
+            roof = {"kernel": PROBE_KERNEL[args.probe], "bound": "hbm", "achieved": round(ach, 1),
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "algorithmic_bytes_per_launch": int(probe["bytes_per_launch"]),
+                    "avg_launch_ms": round(probe["avg_ms"], 5), "launches": probe["n"],
+                    "timing": "HIP events around each launch, eager step after the timed graph replays"
+                    if trainer.graphs else "HIP events around each launch, all timed steps"}
         out = {
             "metric": "training imgs/s Model-A-7M CIFAR-100 32x32 (bf16, bs=512/GPU)",
             "value": round(value, 1), "unit": "imgs/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "bf16", "data": "synthetic (randn images, randint labels; random init)",
             "config": {"workload": f"{args.model} train step: fwd+CE(ls=0.1)+bwd+clip(1.0)+AdamW", "img_size": S,
-                       "per_gpu_batch": B, "global_batch": B * world, "parallelism": f"dp{world}"},
+                       "per_gpu_batch": B, "global_batch": B * world, "parallelism": f"dp{world}",
+                       "execution": "hipGraph replay" if trainer.graphs else "eager launches"},
             "roofline": roof,
         }
         if world == 1 and not args.no_parity:

@@ -336,9 +336,9 @@ extern "C" int ogv_dwconv3x3_bwd(const void* dy, const void* x, const float* w, 
   }
   if (dw || dbias) {
     OGV_DW_DISPATCH(dw_wgrad_launch, dy, x, part, g, dbias ? 1 : 0, s);
-    colreduce(part, sum10, p.S, dbias ? 10L * C : 9L * C, 10L * C, tmp, s);
+    // tap sums -> sum10[0, 9C) (then untransposed into dw), bias sums straight into dbias
+    colreduce(part, sum10, p.S, dbias ? 10L * C : 9L * C, 10L * C, tmp, s, dbias, 9L * C);
     if (dw) dw_weight_untranspose_kernel<<<cdiv(9 * C, 256), 256, 0, s>>>(sum10, dw, C);
-    if (dbias) (void)hipMemcpyAsync(dbias, sum10 + 9 * (size_t)C, C * sizeof(float), hipMemcpyDeviceToDevice, s);
   }
   return check_launch("ogv_dwconv3x3_bwd");
 }

@@ -264,12 +264,10 @@ extern "C" int ogv_layernorm_bwd(const void* dy, const void* x, const float* gam
   hipStream_t s = as_stream(stream);
   float* part = (float*)ws;
   float* tmp = part + (size_t)nb * 2 * C;
-  float* sums = tmp + colreduce_tmp_floats(nb, 2L * C);
   OGV_LN_DISPATCH(ln_bwd_launch, dy, x, gamma, mean, rstd, dx, part, nb, (long)M, C, s);
-  if (dgamma || dbeta) {
-    colreduce(part, sums, nb, 2L * C, 2L * C, tmp, s);
-    if (dgamma) (void)hipMemcpyAsync(dgamma, sums, C * sizeof(float), hipMemcpyDeviceToDevice, s);
-    if (dbeta) (void)hipMemcpyAsync(dbeta, sums + C, C * sizeof(float), hipMemcpyDeviceToDevice, s);
-  }
+  // partials are [nb][dgamma(C) | dbeta(C)]: reduced straight into the caller's buffers
+  if (dgamma && dbeta) colreduce(part, dgamma, nb, 2L * C, 2L * C, tmp, s, dbeta, C);
+  else if (dgamma) colreduce(part, dgamma, nb, C, 2L * C, tmp, s);
+  else if (dbeta) colreduce(part + C, dbeta, nb, C, 2L * C, tmp, s);
   return check_launch("ogv_layernorm_bwd");
 }

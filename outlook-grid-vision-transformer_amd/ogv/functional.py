@@ -51,13 +51,29 @@ def _ws(nbytes: int, device) -> torch.Tensor:
 _warned_fp16 = False
 
 # ------------------------------------------------------------------------------------------------
-# live kernel probe (bench.py): HIP events on the launching stream around the FIRST launch of a
-# named kernel per step, so its average duration inside the timed region can be reported.
+# live kernel probe (bench.py): HIP events on the launching stream around EVERY launch of a named
+# kernel while armed, each with the launch's algorithmic HBM bytes.  (ROCm graphs
+# cannot hold timing events, so the probe is used on eager launches only.)
 # ------------------------------------------------------------------------------------------------
-_PROBE = {"target": None, "armed": False, "pairs": [], "units": None}
+_PROBE = {"target": None, "armed": False, "recs": []}
+
+
+def probe_bytes(name: str, u: dict) -> int:
+    """Algorithmic bytes of one launch: every operand read once, every result written once."""
+    e = u["elem"]
+    if name == "outlook_fwd":   # read v [M,C] + logits [M,k*k*h], write y [M,C]
+        return e * u["M"] * (2 * u["C"] + u["k"] * u["k"] * u["heads"])
+    if name == "grid_fwd":      # read qkv [M,3C], write out [M,C] + fp32 lse [M,h]
+        return e * u["M"] * 4 * u["C"] + 4 * u["M"] * u["heads"]
+    if name == "gemm_fwd":      # read A [M,K] (+ residual [M,N]) + fp32 W [N,K] (+ bias), write out [M,N]
+        return (e * u["M"] * (u["K"] + u["N"] * (2 if u["res"] else 1)) + 4 * u["N"] * u["K"]
+                + (4 * u["N"] if u["bias"] else 0))
+    raise KeyError(name)
 
 
 def probe_arm(target: str):
+    if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+        raise RuntimeError("ogv probe: timing events cannot be recorded into a ROCm graph")
     _PROBE["target"], _PROBE["armed"] = target, True
 
 
@@ -69,10 +85,9 @@ class _probe:
     def __init__(self, name, units):
         self.on = _PROBE["armed"] and _PROBE["target"] == name
         if self.on:
-            _PROBE["armed"] = False           # first launch of the step only
-            _PROBE["units"] = units
             self.e0 = torch.cuda.Event(enable_timing=True)
             self.e1 = torch.cuda.Event(enable_timing=True)
+            self.nbytes = probe_bytes(name, units)
 
     def __enter__(self):
         if self.on:
@@ -82,22 +97,25 @@ class _probe:
     def __exit__(self, *a):
         if self.on:
             self.e1.record()
-            _PROBE["pairs"].append((self.e0, self.e1))
+            _PROBE["recs"].append((self.e0, self.e1, self.nbytes))
         return False
 
 
 def probe_results():
-    """(mean ms per probed launch, units of the last probed launch, n)."""
-    pairs = _PROBE["pairs"]
-    if not pairs:
-        return None, None, 0
+    """{n, avg_ms, bytes_per_launch, achieved_GBs} over the recorded launches, or None."""
+    recs = _PROBE["recs"]
+    if not recs:
+        return None
     torch.cuda.synchronize()
-    ms = [a.elapsed_time(b) for a, b in pairs]
-    return sum(ms) / len(ms), _PROBE["units"], len(ms)
+    ms = [a.elapsed_time(b) for a, b, _ in recs]
+    nbytes = sum(r[2] for r in recs)
+    tot = sum(ms)
+    return {"n": len(recs), "avg_ms": tot / len(recs), "bytes_per_launch": nbytes / len(recs),
+            "achieved_GBs": nbytes / (tot * 1e-3) / 1e9 if tot > 0 else None}
 
 
 def probe_reset():
-    _PROBE["pairs"] = []
+    _PROBE["recs"] = []
 
 
 def compute_dtype(x: torch.Tensor) -> torch.dtype:
@@ -157,8 +175,10 @@ class _Linear(torch.autograd.Function):
         M, K = x2d.shape
         N = w2d.shape[0]
         out = torch.empty((M, N), dtype=x2d.dtype, device=x2d.device)
-        check(lib.ogv_gemm_fwd(_ptr(x2d), x2d.stride(0), _ptr(w2d), _ptr(bias), _ptr(residual), _ptr(row_scale),
-                               int(rps), _ptr(out), N, M, N, K, ACT[act_in], _dt(x2d), _stream()), "ogv_gemm_fwd")
+        with _probe("gemm_fwd", dict(M=M, N=N, K=K, elem=x2d.element_size(), res=residual is not None,
+                                     bias=bias is not None)):
+            check(lib.ogv_gemm_fwd(_ptr(x2d), x2d.stride(0), _ptr(w2d), _ptr(bias), _ptr(residual), _ptr(row_scale),
+                                   int(rps), _ptr(out), N, M, N, K, ACT[act_in], _dt(x2d), _stream()), "ogv_gemm_fwd")
         ctx.save_for_backward(x2d, w2d, row_scale)
         ctx.meta = (M, N, K, int(rps), ACT[act_in], bias is not None, residual is not None)
         return out

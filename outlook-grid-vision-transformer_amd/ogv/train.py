@@ -11,10 +11,17 @@ The reference loop syncs the host ~5x per step (isfinite, float(gnorm), .item()s
 no host syncs: the grad-norm stays on device (clip_grad_norm_ foreach path) and the loss is
 returned as a device tensor.
 
+Execution: the whole step is captured once as a hipGraph (torch.cuda.CUDAGraph) and replayed,
+so ~1200 kernel launches per step cost one graph launch instead of ~1200 Python/HIP launches.
+The learning rate lives in a device tensor the schedule updates before each replay.
+
 Data parallelism (the reference has none): one process per GPU, torch.distributed with the
-"nccl" backend (= RCCL on ROCm) over xGMI; DistributedDataParallel buckets the fp32 gradients
-(7.5 M params = 30 MB for Model-A-7M) and all-reduces them during backward.  Each rank keeps its
-own BatchNorm batch statistics (DDP default).
+"nccl" backend (= RCCL on ROCm) over xGMI.  The step is split at the one exchange the path has:
+graph A = fwd + bwd + flatten of the fp32 gradients into ONE bucket (7.5 M params = 30 MB for
+Model-A-7M, pre-divided by world size); one all_reduce of that bucket (a single large ring
+collective: xGMI links are point-to-point, so one 30 MB message beats many small DDP buckets);
+graph B = unflatten + clip_grad_norm + AdamW.  Parameters and buffers are broadcast from rank 0
+once at start; each rank keeps its own BatchNorm batch statistics.
 """
 from __future__ import annotations
 
@@ -82,7 +89,7 @@ class WarmupCosineLR:
     def __init__(self, optimizer, total_steps: int, warmup_steps: int, min_lr: float = 0.0):
         self.optimizer = optimizer
         self.total_steps, self.warmup_steps, self.min_lr = int(total_steps), int(warmup_steps), float(min_lr)
-        self.base_lrs = [g["lr"] for g in optimizer.param_groups]
+        self.base_lrs = [float(g["lr"]) for g in optimizer.param_groups]
         self.step_num = 0
 
     def lr_at(self, t: int, base: float) -> float:
@@ -94,7 +101,11 @@ class WarmupCosineLR:
     def step(self):
         self.step_num += 1
         for g, base in zip(self.optimizer.param_groups, self.base_lrs):
-            g["lr"] = self.lr_at(self.step_num, base)
+            v = self.lr_at(self.step_num, base)
+            if isinstance(g["lr"], torch.Tensor):
+                g["lr"].fill_(v)      # device-resident lr read by the captured AdamW
+            else:
+                g["lr"] = v
 
     def state_dict(self):
         return {"step_num": self.step_num}
@@ -131,27 +142,130 @@ def wrap_ddp(model: nn.Module, device, bucket_cap_mb: float = 8.0):
 
 
 # ------------------------------------------------------------------------------- step
+def _dist_world():
+    if torch.distributed.is_available() and torch.distributed.is_initialized():
+        return torch.distributed.get_world_size()
+    return 1
+
+
 class Trainer:
-    """Holds model/optimizer/schedule; ``step(x, y)`` is one full training iteration."""
+    """Holds model/optimizer/schedule; ``step(x, y)`` is one full training iteration.
+
+    ``graphs=True`` (HIP device only): the first ``capture_warmup`` calls run eagerly, the next one
+    runs eagerly on a side stream and records the step into hipGraphs, every later call replays
+    them (inputs are copied into the recorded x / y tensors when other tensors are passed).
+    With world_size > 1 gradients are averaged by one all_reduce of a flat bucket (see module doc);
+    pass the bare model (not DDP-wrapped)."""
 
     def __init__(self, model: nn.Module, lr=5e-4, weight_decay=0.05, clip=1.0, label_smoothing=0.1,
-                 total_steps=10_000, warmup_ratio=0.05, min_lr=1e-6, amp_dtype: Optional[torch.dtype] = torch.bfloat16):
+                 total_steps=10_000, warmup_ratio=0.05, min_lr=1e-6, amp_dtype: Optional[torch.dtype] = torch.bfloat16,
+                 graphs: bool = False, capture_warmup: int = 3, capture_hook=None):
         self.model = model
         core = model.module if hasattr(model, "module") else model
-        fused = next(core.parameters()).is_cuda
-        self.opt = torch.optim.AdamW(param_groups_no_wd(core, weight_decay), lr=lr, fused=fused)
+        self.ddp = core is not model
+        dev = next(core.parameters()).device
+        fused = dev.type == "cuda"
+        self.graphs = bool(graphs) and fused
+        lr0 = torch.tensor(float(lr), device=dev) if self.graphs else lr
+        self.opt = torch.optim.AdamW(param_groups_no_wd(core, weight_decay), lr=lr0, fused=fused,
+                                     capturable=self.graphs)
         self.sched = WarmupCosineLR(self.opt, total_steps, int(warmup_ratio * total_steps), min_lr)
         self.params = [p for p in core.parameters() if p.requires_grad]
         self.clip, self.ls, self.amp_dtype = clip, label_smoothing, amp_dtype
+        self.world = 1 if self.ddp else _dist_world()
+        self.capture_warmup = int(capture_warmup)
+        self.capture_hook = capture_hook          # called right before recording starts
+        self._eager_steps = 0
+        self._g = None
+        if self.world > 1:
+            self._sizes = [p.numel() for p in self.params]
+            self.flat = torch.zeros(sum(self._sizes), device=dev, dtype=torch.float32)
+            with torch.no_grad():   # identical start on every rank (what DDP's constructor does)
+                for t in list(core.parameters()) + list(core.buffers()):
+                    torch.distributed.broadcast(t.data, 0)
 
-    def step(self, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
-        self.opt.zero_grad(set_to_none=True)
-        with torch.autocast("cuda", dtype=self.amp_dtype or torch.float32, enabled=self.amp_dtype is not None):
+    # -- pieces of one step -------------------------------------------------------------------
+    def _fwd_bwd(self, x, y):
+        with torch.autocast("cuda", dtype=self.amp_dtype or torch.float32, enabled=self.amp_dtype is not None,
+                            cache_enabled=not self.graphs):
             logits = self.model(x)
         loss = F.cross_entropy(logits.float(), y, label_smoothing=self.ls)
         loss.backward()
+        return loss.detach()
+
+    def _flatten(self):
+        grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in self.params]
+        torch.cat([g.reshape(-1) for g in grads], out=self.flat)
+        self.flat.mul_(1.0 / self.world)
+
+    def _unflatten(self):
+        views = [v.view_as(p) for v, p in zip(self.flat.split(self._sizes), self.params)]
+        for p, v in zip(self.params, views):
+            if p.grad is None:
+                p.grad = torch.empty_like(p)
+        torch._foreach_copy_([p.grad for p in self.params], views)
+
+    def _update(self):
         if self.clip is not None:
             torch.nn.utils.clip_grad_norm_(self.params, self.clip, foreach=True)
         self.opt.step()
+
+    def _allreduce(self):
+        torch.distributed.all_reduce(self.flat)
+
+    def _eager(self, x, y):
+        self.opt.zero_grad(set_to_none=True)
+        loss = self._fwd_bwd(x, y)
+        if self.world > 1:
+            self._flatten()
+            self._allreduce()
+            self._unflatten()
+        self._update()
+        return loss
+
+    def _capture(self, x, y):
+        """This call's update runs eagerly on a side stream (allocator / library warm-up, as graph
+        capture requires); then the step is recorded — recording executes nothing."""
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            loss = self._eager(x, y)
+        torch.cuda.current_stream().wait_stream(side)
+        loss = loss.clone()
+        self.opt.zero_grad(set_to_none=True)
+        self._x, self._y = x, y
+        if self.capture_hook is not None:
+            self.capture_hook()
+        pool = torch.cuda.graph_pool_handle()
+        self._g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self._g, pool=pool):
+            self._loss = self._fwd_bwd(x, y)
+            if self.world > 1:
+                self._flatten()
+            else:
+                self._update()
+        self.graph_grads = [p.grad for p in self.params]   # the tensors the replays write
+        if self.world > 1:
+            self._g2 = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self._g2, pool=pool):
+                self._unflatten()
+                self._update()
+        return loss
+
+    def step(self, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+        if not self.graphs or (self._g is None and self._eager_steps < self.capture_warmup):
+            self._eager_steps += 1
+            loss = self._eager(x, y)
+        elif self._g is None:
+            loss = self._capture(x, y)
+        else:
+            if x is not self._x or y is not self._y:
+                self._x.copy_(x)
+                self._y.copy_(y)
+            self._g.replay()
+            if self.world > 1:
+                self._allreduce()
+                self._g2.replay()
+            loss = self._loss
         self.sched.step()
-        return loss.detach()
+        return loss

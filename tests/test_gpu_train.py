@@ -1,0 +1,157 @@
+"""Training step on the MI355X: hipGraph replay (bench.py's execution mode) vs eager launches.
+
+Replay must reproduce the eager trajectory: same losses and parameters after several steps
+(DropPath off so both paths draw no random numbers; all ogv kernels are deterministic).
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+# Layers outside the OutGridBlocks still on MIOpen (stock torch ops): their bf16 conv weight
+# gradients are not bitwise reproducible run to run (measured up to ~1-2% of the tensor's max
+# on the stem conv), so replay-vs-eager compares them at that level; ogv kernels are
+# deterministic and held to 1e-3.
+MIOPEN_PARAMS = ("stem.", "proj_in.", "downs.", "head_norm.")
+MIOPEN_TOL = 3e-2
+
+
+@pytest.fixture(autouse=True, scope="module")
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import ogv
+    ogv.load()
+
+
+def _model(seed):
+    from ogv.train import MODEL_CONFIGS, build_model
+    cfg = MODEL_CONFIGS["model_a_7m"]
+    torch.manual_seed(seed)
+    m = build_model(dict(type="model_a", num_classes=cfg["num_classes"], stem_dim=cfg["stem_dim"], dpr_max=0.0,
+                         stages=cfg["stages"]))
+    return m.cuda().to(memory_format=torch.channels_last)
+
+
+def _snapshot(model, opt):
+    st = [t.detach().clone() for t in list(model.parameters()) + list(model.buffers())]
+    ost = [{k: v.clone() for k, v in opt.state[p].items()} for g in opt.param_groups for p in g["params"]]
+    lrs = [g["lr"].clone() for g in opt.param_groups]
+    return st, ost, lrs
+
+
+def _restore(model, opt, snap):
+    st, ost, lrs = snap
+    with torch.no_grad():
+        for t, s in zip(list(model.parameters()) + list(model.buffers()), st):
+            t.copy_(s)
+        for (p, d) in zip([p for g in opt.param_groups for p in g["params"]], ost):
+            for k, v in d.items():
+                opt.state[p][k].copy_(v)
+        for g, l in zip(opt.param_groups, lrs):
+            g["lr"].copy_(l)
+
+
+def _batch(B, seed):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    x = torch.randn(B, 3, 32, 32, device="cuda", generator=g).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 100, (B,), device="cuda", generator=g)
+    return x, y
+
+
+def test_graph_replay_matches_eager_step():
+    """Each replayed step == an eager step taken from the identical training state (params,
+    BatchNorm buffers, AdamW moments, device lr), for several consecutive replays: same loss,
+    same clipped gradients, same update.  (Two independently trained copies are not comparable:
+    MIOpen's conv weight-gradient for the stem / downsample convs is not bitwise deterministic and
+    Adam's first steps amplify last-bit gradient noise into sign flips.)"""
+    from ogv.train import Trainer
+    torch.backends.cudnn.benchmark = False
+    x, y = _batch(16, 3)
+    m = _model(11)
+    t = Trainer(m, total_steps=50, warmup_ratio=0.1, graphs=True, capture_warmup=1)
+    l0 = t.step(x, y).float().item()      # eager
+    t.step(x, y)                          # eager on the side stream + capture
+    assert t._g is not None, "graph was not captured"
+    names = [n for n, _ in m.named_parameters()]
+    losses = []
+    for k in range(3):
+        snap = _snapshot(m, t.opt)
+        loss_r = t.step(x, y).float().item()  # replay
+        g_r = [g.detach().clone() for g in t.graph_grads]
+        p_r = [p.detach().clone() for p in m.parameters()]
+        b_r = [b.detach().clone() for b in m.buffers()]
+        _restore(m, t.opt, snap)
+        loss_e = t._eager(x, y).float().item()
+        losses.append(loss_e)
+        assert abs(loss_r - loss_e) <= 1e-6 * max(1.0, abs(loss_e)), (k, loss_r, loss_e)
+        for n, gr, p in zip(names, g_r, m.parameters()):
+            ge = p.grad.detach()
+            scale = max(float(ge.abs().max()), 1e-12)
+            err = float((gr - ge).abs().max())
+            tol = MIOPEN_TOL if n.startswith(MIOPEN_PARAMS) else 1e-3
+            assert err <= tol * scale, f"replay {k}: grad {n} max|d|={err:.3e} scale={scale:.3e}"
+        for n, pr, p in zip(names, p_r, m.parameters()):
+            # Adam turns last-bit gradient noise on near-zero gradients into sign flips: bound by
+            # one lr step either way
+            err = float((pr - p.detach()).abs().max())
+            assert err <= 2 * float(t.opt.param_groups[0]["lr"]) + 1e-7, f"replay {k}: param {n} max|d|={err:.3e}"
+        for (n, b), br in zip(m.named_buffers(), b_r):
+            torch.testing.assert_close(br.float(), b.detach().float(), rtol=1e-5, atol=1e-6,
+                                       msg=lambda s: f"replay {k}: {n}: {s}")
+    assert losses[-1] < l0, (l0, losses)
+
+
+def test_graph_replay_takes_new_inputs():
+    """Passing a different batch to a captured step copies it into the recorded inputs: the
+    replayed loss equals the eager forward loss of that batch at the same parameters."""
+    import torch.nn.functional as F
+    from ogv.train import Trainer
+    batches = [_batch(8, 5), _batch(8, 6)]
+    m = _model(2)
+    t = Trainer(m, total_steps=50, graphs=True, capture_warmup=0)
+    t.step(*batches[0])                   # capture with batch 0
+    for i in (1, 0, 1):
+        x, y = batches[i]
+        with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+            ref = F.cross_entropy(m(x).float(), y, label_smoothing=0.1).item()
+        got = t.step(x, y).float().item()
+        assert abs(got - ref) <= 1e-5 * max(1.0, abs(ref)), (i, got, ref)
+
+
+def _dp_worker(rank, world, port, out):
+    import os
+    import torch.distributed as dist
+    from ogv.train import Trainer
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import ogv
+    ogv.load()
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.backends.cudnn.benchmark = False
+        m = _model(11 + rank)                 # different init: the rank-0 broadcast must fix it
+        t = Trainer(m, total_steps=50, graphs=True, capture_warmup=1)
+        assert t.world == world
+        x, y = _batch(8, 40 + rank)           # per-rank shard
+        losses = [t.step(x, y).float().item() for _ in range(4)]   # eager, capture, replay, replay
+        torch.save({"params": [p.detach().cpu() for p in m.parameters()], "losses": losses}, f"{out}/r{rank}.pt")
+    finally:
+        dist.destroy_process_group()
+
+
+def test_graph_dp_world2_ranks_agree(tmp_path):
+    """world_size 2 on one GPU (gloo carries the all_reduce; RCCL needs one GPU per rank): graph A
+    (fwd+bwd+flatten), all_reduce of the flat bucket, graph B (unflatten+clip+AdamW) keep the two
+    ranks' parameters identical while each rank trains on its own shard."""
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    mp.spawn(_dp_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    r0 = torch.load(tmp_path / "r0.pt", weights_only=True)
+    r1 = torch.load(tmp_path / "r1.pt", weights_only=True)
+    assert r0["losses"] != r1["losses"], "ranks saw the same data"
+    assert all(l == l for l in r0["losses"] + r1["losses"]), "non-finite loss"
+    for a, b in zip(r0["params"], r1["params"]):
+        assert torch.equal(a, b), "ranks diverged"

@@ -166,6 +166,52 @@ int ogv_mbconv_bwd(const void* dout, const void* x, const void* saved, void* dx,
                    void* ws, const ogv_mbconv_desc* desc, const ogv_mbconv_params* params, ogv_dtype dt,
                    void* stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * MaxOutNet around the blocks: 3x3 convolution (padding 1, stride 1|2) -> BatchNorm2d -> act on
+ * NHWC rows.  Replaces the stem  Conv2d(in, stem, 3, 1, 1) + BN + SiLU  (src/model/stem_head.py:
+ * 23-32) and Downsample(kind="conv")  Conv2d(C, C', 3, 2, 1) + BN + SiLU  (src/model/
+ * downsampling.py:28-65).  The convolution is an implicit GEMM on MFMA (tap-major K = 9*Cin);
+ * BatchNorm follows nn.BatchNorm2d (train: biased batch variance for the normalisation, running
+ * statistics updated with momentum and the unbiased variance; eval: running statistics).
+ * x: [B*H*W, Cin] rows -> out: [B*Ho*Wo, Cout], Ho = (H-1)/stride + 1.  w: fp32 [Cout, Cin, 3, 3],
+ * bias nullable (present when use_bn=False).  has_bn=0 skips the BatchNorm (bn_* ignored).
+ * bwd: dx nullable (the stem's input needs no gradient); dw fp32 [Cout, Cin, 3, 3], dbias,
+ * dbn_w, dbn_b fp32 [Cout] nullable, all overwritten.  num_batches_tracked is left to the caller.
+ * ------------------------------------------------------------------------------------------- */
+typedef struct {
+  int B, H, W, Cin, Cout, stride;
+  int has_bn, train;
+  float bn_eps, bn_momentum;
+  int act;
+} ogv_convbn_desc;
+
+typedef struct {
+  const float* w;                                   /* [Cout, Cin, 3, 3] */
+  const float* bias;                                /* [Cout] or NULL */
+  const float *bn_w, *bn_b; float *bn_rm, *bn_rv;   /* [Cout] */
+} ogv_convbn_params;
+
+size_t ogv_convbn_saved_bytes(const ogv_convbn_desc* desc, ogv_dtype dt);
+size_t ogv_convbn_ws_bytes(const ogv_convbn_desc* desc, ogv_dtype dt);
+int ogv_convbn_fwd(const void* x, void* out, void* saved, void* ws, const ogv_convbn_desc* desc,
+                   const ogv_convbn_params* params, ogv_dtype dt, void* stream);
+int ogv_convbn_bwd(const void* dout, const void* x, const void* saved, void* dx, float* dw, float* dbias,
+                   float* dbn_w, float* dbn_b, void* ws, const ogv_convbn_desc* desc,
+                   const ogv_convbn_params* params, ogv_dtype dt, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * BatchNorm2d (+ act) alone on [M, C] NHWC rows: MaxOutNet.head_norm (src/Model_A_OutGridNet.py:
+ * 52,66; act NONE).  saved (>= ogv_bn_act_saved_bytes(C)) keeps mean/invstd/scale/shift for bwd.
+ * ------------------------------------------------------------------------------------------- */
+size_t ogv_bn_act_saved_bytes(int C);
+size_t ogv_bn_act_ws_bytes(int M, int C);
+int ogv_bn_act_fwd(const void* x, void* out, float* saved, void* ws, const float* bn_w, const float* bn_b,
+                   float* running_mean, float* running_var, int M, int C, int train, float eps,
+                   float momentum, int act, ogv_dtype dt, void* stream);
+int ogv_bn_act_bwd(const void* dout, const void* x, const float* saved, void* dx, float* dbn_w, float* dbn_b,
+                   void* ws, const float* bn_w, int M, int C, int train, int act, ogv_dtype dt,
+                   void* stream);
+
 /* Elementwise helpers used by the autograd glue. */
 int ogv_cast(const void* src, ogv_dtype src_dt, void* dst, ogv_dtype dst_dt, size_t n, void* stream);
 

@@ -34,6 +34,8 @@ size_t colreduce_tmp_floats(long R, long n);
 // dst[j] = sum_r src[r*ld + j] for j < n; with dst2, columns j >= n1 go to dst2[j - n1] instead.
 void colreduce(const float* src, float* dst, long R, long n, long ld, float* tmp, hipStream_t s,
                float* dst2 = nullptr, long n1 = 0);
+// fp64 variant (BatchNorm batch statistics); tmp needs colreduce_tmp_floats(R, n) doubles
+void colreduce(const double* src, double* dst, long R, long n, long ld, double* tmp, hipStream_t s);
 
 static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 static inline unsigned cdiv(long a, long b) { return (unsigned)((a + b - 1) / b); }

@@ -14,20 +14,19 @@ namespace ogv {
 
 // ------------------------------------------------------------------ column reducer
 // dst[j] (+)= sum_r src[r*ld + j], j < n.  Block = 64 columns x 4 row lanes; grid.y splits rows.
-__global__ __launch_bounds__(256) void colreduce_kernel(const float* __restrict__ src, float* __restrict__ dst, long R,
-                                                        long n, long ld, long rows_per_chunk, float* __restrict__ dst2,
-                                                        long n1) {
-  __shared__ float red[4][64];
+template <typename T>
+__global__ __launch_bounds__(256) void colreduce_kernel(const T* __restrict__ src, T* __restrict__ dst, long R, long n,
+                                                        long ld, long rows_per_chunk, T* __restrict__ dst2, long n1) {
+  __shared__ T red[4][64];
   const int cx = threadIdx.x & 63, ry = threadIdx.x >> 6;
   const long j = (long)blockIdx.x * 64 + cx;
   const long r0 = (long)blockIdx.y * rows_per_chunk;
   const long r1 = r0 + rows_per_chunk < R ? r0 + rows_per_chunk : R;
-  float acc = 0.f;
+  T acc = 0;
   if (j < n) {
     long r = r0 + ry;
     for (; r + 12 < r1; r += 16) {
-      const float a = src[r * ld + j], b = src[(r + 4) * ld + j], c = src[(r + 8) * ld + j],
-                  d = src[(r + 12) * ld + j];
+      const T a = src[r * ld + j], b = src[(r + 4) * ld + j], c = src[(r + 8) * ld + j], d = src[(r + 12) * ld + j];
       acc += (a + b) + (c + d);
     }
     for (; r < r1; r += 4) acc += src[r * ld + j];
@@ -35,7 +34,7 @@ __global__ __launch_bounds__(256) void colreduce_kernel(const float* __restrict_
   red[ry][cx] = acc;
   __syncthreads();
   if (ry == 0 && j < n) {
-    const float s = (red[0][cx] + red[1][cx]) + (red[2][cx] + red[3][cx]);
+    const T s = (red[0][cx] + red[1][cx]) + (red[2][cx] + red[3][cx]);
     if (dst2 && j >= n1) dst2[j - n1] = s;  // single-pass split destination (gridDim.y == 1)
     else dst[(long)blockIdx.y * n + j] = s;
   }
@@ -49,20 +48,27 @@ size_t colreduce_tmp_floats(long R, long n) {
   return (size_t)(chunks < 64 ? chunks : 64) * n;
 }
 
-void colreduce(const float* src, float* dst, long R, long n, long ld, float* tmp, hipStream_t s, float* dst2,
-               long n1) {
+template <typename T>
+static void colreduce_t(const T* src, T* dst, long R, long n, long ld, T* tmp, hipStream_t s, T* dst2, long n1) {
   const unsigned gx = (unsigned)((n + 63) / 64);
   if (!dst2) n1 = n;
   if (R <= 256) {
-    colreduce_kernel<<<dim3(gx, 1), 256, 0, s>>>(src, dst, R, n, ld, R, dst2, n1);
+    colreduce_kernel<T><<<dim3(gx, 1), 256, 0, s>>>(src, dst, R, n, ld, R, dst2, n1);
     return;
   }
   long chunks = (R + 255) / 256;
   if (chunks > 64) chunks = 64;
   const long per = (R + chunks - 1) / chunks;
   chunks = (R + per - 1) / per;
-  colreduce_kernel<<<dim3(gx, (unsigned)chunks), 256, 0, s>>>(src, tmp, R, n, ld, per, nullptr, n);
-  colreduce_kernel<<<dim3(gx, 1), 256, 0, s>>>(tmp, dst, chunks, n, n, chunks, dst2, n1);
+  colreduce_kernel<T><<<dim3(gx, (unsigned)chunks), 256, 0, s>>>(src, tmp, R, n, ld, per, nullptr, n);
+  colreduce_kernel<T><<<dim3(gx, 1), 256, 0, s>>>(tmp, dst, chunks, n, n, chunks, dst2, n1);
+}
+void colreduce(const float* src, float* dst, long R, long n, long ld, float* tmp, hipStream_t s, float* dst2,
+               long n1) {
+  colreduce_t<float>(src, dst, R, n, ld, tmp, s, dst2, n1);
+}
+void colreduce(const double* src, double* dst, long R, long n, long ld, double* tmp, hipStream_t s) {
+  colreduce_t<double>(src, dst, R, n, ld, tmp, s, nullptr, n);
 }
 
 // ------------------------------------------------------------------ depthwise conv kernels

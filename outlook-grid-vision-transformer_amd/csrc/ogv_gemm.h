@@ -17,9 +17,9 @@ struct Pro {
 };
 
 // Epilogue: out = res + rs[m/rps] * (acc + bias[n]);  out *= act'(Z[m,n]) (zact);
-// optional per-column batch statistics of the stored (rounded) output:
+// optional per-column batch statistics of the stored (rounded) output, accumulated in fp64:
 //   stat[mt][0][n] = sum_rows (out - shift[n]),  stat[mt][1][n] = sum_rows (out - shift[n])^2
-// for each 128-row panel mt (deterministic partials; reduce with colreduce).
+// for each 128-row panel mt (deterministic partials; reduce with the fp64 colreduce).
 struct Epi {
   const float* bias = nullptr;
   const void* res = nullptr;
@@ -27,9 +27,50 @@ struct Epi {
   int rps = 1;
   const void* Z = nullptr;
   int ldz = 0, zact = 0;
-  float* stat = nullptr;
+  double* stat = nullptr;
   const float* stat_shift = nullptr;
 };
+
+// Implicit-GEMM gather for 3x3 / pad-1 convolutions.  The A operand (or the wgrad X operand) is
+// not a dense matrix but rows m = (b*Hr + ry)*Wr + rx of a row grid, and tap-major columns
+// k = tap*Cs + c (tap = 3*ky + kx) that read source pixel (sy, sx) channel c:
+//   forward   (transposed = 0): sy = ry*stride - 1 + ky                       (conv fwd)
+//   transposed(transposed = 1): sy = (ry + 1 - ky) / stride when exact         (conv dgrad)
+// and zero outside the source image.  With Cs % 8 == 0 an 8-wide k chunk is one 16-B load.
+struct ConvG {
+  int Hr = 0, Wr = 0;          // row grid
+  int Hs = 0, Ws = 0, Cs = 0;  // source grid / channels
+  int stride = 1, transposed = 0;
+};
+struct ConvRow {
+  int b, ry, rx;
+};
+__device__ __forceinline__ ConvRow conv_row(const ConvG& g, int m) {
+  ConvRow r;
+  const int hw = g.Hr * g.Wr;
+  r.b = m / hw;
+  const int rem = m - r.b * hw;
+  r.ry = rem / g.Wr;
+  r.rx = rem - r.ry * g.Wr;
+  return r;
+}
+// element offset of source pixel for (row, tap), or -1 when it is padding / not hit by the stride
+__device__ __forceinline__ long conv_src(const ConvG& g, const ConvRow& r, int tap) {
+  const int ky = tap / 3, kx = tap - 3 * ky;
+  int sy, sx;
+  if (!g.transposed) {
+    sy = r.ry * g.stride - 1 + ky;
+    sx = r.rx * g.stride - 1 + kx;
+  } else {
+    const int ny = r.ry + 1 - ky, nx = r.rx + 1 - kx;
+    if (ny < 0 || nx < 0) return -1;
+    sy = ny / g.stride;
+    sx = nx / g.stride;
+    if (sy * g.stride != ny || sx * g.stride != nx) return -1;
+  }
+  if (sy < 0 || sy >= g.Hs || sx < 0 || sx >= g.Ws) return -1;
+  return ((long)(r.b * g.Hs + sy) * g.Ws + sx) * g.Cs;
+}
 
 constexpr int GEMM_BM = 128;
 inline int gemm_stat_rows(int M) { return (M + GEMM_BM - 1) / GEMM_BM; }
@@ -47,6 +88,13 @@ void gemm_dgrad_launch(ogv_dtype dt, const void* dout, int ldd, const float* W, 
 // dW[N,K] = sum_m rs*G[m,n] * pro(X)[m,k];  dbias[n] = sum_m rs*G[m,n]
 size_t wgrad_ws_bytes(int M, int N, int K);
 void gemm_wgrad_launch(ogv_dtype dt, const void* G, int ldg, const void* X, int ldx, const Pro& pro, const float* rs,
-                       int rps, float* dW, float* dbias, int M, int N, int K, void* ws, hipStream_t s);
+                       int rps, float* dW, float* dbias, int M, int N, int K, void* ws, hipStream_t s,
+                       const ConvG* xconv = nullptr);
+
+// Implicit-GEMM 3x3 conv:  out[M, N] = epi( gather(A)[M, 9*Cs] . Wt[N, 9*Cs]^T ),  M = B*Hr*Wr.
+// Wt is tap-major ([N][tap][Cs]).  Used for the conv forward (cv.transposed = 0) and its data
+// gradient (cv.transposed = 1, Wt = the tap-major transposed weights).
+void conv_gemm_launch(ogv_dtype dt, const void* A, const ConvG& cv, const float* Wt, void* out, int M, int N,
+                      const Epi& epi, hipStream_t s);
 
 }  // namespace ogv

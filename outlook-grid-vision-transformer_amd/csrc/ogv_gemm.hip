@@ -63,8 +63,8 @@ __device__ __forceinline__ void pro_apply_run(const Pro& p, float (&v)[E], int m
 // Each thread holds rows 4*(lane>>4)+r (+16*i) of columns (lane&15) (+16*j); sums over its rows,
 // then across the 4 lane groups (xor 16, 32), then across the two M-waves through LDS.
 template <int TN, int WN, int BN>
-__device__ __forceinline__ void stats_store(float (&s1)[TN], float (&s2)[TN], float* lds, int wm, int wn, int lane,
-                                            float* stat, int mt, int n0, int N) {
+__device__ __forceinline__ void stats_store(double (&s1)[TN], double (&s2)[TN], double* lds, int wm, int wn,
+                                            int lane, double* stat, int mt, int n0, int N) {
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     s1[j] += __shfl_xor(s1[j], 16, 64);
@@ -115,13 +115,14 @@ __device__ __forceinline__ void gemm_epilogue_bf16(f32x4 (&acc)[TM][TN], float* 
   const bool vec = full && (ldo & 7) == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0 &&
                    (!res || (reinterpret_cast<uintptr_t>(res) & 15) == 0) &&
                    (!epi.zact || ((epi.ldz & 7) == 0 && (reinterpret_cast<uintptr_t>(Z) & 15) == 0));
-  float bias[8], shift[8], s1[8], s2[8];
+  float bias[8], shift[8];
+  double s1[8], s2[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     bias[q] = (epi.bias && n + q < N) ? epi.bias[n + q] : 0.f;
     shift[q] = (STATS && epi.stat_shift && n + q < N) ? epi.stat_shift[n + q] : 0.f;
-    s1[q] = 0.f;
-    s2[q] = 0.f;
+    s1[q] = 0.0;
+    s2[q] = 0.0;
   }
   __syncthreads();  // main-loop LDS tiles are dead
 #pragma unroll
@@ -180,9 +181,9 @@ __device__ __forceinline__ void gemm_epilogue_bf16(f32x4 (&acc)[TM][TN], float* 
         if constexpr (STATS) {
 #pragma unroll
           for (int q = 0; q < 8; ++q) {
-            const float d = n + q < N ? (float)ob[q] - shift[q] : 0.f;
+            const double d = n + q < N ? (double)(float)ob[q] - (double)shift[q] : 0.0;
             s1[q] += d;
-            s2[q] = fmaf(d, d, s2[q]);
+            s2[q] = fma(d, d, s2[q]);
           }
         }
       }
@@ -203,7 +204,7 @@ __device__ __forceinline__ void gemm_epilogue_bf16(f32x4 (&acc)[TM][TN], float* 
     __syncthreads();
     // [wm][2][BN] partials; lanes < LPR hold their wave's column sums
     constexpr int BN = 2 * WN;
-    float* red = stage_all;
+    double* red = reinterpret_cast<double*>(stage_all);  // 4 x BN doubles
     if (lane < LPR) {
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
@@ -228,11 +229,11 @@ __device__ __forceinline__ void gemm_epilogue_bf16(f32x4 (&acc)[TM][TN], float* 
 // ------------------------------------------------------------------------------------------------
 // fwd / dgrad kernel, bf16
 // ------------------------------------------------------------------------------------------------
-template <int BM, int BN, bool PRO, bool STATS>
+template <int BM, int BN, bool PRO, bool STATS, int AM = 0>
 __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__ A, int lda, Pro pro,
                                                         const float* __restrict__ Wt, int ldw, Epi epi,
                                                         bf16* __restrict__ out, int ldo, int M, int N, int K, int Ka,
-                                                        int Kb, int nMt, int nNt) {
+                                                        int Kb, int nMt, int nNt, ConvG cv) {
   constexpr int BK = 32;
   constexpr int PITCH = BK + 8;  // 80-byte rows: 16-B aligned fragment reads
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
@@ -262,12 +263,39 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
   float4 rb[B_F4];
   const bool a_vec = ((lda & 7) == 0) && ((reinterpret_cast<uintptr_t>(A) & 15) == 0);
   const bool b_vec = ((ldw & 3) == 0) && ((reinterpret_cast<uintptr_t>(Wt) & 15) == 0);
+  ConvRow crow[AM ? A_VECS : 1];
+  const bool c_vec = AM && (cv.Cs & 7) == 0 && ((reinterpret_cast<uintptr_t>(A) & 15) == 0);
+  if constexpr (AM != 0) {
+#pragma unroll
+    for (int i = 0; i < A_VECS; ++i) {
+      const int gm = m0 + (tid + i * 256) / (BK / 8);
+      crow[i] = conv_row(cv, gm < M ? gm : 0);  // rows are fixed per thread across the K loop
+    }
+  }
   auto load_tile = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < A_VECS; ++i) {
       const int idx = tid + i * 256, row = idx / (BK / 8), kv = idx % (BK / 8);
       const int gm = m0 + row, gk = k0 + kv * 8;
       ra[i] = uint4{0u, 0u, 0u, 0u};
+      if constexpr (AM != 0) {
+        if (gm < M && gk < Ka) {
+          if (c_vec) {
+            const int tap = gk / cv.Cs;
+            const long off = conv_src(cv, crow[i], tap);
+            if (off >= 0) ra[i] = *reinterpret_cast<const uint4*>(A + off + (gk - tap * cv.Cs));
+          } else {
+            bf16* e = reinterpret_cast<bf16*>(&ra[i]);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+              const int k = gk + q, tap = k / cv.Cs;
+              const long off = k < Ka ? conv_src(cv, crow[i], tap) : -1;
+              e[q] = off >= 0 ? A[off + (k - tap * cv.Cs)] : (bf16)0.f;
+            }
+          }
+        }
+        continue;
+      }
       if (gm < M) {
         const bf16* src = A + (long)gm * lda + gk;
         if (a_vec && gk + 8 <= Ka) {
@@ -351,11 +379,11 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
 // ------------------------------------------------------------------------------------------------
 // fwd / dgrad kernel, fp32 (exact-f32 MFMA 16x16x4)
 // ------------------------------------------------------------------------------------------------
-template <int BM, int BN, bool PRO, bool STATS>
+template <int BM, int BN, bool PRO, bool STATS, int AM = 0>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__ A, int lda, Pro pro,
                                                        const float* __restrict__ Wt, int ldw, Epi epi,
                                                        float* __restrict__ out, int ldo, int M, int N, int K, int Ka,
-                                                       int Kb, int nMt, int nNt) {
+                                                       int Kb, int nMt, int nNt, ConvG cv) {
   constexpr int BK = 16;
   constexpr int PITCH = BK + 1;
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
@@ -390,12 +418,40 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
     r.w = gk + 3 < lim ? src[3] : 0.f;
     return r;
   };
+  ConvRow crow[AM ? A_F4 : 1];
+  const bool c_vec = AM && (cv.Cs & 3) == 0 && ((reinterpret_cast<uintptr_t>(A) & 15) == 0);
+  if constexpr (AM != 0) {
+#pragma unroll
+    for (int i = 0; i < A_F4; ++i) {
+      const int gm = m0 + (tid + i * 256) / (BK / 4);
+      crow[i] = conv_row(cv, gm < M ? gm : 0);
+    }
+  }
   auto load_tile = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < A_F4; ++i) {
       const int idx = tid + i * 256, row = idx / (BK / 4), kq = idx % (BK / 4);
       const int gm = m0 + row, gk = k0 + kq * 4;
       ra[i] = float4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (AM != 0) {
+        if (gm < M && gk < Ka) {
+          if (c_vec) {
+            const int tap = gk / cv.Cs;
+            const long off = conv_src(cv, crow[i], tap);
+            if (off >= 0) ra[i] = *reinterpret_cast<const float4*>(A + off + (gk - tap * cv.Cs));
+          } else {
+            float e[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const int k = gk + q, tap = k / cv.Cs;
+              const long off = k < Ka ? conv_src(cv, crow[i], tap) : -1;
+              e[q] = off >= 0 ? A[off + (k - tap * cv.Cs)] : 0.f;
+            }
+            ra[i] = make_float4(e[0], e[1], e[2], e[3]);
+          }
+        }
+        continue;
+      }
       if (gm < M) ra[i] = ld4(A + (long)gm * lda + gk, gk, Ka, a_vec);
     }
 #pragma unroll
@@ -452,9 +508,9 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
 
   const float* res = static_cast<const float*>(epi.res);
   const float* Z = static_cast<const float*>(epi.Z);
-  float s1[TN], s2[TN];
+  double s1[TN], s2[TN];
 #pragma unroll
-  for (int j = 0; j < TN; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
+  for (int j = 0; j < TN; ++j) { s1[j] = 0.0; s2[j] = 0.0; }
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
 #pragma unroll
@@ -473,14 +529,15 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
         if (epi.zact) v *= act_grad(epi.zact, Z[(long)m * epi.ldz + n]);
         out[(long)m * ldo + n] = v;
         if constexpr (STATS) {
-          const float d = v - (epi.stat_shift ? epi.stat_shift[n] : 0.f);
+          const double d = (double)v - (double)(epi.stat_shift ? epi.stat_shift[n] : 0.f);
           s1[j] += d;
-          s2[j] = fmaf(d, d, s2[j]);
+          s2[j] = fma(d, d, s2[j]);
         }
       }
     }
   }
-  if constexpr (STATS) stats_store<TN, WN, BN>(s1, s2, As, wm, wn, lane, epi.stat, mt, n0, N);
+  if constexpr (STATS)
+    stats_store<TN, WN, BN>(s1, s2, reinterpret_cast<double*>(As), wm, wn, lane, epi.stat, mt, n0, N);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -490,11 +547,11 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
 // j>=4: m = 16+4g+j-4) identically for both operands, which makes each 32-lane half read 8
 // distinct rows: with an 80-element pitch the reads are bank-conflict free.
 // ------------------------------------------------------------------------------------------------
-template <int BN, int BK, bool PRO>
+template <int BN, int BK, bool PRO, int AM = 0>
 __global__ __launch_bounds__(256) void wgrad_bf16_kernel(const bf16* __restrict__ G, int ldg, const bf16* __restrict__ X,
                                                          int ldx, Pro pro, const float* __restrict__ rs, int rps,
                                                          float* __restrict__ part, long ldp, int want_bias, int M, int N,
-                                                         int K, int mchunk, int nNt, int tiles, int S) {
+                                                         int K, int mchunk, int nNt, int tiles, int S, ConvG cv) {
   constexpr int MS = 32;
   constexpr int GP = BN + 16, XP = BK + 16;  // 16 * odd elements: conflict-free transposed reads
   constexpr int GV = MS * BN / 8 / 256, XV = MS * BK / 8 / 256;
@@ -548,6 +605,26 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(const bf16* __restrict_
     for (int i = 0; i < XV; ++i) {
       const int gm = m0 + xrow + i * (256 / XC);
       xr[i] = uint4{0u, 0u, 0u, 0u};
+      if constexpr (AM != 0) {  // implicit-GEMM conv: X = gather(x), tap-major columns
+        const int k = k0 + xc8;
+        if (gm < mend && k < K) {
+          const ConvRow cr = conv_row(cv, gm);
+          if ((cv.Cs & 7) == 0 && ((reinterpret_cast<uintptr_t>(X) & 15) == 0)) {
+            const int tap = k / cv.Cs;
+            const long off = conv_src(cv, cr, tap);
+            if (off >= 0) xr[i] = *reinterpret_cast<const uint4*>(X + off + (k - tap * cv.Cs));
+          } else {
+            bf16* e = reinterpret_cast<bf16*>(&xr[i]);
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+              const int kk = k + t, tap = kk / cv.Cs;
+              const long off = kk < K ? conv_src(cv, cr, tap) : -1;
+              e[t] = off >= 0 ? X[off + (kk - tap * cv.Cs)] : (bf16)0.f;
+            }
+          }
+        }
+        continue;
+      }
       if (gm < mend) {
         const bf16* src = X + (long)gm * ldx + k0 + xc8;
         if (x_vec) xr[i] = *reinterpret_cast<const uint4*>(src);
@@ -656,11 +733,11 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(const bf16* __restrict_
 }
 
 // wgrad, fp32: f32 MFMA fragments read straight from the [m][col] tiles (k = lane>>4 layout).
-template <bool PRO>
+template <bool PRO, int AM = 0>
 __global__ __launch_bounds__(256) void wgrad_f32_kernel(const float* __restrict__ G, int ldg, const float* __restrict__ X,
                                                         int ldx, Pro pro, const float* __restrict__ rs, int rps,
                                                         float* __restrict__ part, long ldp, int want_bias, int M,
-                                                        int N, int K, int mchunk, int nNt) {
+                                                        int N, int K, int mchunk, int nNt, ConvG cv) {
   constexpr int BN = 64, BKK = 64, MS = 16, PITCH = 68;
   __shared__ __attribute__((aligned(16))) float Gs[MS * PITCH];
   __shared__ __attribute__((aligned(16))) float Xs[MS * PITCH];
@@ -696,7 +773,15 @@ __global__ __launch_bounds__(256) void wgrad_f32_kernel(const float* __restrict_
 #pragma unroll
           for (int t = 0; t < 4; ++t) gv[t] = n0 + scol + t < N ? gsrc[t] : 0.f;
         }
-        if (x_vec && k0 + scol + 4 <= K) {
+        if constexpr (AM != 0) {  // implicit-GEMM conv: X = gather(x), tap-major columns
+          const ConvRow cr = conv_row(cv, gm);
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const int kk = k0 + scol + t, tap = kk / cv.Cs;
+            const long off = kk < K ? conv_src(cv, cr, tap) : -1;
+            xv[t] = off >= 0 ? X[off + (kk - tap * cv.Cs)] : 0.f;
+          }
+        } else if (x_vec && k0 + scol + 4 <= K) {
           const float4 t = *reinterpret_cast<const float4*>(xsrc);
           xv[0] = t.x; xv[1] = t.y; xv[2] = t.z; xv[3] = t.w;
         } else {
@@ -863,10 +948,10 @@ static void launch_mm(const void* A, int lda, const Pro& pro, const float* Wt, i
   const unsigned grid = (unsigned)(((nMt + 7) / 8) * 8 * nNt);
   if constexpr (sizeof(T) == 2)
     gemm_bf16_kernel<BM, BN, PRO, STATS><<<grid, 256, 0, s>>>((const bf16*)A, lda, pro, Wt, ldw, epi, (bf16*)out, ldo,
-                                                              M, N, K, Ka, Kb, nMt, nNt);
+                                                              M, N, K, Ka, Kb, nMt, nNt, ConvG());
   else
     gemm_f32_kernel<BM, BN, PRO, STATS><<<grid, 256, 0, s>>>((const float*)A, lda, pro, Wt, ldw, epi, (float*)out, ldo,
-                                                             M, N, K, Ka, Kb, nMt, nNt);
+                                                             M, N, K, Ka, Kb, nMt, nNt, ConvG());
 }
 
 template <typename T, bool PRO, bool STATS>
@@ -911,6 +996,47 @@ void gemm_fwd_launch(ogv_dtype dt, const void* A, int lda, const Pro& pro, const
   }
   if (dt == OGV_BF16) launch_mm_any<bf16>(A, lda, pro, W, ldw, out, ldo, M, N, K, Ka, Kb, epi, s);
   else launch_mm_any<float>(A, lda, pro, W, ldw, out, ldo, M, N, K, Ka, Kb, epi, s);
+}
+
+template <typename T, bool STATS>
+static void launch_conv_mm(const void* A, const ConvG& cv, const float* Wt, void* out, int M, int N, int K,
+                           const Epi& epi, hipStream_t s) {
+  constexpr int BM = GEMM_BM;
+  const int nMt = (M + BM - 1) / BM;
+  const int Kp = (K + 31) / 32 * 32;  // loop bound: whole BK slabs, zero-filled past K
+  if (N > 64) {
+    const int nNt = (N + 127) / 128;
+    const unsigned grid = (unsigned)(((nMt + 7) / 8) * 8 * nNt);
+    if constexpr (sizeof(T) == 2)
+      gemm_bf16_kernel<BM, 128, false, STATS, 1><<<grid, 256, 0, s>>>((const bf16*)A, 0, Pro(), Wt, K, epi, (bf16*)out,
+                                                                      N, M, N, Kp, K, K, nMt, nNt, cv);
+    else
+      gemm_f32_kernel<BM, 128, false, STATS, 1><<<grid, 256, 0, s>>>((const float*)A, 0, Pro(), Wt, K, epi,
+                                                                     (float*)out, N, M, N, Kp, K, K, nMt, nNt, cv);
+  } else {
+    const int nNt = (N + 63) / 64;
+    const unsigned grid = (unsigned)(((nMt + 7) / 8) * 8 * nNt);
+    if constexpr (sizeof(T) == 2)
+      gemm_bf16_kernel<BM, 64, false, STATS, 1><<<grid, 256, 0, s>>>((const bf16*)A, 0, Pro(), Wt, K, epi, (bf16*)out,
+                                                                     N, M, N, Kp, K, K, nMt, nNt, cv);
+    else
+      gemm_f32_kernel<BM, 64, false, STATS, 1><<<grid, 256, 0, s>>>((const float*)A, 0, Pro(), Wt, K, epi,
+                                                                    (float*)out, N, M, N, Kp, K, K, nMt, nNt, cv);
+  }
+}
+
+void conv_gemm_launch(ogv_dtype dt, const void* A, const ConvG& cv, const float* Wt, void* out, int M, int N,
+                      const Epi& epi, hipStream_t s) {
+  if (M <= 0) return;
+  const int K = 9 * cv.Cs;
+  const bool st = epi.stat != nullptr;
+  if (dt == OGV_BF16) {
+    if (st) launch_conv_mm<bf16, true>(A, cv, Wt, out, M, N, K, epi, s);
+    else launch_conv_mm<bf16, false>(A, cv, Wt, out, M, N, K, epi, s);
+  } else {
+    if (st) launch_conv_mm<float, true>(A, cv, Wt, out, M, N, K, epi, s);
+    else launch_conv_mm<float, false>(A, cv, Wt, out, M, N, K, epi, s);
+  }
 }
 
 static inline int pad8(int n) { return (n + 7) / 8 * 8; }
@@ -974,25 +1100,30 @@ size_t wgrad_ws_bytes(int M, int N, int K) {
 template <int BN, int BK>
 static void launch_wgrad_bf16(const WgradPlan& p, const void* G, int ldg, const void* X, int ldx, const Pro& pro,
                               const float* rs, int rps, float* part, long ldp, bool bias, int M, int N, int K,
-                              hipStream_t s) {
+                              hipStream_t s, const ConvG* xc) {
   const int tiles = p.nNt * p.nKt;
   const unsigned grid = (unsigned)(((p.S + 7) / 8) * 8 * tiles);
-  if (pro.any())
+  const ConvG cv = xc ? *xc : ConvG();
+  if (xc)
+    wgrad_bf16_kernel<BN, BK, false, 1><<<grid, 256, 0, s>>>((const bf16*)G, ldg, (const bf16*)X, ldx, pro, rs, rps,
+                                                             part, ldp, bias, M, N, K, p.mchunk, p.nNt, tiles, p.S, cv);
+  else if (pro.any())
     wgrad_bf16_kernel<BN, BK, true><<<grid, 256, 0, s>>>((const bf16*)G, ldg, (const bf16*)X, ldx, pro, rs, rps, part,
-                                                         ldp, bias, M, N, K, p.mchunk, p.nNt, tiles, p.S);
+                                                         ldp, bias, M, N, K, p.mchunk, p.nNt, tiles, p.S, cv);
   else
     wgrad_bf16_kernel<BN, BK, false><<<grid, 256, 0, s>>>((const bf16*)G, ldg, (const bf16*)X, ldx, pro, rs, rps, part,
-                                                          ldp, bias, M, N, K, p.mchunk, p.nNt, tiles, p.S);
+                                                          ldp, bias, M, N, K, p.mchunk, p.nNt, tiles, p.S, cv);
 }
 
 void gemm_wgrad_launch(ogv_dtype dt, const void* G, int ldg, const void* X, int ldx, const Pro& pro, const float* rs,
-                       int rps, float* dW, float* dbias, int M, int N, int K, void* ws, hipStream_t s) {
+                       int rps, float* dW, float* dbias, int M, int N, int K, void* ws, hipStream_t s,
+                       const ConvG* xc) {
   if (M <= 0) {
     (void)hipMemsetAsync(dW, 0, (size_t)N * K * sizeof(float), s);
     if (dbias) (void)hipMemsetAsync(dbias, 0, (size_t)N * sizeof(float), s);
     return;
   }
-  if (dt == OGV_F32 && M <= 2048) {
+  if (dt == OGV_F32 && M <= 2048 && !xc) {
     dim3 grid(cdiv(K, 64) + (dbias ? 1 : 0), N);
     small_wgrad_kernel<<<grid, 256, 0, s>>>((const float*)G, ldg, (const float*)X, ldx, pro, rs, rps, dW, dbias, M, N,
                                             K);
@@ -1004,18 +1135,23 @@ void gemm_wgrad_launch(ogv_dtype dt, const void* G, int ldg, const void* X, int 
   float* tmp = part + (size_t)p.S * ldp;
   if (dt == OGV_BF16) {
     const bool b = dbias != nullptr;
-    if (p.BN == 128 && p.BK == 128) launch_wgrad_bf16<128, 128>(p, G, ldg, X, ldx, pro, rs, rps, part, ldp, b, M, N, K, s);
-    else if (p.BN == 128) launch_wgrad_bf16<128, 64>(p, G, ldg, X, ldx, pro, rs, rps, part, ldp, b, M, N, K, s);
-    else if (p.BK == 128) launch_wgrad_bf16<64, 128>(p, G, ldg, X, ldx, pro, rs, rps, part, ldp, b, M, N, K, s);
-    else launch_wgrad_bf16<64, 64>(p, G, ldg, X, ldx, pro, rs, rps, part, ldp, b, M, N, K, s);
+    if (p.BN == 128 && p.BK == 128)
+      launch_wgrad_bf16<128, 128>(p, G, ldg, X, ldx, pro, rs, rps, part, ldp, b, M, N, K, s, xc);
+    else if (p.BN == 128) launch_wgrad_bf16<128, 64>(p, G, ldg, X, ldx, pro, rs, rps, part, ldp, b, M, N, K, s, xc);
+    else if (p.BK == 128) launch_wgrad_bf16<64, 128>(p, G, ldg, X, ldx, pro, rs, rps, part, ldp, b, M, N, K, s, xc);
+    else launch_wgrad_bf16<64, 64>(p, G, ldg, X, ldx, pro, rs, rps, part, ldp, b, M, N, K, s, xc);
   } else {
     dim3 grid(p.nNt * p.nKt, p.S);
-    if (pro.any())
+    const ConvG cv = xc ? *xc : ConvG();
+    if (xc)
+      wgrad_f32_kernel<false, 1><<<grid, 256, 0, s>>>((const float*)G, ldg, (const float*)X, ldx, pro, rs, rps, part,
+                                                      ldp, dbias != nullptr, M, N, K, p.mchunk, p.nNt, cv);
+    else if (pro.any())
       wgrad_f32_kernel<true><<<grid, 256, 0, s>>>((const float*)G, ldg, (const float*)X, ldx, pro, rs, rps, part, ldp,
-                                                  dbias != nullptr, M, N, K, p.mchunk, p.nNt);
+                                                  dbias != nullptr, M, N, K, p.mchunk, p.nNt, cv);
     else
       wgrad_f32_kernel<false><<<grid, 256, 0, s>>>((const float*)G, ldg, (const float*)X, ldx, pro, rs, rps, part, ldp,
-                                                   dbias != nullptr, M, N, K, p.mchunk, p.nNt);
+                                                   dbias != nullptr, M, N, K, p.mchunk, p.nNt, cv);
   }
   colreduce(part, dW, p.S, dbias ? ldp : (long)N * K, ldp, tmp, s, dbias, (long)N * K);
 }

@@ -17,6 +17,7 @@
 // HBM passes over the [M, mid] tensors: fwd 4 (e write, e read+d write, d read for the pool, d
 // read for project), bwd 9.
 #include "ogv_gemm.h"
+#include "ogv_bn.h"
 
 namespace ogv {
 
@@ -36,7 +37,7 @@ static RowPlan row_plan(int K) {
 // ------------------------------------------------------------------ BN finalize / coefficients
 // train: mean = shift + S1/n, var = S2/n - (S1/n)^2; running stats updated (unbiased var).
 // eval : mean/var = running stats.  Emits invstd, sc = gamma*invstd, sh = beta - mean*sc.
-__global__ void bn_finalize_kernel(const float* __restrict__ sums, int K, double n, const float* __restrict__ gamma,
+__global__ void bn_finalize_kernel(const double* __restrict__ sums, int K, double n, const float* __restrict__ gamma,
                                    const float* __restrict__ beta, float eps, float momentum, float* rm, float* rv,
                                    float* __restrict__ mean_out, float* __restrict__ invstd_out, float* __restrict__ sc,
                                    float* __restrict__ sh, int train) {
@@ -76,6 +77,17 @@ __global__ void bn_coeffs_kernel(const float* __restrict__ S, int K, float n, co
   coef[c] = (gamma ? gamma[c] : 1.f) * invstd[c];
   coef[K + c] = train ? sdy / n : 0.f;
   coef[2 * K + c] = train ? sdyx / n : 0.f;
+}
+
+void bn_finalize_launch(const double* sums, int K, double n, const float* gamma, const float* beta, float eps,
+                        float momentum, float* rm, float* rv, float* mean, float* invstd, float* sc, float* sh, int train,
+                        hipStream_t s) {
+  bn_finalize_kernel<<<cdiv(K, 256), 256, 0, s>>>(sums, K, n, gamma, beta, eps, momentum, rm, rv, mean, invstd, sc, sh,
+                                                   train);
+}
+void bn_coeffs_launch(const float* S, int K, float n, const float* gamma, const float* invstd, float* dgamma,
+                      float* dbeta, float* coef, int train, hipStream_t s) {
+  bn_coeffs_kernel<<<cdiv(K, 256), 256, 0, s>>>(S, K, n, gamma, invstd, dgamma, dbeta, coef, train);
 }
 
 // ------------------------------------------------------------------ depthwise conv with BN fusion
@@ -151,48 +163,12 @@ __device__ __forceinline__ void stage_tile(float* tile, const T* __restrict__ sr
   }
 }
 
-// Sum q[NQ][V] over the 64 slots of each of the 4 channel chunks (chunk = tid & 3,
-// slot = tid >> 2): xor-shuffles over lane bits 2..5 inside each wave, then the 4 waves through
-// LDS (4*NQ*4*V floats; the LDS may be reused).  out[k*qstride + c], c = cbase + chunk*V + i < C.
-template <int NQ, int V>
-__device__ __forceinline__ void chunk_reduce_store(float (&q)[NQ][V], float* lds, float* out, long qstride, int C,
-                                                   int cbase) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-  for (int k = 0; k < NQ; ++k)
-#pragma unroll
-    for (int i = 0; i < V; ++i) {
-      float v = q[k][i];
-      v += __shfl_xor(v, 4, 64);
-      v += __shfl_xor(v, 8, 64);
-      v += __shfl_xor(v, 16, 64);
-      v += __shfl_xor(v, 32, 64);
-      q[k][i] = v;
-    }
-  __syncthreads();
-  if (lane < 4) {
-#pragma unroll
-    for (int k = 0; k < NQ; ++k)
-#pragma unroll
-      for (int i = 0; i < V; ++i) lds[((wave * NQ + k) * 4 + lane) * V + i] = q[k][i];
-  }
-  __syncthreads();
-  for (int idx = threadIdx.x; idx < NQ * 4 * V; idx += 256) {
-    const int k = idx / (4 * V), r = idx - k * 4 * V;
-    const int ch = r / V, i = r - ch * V;
-    float sum = 0.f;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) sum += lds[((w * NQ + k) * 4 + ch) * V + i];
-    const int c = cbase + ch * V + i;
-    if (c < C) out[(long)k * qstride + c] = sum;
-  }
-}
 
 // d = dw3x3(act(e*sc1 + sh1)) (+ stats of the rounded output minus shift)
 template <typename T, int V>
 __global__ __launch_bounds__(256) void dw_fwd_tile_kernel(const T* __restrict__ e, const float* __restrict__ wdw,
                                                           const float* __restrict__ sc, const float* __restrict__ sh,
-                                                          int act, T* __restrict__ out, float* __restrict__ stat,
+                                                          int act, T* __restrict__ out, double* __restrict__ stat,
                                                           const float* __restrict__ shift, DwTile t) {
   extern __shared__ __attribute__((aligned(16))) float tile[];
   const TileIdx ti = tile_idx(t);
@@ -200,9 +176,9 @@ __global__ __launch_bounds__(256) void dw_fwd_tile_kernel(const T* __restrict__ 
   __syncthreads();
   const int chunk = threadIdx.x & 3, slot = threadIdx.x >> 2;
   const int c = ti.ct * t.CT + chunk * V;
-  float q[2][V];
+  double q[2][V];  // BN batch statistics in fp64 (no cancellation when the mean is far from the shift)
 #pragma unroll
-  for (int i = 0; i < V; ++i) { q[0][i] = 0.f; q[1][i] = 0.f; }
+  for (int i = 0; i < V; ++i) { q[0][i] = 0.0; q[1][i] = 0.0; }
   if (c < t.C) {
     float w[9][V], sft[V];
 #pragma unroll
@@ -237,14 +213,16 @@ __global__ __launch_bounds__(256) void dw_fwd_tile_kernel(const T* __restrict__ 
 #pragma unroll
       for (int i = 0; i < V; ++i) {
         of[i] = to_f(from_f<T>(acc[i]));
-        const float dl = of[i] - sft[i];
+        const double dl = (double)of[i] - (double)sft[i];
         q[0][i] += dl;
-        q[1][i] = fmaf(dl, dl, q[1][i]);
+        q[1][i] = fma(dl, dl, q[1][i]);
       }
       store_vec<T, V>(out + ((ti.b * t.H + y) * t.W + x) * t.C + c, of);
     }
   }
-  if (stat) chunk_reduce_store<2, V>(q, tile, stat + ti.rid * 2 * t.C, t.C, t.C, ti.ct * t.CT);
+  if (stat)
+    chunk_reduce_store<2, V, double>(q, reinterpret_cast<double*>(tile), stat + ti.rid * 2 * t.C, t.C, t.C,
+                                     ti.ct * t.CT);
 }
 
 // dy1 = (dw3x3^T dd) * act'(e*sc1 + sh1) -> out; stats: sum dy1, sum dy1*(e - mean1)*invstd1
@@ -635,7 +613,7 @@ static long dw_slices(long P, const RowPlan& rp) {   // row slices for the globa
 }
 
 struct FwdWs {
-  float *stat1, *stat2, *stat3, *sums, *tmp;
+  double *stat1, *stat2, *stat3, *sums, *tmp;  // fp64 BatchNorm batch statistics
   char* gemm;
 };
 static FwdWs fwd_ws_layout(void* base, const ogv_mbconv_desc& s, size_t* total) {
@@ -645,12 +623,12 @@ static FwdWs fwd_ws_layout(void* base, const ogv_mbconv_desc& s, size_t* total) 
   const long S2 = dw_tile_plan(s.B, s.H, s.W, s.mid, 4).rows();
   const long R1 = gemm_stat_rows((int)M);
   FwdWs w;
-  w.stat1 = b.take<float>(R1 * 2 * s.mid);
-  w.stat2 = b.take<float>(S2 * 2 * s.mid);
-  w.stat3 = b.take<float>(R1 * 2 * s.C);
-  w.sums = b.take<float>(2 * (size_t)(s.mid > s.C ? s.mid : s.C));
+  w.stat1 = b.take<double>(R1 * 2 * s.mid);
+  w.stat2 = b.take<double>(S2 * 2 * s.mid);
+  w.stat3 = b.take<double>(R1 * 2 * s.C);
+  w.sums = b.take<double>(2 * (size_t)(s.mid > s.C ? s.mid : s.C));
   long Rmax = R1 > S2 ? R1 : S2;
-  w.tmp = b.take<float>(colreduce_tmp_floats(Rmax, 2L * (s.mid > s.C ? s.mid : s.C)) + 16);
+  w.tmp = b.take<double>(colreduce_tmp_floats(Rmax, 2L * (s.mid > s.C ? s.mid : s.C)) + 16);
   w.gemm = b.take<char>(64);
   if (total) *total = b.off + 256;
   return w;
@@ -711,7 +689,7 @@ static BwdWs bwd_ws_layout(void* base, const ogv_mbconv_desc& s, size_t esz, siz
 template <typename T>
 struct Ops {
   template <int V>
-  static void dw_fwd(const void* e, const float* w, const float* sc, const float* sh, int act, void* out, float* stat,
+  static void dw_fwd(const void* e, const float* w, const float* sc, const float* sh, int act, void* out, double* stat,
                      const float* shift, const DwTile& t, hipStream_t st) {
     const unsigned nb = (unsigned)(t.rows() * t.nct);
     dw_fwd_tile_kernel<T, V><<<nb, 256, t.lds_bytes(), st>>>((const T*)e, w, sc, sh, act, (T*)out, stat, shift, t);

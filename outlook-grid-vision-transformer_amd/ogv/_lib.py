@@ -39,7 +39,18 @@ class MBConvGrads(ctypes.Structure):
     _fields_ = [(n, _p) for n in MBCONV_GRAD_FIELDS]
 
 
+class ConvBNDesc(ctypes.Structure):
+    _fields_ = [("B", _i), ("H", _i), ("W", _i), ("Cin", _i), ("Cout", _i), ("stride", _i), ("has_bn", _i),
+                ("train", _i), ("bn_eps", _f), ("bn_momentum", _f), ("act", _i)]
+
+
+class ConvBNParams(ctypes.Structure):
+    _fields_ = [(n, _p) for n in ("w", "bias", "bn_w", "bn_b", "bn_rm", "bn_rv")]
+
+
 _PD = ctypes.POINTER(MBConvDesc)
+_PCD = ctypes.POINTER(ConvBNDesc)
+_PCP = ctypes.POINTER(ConvBNParams)
 _PP = ctypes.POINTER(MBConvParams)
 _PG = ctypes.POINTER(MBConvGrads)
 
@@ -67,6 +78,14 @@ SIGNATURES = {
     "ogv_mbconv_ws_bytes": (_sz, [_PD, _i]),
     "ogv_mbconv_fwd": (_i, [_p, _p, _p, _p, _PD, _PP, _i, _p]),
     "ogv_mbconv_bwd": (_i, [_p, _p, _p, _p, _PG, _p, _PD, _PP, _i, _p]),
+    "ogv_convbn_saved_bytes": (_sz, [_PCD, _i]),
+    "ogv_convbn_ws_bytes": (_sz, [_PCD, _i]),
+    "ogv_convbn_fwd": (_i, [_p, _p, _p, _p, _PCD, _PCP, _i, _p]),
+    "ogv_convbn_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _PCD, _PCP, _i, _p]),
+    "ogv_bn_act_saved_bytes": (_sz, [_i]),
+    "ogv_bn_act_ws_bytes": (_sz, [_i, _i]),
+    "ogv_bn_act_fwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _f, _f, _i, _i, _p]),
+    "ogv_bn_act_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p]),
     "ogv_cast": (_i, [_p, _i, _p, _i, _sz, _p]),
 }
 

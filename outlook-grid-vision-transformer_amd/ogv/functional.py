@@ -439,3 +439,119 @@ def mbconv_fused(x, B, H, W, mid, se, train, eps, momentum, act, params, buffers
             ACT[act])
     y = _MBConv.apply(x2d, geom, buffers, *[f32(t).contiguous() for t in params])
     return rows_to_nchw(y, B, H, W)
+
+
+# ------------------------------------------------------------------------------------------------
+# MaxOutNet around the blocks: conv3x3 -> BatchNorm2d -> act (stem, downsample), BatchNorm alone
+# (head).  src/model/stem_head.py:23-32, src/model/downsampling.py:28-65, Model_A_OutGridNet.py:66
+# ------------------------------------------------------------------------------------------------
+def _bn_args(bn):
+    """(has_bn, train, eps, momentum, running_mean, running_var) of an nn.BatchNorm2d or None."""
+    if bn is None:
+        return 0, 0, 1e-5, 0.1, None, None
+    if not bn.track_running_stats or bn.running_mean is None or bn.momentum is None:
+        raise NotImplementedError("ogv BatchNorm: needs track_running_stats=True and a float momentum "
+                                  "(the reference's nn.BatchNorm2d defaults)")
+    return 1, int(bool(bn.training)), float(bn.eps), float(bn.momentum), bn.running_mean, bn.running_var
+
+
+class _ConvBN(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x2d, geom, rm, rv, w, bias, bn_w, bn_b):
+        lib = _lib.load()
+        B, H, W, Cin, Cout, stride = geom[:6]
+        desc = _lib.ConvBNDesc(*geom)
+        P = _lib.ConvBNParams(_ptr(w), _ptr(bias), _ptr(bn_w), _ptr(bn_b), _ptr(rm), _ptr(rv))
+        dt = _dt(x2d)
+        Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
+        out = torch.empty((B * Ho * Wo, Cout), dtype=x2d.dtype, device=x2d.device)
+        saved = torch.empty(lib.ogv_convbn_saved_bytes(ctypes.byref(desc), dt), dtype=torch.uint8, device=x2d.device)
+        ws = _ws(lib.ogv_convbn_ws_bytes(ctypes.byref(desc), dt), x2d.device)
+        check(lib.ogv_convbn_fwd(_ptr(x2d), _ptr(out), _ptr(saved), _ptr(ws), ctypes.byref(desc), ctypes.byref(P), dt,
+                                 _stream()), "ogv_convbn_fwd")
+        ctx.save_for_backward(x2d, saved, w, bias, bn_w, bn_b)
+        ctx.geom = geom
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        lib = _lib.load()
+        x2d, saved, w, bias, bn_w, bn_b = ctx.saved_tensors
+        desc = _lib.ConvBNDesc(*ctx.geom)
+        P = _lib.ConvBNParams(_ptr(w), _ptr(bias), _ptr(bn_w), _ptr(bn_b), None, None)
+        dt = _dt(x2d)
+        dout = dout.to(x2d.dtype).contiguous()
+        dx = torch.empty_like(x2d) if ctx.needs_input_grad[0] else None
+        dw = torch.empty_like(w)
+        db = torch.empty_like(bias) if bias is not None else None
+        dg = torch.empty_like(bn_w) if bn_w is not None else None
+        dbb = torch.empty_like(bn_b) if bn_b is not None else None
+        ws = _ws(lib.ogv_convbn_ws_bytes(ctypes.byref(desc), dt), x2d.device)
+        check(lib.ogv_convbn_bwd(_ptr(dout), _ptr(x2d), _ptr(saved), _ptr(dx), _ptr(dw), _ptr(db), _ptr(dg), _ptr(dbb),
+                                 _ptr(ws), ctypes.byref(desc), ctypes.byref(P), dt, _stream()), "ogv_convbn_bwd")
+        return dx, None, None, None, dw, db, dg, dbb
+
+
+def conv3x3_bn_act(x, conv, bn=None, act=None):
+    """act(BN(conv(x))) for an nn.Conv2d(Cin, Cout, 3, stride 1|2, padding 1) and an optional
+    nn.BatchNorm2d(Cout); x NCHW (any memory format) -> channels_last NCHW."""
+    require_device(x, conv.weight, what="ogv.conv3x3_bn_act")
+    if (tuple(conv.kernel_size) != (3, 3) or tuple(conv.padding) != (1, 1) or conv.groups != 1
+            or tuple(conv.dilation) != (1, 1) or conv.stride[0] != conv.stride[1] or conv.stride[0] not in (1, 2)):
+        raise NotImplementedError("ogv.conv3x3_bn_act: needs a dense 3x3 conv, padding 1, stride 1 or 2")
+    B, Cin, H, W = x.shape
+    Cout, stride = conv.out_channels, conv.stride[0]
+    has_bn, train, eps, mom, rm, rv = _bn_args(bn)
+    x2d = _rows_contig(nchw_to_rows(x.to(compute_dtype(x))))
+    geom = (int(B), int(H), int(W), int(Cin), int(Cout), int(stride), has_bn, train, eps, mom, ACT[act])
+    y = _ConvBN.apply(x2d, geom, rm, rv, f32(conv.weight).contiguous(), f32(conv.bias),
+                      f32(bn.weight) if has_bn else None, f32(bn.bias) if has_bn else None)
+    if has_bn and train:
+        bn.num_batches_tracked.add_(1)
+    return rows_to_nchw(y, B, (H - 1) // stride + 1, (W - 1) // stride + 1)
+
+
+class _BNAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x2d, meta, rm, rv, bn_w, bn_b):
+        lib = _lib.load()
+        train, eps, mom, act = meta
+        M, C = x2d.shape
+        dt = _dt(x2d)
+        out = torch.empty_like(x2d)
+        saved = torch.empty(lib.ogv_bn_act_saved_bytes(C) // 4, dtype=torch.float32, device=x2d.device)
+        ws = _ws(lib.ogv_bn_act_ws_bytes(M, C), x2d.device)
+        check(lib.ogv_bn_act_fwd(_ptr(x2d), _ptr(out), _ptr(saved), _ptr(ws), _ptr(bn_w), _ptr(bn_b), _ptr(rm), _ptr(rv),
+                                 M, C, train, eps, mom, act, dt, _stream()), "ogv_bn_act_fwd")
+        ctx.save_for_backward(x2d, saved, bn_w, bn_b)
+        ctx.meta = meta
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        lib = _lib.load()
+        x2d, saved, bn_w, bn_b = ctx.saved_tensors
+        train, eps, mom, act = ctx.meta
+        M, C = x2d.shape
+        dt = _dt(x2d)
+        dout = dout.to(x2d.dtype).contiguous()
+        dx = torch.empty_like(x2d)
+        dg = torch.empty_like(bn_w) if bn_w is not None else None
+        dbb = torch.empty_like(bn_b) if bn_b is not None else None
+        ws = _ws(lib.ogv_bn_act_ws_bytes(M, C), x2d.device)
+        check(lib.ogv_bn_act_bwd(_ptr(dout), _ptr(x2d), _ptr(saved), _ptr(dx), _ptr(dg), _ptr(dbb), _ptr(ws), _ptr(bn_w),
+                                 M, C, train, act, dt, _stream()), "ogv_bn_act_bwd")
+        return dx, None, None, None, dg, dbb
+
+
+def batchnorm_act_nchw(x, bn, act=None):
+    """act(BatchNorm2d(x)) on a channels_last view of x (nn.BatchNorm2d semantics)."""
+    require_device(x, what="ogv.batchnorm")
+    has_bn, train, eps, mom, rm, rv = _bn_args(bn)
+    B, C, H, W = x.shape
+    x2d = _rows_contig(nchw_to_rows(x.to(compute_dtype(x))))
+    y = _BNAct.apply(x2d, (train, eps, mom, ACT[act]), rm, rv, f32(bn.weight) if bn.affine else None,
+                     f32(bn.bias) if bn.affine else None)
+    if train:
+        bn.num_batches_tracked.add_(1)
+    return rows_to_nchw(y, B, H, W)

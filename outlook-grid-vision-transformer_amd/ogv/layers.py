@@ -79,6 +79,14 @@ class LayerNorm(nn.LayerNorm):
         return y.view(x.shape)
 
 
+class BatchNorm2d(nn.BatchNorm2d):
+    """nn.BatchNorm2d on the native BN kernels (NHWC rows; train batch statistics with the
+    running-stat update, or eval running statistics).  Same parameters/buffers as the stock module."""
+
+    def forward(self, x):
+        return OF.batchnorm_act_nchw(x, self, None)
+
+
 def drop_path_scale(dp: nn.Module, x: torch.Tensor):
     """Per-sample DropPath factor mask/keep as an fp32 [B] tensor, or None when the module is an
     identity (eval, p == 0, nn.Identity).  Same Bernoulli(keep) draw as the reference

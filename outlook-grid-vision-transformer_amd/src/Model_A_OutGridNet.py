@@ -2,7 +2,9 @@
 
 Drop-in for src/Model_A_OutGridNet.py:9-67 — the same constructor, module names
 (stem, proj_in, stages.<s>.<b>, downs.<s>, head_norm, classifier) and state_dict.  The blocks
-come from our src.model (HIP kernels); stem/downsample/head stay stock PyTorch-ROCm ops.
+come from our src.model (HIP kernels); the stem / downsample conv3x3+BN+SiLU, the 1x1 proj_in and
+the head BatchNorm run on the native conv/GEMM/BN kernels as well (ogv_convbn_*, ogv_gemm_*,
+ogv_bn_act_*).
 """
 from src.model.Out_Grid_Block import *  # noqa: F401,F403
 from src.model.downsampling import *  # noqa: F401,F403
@@ -13,6 +15,7 @@ from src.model.downsampling import Downsample, DownsampleConfig
 from src.model.stem_head import ConvStem, List, make_dpr
 from src.stage_config import StageCfg
 import torch.nn as nn
+from ogv.layers import BatchNorm2d, Conv1x1
 
 
 class MaxOutNet(nn.Module):
@@ -23,7 +26,7 @@ class MaxOutNet(nn.Module):
         assert len(stages) >= 1
         self.stem = ConvStem(in_ch, stem_dim, act="silu", use_bn=True)
         first = stages[0].dim
-        self.proj_in = nn.Conv2d(stem_dim, first, kernel_size=1, bias=True) if stem_dim != first else nn.Identity()
+        self.proj_in = Conv1x1(stem_dim, first, bias=True) if stem_dim != first else nn.Identity()
         rates = iter(make_dpr(sum(s.depth for s in stages), dpr_max))
         self.stages = nn.ModuleList()
         self.downs = nn.ModuleList()
@@ -32,7 +35,7 @@ class MaxOutNet(nn.Module):
                 OutGridBlock(StageCfg(**{**scfg.__dict__, "drop_path": next(rates)})) for _ in range(scfg.depth)))
             if si + 1 < len(stages):
                 self.downs.append(Downsample(scfg.dim, stages[si + 1].dim, cfg=down_cfg))
-        self.head_norm = nn.BatchNorm2d(stages[-1].dim)
+        self.head_norm = BatchNorm2d(stages[-1].dim)
         self.classifier = nn.Linear(stages[-1].dim, num_classes)
 
     def forward(self, x):

@@ -1,5 +1,8 @@
-"""Stage-transition downsampling — drop-in for src/model/downsampling.py (stock ops; outside the
-OutGridBlock hot path)."""
+"""Stage-transition downsampling — drop-in for src/model/downsampling.py.
+
+kind="conv" (every reference config) keeps the module tree ``op.0`` Conv2d(3x3, stride 2),
+``op.1`` BatchNorm2d / Identity, ``op.2`` activation and runs them as one native op
+(ogv_convbn_fwd/bwd).  kind="pool" (AvgPool2d + 1x1 conv) stays on stock ops."""
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -43,4 +46,12 @@ class Downsample(nn.Module):
         self.op = nn.Sequential(*layers, norm, make_activation(cfg.act))
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        return self.op(x)
+        if self.kind != "conv":
+            return self.op(x)
+        from ogv import functional as OF
+        from ogv.layers import act_name
+        conv, norm, act = self.op[0], self.op[1], self.op[2]
+        a = act_name(act)
+        if a is None and not isinstance(act, nn.Identity):
+            raise NotImplementedError(f"ogv Downsample: unsupported activation {type(act).__name__}")
+        return OF.conv3x3_bn_act(x, conv, norm if isinstance(norm, nn.BatchNorm2d) else None, a)

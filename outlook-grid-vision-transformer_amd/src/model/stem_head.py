@@ -1,5 +1,8 @@
-"""Stem conv and drop-path schedule — drop-in for src/model/stem_head.py (stock PyTorch-ROCm ops;
-the 3x3 stem is outside the OutGridBlock hot path)."""
+"""Stem conv and drop-path schedule — drop-in for src/model/stem_head.py.
+
+ConvStem keeps the reference's module tree (``stem.0`` Conv2d, ``stem.1`` BatchNorm2d, ``stem.2``
+activation; same state_dict) and runs conv3x3 -> BN -> act as one native op
+(ogv_convbn_fwd/bwd: implicit-GEMM conv on MFMA with the BN statistics in its epilogue)."""
 from dataclasses import dataclass
 from typing import List
 import torch.nn as nn
@@ -28,4 +31,10 @@ class ConvStem(nn.Module):
         )
 
     def forward(self, x):
-        return self.stem(x)
+        from ogv import functional as OF
+        from ogv.layers import act_name
+        conv, norm, act = self.stem[0], self.stem[1], self.stem[2]
+        a = act_name(act)
+        if a is None and not isinstance(act, nn.Identity):
+            raise NotImplementedError(f"ogv ConvStem: unsupported activation {type(act).__name__}")
+        return OF.conv3x3_bn_act(x, conv, norm if isinstance(norm, nn.BatchNorm2d) else None, a)

@@ -93,6 +93,18 @@ __device__ __forceinline__ void store_vec(T* __restrict__ p, const float* in) {
   }
 }
 
+// ---------------------------------------------------------------- XCD-aware block order
+// Hardware block i runs on XCD i % 8.  Logical block id = (i % 8) * per + i / 8 hands each XCD a
+// contiguous range of logical ids, so blocks that differ only in the fastest index (e.g. the
+// channel tiles of one row slice of an NHWC tensor, which read the same cache lines) share one
+// L2.  Launch xcd_grid(nb) blocks; xcd_block() returns false for the padding blocks.
+static inline unsigned xcd_grid(long nb) { return (unsigned)(((nb + 7) / 8) * 8); }
+__device__ __forceinline__ bool xcd_block(long nb, long& id) {
+  const long per = (nb + 7) / 8;
+  id = (long)(blockIdx.x & 7) * per + (blockIdx.x >> 3);
+  return id < nb;
+}
+
 // ---------------------------------------------------------------- activations (exact erf GELU)
 // logistic sigmoid with the hardware reciprocal (v_rcp_f32, 1 ulp) instead of an IEEE division
 __device__ __forceinline__ float fast_sigmoid(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }

@@ -53,17 +53,23 @@ __global__ void bn_identity_kernel(float* __restrict__ mean, float* __restrict__
 }
 
 // ------------------------------------------------------------------ BatchNorm(+act) passes
-// Block = (4 chunks of V channels) x (64 row slots), one row slice per blockIdx.y; partials go to
-// stat[slice][q][C] and a colreduce sums the slices (fixed order: deterministic).
+// Block = (4 chunks of V channels) x (64 row slots) for one (channel tile, row slice), XCD-aware
+// order (xcd_block); partials go to stat[slice][q][C] and a colreduce sums the slices in a fixed
+// order (deterministic).
 
 // stat = [sum (x - shift), sum (x - shift)^2]   (BatchNorm batch statistics, fp64)
 template <typename T, int V>
 __global__ __launch_bounds__(256) void bn_stats_kernel(const T* __restrict__ x, const float* __restrict__ shift,
                                                        double* __restrict__ stat, long M, int C, long per) {
   __shared__ double lds[4 * 2 * 4 * 8];
+  const int gx = (C + 4 * V - 1) / (4 * V);
+  long lid;
+  if (!xcd_block((long)gx * ((M + per - 1) / per), lid)) return;
+  const int bx = (int)(lid % gx);
+  const long by = lid / gx;
   const int chunk = threadIdx.x & 3, slot = threadIdx.x >> 2;
-  const int c0 = (blockIdx.x * 4 + chunk) * V;
-  const long r0 = (long)blockIdx.y * per, r1 = r0 + per < M ? r0 + per : M;
+  const int c0 = (bx * 4 + chunk) * V;
+  const long r0 = by * per, r1 = r0 + per < M ? r0 + per : M;
   double q[2][V];
 #pragma unroll
   for (int i = 0; i < V; ++i) { q[0][i] = 0.0; q[1][i] = 0.0; }
@@ -81,7 +87,7 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const T* __restrict__ x, 
       }
     }
   }
-  chunk_reduce_store<2, V, double>(q, lds, stat + (long)blockIdx.y * 2 * C, C, C, blockIdx.x * 4 * V);
+  chunk_reduce_store<2, V, double>(q, lds, stat + by * 2 * C, C, C, bx * 4 * V);
 }
 
 // out = act(y*sc + sh)
@@ -112,9 +118,14 @@ __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(const T* __restr
                                                                 const float* __restrict__ invstd,
                                                                 float* __restrict__ stat, long M, int C, long per) {
   __shared__ float lds[4 * 2 * 4 * 8];
+  const int gx = (C + 4 * V - 1) / (4 * V);
+  long lid;
+  if (!xcd_block((long)gx * ((M + per - 1) / per), lid)) return;
+  const int bx = (int)(lid % gx);
+  const long by = lid / gx;
   const int chunk = threadIdx.x & 3, slot = threadIdx.x >> 2;
-  const int c0 = (blockIdx.x * 4 + chunk) * V;
-  const long r0 = (long)blockIdx.y * per, r1 = r0 + per < M ? r0 + per : M;
+  const int c0 = (bx * 4 + chunk) * V;
+  const long r0 = by * per, r1 = r0 + per < M ? r0 + per : M;
   float q[2][V];
 #pragma unroll
   for (int i = 0; i < V; ++i) { q[0][i] = 0.f; q[1][i] = 0.f; }
@@ -136,7 +147,7 @@ __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(const T* __restr
       }
     }
   }
-  chunk_reduce_store<2, V>(q, lds, stat + (long)blockIdx.y * 2 * C, C, C, blockIdx.x * 4 * V);
+  chunk_reduce_store<2, V>(q, lds, stat + by * 2 * C, C, C, bx * 4 * V);
 }
 
 // out = coef0*(dz - coef1 - (y - mean)*invstd*coef2),  dz = da*act'(y*sc + sh)
@@ -190,8 +201,7 @@ static RowSlices row_slices(long M) {
 template <typename T, int V>
 static void bn_stats_run(const void* x, const float* shift, double* stat, long M, int C, const RowSlices& rs,
                          hipStream_t s) {
-  dim3 g(cdiv(C, 4 * V), (unsigned)rs.S);
-  bn_stats_kernel<T, V><<<g, 256, 0, s>>>((const T*)x, shift, stat, M, C, rs.per);
+  bn_stats_kernel<T, V><<<xcd_grid((long)cdiv(C, 4 * V) * rs.S), 256, 0, s>>>((const T*)x, shift, stat, M, C, rs.per);
 }
 template <typename T, int V>
 static void bn_apply_run(const void* y, const float* sc, const float* sh, int act, void* out, long M, int C,
@@ -202,8 +212,7 @@ template <typename T, int V>
 static void bn_bwd_reduce_run(const void* da, const void* y, const float* sc, const float* sh, int act,
                               const float* mean, const float* invstd, float* stat, long M, int C, const RowSlices& rs,
                               hipStream_t s) {
-  dim3 g(cdiv(C, 4 * V), (unsigned)rs.S);
-  bn_act_bwd_reduce_kernel<T, V><<<g, 256, 0, s>>>((const T*)da, (const T*)y, sc, sh, act, mean, invstd, stat, M, C,
+  bn_act_bwd_reduce_kernel<T, V><<<xcd_grid((long)cdiv(C, 4 * V) * rs.S), 256, 0, s>>>((const T*)da, (const T*)y, sc, sh, act, mean, invstd, stat, M, C,
                                                    rs.per);
 }
 template <typename T, int V>

@@ -91,6 +91,14 @@ void gemm_wgrad_launch(ogv_dtype dt, const void* G, int ldg, const void* X, int 
                        int rps, float* dW, float* dbias, int M, int N, int K, void* ws, hipStream_t s,
                        const ConvG* xconv = nullptr);
 
+// Small-M fp32 GEMM with split-K (SE MLP: M = batch rows): out = epi(pro(A)[M,K] . W[N,K]^T);
+// ws >= splitk_ws_bytes(M, N, K).  Epilogue: bias, rs, res, zact (no stats).
+size_t splitk_ws_bytes(int M, int N, int K);
+void gemm_fwd_splitk_f32(const float* A, int lda, const Pro& pro, const float* W, int ldw, float* out, int ldo, int M,
+                         int N, int K, const Epi& epi, void* ws, hipStream_t s);
+// WT[k][n] = W[n][k] (fp32), zero for n in [N, ldt)
+void transpose_f32_launch(const float* W, float* WT, int N, int K, int ldt, hipStream_t s);
+
 // Implicit-GEMM 3x3 conv:  out[M, N] = epi( gather(A)[M, 9*Cs] . Wt[N, 9*Cs]^T ),  M = B*Hr*Wr.
 // Wt is tap-major ([N][tap][Cs]).  Used for the conv forward (cv.transposed = 0) and its data
 // gradient (cv.transposed = 1, Wt = the tap-major transposed weights).

@@ -229,7 +229,7 @@ __device__ __forceinline__ void gemm_epilogue_bf16(f32x4 (&acc)[TM][TN], float* 
 // ------------------------------------------------------------------------------------------------
 // fwd / dgrad kernel, bf16
 // ------------------------------------------------------------------------------------------------
-template <int BM, int BN, bool PRO, bool STATS, int AM = 0>
+template <int BM, int BN, bool PRO, bool STATS, int AM = 0, bool BT = false>
 __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__ A, int lda, Pro pro,
                                                         const float* __restrict__ Wt, int ldw, Epi epi,
                                                         bf16* __restrict__ out, int ldo, int M, int N, int K, int Ka,
@@ -309,6 +309,23 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
     }
 #pragma unroll
     for (int i = 0; i < B_F4; ++i) {
+      if constexpr (BT) {  // W stored [reduction][output]: 4 consecutive output columns of one row
+        const int idx = tid + i * 256, kr = idx / (BN / 4), nq = idx % (BN / 4);
+        const int gk = k0 + kr, gn = n0 + nq * 4;
+        rb[i] = float4{0.f, 0.f, 0.f, 0.f};
+        if (gk < Kb) {
+          const float* src = Wt + (long)gk * ldw + gn;
+          if (b_vec && gn + 4 <= N) {
+            rb[i] = *reinterpret_cast<const float4*>(src);
+          } else {
+            rb[i].x = gn < N ? src[0] : 0.f;
+            rb[i].y = gn + 1 < N ? src[1] : 0.f;
+            rb[i].z = gn + 2 < N ? src[2] : 0.f;
+            rb[i].w = gn + 3 < N ? src[3] : 0.f;
+          }
+        }
+        continue;
+      }
       const int idx = tid + i * 256, row = idx / (BK / 4), kq = idx % (BK / 4);
       const int gn = n0 + row, gk = k0 + kq * 4;
       rb[i] = float4{0.f, 0.f, 0.f, 0.f};
@@ -346,6 +363,12 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
     }
 #pragma unroll
     for (int i = 0; i < B_F4; ++i) {
+      if constexpr (BT) {  // stage as loaded: Bs[kr][n] (pitch BN+16), read back with transposed LDS reads
+        const int idx = tid + i * 256, kr = idx / (BN / 4), nq = idx % (BN / 4);
+        bf16x4 b = {(bf16)rb[i].x, (bf16)rb[i].y, (bf16)rb[i].z, (bf16)rb[i].w};
+        *reinterpret_cast<bf16x4*>(Bs + kr * (BN + 16) + nq * 4) = b;
+        continue;
+      }
       const int idx = tid + i * 256, row = idx / (BK / 4), kq = idx % (BK / 4);
       bf16x4 b = {(bf16)rb[i].x, (bf16)rb[i].y, (bf16)rb[i].z, (bf16)rb[i].w};
       *reinterpret_cast<bf16x4*>(Bs + row * PITCH + kq * 4) = b;
@@ -358,12 +381,37 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
     __syncthreads();
     if (k0 + BK < K) load_tile(k0 + BK);  // next tile's HBM latency hides under this tile's MFMAs
     bf16x8 af[TM], bfg[TN];
+    if constexpr (BT) {
+      // B fragments from the [k][n] tile via ds_read_b64_tr_b16: lane (g = lane>>4, c = lane&15) gets
+      // column c at k = {4g..4g+3, 16+4g..16+4g+3}; A fragments are read in that same k order.
+      typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+      typedef __attribute__((ext_vector_type(8))) short s16x8;
+      const int g = lane >> 4, c16 = lane & 15, q = c16 >> 2, p4 = (c16 & 3) * 4;
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
-      af[i] = *reinterpret_cast<const bf16x8*>(As + (wm * WM + i * 16 + (lane & 15)) * PITCH + 8 * (lane >> 4));
+      for (int i = 0; i < TM; ++i) {
+        const bf16* arow = As + (wm * WM + i * 16 + c16) * PITCH;
+        const s16x4 lo = *reinterpret_cast<const s16x4*>(arow + 4 * g);
+        const s16x4 hi = *reinterpret_cast<const s16x4*>(arow + 16 + 4 * g);
+        const s16x8 a8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        af[i] = __builtin_bit_cast(bf16x8, a8);
+      }
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
-      bfg[j] = *reinterpret_cast<const bf16x8*>(Bs + (wn * WN + j * 16 + (lane & 15)) * PITCH + 8 * (lane >> 4));
+      for (int j = 0; j < TN; ++j) {
+        const int col = wn * WN + j * 16 + p4;
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Bs + (4 * g + q) * (BN + 16) + col));
+        const s16x4 hi =
+            __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Bs + (16 + 4 * g + q) * (BN + 16) + col));
+        const s16x8 b8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        bfg[j] = __builtin_bit_cast(bf16x8, b8);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        af[i] = *reinterpret_cast<const bf16x8*>(As + (wm * WM + i * 16 + (lane & 15)) * PITCH + 8 * (lane >> 4));
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        bfg[j] = *reinterpret_cast<const bf16x8*>(Bs + (wn * WN + j * 16 + (lane & 15)) * PITCH + 8 * (lane >> 4));
+    }
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -379,18 +427,31 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
 // ------------------------------------------------------------------------------------------------
 // fwd / dgrad kernel, fp32 (exact-f32 MFMA 16x16x4)
 // ------------------------------------------------------------------------------------------------
-template <int BM, int BN, bool PRO, bool STATS, int AM = 0>
+template <int BM, int BN, bool PRO, bool STATS, int AM = 0, bool BT = false>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__ A, int lda, Pro pro,
                                                        const float* __restrict__ Wt, int ldw, Epi epi,
                                                        float* __restrict__ out, int ldo, int M, int N, int K, int Ka,
-                                                       int Kb, int nMt, int nNt, ConvG cv) {
+                                                       int Kb, int nMt, int nNt, ConvG cv, int kc = 0) {
+  if (kc > 0) {  // split-K: blockIdx.y owns columns [y*kc, y*kc + kc); raw partial to out[y]
+    const int ofs = blockIdx.y * kc;
+    A += ofs;
+    Wt += ofs;
+    Ka = min(Ka - ofs, kc);
+    Kb = min(Kb - ofs, kc);
+    if (pro.sc) pro.sc += ofs;
+    if (pro.sh) pro.sh += ofs;
+    if (pro.gate) pro.gate += ofs;
+    out += (long)blockIdx.y * M * ldo;
+    K = kc;
+  }
   constexpr int BK = 16;
   constexpr int PITCH = BK + 1;
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
   constexpr int A_F4 = BM * BK / 4 / 256;
   constexpr int B_F4 = BN * BK / 4 / 256;
-  __shared__ float As[BM * PITCH];
-  __shared__ float Bs[BN * PITCH];
+  constexpr int B_FLOATS = (BT && BK * (BN + 16) > BN * PITCH) ? BK * (BN + 16) : BN * PITCH;
+  __shared__ __attribute__((aligned(16))) float As[BM * PITCH];
+  __shared__ __attribute__((aligned(16))) float Bs[B_FLOATS];
 
   const int bid = blockIdx.x;
   const int xcd = bid & 7, local = bid >> 3;
@@ -456,6 +517,13 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
     }
 #pragma unroll
     for (int i = 0; i < B_F4; ++i) {
+      if constexpr (BT) {  // W stored [reduction][output]
+        const int idx = tid + i * 256, kr = idx / (BN / 4), nq = idx % (BN / 4);
+        const int gk = k0 + kr, gn = n0 + nq * 4;
+        rb[i] = float4{0.f, 0.f, 0.f, 0.f};
+        if (gk < Kb) rb[i] = ld4(Wt + (long)gk * ldw + gn, gn, N, b_vec);
+        continue;
+      }
       const int idx = tid + i * 256, row = idx / (BK / 4), kq = idx % (BK / 4);
       const int gn = n0 + row, gk = k0 + kq * 4;
       rb[i] = float4{0.f, 0.f, 0.f, 0.f};
@@ -480,6 +548,11 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
     }
 #pragma unroll
     for (int i = 0; i < B_F4; ++i) {
+      if constexpr (BT) {  // Bs[kr][n], pitch BN+16 (the 16x16x4 B fragment reads [k][n] directly)
+        const int idx = tid + i * 256, kr = idx / (BN / 4), nq = idx % (BN / 4);
+        *reinterpret_cast<float4*>(Bs + kr * (BN + 16) + nq * 4) = rb[i];
+        continue;
+      }
       const int idx = tid + i * 256, row = idx / (BK / 4), kq = idx % (BK / 4);
       float* d = Bs + row * PITCH + kq * 4;
       d[0] = rb[i].x; d[1] = rb[i].y; d[2] = rb[i].z; d[3] = rb[i].w;
@@ -497,7 +570,9 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
 #pragma unroll
       for (int i = 0; i < TM; ++i) af[i] = As[(wm * WM + i * 16 + (lane & 15)) * PITCH + ks + (lane >> 4)];
 #pragma unroll
-      for (int j = 0; j < TN; ++j) bfg[j] = Bs[(wn * WN + j * 16 + (lane & 15)) * PITCH + ks + (lane >> 4)];
+      for (int j = 0; j < TN; ++j)
+        bfg[j] = BT ? Bs[(ks + (lane >> 4)) * (BN + 16) + wn * WN + j * 16 + (lane & 15)]
+                    : Bs[(wn * WN + j * 16 + (lane & 15)) * PITCH + ks + (lane >> 4)];
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -876,50 +951,6 @@ __global__ __launch_bounds__(256) void small_fwd_kernel(const float* __restrict_
   out[(long)m * ldo + n] = v;
 }
 
-// dW[n][k] = sum_m rs*G[m,n] * pro(X)[m,k], dbias[n] = sum_m rs*G[m,n].
-// Block = 64 k-columns of one n; its 4 waves take interleaved quarters of M (coalesced X rows),
-// partials combined through LDS in a fixed order.  Column block kb == nKb carries dbias.
-__global__ __launch_bounds__(256) void small_wgrad_kernel(const float* __restrict__ G, int ldg,
-                                                          const float* __restrict__ X, int ldx, Pro pro,
-                                                          const float* __restrict__ rs, int rps, float* __restrict__ dW,
-                                                          float* __restrict__ dbias, int M, int N, int K) {
-  __shared__ float part[4][64];
-  const int nKb = (K + 63) / 64;
-  const int n = blockIdx.y, kb = blockIdx.x;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const bool bias_blk = kb == nKb;
-  const int k = kb * 64 + lane;
-  const bool p = pro.act != OGV_ACT_NONE || pro.sc || pro.sh || pro.gate;
-  float acc0 = 0.f, acc1 = 0.f;
-  if (bias_blk) {
-    if (lane == 0)
-      for (int m = wv; m < M; m += 4) acc0 += G[(long)m * ldg + n] * (rs ? rs[m / rps] : 1.f);
-  } else if (k < K) {
-    int m = wv;
-    for (; m + 4 < M; m += 8) {
-      const float x0 = X[(long)m * ldx + k], x1 = X[(long)(m + 4) * ldx + k];
-      const float g0 = G[(long)m * ldg + n] * (rs ? rs[m / rps] : 1.f);
-      const float g1 = G[(long)(m + 4) * ldg + n] * (rs ? rs[(m + 4) / rps] : 1.f);
-      acc0 = fmaf(g0, p ? pro_apply(pro, x0, m, k) : x0, acc0);
-      acc1 = fmaf(g1, p ? pro_apply(pro, x1, m + 4, k) : x1, acc1);
-    }
-    if (m < M) {
-      const float x0 = X[(long)m * ldx + k];
-      acc0 = fmaf(G[(long)m * ldg + n] * (rs ? rs[m / rps] : 1.f), p ? pro_apply(pro, x0, m, k) : x0, acc0);
-    }
-  }
-  part[wv][lane] = acc0 + acc1;
-  __syncthreads();
-  if (wv == 0) {
-    const float v = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
-    if (bias_blk) {
-      if (lane == 0) dbias[n] = v;
-    } else if (k < K) {
-      dW[(long)n * K + k] = v;
-    }
-  }
-}
-
 // WT[k][n] = W[n][k]  (fp32, 32x32 tiles through LDS), zero for n in [N, ldt)
 __global__ __launch_bounds__(256) void transpose_f32_kernel(const float* __restrict__ W, float* __restrict__ WT, int N,
                                                             int K, int ldt) {
@@ -1039,17 +1070,96 @@ void conv_gemm_launch(ogv_dtype dt, const void* A, const ConvG& cv, const float*
   }
 }
 
-static inline int pad8(int n) { return (n + 7) / 8 * 8; }
-size_t dgrad_ws_bytes(int N, int K) { return (size_t)pad8(N) * K * sizeof(float); }
+// ------------------------------------------------------------------ small-M fp32 GEMMs (SE MLP)
+// M = batch rows (512), K up to 1024: one K-serial block per 128-row tile would be latency-bound,
+// so K is split over blockIdx.y (exact-f32 MFMA, raw partials), then one pass sums the partials in
+// a fixed order and applies the epilogue.
+struct SplitPlan {
+  int S, kc, nNt, BN;
+};
+static SplitPlan splitk_plan(int M, int N, int K) {
+  SplitPlan p;
+  p.BN = N > 64 ? 128 : 64;
+  p.nNt = (N + p.BN - 1) / p.BN;
+  const long tiles = (long)((M + GEMM_BM - 1) / GEMM_BM) * p.nNt;
+  long S = (256 + tiles - 1) / tiles;
+  S = std::min(S, (long)((K + 31) / 32));                          // >= 2 MFMA K-steps per chunk
+  S = std::min(S, std::max(1L, (4L << 20) / ((long)M * N)));       // partials <= 16 MB
+  S = std::max(1L, std::min(S, 32L));
+  p.kc = (int)(((K + S - 1) / S + 15) / 16 * 16);
+  p.S = (K + p.kc - 1) / p.kc;
+  return p;
+}
+
+size_t splitk_ws_bytes(int M, int N, int K) {
+  const SplitPlan p = splitk_plan(M > 0 ? M : 1, N, K);
+  return (size_t)p.S * (M > 0 ? M : 1) * N * sizeof(float) + 256;
+}
+
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ part, int S, int M, int N,
+                                                            Epi epi, float* __restrict__ out, int ldo) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)M * N) return;
+  const int m = (int)(i / N), n = (int)(i - (long)m * N);
+  float v = 0.f;
+  for (int s = 0; s < S; ++s) v += part[(long)s * M * N + i];
+  if (epi.bias) v += epi.bias[n];
+  if (epi.rs) v *= epi.rs[m / epi.rps];
+  if (epi.res) v += static_cast<const float*>(epi.res)[(long)m * ldo + n];
+  if (epi.zact) v *= act_grad(epi.zact, static_cast<const float*>(epi.Z)[(long)m * epi.ldz + n]);
+  out[(long)m * ldo + n] = v;
+}
+
+void gemm_fwd_splitk_f32(const float* A, int lda, const Pro& pro, const float* W, int ldw, float* out, int ldo, int M,
+                         int N, int K, const Epi& epi, void* ws, hipStream_t s) {
+  if (M <= 0) return;
+  const SplitPlan p = splitk_plan(M, N, K);
+  float* part = (float*)ws;
+  const int nMt = (M + GEMM_BM - 1) / GEMM_BM;
+  dim3 grid((unsigned)(((nMt + 7) / 8) * 8 * p.nNt), (unsigned)p.S);
+  const bool pr = pro.any();
+  if (p.BN == 128) {
+    if (pr) gemm_f32_kernel<GEMM_BM, 128, true, false><<<grid, 256, 0, s>>>(A, lda, pro, W, ldw, Epi(), part, N, M, N,
+                                                                           p.kc, K, K, nMt, p.nNt, ConvG(), p.kc);
+    else gemm_f32_kernel<GEMM_BM, 128, false, false><<<grid, 256, 0, s>>>(A, lda, pro, W, ldw, Epi(), part, N, M, N,
+                                                                          p.kc, K, K, nMt, p.nNt, ConvG(), p.kc);
+  } else {
+    if (pr) gemm_f32_kernel<GEMM_BM, 64, true, false><<<grid, 256, 0, s>>>(A, lda, pro, W, ldw, Epi(), part, N, M, N,
+                                                                          p.kc, K, K, nMt, p.nNt, ConvG(), p.kc);
+    else gemm_f32_kernel<GEMM_BM, 64, false, false><<<grid, 256, 0, s>>>(A, lda, pro, W, ldw, Epi(), part, N, M, N,
+                                                                         p.kc, K, K, nMt, p.nNt, ConvG(), p.kc);
+  }
+  splitk_reduce_kernel<<<cdiv((long)M * N, 256), 256, 0, s>>>(part, p.S, M, N, epi, out, ldo);
+}
+
+void transpose_f32_launch(const float* W, float* WT, int N, int K, int ldt, hipStream_t s) {
+  dim3 tg(cdiv(K, 32), cdiv(ldt, 32));
+  transpose_f32_kernel<<<tg, 256, 0, s>>>(W, WT, N, K, ldt);
+}
+
+size_t dgrad_ws_bytes(int N, int K) { return 256; }
+
+template <typename T, int BN>
+static void launch_mm_bt(const void* A, int lda, const float* W, int ldw, void* out, int ldo, int M, int N, int K,
+                         const Epi& epi, hipStream_t s) {
+  constexpr int BM = GEMM_BM;
+  const int nMt = (M + BM - 1) / BM, nNt = (N + BN - 1) / BN;
+  const unsigned grid = (unsigned)(((nMt + 7) / 8) * 8 * nNt);
+  const int Kp = (K + 31) / 32 * 32;
+  if constexpr (sizeof(T) == 2)
+    gemm_bf16_kernel<BM, BN, false, false, 0, true><<<grid, 256, 0, s>>>((const bf16*)A, lda, Pro(), W, ldw, epi,
+                                                                         (bf16*)out, ldo, M, N, Kp, K, K, nMt, nNt,
+                                                                         ConvG());
+  else
+    gemm_f32_kernel<BM, BN, false, false, 0, true><<<grid, 256, 0, s>>>((const float*)A, lda, Pro(), W, ldw, epi,
+                                                                        (float*)out, ldo, M, N, Kp, K, K, nMt, nNt,
+                                                                        ConvG());
+}
 
 void gemm_dgrad_launch(ogv_dtype dt, const void* dout, int ldd, const float* W, const void* Z, int ldz, int zact,
                        const float* rs, int rps, const void* res, void* dA, int lda, int M, int N, int K, void* ws,
                        hipStream_t s) {
   if (M <= 0) return;
-  float* WT = (float*)ws;  // [K][Np], zero beyond N
-  const int Np = pad8(N);
-  dim3 tg(cdiv(K, 32), cdiv(Np, 32));
-  transpose_f32_kernel<<<tg, 256, 0, s>>>(W, WT, N, K, Np);
   Epi e;
   e.rs = rs;
   e.rps = rps;
@@ -1057,8 +1167,14 @@ void gemm_dgrad_launch(ogv_dtype dt, const void* dout, int ldd, const float* W, 
   e.ldz = ldz;
   e.zact = zact;
   e.res = res;
-  // dA[M,K] = dout[M,N] . WT[K,Np]^T
-  gemm_fwd_launch(dt, dout, ldd, Pro(), WT, Np, dA, lda, M, K, Np, N, Np, e, s);
+  // dA[M,K] = dout[M,N] . W[N,K]: W read as [reduction N][output K] (no transposed copy)
+  if (dt == OGV_BF16) {
+    if (K > 64) launch_mm_bt<bf16, 128>(dout, ldd, W, K, dA, lda, M, K, N, e, s);
+    else launch_mm_bt<bf16, 64>(dout, ldd, W, K, dA, lda, M, K, N, e, s);
+  } else {
+    if (K > 64) launch_mm_bt<float, 128>(dout, ldd, W, K, dA, lda, M, K, N, e, s);
+    else launch_mm_bt<float, 64>(dout, ldd, W, K, dA, lda, M, K, N, e, s);
+  }
 }
 
 // Split-M plan.  bf16: tiles of BN x BK in {64,128}^2, slab partials [S][N*K + N] (dW then
@@ -1075,7 +1191,7 @@ static WgradPlan wgrad_plan(ogv_dtype dt, int M, int N, int K) {
   p.nKt = (K + p.BK - 1) / p.BK;
   const long tiles = (long)p.nNt * p.nKt;
   long S = (1024 + tiles - 1) / tiles;
-  S = std::min(S, ((long)M + 255) / 256);
+  S = std::min(S, ((long)M + (M <= 4096 ? 31 : 255)) / (M <= 4096 ? 32 : 256));  // small M (SE): 32-row slabs
   const double data = 2.0 * M * (N + K) * (dt == OGV_BF16 ? 2 : 4);
   const long cap = (long)(std::max(data / 4, 16.0 * (1 << 20)) / (4.0 * ((double)N * K + N)));
   S = std::max(1L, std::min(S, cap));
@@ -1121,12 +1237,6 @@ void gemm_wgrad_launch(ogv_dtype dt, const void* G, int ldg, const void* X, int 
   if (M <= 0) {
     (void)hipMemsetAsync(dW, 0, (size_t)N * K * sizeof(float), s);
     if (dbias) (void)hipMemsetAsync(dbias, 0, (size_t)N * sizeof(float), s);
-    return;
-  }
-  if (dt == OGV_F32 && M <= 2048 && !xc) {
-    dim3 grid(cdiv(K, 64) + (dbias ? 1 : 0), N);
-    small_wgrad_kernel<<<grid, 256, 0, s>>>((const float*)G, ldg, (const float*)X, ldx, pro, rs, rps, dW, dbias, M, N,
-                                            K);
     return;
   }
   const WgradPlan p = wgrad_plan(dt, M, N, K);

@@ -121,9 +121,21 @@ struct TileIdx {
   int ct, colt, band;
   long b, rid;
 };
-__device__ __forceinline__ TileIdx tile_idx(const DwTile& t) {
+// XCD-aware block order: hardware block i runs on XCD i % 8, so logical tile
+// id = (i % 8) * per_xcd + i / 8 gives each XCD a contiguous run of logical tiles.  Channel
+// tiles are the fastest index: the nct blocks that share a pixel tile's cache lines (a block
+// reads only CT of the C channels of each NHWC pixel) land on one XCD / one L2 back to back.
+static unsigned dw_grid(const DwTile& t) {
+  const long nb = t.rows() * t.nct;
+  return (unsigned)(((nb + 7) / 8) * 8);
+}
+__device__ __forceinline__ bool tile_valid(const DwTile& t, long& id) {
+  const long nb = t.rows() * t.nct, per = (nb + 7) / 8;
+  id = (long)(blockIdx.x & 7) * per + (blockIdx.x >> 3);
+  return id < nb;
+}
+__device__ __forceinline__ TileIdx tile_idx(const DwTile& t, long id) {
   TileIdx i;
-  long id = blockIdx.x;
   i.ct = (int)(id % t.nct); id /= t.nct;
   i.colt = (int)(id % t.ncolt); id /= t.ncolt;
   i.band = (int)(id % t.nbands);
@@ -171,7 +183,9 @@ __global__ __launch_bounds__(256) void dw_fwd_tile_kernel(const T* __restrict__ 
                                                           int act, T* __restrict__ out, double* __restrict__ stat,
                                                           const float* __restrict__ shift, DwTile t) {
   extern __shared__ __attribute__((aligned(16))) float tile[];
-  const TileIdx ti = tile_idx(t);
+  long tid_ = 0;
+  if (!tile_valid(t, tid_)) return;
+  const TileIdx ti = tile_idx(t, tid_);
   stage_tile<T, V, true>(tile, e, t, ti, sc, sh, act);
   __syncthreads();
   const int chunk = threadIdx.x & 3, slot = threadIdx.x >> 2;
@@ -234,7 +248,9 @@ __global__ __launch_bounds__(256) void dw_dgrad_tile_kernel(const T* __restrict_
                                                             const float* __restrict__ invstd, int act,
                                                             T* __restrict__ out, float* __restrict__ stat, DwTile t) {
   extern __shared__ __attribute__((aligned(16))) float tile[];
-  const TileIdx ti = tile_idx(t);
+  long tid_ = 0;
+  if (!tile_valid(t, tid_)) return;
+  const TileIdx ti = tile_idx(t, tid_);
   stage_tile<T, V, false>(tile, dd, t, ti, nullptr, nullptr, 0);
   __syncthreads();
   const int chunk = threadIdx.x & 3, slot = threadIdx.x >> 2;
@@ -296,7 +312,9 @@ __global__ __launch_bounds__(256) void dw_wgrad_tile_kernel(const T* __restrict_
                                                             const float* __restrict__ sc, const float* __restrict__ sh,
                                                             int act, float* __restrict__ part, DwTile t) {
   extern __shared__ __attribute__((aligned(16))) float tile[];
-  const TileIdx ti = tile_idx(t);
+  long tid_ = 0;
+  if (!tile_valid(t, tid_)) return;
+  const TileIdx ti = tile_idx(t, tid_);
   stage_tile<T, V, true>(tile, e, t, ti, sc, sh, act);
   __syncthreads();
   const int chunk = threadIdx.x & 3, slot = threadIdx.x >> 2;
@@ -346,11 +364,15 @@ __global__ void tapmajor_to_chan_kernel(const float* __restrict__ s, float* __re
 template <typename T, int V>
 __global__ __launch_bounds__(256) void se_pool_kernel(const T* __restrict__ d, const float* __restrict__ sc,
                                                       const float* __restrict__ sh, int act, float* __restrict__ pooled,
-                                                      int HW, int K) {
+                                                      int HW, int K, int B) {
   __shared__ float lds[4 * 1 * 4 * 8];
+  const int gx = (K + 4 * V - 1) / (4 * V);
+  long lid;
+  if (!xcd_block((long)gx * B, lid)) return;
+  const int bx = (int)(lid % gx);
   const int chunk = threadIdx.x & 3, slot = threadIdx.x >> 2;
-  const int c0 = (blockIdx.x * 4 + chunk) * V;
-  const long b = blockIdx.y;
+  const int c0 = (bx * 4 + chunk) * V;
+  const long b = lid / gx;
   float q[1][V];
 #pragma unroll
   for (int i = 0; i < V; ++i) q[0][i] = 0.f;
@@ -368,7 +390,7 @@ __global__ __launch_bounds__(256) void se_pool_kernel(const T* __restrict__ d, c
 #pragma unroll
     for (int i = 0; i < V; ++i) q[0][i] *= inv;
   }
-  chunk_reduce_store<1, V>(q, lds, pooled + b * K, K, K, blockIdx.x * 4 * V);
+  chunk_reduce_store<1, V>(q, lds, pooled + b * K, K, K, bx * 4 * V);
 }
 
 __global__ void sigmoid_kernel(const float* __restrict__ z, float* __restrict__ g, long n) {
@@ -393,9 +415,13 @@ __global__ __launch_bounds__(256) void se_bwd_reduce_kernel(const T* __restrict_
                                                             const float* __restrict__ invstd, int act,
                                                             float* __restrict__ R, int B, int HW, int K) {
   __shared__ float lds[4 * 5 * 4 * 8];
+  const int gx = (K + 4 * V - 1) / (4 * V);
+  long lid;
+  if (!xcd_block((long)gx * B, lid)) return;
+  const int bx = (int)(lid % gx);
   const int chunk = threadIdx.x & 3, slot = threadIdx.x >> 2;
-  const int c0 = (blockIdx.x * 4 + chunk) * V;
-  const long b = blockIdx.y;
+  const int c0 = (bx * 4 + chunk) * V;
+  const long b = lid / gx;
   float q[5][V];
 #pragma unroll
   for (int k = 0; k < 5; ++k)
@@ -432,7 +458,7 @@ __global__ __launch_bounds__(256) void se_bwd_reduce_kernel(const T* __restrict_
       }
     }
   }
-  chunk_reduce_store<5, V>(q, lds, R + b * K, (long)B * K, K, blockIdx.x * 4 * V);
+  chunk_reduce_store<5, V>(q, lds, R + b * K, (long)B * K, K, bx * 4 * V);
 }
 
 // BN2 reductions from the per-image sums: dy2 = (dA3*gate + dpool/HW) * s'
@@ -493,9 +519,14 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* __restrict_
                                                             const float* __restrict__ invstd, float* __restrict__ stat,
                                                             long M, int K, long rows_per_slice) {
   __shared__ float lds[4 * 2 * 4 * 8];
+  const int gx = (K + 4 * V - 1) / (4 * V);
+  long lid;
+  if (!xcd_block((long)gx * ((M + rows_per_slice - 1) / rows_per_slice), lid)) return;
+  const int bx = (int)(lid % gx);
+  const long by = lid / gx;
   const int chunk = threadIdx.x & 3, slot = threadIdx.x >> 2;
-  const int c0 = (blockIdx.x * 4 + chunk) * V;
-  const long r0 = (long)blockIdx.y * rows_per_slice;
+  const int c0 = (bx * 4 + chunk) * V;
+  const long r0 = by * rows_per_slice;
   const long r1 = r0 + rows_per_slice < M ? r0 + rows_per_slice : M;
   float q[2][V];
 #pragma unroll
@@ -515,7 +546,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* __restrict_
       }
     }
   }
-  chunk_reduce_store<2, V>(q, lds, stat + (long)blockIdx.y * 2 * K, K, K, blockIdx.x * 4 * V);
+  chunk_reduce_store<2, V>(q, lds, stat + by * 2 * K, K, K, bx * 4 * V);
 }
 
 // out = ca*(dy - cb - (x-mean)*invstd*cc)
@@ -614,6 +645,7 @@ static long dw_slices(long P, const RowPlan& rp) {   // row slices for the globa
 
 struct FwdWs {
   double *stat1, *stat2, *stat3, *sums, *tmp;  // fp64 BatchNorm batch statistics
+  float* split;                                // SE split-K partials
   char* gemm;
 };
 static FwdWs fwd_ws_layout(void* base, const ogv_mbconv_desc& s, size_t* total) {
@@ -629,6 +661,7 @@ static FwdWs fwd_ws_layout(void* base, const ogv_mbconv_desc& s, size_t* total) 
   w.sums = b.take<double>(2 * (size_t)(s.mid > s.C ? s.mid : s.C));
   long Rmax = R1 > S2 ? R1 : S2;
   w.tmp = b.take<double>(colreduce_tmp_floats(Rmax, 2L * (s.mid > s.C ? s.mid : s.C)) + 16);
+  w.split = b.take<float>(std::max(splitk_ws_bytes(s.B, s.se, s.mid), splitk_ws_bytes(s.B, s.mid, s.se)) / 4 + 64);
   w.gemm = b.take<char>(64);
   if (total) *total = b.off + 256;
   return w;
@@ -637,6 +670,7 @@ static FwdWs fwd_ws_layout(void* base, const ogv_mbconv_desc& s, size_t* total) 
 struct BwdWs {
   void *dp, *bufA, *bufB;
   float *stat, *S, *coef, *R, *dgate, *dz2, *dh, *dz1, *dpool, *part9, *tmp, *sums9, *terms;
+  float *wtse, *split;  // transposed SE weight, split-K partials
   char* gemm;
 };
 static size_t max3(size_t a, size_t b, size_t c) { return a > b ? (a > c ? a : c) : (b > c ? b : c); }
@@ -665,6 +699,8 @@ static BwdWs bwd_ws_layout(void* base, const ogv_mbconv_desc& s, size_t esz, siz
   w.tmp = b.take<float>(max3(max3(colreduce_tmp_floats(Smax, 2 * K2), colreduce_tmp_floats(S2, 9L * s.mid), 16),
                              colreduce_tmp_floats(s.B, 2L * s.mid), 16));
   w.sums9 = b.take<float>(9 * (size_t)s.mid);
+  w.wtse = b.take<float>((size_t)s.mid * s.se);
+  w.split = b.take<float>(std::max(splitk_ws_bytes(s.B, s.se, s.mid), splitk_ws_bytes(s.B, s.mid, s.se)) / 4 + 64);
   const size_t g = max3(max3(dgrad_ws_bytes(s.C, s.mid), dgrad_ws_bytes(s.mid, s.C), wgrad_ws_bytes((int)M, s.C, s.mid)),
                         max3(wgrad_ws_bytes((int)M, s.mid, s.C), wgrad_ws_bytes(s.B, s.mid, s.se),
                              wgrad_ws_bytes(s.B, s.se, s.mid)),
@@ -691,32 +727,33 @@ struct Ops {
   template <int V>
   static void dw_fwd(const void* e, const float* w, const float* sc, const float* sh, int act, void* out, double* stat,
                      const float* shift, const DwTile& t, hipStream_t st) {
-    const unsigned nb = (unsigned)(t.rows() * t.nct);
+    const unsigned nb = dw_grid(t);
     dw_fwd_tile_kernel<T, V><<<nb, 256, t.lds_bytes(), st>>>((const T*)e, w, sc, sh, act, (T*)out, stat, shift, t);
   }
   template <int V>
   static void dw_dgrad(const void* dd, const float* w, const void* e, const float* sc, const float* sh,
                        const float* mean, const float* inv, int act, void* out, float* stat, const DwTile& t,
                        hipStream_t st) {
-    const unsigned nb = (unsigned)(t.rows() * t.nct);
+    const unsigned nb = dw_grid(t);
     dw_dgrad_tile_kernel<T, V><<<nb, 256, t.lds_bytes(), st>>>((const T*)dd, w, (const T*)e, sc, sh, mean, inv, act,
                                                               (T*)out, stat, t);
   }
   template <int V>
   static void dw_wgrad(const void* dd, const void* e, const float* sc, const float* sh, int act, float* part,
                        const DwTile& t, hipStream_t st) {
-    const unsigned nb = (unsigned)(t.rows() * t.nct);
+    const unsigned nb = dw_grid(t);
     dw_wgrad_tile_kernel<T, V><<<nb, 256, t.lds_bytes(), st>>>((const T*)dd, (const T*)e, sc, sh, act, part, t);
   }
   template <int V>
   static void pool(const void* d, const float* sc, const float* sh, int act, float* pooled, int B, int HW, int K,
                    const RowPlan& rp, hipStream_t st) {
-    se_pool_kernel<T, V><<<dim3(cdiv(K, 4 * V), B), 256, 0, st>>>((const T*)d, sc, sh, act, pooled, HW, K);
+    se_pool_kernel<T, V><<<xcd_grid((long)cdiv(K, 4 * V) * B), 256, 0, st>>>((const T*)d, sc, sh, act, pooled, HW, K,
+                                                                           B);
   }
   template <int V>
   static void se_reduce(const void* dA3, const void* d, const float* sc, const float* sh, const float* mean,
                         const float* inv, int act, float* R, int B, int HW, int K, const RowPlan& rp, hipStream_t st) {
-    se_bwd_reduce_kernel<T, V><<<dim3(cdiv(K, 4 * V), B), 256, 0, st>>>((const T*)dA3, (const T*)d, sc, sh, mean, inv,
+    se_bwd_reduce_kernel<T, V><<<xcd_grid((long)cdiv(K, 4 * V) * B), 256, 0, st>>>((const T*)dA3, (const T*)d, sc, sh, mean, inv,
                                                                         act, R, B, HW, K);
   }
   template <int V>
@@ -729,7 +766,7 @@ struct Ops {
   template <int V>
   static void bn_reduce(const void* dy, const void* x, const float* mean, const float* inv, float* stat, long M, int K,
                         const RowPlan& rp, long S, long per, hipStream_t st) {
-    bn_bwd_reduce_kernel<T, V><<<dim3(cdiv(K, 4 * V), S), 256, 0, st>>>((const T*)dy, (const T*)x, mean, inv, stat, M,
+    bn_bwd_reduce_kernel<T, V><<<xcd_grid((long)cdiv(K, 4 * V) * S), 256, 0, st>>>((const T*)dy, (const T*)x, mean, inv, stat, M,
                                                                         K, per);
   }
   template <int V>
@@ -779,13 +816,12 @@ static void mbconv_fwd_impl(const void* x, void* out, const Saved& sv, const Fwd
     OGV_V_DISPATCH(rp.V, O::template pool, sv.d, sv.sc2, sv.sh2, s.act, sv.pooled, s.B, HW, s.mid, rp, st);
     Epi e1;
     e1.bias = P.se_b1;
-    gemm_fwd_launch(OGV_F32, sv.pooled, s.mid, Pro(), P.se_w1, s.mid, sv.z1, s.se, s.B, s.se, s.mid, s.mid, s.mid, e1,
-                    st);
+    gemm_fwd_splitk_f32(sv.pooled, s.mid, Pro(), P.se_w1, s.mid, sv.z1, s.se, s.B, s.se, s.mid, e1, w.split, st);
     Pro p2;
     p2.act = s.act;
     Epi e2;
     e2.bias = P.se_b2;
-    gemm_fwd_launch(OGV_F32, sv.z1, s.se, p2, P.se_w2, s.se, sv.z2, s.mid, s.B, s.mid, s.se, s.se, s.se, e2, st);
+    gemm_fwd_splitk_f32(sv.z1, s.se, p2, P.se_w2, s.se, sv.z2, s.mid, s.B, s.mid, s.se, e2, w.split, st);
     sigmoid_kernel<<<cdiv((long)s.B * s.mid, 256), 256, 0, st>>>(sv.z2, sv.gate, (long)s.B * s.mid);
   }
   // 4) project GEMM on act(BN2(d)) * gate (+ BN3 stats), then out = x + BN3(p)
@@ -848,12 +884,20 @@ static void mbconv_bwd_impl(const void* dout, const void* x, const Saved& sv, vo
     Pro p2;
     p2.act = s.act;
     gemm_wgrad_launch(OGV_F32, w.dz2, s.mid, sv.z1, s.se, p2, nullptr, 1, G.se_w2, G.se_b2, s.B, s.mid, s.se, w.gemm, st);
-    gemm_dgrad_launch(OGV_F32, w.dz2, s.mid, P.se_w2, sv.z1, s.se, s.act, nullptr, 1, nullptr, w.dz1, s.se, s.B, s.mid,
-                      s.se, w.gemm, st);
+    {  // dz1 = act'(z1) * (dz2 . W2):  W2 [mid, se] -> W2^T [se, mid]
+      transpose_f32_launch(P.se_w2, w.wtse, s.mid, s.se, s.mid, st);
+      Epi e;
+      e.Z = sv.z1;
+      e.ldz = s.se;
+      e.zact = s.act;
+      gemm_fwd_splitk_f32(w.dz2, s.mid, Pro(), w.wtse, s.mid, w.dz1, s.se, s.B, s.se, s.mid, e, w.split, st);
+    }
     gemm_wgrad_launch(OGV_F32, w.dz1, s.se, sv.pooled, s.mid, Pro(), nullptr, 1, G.se_w1, G.se_b1, s.B, s.se, s.mid,
                       w.gemm, st);
-    gemm_dgrad_launch(OGV_F32, w.dz1, s.se, P.se_w1, nullptr, 0, 0, nullptr, 1, nullptr, w.dpool, s.mid, s.B, s.se,
-                      s.mid, w.gemm, st);
+    {  // dpool = dz1 . W1:  W1 [se, mid] -> W1^T [mid, se]
+      transpose_f32_launch(P.se_w1, w.wtse, s.se, s.mid, s.se, st);
+      gemm_fwd_splitk_f32(w.dz1, s.se, Pro(), w.wtse, s.se, w.dpool, s.mid, s.B, s.mid, s.se, Epi(), w.split, st);
+    }
   }
   // B5) BN2 backward: dd = ca*(dy2 - cb - dhat*cc)  -> bufB
   {

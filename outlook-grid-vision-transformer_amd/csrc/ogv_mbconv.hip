@@ -91,264 +91,325 @@ void bn_coeffs_launch(const float* S, int K, float n, const float* gamma, const 
 }
 
 // ------------------------------------------------------------------ depthwise conv with BN fusion
-// ---- LDS-tiled depthwise kernels -------------------------------------------------------------
-// Block = (image b, band of TR rows, column tile of TW, channel tile of CT = 4*V channels).
-// The (TR+2) x (TW+2) x CT input tile (1-pixel halo, zero outside the image) is staged into LDS as
-// fp32 with the producer's BatchNorm + activation applied ONCE per element; 256 threads =
-// 64 pixel slots x 4 channel chunks then compute from LDS.  Per-block statistics partials go to
-// row rid = (b*nbands + band)*ncolt + colt of a [rows][Q][C] slab (Q quantities).
+// ---- row-streaming depthwise kernels -------------------------------------------------------
+// Block = (image b, column strip of TW <= 32 pixels, channel tile of CT = chunks*V channels), XCD-aware
+// order with the channel tile fastest.  The block walks down the image DW_R output rows per step:
+// a (DW_R+2)-row ring in LDS holds input rows y-1 .. y+DW_R (TW+2 pixels with the column halo, zero
+// outside the image, the producer's BatchNorm + activation applied once per element as it is
+// staged) and the next DW_R rows are loaded into registers while the current ones are computed, so
+// every input element is read from HBM once and ~DW_R rows per block are in flight.  chunks is
+// chosen so that one output row is ~256 (pixel, V-channel chunk) items: one per thread per row.
+// Statistics / weight-gradient partials are reduced once per block into row rid = b*ncolt + colt
+// of a [rows][Q][C] slab.
+constexpr int DW_R = 4;
 struct DwTile {
-  int B, H, W, C, TR, TW, nbands, ncolt, nct, CT, PP;
-  __host__ __device__ long rows() const { return (long)B * nbands * ncolt; }
-  __host__ __device__ size_t lds_bytes() const { return (size_t)(TR + 2) * (TW + 2) * PP * sizeof(float); }
+  int B, H, W, C, TW, ncolt, chunks, CT, nct, PP, ldq;
+  __host__ __device__ long rows() const { return (long)B * ncolt; }
+  __host__ __device__ long nblocks() const { return rows() * nct; }
+  size_t ring_bytes() const { return (size_t)(DW_R + 2) * (TW + 2) * PP * sizeof(float); }
+  size_t lds_bytes(int nq, int V, size_t asz) const {
+    const size_t red = (size_t)4 * chunks * nq * V * asz;
+    return ring_bytes() > red ? ring_bytes() : red;
+  }
 };
 static DwTile dw_tile_plan(int B, int H, int W, int C, int V) {
   DwTile t;
   t.B = B; t.H = H; t.W = W; t.C = C;
   t.TW = W < 32 ? W : 32;
-  int tr = 128 / t.TW;
-  const int hcap = H < 32 ? H : 32;
-  t.TR = tr < 1 ? 1 : (tr > hcap ? hcap : tr);
-  t.nbands = (H + t.TR - 1) / t.TR;
   t.ncolt = (W + t.TW - 1) / t.TW;
-  t.CT = 4 * V;
-  t.PP = t.CT + 4;
+  int ch = 1;
+  while (ch * 2 * t.TW <= 256 && ch < 64) ch *= 2;            // ~256 items per output row
+  while (ch > 1 && (ch / 2) * V >= C) ch /= 2;                // do not exceed the channel count
+  t.chunks = ch;
+  t.CT = ch * V;
   t.nct = (C + t.CT - 1) / t.CT;
+  t.PP = t.CT + 4;
+  t.ldq = ((t.TW + 2) * ch + 255) / 256;                      // row-load items per thread (<= 3)
   return t;
 }
+static unsigned dw_grid(const DwTile& t) { return xcd_grid(t.nblocks()); }
 
 struct TileIdx {
-  int ct, colt, band;
+  int ct, colt, x0, tw;
   long b, rid;
 };
-// XCD-aware block order: hardware block i runs on XCD i % 8, so logical tile
-// id = (i % 8) * per_xcd + i / 8 gives each XCD a contiguous run of logical tiles.  Channel
-// tiles are the fastest index: the nct blocks that share a pixel tile's cache lines (a block
-// reads only CT of the C channels of each NHWC pixel) land on one XCD / one L2 back to back.
-static unsigned dw_grid(const DwTile& t) {
-  const long nb = t.rows() * t.nct;
-  return (unsigned)(((nb + 7) / 8) * 8);
-}
-__device__ __forceinline__ bool tile_valid(const DwTile& t, long& id) {
-  const long nb = t.rows() * t.nct, per = (nb + 7) / 8;
-  id = (long)(blockIdx.x & 7) * per + (blockIdx.x >> 3);
-  return id < nb;
-}
-__device__ __forceinline__ TileIdx tile_idx(const DwTile& t, long id) {
-  TileIdx i;
+__device__ __forceinline__ bool tile_idx(const DwTile& t, TileIdx& i) {
+  long id;
+  if (!xcd_block(t.nblocks(), id)) return false;
   i.ct = (int)(id % t.nct); id /= t.nct;
-  i.colt = (int)(id % t.ncolt); id /= t.ncolt;
-  i.band = (int)(id % t.nbands);
-  i.b = id / t.nbands;
-  i.rid = (i.b * t.nbands + i.band) * t.ncolt + i.colt;
-  return i;
+  i.colt = (int)(id % t.ncolt);
+  i.b = id / t.ncolt;
+  i.rid = i.b * t.ncolt + i.colt;
+  i.x0 = i.colt * t.TW;
+  i.tw = t.W - i.x0 < t.TW ? t.W - i.x0 : t.TW;
+  return true;
 }
 
-// stage tile[r][c][ch] = pro(src[b, y0-1+r, x0-1+c, c0+ch]) (0 outside image / channels)
-template <typename T, int V, bool PRO>
-__device__ __forceinline__ void stage_tile(float* tile, const T* __restrict__ src, const DwTile& t, const TileIdx& ti,
-                                           const float* __restrict__ sc, const float* __restrict__ sh, int act) {
-  const int y0 = ti.band * t.TR - 1, x0 = ti.colt * t.TW - 1, c0 = ti.ct * t.CT;
-  const int tw2 = t.TW + 2;
-  const int n = (t.TR + 2) * tw2 * 4;
-  for (int idx = threadIdx.x; idx < n; idx += 256) {
-    const int chunk = idx & 3, pix = idx >> 2;
-    const int r = pix / tw2, cc = pix - r * tw2;
-    const int y = y0 + r, x = x0 + cc, c = c0 + chunk * V;
-    float v[V];
-    if (y >= 0 && y < t.H && x >= 0 && x < t.W && c < t.C) {
-      load_vec<T, V>(src + ((ti.b * t.H + y) * t.W + x) * t.C + c, v);
-      if constexpr (PRO) {
-        float s[V], h[V];
-        load_vec<float, V>(sc + c, s);
-        load_vec<float, V>(sh + c, h);
+__device__ __forceinline__ int ring_slot(int r) { return (r + DW_R + 2) % (DW_R + 2); }
+__device__ __forceinline__ const float* ring_px(const float* ring, const DwTile& t, int r, int px) {
+  return ring + ((size_t)ring_slot(r) * (t.TW + 2) + px) * t.PP;
+}
+
+// Up to DW_R input rows (TW+2 pixels incl. halo) of the block's channel tile, in registers.
+template <typename T, int V, int LDQ, bool PRO>
+struct RowPipe {
+  float v[DW_R][LDQ][V];
+  __device__ __forceinline__ void load(const T* __restrict__ src, const DwTile& t, const TileIdx& ti, int y0, int nr,
+                                       int c, bool cok, const float* s, const float* h, int act) {
+    const int n = (ti.tw + 2) * t.chunks;
 #pragma unroll
-        for (int i = 0; i < V; ++i) v[i] = act_fwd(act, fmaf(v[i], s[i], h[i]));
+    for (int r = 0; r < DW_R; ++r)
+#pragma unroll
+      for (int j = 0; j < LDQ; ++j) {
+        const int i = threadIdx.x + j * 256, y = y0 + r;
+        const int x = ti.x0 - 1 + i / t.chunks;
+        if (r < nr && i < n && cok && y >= 0 && y < t.H && x >= 0 && x < t.W) {
+          load_vec<T, V>(src + ((ti.b * t.H + y) * t.W + x) * t.C + c, v[r][j]);
+          if constexpr (PRO) {
+#pragma unroll
+            for (int k = 0; k < V; ++k) v[r][j][k] = act_fwd(act, fmaf(v[r][j][k], s[k], h[k]));
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < V; ++k) v[r][j][k] = 0.f;
+        }
       }
-    } else {
+  }
+  __device__ __forceinline__ void store(float* ring, const DwTile& t, const TileIdx& ti, int y0, int nr,
+                                        int chunk) const {
+    const int n = (ti.tw + 2) * t.chunks;
 #pragma unroll
-      for (int i = 0; i < V; ++i) v[i] = 0.f;
+    for (int r = 0; r < DW_R; ++r) {
+      if (r >= nr) break;
+      float* slot = ring + (size_t)ring_slot(y0 + r) * (t.TW + 2) * t.PP;
+#pragma unroll
+      for (int j = 0; j < LDQ; ++j) {
+        const int i = threadIdx.x + j * 256;
+        if (i < n) {
+          float* d = slot + (i / t.chunks) * t.PP + chunk * V;
+#pragma unroll
+          for (int k = 0; k < V; k += 4)
+            *reinterpret_cast<float4*>(d + k) = make_float4(v[r][j][k], v[r][j][k + 1], v[r][j][k + 2], v[r][j][k + 3]);
+        }
+      }
     }
-    float* d = tile + pix * t.PP + chunk * V;
+  }
+};
+
+// Sum the per-thread q[NQ][V] over the threads sharing a channel chunk (chunk = tid % chunks):
+// xor-shuffles inside each wave, then the 4 waves through LDS (reused ring).  out[k*qstride + c].
+template <int NQ, int V, typename A>
+__device__ __forceinline__ void dw_reduce_store(A (&q)[NQ][V], float* lds_raw, int chunks, A* out, long qstride,
+                                                int C, int c0) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
-    for (int i = 0; i < V; i += 4) *reinterpret_cast<float4*>(d + i) = make_float4(v[i], v[i + 1], v[i + 2], v[i + 3]);
+  for (int k = 0; k < NQ; ++k)
+#pragma unroll
+    for (int i = 0; i < V; ++i)
+      for (int o = chunks; o < 64; o <<= 1) q[k][i] += __shfl_xor(q[k][i], o, 64);
+  A* lds = reinterpret_cast<A*>(lds_raw);
+  __syncthreads();
+  if (lane < chunks) {
+#pragma unroll
+    for (int k = 0; k < NQ; ++k)
+#pragma unroll
+      for (int i = 0; i < V; ++i) lds[((wave * chunks + lane) * NQ + k) * V + i] = q[k][i];
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < chunks * NQ * V; idx += 256) {
+    const int ch = idx / (NQ * V), r = idx - ch * NQ * V, k = r / V, i = r - k * V;
+    A sum = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) sum += lds[((w * chunks + ch) * NQ + k) * V + i];
+    const int c = c0 + ch * V + i;
+    if (c < C) out[(long)k * qstride + c] = sum;
   }
 }
 
+// The shared row walk: ring <- rows -1, 0; regs <- rows 1..R; per step: store regs (rows y+1..y+R),
+// prefetch rows y+R+1..y+2R, compute output rows y..y+R-1 through body(y_row, px, it).
+template <typename T, int V, int LDQ, bool PRO, typename Body>
+__device__ __forceinline__ void dw_walk(float* ring, const T* __restrict__ src, const DwTile& t, const TileIdx& ti,
+                                        int c, int chunk, bool cok, const float* s, const float* h, int act,
+                                        Body&& body) {
+  RowPipe<T, V, LDQ, PRO> rp;
+  rp.load(src, t, ti, -1, 2, c, cok, s, h, act);
+  rp.store(ring, t, ti, -1, 2, chunk);
+  rp.load(src, t, ti, 1, DW_R, c, cok, s, h, act);
+  const int nitems = ti.tw * t.chunks;
+  for (int y = 0; y < t.H; y += DW_R) {
+    rp.store(ring, t, ti, y + 1, DW_R, chunk);
+    __syncthreads();
+    if (y + DW_R < t.H) rp.load(src, t, ti, y + DW_R + 1, DW_R, c, cok, s, h, act);
+    if (cok) {
+#pragma unroll
+      for (int r = 0; r < DW_R; ++r) {
+        const int yy = y + r;
+        if (yy >= t.H) break;
+        for (int it = threadIdx.x; it < nitems; it += 256) body(yy, it / t.chunks);
+      }
+    }
+    __syncthreads();
+  }
+}
 
-// d = dw3x3(act(e*sc1 + sh1)) (+ stats of the rounded output minus shift)
-template <typename T, int V>
+// d = dw3x3(act(e*sc1 + sh1)) (+ fp64 stats of the rounded output minus shift)
+template <typename T, int V, int LDQ>
 __global__ __launch_bounds__(256) void dw_fwd_tile_kernel(const T* __restrict__ e, const float* __restrict__ wdw,
                                                           const float* __restrict__ sc, const float* __restrict__ sh,
                                                           int act, T* __restrict__ out, double* __restrict__ stat,
                                                           const float* __restrict__ shift, DwTile t) {
-  extern __shared__ __attribute__((aligned(16))) float tile[];
-  long tid_ = 0;
-  if (!tile_valid(t, tid_)) return;
-  const TileIdx ti = tile_idx(t, tid_);
-  stage_tile<T, V, true>(tile, e, t, ti, sc, sh, act);
-  __syncthreads();
-  const int chunk = threadIdx.x & 3, slot = threadIdx.x >> 2;
+  extern __shared__ __attribute__((aligned(16))) float ring[];
+  TileIdx ti;
+  if (!tile_idx(t, ti)) return;
+  const int chunk = threadIdx.x % t.chunks;
   const int c = ti.ct * t.CT + chunk * V;
-  double q[2][V];  // BN batch statistics in fp64 (no cancellation when the mean is far from the shift)
+  const bool cok = c < t.C;
+  float w[9][V], s[V], h[V], sft[V];
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) w[k][i] = cok ? wdw[(c + i) * 9 + k] : 0.f;
+    s[i] = cok ? sc[c + i] : 0.f;
+    h[i] = cok ? sh[c + i] : 0.f;
+    sft[i] = (cok && shift) ? shift[c + i] : 0.f;
+  }
+  double q[2][V];  // BN batch statistics in fp64
 #pragma unroll
   for (int i = 0; i < V; ++i) { q[0][i] = 0.0; q[1][i] = 0.0; }
-  if (c < t.C) {
-    float w[9][V], sft[V];
+  dw_walk<T, V, LDQ, true>(ring, e, t, ti, c, chunk, cok, s, h, act, [&](int y, int px) {
+    float acc[V];
+#pragma unroll
+    for (int i = 0; i < V; ++i) acc[i] = 0.f;
+#pragma unroll
+    for (int ki = 0; ki < 3; ++ki)
+#pragma unroll
+      for (int kj = 0; kj < 3; ++kj) {
+        const float* src = ring_px(ring, t, y - 1 + ki, px + kj) + chunk * V;
+#pragma unroll
+        for (int i = 0; i < V; i += 4) {
+          const float4 a = *reinterpret_cast<const float4*>(src + i);
+          acc[i] = fmaf(w[ki * 3 + kj][i], a.x, acc[i]);
+          acc[i + 1] = fmaf(w[ki * 3 + kj][i + 1], a.y, acc[i + 1]);
+          acc[i + 2] = fmaf(w[ki * 3 + kj][i + 2], a.z, acc[i + 2]);
+          acc[i + 3] = fmaf(w[ki * 3 + kj][i + 3], a.w, acc[i + 3]);
+        }
+      }
+    float of[V];
 #pragma unroll
     for (int i = 0; i < V; ++i) {
-#pragma unroll
-      for (int k = 0; k < 9; ++k) w[k][i] = wdw[(c + i) * 9 + k];
-      sft[i] = shift ? shift[c + i] : 0.f;
+      of[i] = to_f(from_f<T>(acc[i]));
+      const double dl = (double)of[i] - (double)sft[i];
+      q[0][i] += dl;
+      q[1][i] = fma(dl, dl, q[1][i]);
     }
-    const int tw2 = t.TW + 2;
-    for (int o = slot; o < t.TR * t.TW; o += 64) {
-      const int ry = o / t.TW, cx = o - ry * t.TW;
-      const int y = ti.band * t.TR + ry, x = ti.colt * t.TW + cx;
-      if (y >= t.H || x >= t.W) continue;
-      float acc[V];
-#pragma unroll
-      for (int i = 0; i < V; ++i) acc[i] = 0.f;
-#pragma unroll
-      for (int ki = 0; ki < 3; ++ki)
-#pragma unroll
-        for (int kj = 0; kj < 3; ++kj) {
-          const float* src = tile + ((ry + ki) * tw2 + cx + kj) * t.PP + chunk * V;
-#pragma unroll
-          for (int i = 0; i < V; i += 4) {
-            const float4 a = *reinterpret_cast<const float4*>(src + i);
-            acc[i] = fmaf(w[ki * 3 + kj][i], a.x, acc[i]);
-            acc[i + 1] = fmaf(w[ki * 3 + kj][i + 1], a.y, acc[i + 1]);
-            acc[i + 2] = fmaf(w[ki * 3 + kj][i + 2], a.z, acc[i + 2]);
-            acc[i + 3] = fmaf(w[ki * 3 + kj][i + 3], a.w, acc[i + 3]);
-          }
-        }
-      float of[V];
-#pragma unroll
-      for (int i = 0; i < V; ++i) {
-        of[i] = to_f(from_f<T>(acc[i]));
-        const double dl = (double)of[i] - (double)sft[i];
-        q[0][i] += dl;
-        q[1][i] = fma(dl, dl, q[1][i]);
-      }
-      store_vec<T, V>(out + ((ti.b * t.H + y) * t.W + x) * t.C + c, of);
-    }
-  }
-  if (stat)
-    chunk_reduce_store<2, V, double>(q, reinterpret_cast<double*>(tile), stat + ti.rid * 2 * t.C, t.C, t.C,
-                                     ti.ct * t.CT);
+    store_vec<T, V>(out + ((ti.b * t.H + y) * t.W + ti.x0 + px) * t.C + c, of);
+  });
+  if (stat) dw_reduce_store<2, V, double>(q, ring, t.chunks, stat + ti.rid * 2 * t.C, t.C, t.C, ti.ct * t.CT);
 }
 
 // dy1 = (dw3x3^T dd) * act'(e*sc1 + sh1) -> out; stats: sum dy1, sum dy1*(e - mean1)*invstd1
-template <typename T, int V>
+template <typename T, int V, int LDQ>
 __global__ __launch_bounds__(256) void dw_dgrad_tile_kernel(const T* __restrict__ dd, const float* __restrict__ wdw,
                                                             const T* __restrict__ e, const float* __restrict__ sc,
                                                             const float* __restrict__ sh,
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ invstd, int act,
                                                             T* __restrict__ out, float* __restrict__ stat, DwTile t) {
-  extern __shared__ __attribute__((aligned(16))) float tile[];
-  long tid_ = 0;
-  if (!tile_valid(t, tid_)) return;
-  const TileIdx ti = tile_idx(t, tid_);
-  stage_tile<T, V, false>(tile, dd, t, ti, nullptr, nullptr, 0);
-  __syncthreads();
-  const int chunk = threadIdx.x & 3, slot = threadIdx.x >> 2;
+  extern __shared__ __attribute__((aligned(16))) float ring[];
+  TileIdx ti;
+  if (!tile_idx(t, ti)) return;
+  const int chunk = threadIdx.x % t.chunks;
   const int c = ti.ct * t.CT + chunk * V;
+  const bool cok = c < t.C;
+  float w[9][V], s[V], h[V], mu[V], is[V];
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) w[k][i] = cok ? wdw[(c + i) * 9 + k] : 0.f;
+    s[i] = cok ? sc[c + i] : 0.f;
+    h[i] = cok ? sh[c + i] : 0.f;
+    mu[i] = cok ? mean[c + i] : 0.f;
+    is[i] = cok ? invstd[c + i] : 0.f;
+  }
   float q[2][V];
 #pragma unroll
   for (int i = 0; i < V; ++i) { q[0][i] = 0.f; q[1][i] = 0.f; }
-  if (c < t.C) {
-    float w[9][V], s[V], h[V], mu[V], is[V];
+  dw_walk<T, V, LDQ, false>(ring, dd, t, ti, c, chunk, cok, s, h, 0, [&](int y, int px) {
+    const long off = ((ti.b * t.H + y) * t.W + ti.x0 + px) * t.C + c;
+    float ev[V];
+    load_vec<T, V>(e + off, ev);
+    float acc[V];
+#pragma unroll
+    for (int i = 0; i < V; ++i) acc[i] = 0.f;
+#pragma unroll
+    for (int ki = 0; ki < 3; ++ki)
+#pragma unroll
+      for (int kj = 0; kj < 3; ++kj) {
+        // transposed conv: dd row y+1-ki, column x+1-kj  (ring pixel px + 2 - kj)
+        const float* src = ring_px(ring, t, y + 1 - ki, px + 2 - kj) + chunk * V;
+#pragma unroll
+        for (int i = 0; i < V; i += 4) {
+          const float4 a = *reinterpret_cast<const float4*>(src + i);
+          acc[i] = fmaf(w[ki * 3 + kj][i], a.x, acc[i]);
+          acc[i + 1] = fmaf(w[ki * 3 + kj][i + 1], a.y, acc[i + 1]);
+          acc[i + 2] = fmaf(w[ki * 3 + kj][i + 2], a.z, acc[i + 2]);
+          acc[i + 3] = fmaf(w[ki * 3 + kj][i + 3], a.w, acc[i + 3]);
+        }
+      }
+    float o2[V];
 #pragma unroll
     for (int i = 0; i < V; ++i) {
-#pragma unroll
-      for (int k = 0; k < 9; ++k) w[k][i] = wdw[(c + i) * 9 + k];
+      o2[i] = to_f(from_f<T>(acc[i] * act_grad(act, fmaf(ev[i], s[i], h[i]))));
+      q[0][i] += o2[i];
+      q[1][i] = fmaf(o2[i], (ev[i] - mu[i]) * is[i], q[1][i]);
     }
-    load_vec<float, V>(sc + c, s);
-    load_vec<float, V>(sh + c, h);
-    load_vec<float, V>(mean + c, mu);
-    load_vec<float, V>(invstd + c, is);
-    const int tw2 = t.TW + 2;
-    for (int o = slot; o < t.TR * t.TW; o += 64) {
-      const int ry = o / t.TW, cx = o - ry * t.TW;
-      const int y = ti.band * t.TR + ry, x = ti.colt * t.TW + cx;
-      if (y >= t.H || x >= t.W) continue;
-      float acc[V];
-#pragma unroll
-      for (int i = 0; i < V; ++i) acc[i] = 0.f;
-#pragma unroll
-      for (int ki = 0; ki < 3; ++ki)
-#pragma unroll
-        for (int kj = 0; kj < 3; ++kj) {
-          const float* src = tile + ((ry + 2 - ki) * tw2 + cx + 2 - kj) * t.PP + chunk * V;
-#pragma unroll
-          for (int i = 0; i < V; i += 4) {
-            const float4 a = *reinterpret_cast<const float4*>(src + i);
-            acc[i] = fmaf(w[ki * 3 + kj][i], a.x, acc[i]);
-            acc[i + 1] = fmaf(w[ki * 3 + kj][i + 1], a.y, acc[i + 1]);
-            acc[i + 2] = fmaf(w[ki * 3 + kj][i + 2], a.z, acc[i + 2]);
-            acc[i + 3] = fmaf(w[ki * 3 + kj][i + 3], a.w, acc[i + 3]);
-          }
-        }
-      const long off = ((ti.b * t.H + y) * t.W + x) * t.C + c;
-      float ev[V], o2[V];
-      load_vec<T, V>(e + off, ev);
-#pragma unroll
-      for (int i = 0; i < V; ++i) {
-        o2[i] = to_f(from_f<T>(acc[i] * act_grad(act, fmaf(ev[i], s[i], h[i]))));
-        q[0][i] += o2[i];
-        q[1][i] = fmaf(o2[i], (ev[i] - mu[i]) * is[i], q[1][i]);
-      }
-      store_vec<T, V>(out + off, o2);
-    }
-  }
-  chunk_reduce_store<2, V>(q, tile, stat + ti.rid * 2 * t.C, t.C, t.C, ti.ct * t.CT);
+    store_vec<T, V>(out + off, o2);
+  });
+  dw_reduce_store<2, V, float>(q, ring, t.chunks, stat + ti.rid * 2 * t.C, t.C, t.C, ti.ct * t.CT);
 }
 
 // dWdw partials: part[rid][tap][c] = sum over the block's pixels dd[p,c] * act(e*sc1+sh1)[p+tap, c]
-template <typename T, int V>
+template <typename T, int V, int LDQ>
 __global__ __launch_bounds__(256) void dw_wgrad_tile_kernel(const T* __restrict__ dd, const T* __restrict__ e,
                                                             const float* __restrict__ sc, const float* __restrict__ sh,
                                                             int act, float* __restrict__ part, DwTile t) {
-  extern __shared__ __attribute__((aligned(16))) float tile[];
-  long tid_ = 0;
-  if (!tile_valid(t, tid_)) return;
-  const TileIdx ti = tile_idx(t, tid_);
-  stage_tile<T, V, true>(tile, e, t, ti, sc, sh, act);
-  __syncthreads();
-  const int chunk = threadIdx.x & 3, slot = threadIdx.x >> 2;
+  extern __shared__ __attribute__((aligned(16))) float ring[];
+  TileIdx ti;
+  if (!tile_idx(t, ti)) return;
+  const int chunk = threadIdx.x % t.chunks;
   const int c = ti.ct * t.CT + chunk * V;
+  const bool cok = c < t.C;
+  float s[V], h[V];
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    s[i] = cok ? sc[c + i] : 0.f;
+    h[i] = cok ? sh[c + i] : 0.f;
+  }
   float q[9][V];
 #pragma unroll
   for (int k = 0; k < 9; ++k)
 #pragma unroll
     for (int i = 0; i < V; ++i) q[k][i] = 0.f;
-  if (c < t.C) {
-    const int tw2 = t.TW + 2;
-    for (int o = slot; o < t.TR * t.TW; o += 64) {
-      const int ry = o / t.TW, cx = o - ry * t.TW;
-      const int y = ti.band * t.TR + ry, x = ti.colt * t.TW + cx;
-      if (y >= t.H || x >= t.W) continue;
-      float g[V];
-      load_vec<T, V>(dd + ((ti.b * t.H + y) * t.W + x) * t.C + c, g);
+  dw_walk<T, V, LDQ, true>(ring, e, t, ti, c, chunk, cok, s, h, act, [&](int y, int px) {
+    float g[V];
+    load_vec<T, V>(dd + ((ti.b * t.H + y) * t.W + ti.x0 + px) * t.C + c, g);
 #pragma unroll
-      for (int ki = 0; ki < 3; ++ki)
+    for (int ki = 0; ki < 3; ++ki)
 #pragma unroll
-        for (int kj = 0; kj < 3; ++kj) {
-          const float* src = tile + ((ry + ki) * tw2 + cx + kj) * t.PP + chunk * V;
+      for (int kj = 0; kj < 3; ++kj) {
+        const float* src = ring_px(ring, t, y - 1 + ki, px + kj) + chunk * V;
 #pragma unroll
-          for (int i = 0; i < V; i += 4) {
-            const float4 a = *reinterpret_cast<const float4*>(src + i);
-            q[ki * 3 + kj][i] = fmaf(g[i], a.x, q[ki * 3 + kj][i]);
-            q[ki * 3 + kj][i + 1] = fmaf(g[i + 1], a.y, q[ki * 3 + kj][i + 1]);
-            q[ki * 3 + kj][i + 2] = fmaf(g[i + 2], a.z, q[ki * 3 + kj][i + 2]);
-            q[ki * 3 + kj][i + 3] = fmaf(g[i + 3], a.w, q[ki * 3 + kj][i + 3]);
-          }
+        for (int i = 0; i < V; i += 4) {
+          const float4 a = *reinterpret_cast<const float4*>(src + i);
+          q[ki * 3 + kj][i] = fmaf(g[i], a.x, q[ki * 3 + kj][i]);
+          q[ki * 3 + kj][i + 1] = fmaf(g[i + 1], a.y, q[ki * 3 + kj][i + 1]);
+          q[ki * 3 + kj][i + 2] = fmaf(g[i + 2], a.z, q[ki * 3 + kj][i + 2]);
+          q[ki * 3 + kj][i + 3] = fmaf(g[i + 3], a.w, q[ki * 3 + kj][i + 3]);
         }
-    }
-  }
-  chunk_reduce_store<9, V>(q, tile, part + ti.rid * 9 * t.C, t.C, t.C, ti.ct * t.CT);
+      }
+  });
+  dw_reduce_store<9, V, float>(q, ring, t.chunks, part + ti.rid * 9 * t.C, t.C, t.C, ti.ct * t.CT);
 }
 
 // dw[c*9 + tap] = s[tap*C + c]
@@ -727,22 +788,32 @@ struct Ops {
   template <int V>
   static void dw_fwd(const void* e, const float* w, const float* sc, const float* sh, int act, void* out, double* stat,
                      const float* shift, const DwTile& t, hipStream_t st) {
-    const unsigned nb = dw_grid(t);
-    dw_fwd_tile_kernel<T, V><<<nb, 256, t.lds_bytes(), st>>>((const T*)e, w, sc, sh, act, (T*)out, stat, shift, t);
+    const size_t lds = t.lds_bytes(2, V, sizeof(double));
+    if (t.ldq <= 2)
+      dw_fwd_tile_kernel<T, V, 2><<<dw_grid(t), 256, lds, st>>>((const T*)e, w, sc, sh, act, (T*)out, stat, shift, t);
+    else
+      dw_fwd_tile_kernel<T, V, 3><<<dw_grid(t), 256, lds, st>>>((const T*)e, w, sc, sh, act, (T*)out, stat, shift, t);
   }
   template <int V>
   static void dw_dgrad(const void* dd, const float* w, const void* e, const float* sc, const float* sh,
                        const float* mean, const float* inv, int act, void* out, float* stat, const DwTile& t,
                        hipStream_t st) {
-    const unsigned nb = dw_grid(t);
-    dw_dgrad_tile_kernel<T, V><<<nb, 256, t.lds_bytes(), st>>>((const T*)dd, w, (const T*)e, sc, sh, mean, inv, act,
-                                                              (T*)out, stat, t);
+    const size_t lds = t.lds_bytes(2, V, sizeof(float));
+    if (t.ldq <= 2)
+      dw_dgrad_tile_kernel<T, V, 2><<<dw_grid(t), 256, lds, st>>>((const T*)dd, w, (const T*)e, sc, sh, mean, inv, act,
+                                                                  (T*)out, stat, t);
+    else
+      dw_dgrad_tile_kernel<T, V, 3><<<dw_grid(t), 256, lds, st>>>((const T*)dd, w, (const T*)e, sc, sh, mean, inv, act,
+                                                                  (T*)out, stat, t);
   }
   template <int V>
   static void dw_wgrad(const void* dd, const void* e, const float* sc, const float* sh, int act, float* part,
                        const DwTile& t, hipStream_t st) {
-    const unsigned nb = dw_grid(t);
-    dw_wgrad_tile_kernel<T, V><<<nb, 256, t.lds_bytes(), st>>>((const T*)dd, (const T*)e, sc, sh, act, part, t);
+    const size_t lds = t.lds_bytes(9, V, sizeof(float));
+    if (t.ldq <= 2)
+      dw_wgrad_tile_kernel<T, V, 2><<<dw_grid(t), 256, lds, st>>>((const T*)dd, (const T*)e, sc, sh, act, part, t);
+    else
+      dw_wgrad_tile_kernel<T, V, 3><<<dw_grid(t), 256, lds, st>>>((const T*)dd, (const T*)e, sc, sh, act, part, t);
   }
   template <int V>
   static void pool(const void* d, const float* sc, const float* sh, int act, float* pooled, int B, int HW, int K,

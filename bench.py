@@ -50,7 +50,7 @@ def parse():
 
 
 PROBE_KERNEL = {  # probe name -> kernel symbol(s) it times (rocprofv3 names)
-    "gemm_fwd": "ogv::gemm_bf16_kernel<128,{128|64},*,false> (Linear / 1x1-conv forward launches)",
+    "gemm_fwd": "ogv::gemm_bf16_kernel<{128|64},{128|64},*,false,0,false> (Linear / 1x1-conv forward launches)",
     "outlook_fwd": "ogv::outlook_fwd_kernel",
     "grid_fwd": "ogv::grid_fwd_kernel",
 }

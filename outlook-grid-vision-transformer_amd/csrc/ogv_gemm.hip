@@ -971,10 +971,17 @@ __global__ __launch_bounds__(256) void transpose_f32_kernel(const float* __restr
 // ------------------------------------------------------------------------------------------------
 // internal launchers
 // ------------------------------------------------------------------------------------------------
-template <typename T, int BN, bool PRO, bool STATS>
+template <typename T, int BN, bool PRO, bool STATS, int BM = GEMM_BM>
 static void launch_mm(const void* A, int lda, const Pro& pro, const float* Wt, int ldw, void* out, int ldo, int M,
                       int N, int K, int Ka, int Kb, const Epi& epi, hipStream_t s) {
-  constexpr int BM = GEMM_BM;
+  if constexpr (!STATS && BM == GEMM_BM) {
+    // small M (the last stage, M = 8192): 64-row tiles double the blocks and the K-slabs in flight
+    // (measured: a loss already at M = 32768, where W-tile reloads dominate)
+    if (M <= 16384) {
+      launch_mm<T, BN, PRO, STATS, 64>(A, lda, pro, Wt, ldw, out, ldo, M, N, K, Ka, Kb, epi, s);
+      return;
+    }
+  }
   const int nMt = (M + BM - 1) / BM, nNt = (N + BN - 1) / BN;
   const unsigned grid = (unsigned)(((nMt + 7) / 8) * 8 * nNt);
   if constexpr (sizeof(T) == 2)
@@ -1139,10 +1146,15 @@ void transpose_f32_launch(const float* W, float* WT, int N, int K, int ldt, hipS
 
 size_t dgrad_ws_bytes(int N, int K) { return 256; }
 
-template <typename T, int BN>
+template <typename T, int BN, int BM = GEMM_BM>
 static void launch_mm_bt(const void* A, int lda, const float* W, int ldw, void* out, int ldo, int M, int N, int K,
                          const Epi& epi, hipStream_t s) {
-  constexpr int BM = GEMM_BM;
+  if constexpr (BM == GEMM_BM) {
+    if (M <= 16384) {
+      launch_mm_bt<T, BN, 64>(A, lda, W, ldw, out, ldo, M, N, K, epi, s);
+      return;
+    }
+  }
   const int nMt = (M + BM - 1) / BM, nNt = (N + BN - 1) / BN;
   const unsigned grid = (unsigned)(((nMt + 7) / 8) * 8 * nNt);
   const int Kp = (K + 31) / 32 * 32;

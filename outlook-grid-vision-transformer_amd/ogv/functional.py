@@ -37,6 +37,42 @@ def _dt(t: torch.Tensor) -> int:
     raise TypeError(f"ogv kernels support float32 and bfloat16 activations, got {t.dtype}")
 
 
+_SIDE = {}
+
+
+def _side_stream(device):
+    s = _SIDE.get(device.index)
+    if s is None:
+        s = _SIDE[device.index] = torch.cuda.Stream(device=device)
+    return s
+
+
+class _fork:
+    """Context manager yielding the stream handle for the forked work: a side stream that waits on
+    the current stream at entry and that the current stream waits on at exit (enabled), or the
+    current stream itself (disabled).  Tensors touched on the side stream are recorded on it so the
+    caching allocator does not hand their memory out early."""
+
+    def __init__(self, enabled, *tensors):
+        self.enabled = bool(enabled)
+        self.tensors = [t for t in tensors if t is not None]
+
+    def __enter__(self):
+        self.main = torch.cuda.current_stream()
+        if not self.enabled:
+            return _vp(self.main.cuda_stream)
+        self.side = _side_stream(self.main.device)
+        self.side.wait_stream(self.main)
+        for t in self.tensors:
+            t.record_stream(self.side)
+        return _vp(self.side.cuda_stream)
+
+    def __exit__(self, *a):
+        if self.enabled:
+            self.main.wait_stream(self.side)
+        return False
+
+
 def require_device(*tensors, what="ogv"):
     for t in tensors:
         if t is not None and not t.is_cuda:
@@ -189,19 +225,28 @@ class _Linear(torch.autograd.Function):
         x2d, w2d, rs = ctx.saved_tensors
         M, N, K, rps, act, has_bias, has_res = ctx.meta
         dout = dout.to(x2d.dtype).contiguous()
-        dt, st = _dt(x2d), _stream()
+        dt = _dt(x2d)
         dx = dw = db = dres = None
-        if ctx.needs_input_grad[0]:
+        want_dx = ctx.needs_input_grad[0]
+        want_dw = ctx.needs_input_grad[1] or (has_bias and ctx.needs_input_grad[2])
+        if want_dx:
             dx = torch.empty((M, K), dtype=x2d.dtype, device=x2d.device)
-            ws = _ws(lib.ogv_gemm_dgrad_ws_bytes(N, K), x2d.device)
-            check(lib.ogv_gemm_dgrad(_ptr(dout), N, _ptr(w2d), _ptr(x2d) if act else None, x2d.stride(0), _ptr(rs),
-                                     rps, _ptr(dx), K, M, N, K, act, _ptr(ws), dt, st), "ogv_gemm_dgrad")
-        if ctx.needs_input_grad[1] or (has_bias and ctx.needs_input_grad[2]):
+            ws_d = _ws(lib.ogv_gemm_dgrad_ws_bytes(N, K), x2d.device)
+        if want_dw:
             dw = torch.empty((N, K), dtype=torch.float32, device=x2d.device)
             db = torch.empty((N,), dtype=torch.float32, device=x2d.device) if has_bias else None
-            ws = _ws(lib.ogv_gemm_wgrad_ws_bytes(M, N, K), x2d.device)
-            check(lib.ogv_gemm_wgrad(_ptr(dout), N, _ptr(x2d), x2d.stride(0), _ptr(rs), rps, _ptr(dw), _ptr(db), M, N,
-                                     K, act, _ptr(ws), dt, st), "ogv_gemm_wgrad")
+            ws_w = _ws(lib.ogv_gemm_wgrad_ws_bytes(M, N, K), x2d.device)
+        # dgrad and wgrad are independent: the weight gradient runs on a side stream (forked from and
+        # joined back into the current one, also inside a captured graph) so the two latency-bound
+        # GEMMs overlap.
+        with _fork(want_dx and want_dw, dout, x2d, rs, dw, db, ws_w if want_dw else None) as side:
+            if want_dw:
+                check(lib.ogv_gemm_wgrad(_ptr(dout), N, _ptr(x2d), x2d.stride(0), _ptr(rs), rps, _ptr(dw), _ptr(db),
+                                         M, N, K, act, _ptr(ws_w), dt, side), "ogv_gemm_wgrad")
+            if want_dx:
+                check(lib.ogv_gemm_dgrad(_ptr(dout), N, _ptr(w2d), _ptr(x2d) if act else None, x2d.stride(0),
+                                         _ptr(rs), rps, _ptr(dx), K, M, N, K, act, _ptr(ws_d), dt, _stream()),
+                      "ogv_gemm_dgrad")
         if has_res and ctx.needs_input_grad[3]:
             dres = dout
         return dx, dw, db, dres, None, None, None

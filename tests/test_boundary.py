@@ -48,7 +48,8 @@ def test_host_validation_without_gpu():
     assert rc == 1
     rc = lib.ogv_gemm_fwd(x, 4, x, None, None, None, 0, x, 8, 16, 8, 8, 0, 0, None)  # lda < K
     assert rc == 1
-    assert lib.ogv_gemm_dgrad_ws_bytes(18, 48) == 24 * 48 * 4
+    # dgrad reads W as [reduction][output] directly (no transposed copy): a fixed small workspace
+    assert 0 < lib.ogv_gemm_dgrad_ws_bytes(18, 48) <= 4096
     assert lib.ogv_gemm_wgrad_ws_bytes(524288, 192, 48) > 0
     assert lib.ogv_layernorm_bwd_ws_bytes(1000, 48) > 0
 

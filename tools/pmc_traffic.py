@@ -19,7 +19,7 @@ import re
 PROBES = {
     # bench.py's "gemm_fwd" probe: every Linear / 1x1-conv forward GEMM launch (the only users of the
     # plain bf16 GEMM instantiation: no BN statistics, no conv gather, no transposed weights)
-    "gemm_fwd": r"gemm_bf16_kernel<128, (128|64), (true|false), false, 0, false>",
+    "gemm_fwd": r"gemm_bf16_kernel<(128|64), (128|64), (true|false), false, 0, false>",
     "outlook_fwd": r"outlook_fwd_kernel",
     "grid_fwd": r"grid_fwd_kernel",
 }

@@ -38,6 +38,10 @@ enum {
 
 const char* ogv_version(void);
 const char* ogv_last_error(void);
+/* Tuning switch (no reference counterpart; process-wide, set before capture):
+ *   "sgemm" 1 (default) / 0: persistent streaming kernel for tall-skinny bf16 projections on/off.
+ * Returns OGV_ERR_ARG for an unknown name. */
+int ogv_set_option(const char* name, int value);
 
 /* ---------------------------------------------------------------------------------------------
  * Outlook aggregation.  Replaces, for stride 1:

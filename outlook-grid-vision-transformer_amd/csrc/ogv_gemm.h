@@ -16,6 +16,46 @@ struct Pro {
   bool any() const { return act != OGV_ACT_NONE || sc || sh || gate; }
 };
 
+__device__ __forceinline__ float pro_apply(const Pro& p, float v, int m, int k) {
+  if (p.sc) v *= p.sc[k];
+  if (p.sh) v += p.sh[k];
+  v = act_fwd(p.act, v);
+  if (p.gate) v *= p.gate[(long)(m / p.rps) * p.gld + k];
+  return v;
+}
+
+// E consecutive columns k..k+E-1 of row m; per-column parameters fetched as vectors when the
+// run is full and 16-B aligned (k % 4 == 0, gld % 4 == 0), element-wise otherwise.
+template <int E>
+__device__ __forceinline__ void pro_apply_run(const Pro& p, float (&v)[E], int m, int k, int Ka) {
+  if (k + E <= Ka && (k & 3) == 0 && (p.gld & 3) == 0) {
+    if (p.sc) {
+      float t[E];
+      load_vec<float, E>(p.sc + k, t);
+#pragma unroll
+      for (int i = 0; i < E; ++i) v[i] *= t[i];
+    }
+    if (p.sh) {
+      float t[E];
+      load_vec<float, E>(p.sh + k, t);
+#pragma unroll
+      for (int i = 0; i < E; ++i) v[i] += t[i];
+    }
+#pragma unroll
+    for (int i = 0; i < E; ++i) v[i] = act_fwd(p.act, v[i]);
+    if (p.gate) {
+      float t[E];
+      load_vec<float, E>(p.gate + (long)(m / p.rps) * p.gld + k, t);
+#pragma unroll
+      for (int i = 0; i < E; ++i) v[i] *= t[i];
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < E; ++i)
+      if (k + i < Ka) v[i] = pro_apply(p, v[i], m, k + i);
+  }
+}
+
 // Epilogue: out = res + rs[m/rps] * (acc + bias[n]);  out *= act'(Z[m,n]) (zact);
 // optional per-column batch statistics of the stored (rounded) output, accumulated in fp64:
 //   stat[mt][0][n] = sum_rows (out - shift[n]),  stat[mt][1][n] = sum_rows (out - shift[n])^2
@@ -76,7 +116,9 @@ constexpr int GEMM_BM = 128;
 inline int gemm_stat_rows(int M) { return (M + GEMM_BM - 1) / GEMM_BM; }
 
 // out[M,N] = epi( pro(A)[M,K] . W[N,K]^T );  Ka / Kb = valid reduction columns of A / W.
-void gemm_fwd_launch(ogv_dtype dt, const void* A, int lda, const Pro& pro, const float* W, int ldw, void* out,
+// Returns the number of BatchNorm partial rows written to epi.stat (<= gemm_stat_rows(M)); the
+// caller reduces exactly that many.
+int gemm_fwd_launch(ogv_dtype dt, const void* A, int lda, const Pro& pro, const float* W, int ldw, void* out,
                      int ldo, int M, int N, int K, int Ka, int Kb, const Epi& epi, hipStream_t s);
 
 // dA[M,K] = act'(Z) * rs * (dOut[M,N] . W[N,K]);  ws >= dgrad_ws_bytes(N, K); res added if given
@@ -104,5 +146,13 @@ void transpose_f32_launch(const float* W, float* WT, int N, int K, int ldt, hipS
 // gradient (cv.transposed = 1, Wt = the tap-major transposed weights).
 void conv_gemm_launch(ogv_dtype dt, const void* A, const ConvG& cv, const float* Wt, void* out, int M, int N,
                       const Epi& epi, hipStream_t s);
+
+// Persistent streaming GEMM (ogv_sgemm.hip) for tall-skinny bf16 shapes; 0 / false = not handled.
+int sgemm_fwd_try(const void* A, int lda, const Pro& pro, const float* W, int ldw, void* out, int ldo, int M,
+                  int N, int K, const Epi& epi, hipStream_t s);
+bool sgemm_dgrad_try(const void* dout, int ldd, const float* W, void* dA, int lda, int M, int Nf, int Kf,
+                     const Epi& epi, hipStream_t s);
+int sgemm_mode();
+void set_sgemm_mode(int v);
 
 }  // namespace ogv

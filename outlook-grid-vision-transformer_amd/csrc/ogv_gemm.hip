@@ -19,46 +19,6 @@
 
 namespace ogv {
 
-__device__ __forceinline__ float pro_apply(const Pro& p, float v, int m, int k) {
-  if (p.sc) v *= p.sc[k];
-  if (p.sh) v += p.sh[k];
-  v = act_fwd(p.act, v);
-  if (p.gate) v *= p.gate[(long)(m / p.rps) * p.gld + k];
-  return v;
-}
-
-// E consecutive columns k..k+E-1 of row m; per-column parameters fetched as vectors when the
-// run is full and 16-B aligned (k % 4 == 0, gld % 4 == 0), element-wise otherwise.
-template <int E>
-__device__ __forceinline__ void pro_apply_run(const Pro& p, float (&v)[E], int m, int k, int Ka) {
-  if (k + E <= Ka && (k & 3) == 0 && (p.gld & 3) == 0) {
-    if (p.sc) {
-      float t[E];
-      load_vec<float, E>(p.sc + k, t);
-#pragma unroll
-      for (int i = 0; i < E; ++i) v[i] *= t[i];
-    }
-    if (p.sh) {
-      float t[E];
-      load_vec<float, E>(p.sh + k, t);
-#pragma unroll
-      for (int i = 0; i < E; ++i) v[i] += t[i];
-    }
-#pragma unroll
-    for (int i = 0; i < E; ++i) v[i] = act_fwd(p.act, v[i]);
-    if (p.gate) {
-      float t[E];
-      load_vec<float, E>(p.gate + (long)(m / p.rps) * p.gld + k, t);
-#pragma unroll
-      for (int i = 0; i < E; ++i) v[i] *= t[i];
-    }
-  } else {
-#pragma unroll
-    for (int i = 0; i < E; ++i)
-      if (k + i < Ka) v[i] = pro_apply(p, v[i], m, k + i);
-  }
-}
-
 // Column statistics of a wave's accumulator tile -> per-panel partials (deterministic).
 // Each thread holds rows 4*(lane>>4)+r (+16*i) of columns (lane&15) (+16*j); sums over its rows,
 // then across the 4 lane groups (xor 16, 32), then across the two M-waves through LDS.
@@ -1015,9 +975,13 @@ static bool tiny(int M, int N, ogv_dtype dt, const Epi& epi) {
   return dt == OGV_F32 && epi.stat == nullptr && M <= 2048 && (long)M * N <= (1L << 20);
 }
 
-void gemm_fwd_launch(ogv_dtype dt, const void* A, int lda, const Pro& pro, const float* W, int ldw, void* out, int ldo,
-                     int M, int N, int K, int Ka, int Kb, const Epi& epi, hipStream_t s) {
-  if (M <= 0) return;
+int gemm_fwd_launch(ogv_dtype dt, const void* A, int lda, const Pro& pro, const float* W, int ldw, void* out, int ldo,
+                    int M, int N, int K, int Ka, int Kb, const Epi& epi, hipStream_t s) {
+  if (M <= 0) return 0;
+  if (dt == OGV_BF16 && Ka == K && Kb == K) {
+    const int r = sgemm_fwd_try(A, lda, pro, W, ldw, out, ldo, M, N, K, epi, s);
+    if (r > 0) return r;
+  }
   if (tiny(M, N, dt, epi)) {
     const int K0 = Ka < Kb ? Ka : Kb;
     const long outs = (long)M * N;
@@ -1030,10 +994,11 @@ void gemm_fwd_launch(ogv_dtype dt, const void* A, int lda, const Pro& pro, const
     else
       small_fwd_kernel<4><<<cdiv(outs * 4, 256), 256, 0, s>>>((const float*)A, lda, pro, W, ldw, epi, (float*)out, ldo,
                                                                M, N, Ka, Kb);
-    return;
+    return 1;
   }
   if (dt == OGV_BF16) launch_mm_any<bf16>(A, lda, pro, W, ldw, out, ldo, M, N, K, Ka, Kb, epi, s);
   else launch_mm_any<float>(A, lda, pro, W, ldw, out, ldo, M, N, K, Ka, Kb, epi, s);
+  return gemm_stat_rows(M);
 }
 
 template <typename T, bool STATS>
@@ -1180,6 +1145,7 @@ void gemm_dgrad_launch(ogv_dtype dt, const void* dout, int ldd, const float* W, 
   e.zact = zact;
   e.res = res;
   // dA[M,K] = dout[M,N] . W[N,K]: W read as [reduction N][output K] (no transposed copy)
+  if (dt == OGV_BF16 && sgemm_dgrad_try(dout, ldd, W, dA, lda, M, N, K, e, s)) return;
   if (dt == OGV_BF16) {
     if (K > 64) launch_mm_bt<bf16, 128>(dout, ldd, W, K, dA, lda, M, K, N, e, s);
     else launch_mm_bt<bf16, 64>(dout, ldd, W, K, dA, lda, M, K, N, e, s);

@@ -866,8 +866,8 @@ static void mbconv_fwd_impl(const void* x, void* out, const Saved& sv, const Fwd
   {
     Epi e;
     if (tr) { e.stat = w.stat1; e.stat_shift = P.bn1_rm; }
-    gemm_fwd_launch(dt, x, s.C, Pro(), P.w_expand, s.C, sv.e, s.mid, (int)M, s.mid, s.C, s.C, s.C, e, st);
-    if (tr) colreduce(w.stat1, w.sums, gemm_stat_rows((int)M), 2L * s.mid, 2L * s.mid, w.tmp, st);
+    const int R = gemm_fwd_launch(dt, x, s.C, Pro(), P.w_expand, s.C, sv.e, s.mid, (int)M, s.mid, s.C, s.C, s.C, e, st);
+    if (tr) colreduce(w.stat1, w.sums, R, 2L * s.mid, 2L * s.mid, w.tmp, st);
     bn_finalize_kernel<<<cdiv(s.mid, 256), 256, 0, st>>>(w.sums, s.mid, (double)M, P.bn1_w, P.bn1_b, s.bn_eps,
                                                          s.bn_momentum, P.bn1_rm, P.bn1_rv, sv.mean1, sv.inv1, sv.sc1,
                                                          sv.sh1, s.train);
@@ -906,8 +906,8 @@ static void mbconv_fwd_impl(const void* x, void* out, const Saved& sv, const Fwd
     pr.gld = s.mid;
     Epi e;
     if (tr) { e.stat = w.stat3; e.stat_shift = P.bn3_rm; }
-    gemm_fwd_launch(dt, sv.d, s.mid, pr, P.w_proj, s.mid, sv.p, s.C, (int)M, s.C, s.mid, s.mid, s.mid, e, st);
-    if (tr) colreduce(w.stat3, w.sums, gemm_stat_rows((int)M), 2L * s.C, 2L * s.C, w.tmp, st);
+    const int R = gemm_fwd_launch(dt, sv.d, s.mid, pr, P.w_proj, s.mid, sv.p, s.C, (int)M, s.C, s.mid, s.mid, s.mid, e, st);
+    if (tr) colreduce(w.stat3, w.sums, R, 2L * s.C, 2L * s.C, w.tmp, st);
     bn_finalize_kernel<<<cdiv(s.C, 256), 256, 0, st>>>(w.sums, s.C, (double)M, P.bn3_w, P.bn3_b, s.bn_eps,
                                                        s.bn_momentum, P.bn3_rm, P.bn3_rv, sv.mean3, sv.inv3, sv.sc3,
                                                        sv.sh3, s.train);

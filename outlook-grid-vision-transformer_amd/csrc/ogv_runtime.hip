@@ -1,5 +1,6 @@
 // Library runtime: version, thread-local last error, launch checking, dtype casts.
 #include "ogv_common.h"
+#include "ogv_gemm.h"
 
 namespace ogv {
 
@@ -34,6 +35,16 @@ using namespace ogv;
 
 extern "C" const char* ogv_version(void) { return "ogv-hip 0.1.0 (gfx950)"; }
 extern "C" const char* ogv_last_error(void) { return g_err; }
+
+extern "C" int ogv_set_option(const char* name, int value) {
+  OGV_REQUIRE(name, "ogv_set_option: null name");
+  if (!strcmp(name, "sgemm")) {
+    set_sgemm_mode(value ? 1 : 0);
+    return OGV_OK;
+  }
+  set_error("ogv_set_option: unknown option '%s'", name);
+  return OGV_ERR_ARG;
+}
 
 extern "C" int ogv_cast(const void* src, ogv_dtype sdt, void* dst, ogv_dtype ddt, size_t n, void* stream) {
   OGV_REQUIRE(src && dst, "ogv_cast: null pointer");

@@ -1,0 +1,412 @@
+// Persistent streaming GEMM for the tall-skinny projections (gfx950).
+//
+// The 1x1 projections of the OutGridBlock are out[M,N] = A[M,K] . B[N,K]^T with M = B*H*W in the
+// hundreds of thousands and N*K <= 384*96 at the large-M stages: an HBM stream of A and out with a
+// weight tile small enough to live in LDS.  So, unlike a classic tiled GEMM:
+//   * each workgroup converts its weight tile to bf16 into LDS ONCE (one barrier in the kernel),
+//   * every wave then walks its own sequence of 16*RS-row panels with no block barriers: the A
+//     fragments are loaded straight from HBM into registers in MFMA layout (16 B per lane; lane l
+//     reads row l&15, k = 8*(l>>4) of a 32-wide k step), the NEXT panel's fragments are in flight
+//     while the current one is multiplied, and the B fragments come from the LDS tile,
+//   * the epilogue stages each 16 x 64 accumulator block through a wave-private LDS slab and
+//     re-reads it as 8-column runs: 16-B residual / Z loads and 16-B stores of out,
+//   * BatchNorm column statistics (fp64, shifted) accumulate in wave-private LDS across panels and
+//     leave the kernel as ONE partial row per workgroup (gridDim.x rows instead of M/128).
+// B[n][k] = W[n*ldw + k] (forward: W is [N][K]) or W[k*ldw + n] (BT, data gradient: the forward
+// weight [Nf][Kf] read as [reduction][output], transposed while it is staged).
+// A / out rows whose index is >= M are neither read nor written; k >= K is zero in both operands.
+#include "ogv_gemm.h"
+
+namespace ogv {
+
+constexpr int SG_CW = 64;  // output columns per accumulator chunk (4 MFMA n-subtiles)
+constexpr int SG_NW = 8;   // waves per workgroup (they share one weight tile)
+
+template <int KT>
+__host__ __device__ constexpr int sg_kp() { return KT * 32 + 8; }  // W tile pitch: 16(4KT+1) B, conflict-free
+
+// PA: -1 = no A prologue, else the prologue's activation (OGV_ACT_*; sc / sh / gate applied when
+// non-null).  ZA: activation whose derivative at Z scales the output (0 = none).  All operand
+// rows are 16-B aligned runs (checked by the host): N, K, lda, ldo, ldz multiples of 8.
+//
+// The product is computed transposed, D[n][m] = W-tile . A^T (v_mfma_f32_16x16x32_bf16 with the
+// weight fragment as the A operand), so each lane's accumulator holds 4 CONSECUTIVE output
+// columns of one row: bias / residual / Z are read and out is written as 8-byte runs straight
+// from registers (the four lanes of a row group cover 32 contiguous bytes per instruction, the
+// four n-subtiles of a chunk the whole 128-byte line), with no LDS staging and no wave barrier.
+template <int KT, int RS, int PA, int ZA, bool STATS, bool BT>
+__global__ __launch_bounds__(SG_NW * 64) void sgemm_bf16_kernel(const bf16* __restrict__ A, int lda, Pro pro,
+                                                                const float* __restrict__ W, int ldw, Epi epi,
+                                                                bf16* __restrict__ out, int ldo, int M, int N, int K,
+                                                                int NB) {
+  constexpr int KP = sg_kp<KT>();
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n0 = blockIdx.y * NB;
+  const int nb = min(NB, N - n0);  // multiple of 8
+  const int nbp = (nb + SG_CW - 1) / SG_CW * SG_CW;
+  bf16* Ws = reinterpret_cast<bf16*>(smem);
+  double* sacc = reinterpret_cast<double*>(smem + (size_t)nbp * KP * 2);
+  float* cvec = reinterpret_cast<float*>(sacc + (STATS ? SG_NW * 2 * nbp : 0));  // [bias | stat shift]
+
+  // ---- weight tile -> LDS (bf16), zero outside [0,nb) x [0,K)
+  if constexpr (!BT) {
+    constexpr int QPR = KT * 32 / 4;  // float4 quads per tile row
+    const bool wv = ((ldw & 3) == 0) && ((reinterpret_cast<uintptr_t>(W) & 15) == 0);
+    for (int idx = tid; idx < nbp * QPR; idx += SG_NW * 64) {
+      const int r = idx / QPR, k = (idx - r * QPR) * 4;
+      float4 v = float4{0.f, 0.f, 0.f, 0.f};
+      if (r < nb) {
+        const float* src = W + (long)(n0 + r) * ldw + k;
+        if (wv && k + 4 <= K) v = *reinterpret_cast<const float4*>(src);
+        else {
+          v.x = k < K ? src[0] : 0.f;
+          v.y = k + 1 < K ? src[1] : 0.f;
+          v.z = k + 2 < K ? src[2] : 0.f;
+          v.w = k + 3 < K ? src[3] : 0.f;
+        }
+      }
+      bf16x4 b = {(bf16)v.x, (bf16)v.y, (bf16)v.z, (bf16)v.w};
+      *reinterpret_cast<bf16x4*>(Ws + r * KP + k) = b;
+    }
+  } else {  // W is [reduction][output]: 4 consecutive output columns per 16-B load
+    const bool wv = ((ldw & 3) == 0) && ((reinterpret_cast<uintptr_t>(W) & 15) == 0) && ((n0 & 3) == 0);
+    const int q4 = nbp / 4;
+    for (int idx = tid; idx < q4 * KT * 32; idx += SG_NW * 64) {
+      const int k = idx / q4, r = (idx - k * q4) * 4;
+      float4 v = float4{0.f, 0.f, 0.f, 0.f};
+      if (k < K && r < nb) {
+        const float* src = W + (long)k * ldw + n0 + r;
+        if (wv && r + 4 <= nb) v = *reinterpret_cast<const float4*>(src);
+        else {
+          v.x = src[0];
+          v.y = r + 1 < nb ? src[1] : 0.f;
+          v.z = r + 2 < nb ? src[2] : 0.f;
+          v.w = r + 3 < nb ? src[3] : 0.f;
+        }
+      }
+      Ws[(r + 0) * KP + k] = (bf16)v.x;
+      Ws[(r + 1) * KP + k] = (bf16)v.y;
+      Ws[(r + 2) * KP + k] = (bf16)v.z;
+      Ws[(r + 3) * KP + k] = (bf16)v.w;
+    }
+  }
+  if constexpr (STATS) {
+    for (int i = lane; i < 2 * nbp; i += 64) sacc[wave * 2 * nbp + i] = 0.0;
+  }
+  for (int c = tid; c < nbp; c += SG_NW * 64) {
+    cvec[c] = (epi.bias && c < nb) ? epi.bias[n0 + c] : 0.f;
+    if (STATS) cvec[nbp + c] = (epi.stat_shift && c < nb) ? epi.stat_shift[n0 + c] : 0.f;
+  }
+  __syncthreads();
+
+  const int fr = lane & 15, fg = lane >> 4;
+  const long P = ((long)M + 16 * RS - 1) / (16 * RS);
+  const long GW = (long)gridDim.x * SG_NW;
+  const bf16* res = static_cast<const bf16*>(epi.res);
+  const bf16* Z = static_cast<const bf16*>(epi.Z);
+
+  for (long p = (long)blockIdx.x * SG_NW + wave; p < P; p += GW) {
+    const long mp = p * 16 * RS;
+    bf16x8 a[RS][KT];
+    long m[RS];
+    float rsc[RS];
+#pragma unroll
+    for (int i = 0; i < RS; ++i) {
+      m[i] = mp + i * 16 + fr;
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt) {
+        const int k = kt * 32 + fg * 8;
+        bf16x8 v = {};
+        if (m[i] < M && k < K) v = *reinterpret_cast<const bf16x8*>(A + m[i] * lda + k);
+        a[i][kt] = v;
+      }
+      rsc[i] = (epi.rs && m[i] < M) ? epi.rs[m[i] / epi.rps] : 1.f;
+    }
+    if constexpr (PA >= 0) {
+#pragma unroll
+      for (int i = 0; i < RS; ++i) {
+#pragma unroll
+        for (int kt = 0; kt < KT; ++kt) {
+          const int k = kt * 32 + fg * 8;
+          if (m[i] < M && k < K) {
+            float f[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) f[q] = (float)a[i][kt][q];
+            if (pro.sc) {
+              float t[8];
+              load_vec<float, 8>(pro.sc + k, t);
+#pragma unroll
+              for (int q = 0; q < 8; ++q) f[q] *= t[q];
+            }
+            if (pro.sh) {
+              float t[8];
+              load_vec<float, 8>(pro.sh + k, t);
+#pragma unroll
+              for (int q = 0; q < 8; ++q) f[q] += t[q];
+            }
+#pragma unroll
+            for (int q = 0; q < 8; ++q) f[q] = act_fwd(PA, f[q]);
+            if (pro.gate) {
+              float t[8];
+              load_vec<float, 8>(pro.gate + (m[i] / pro.rps) * pro.gld + k, t);
+#pragma unroll
+              for (int q = 0; q < 8; ++q) f[q] *= t[q];
+            }
+#pragma unroll
+            for (int q = 0; q < 8; ++q) a[i][kt][q] = (bf16)f[q];
+          }
+        }
+      }
+    }
+    for (int c0 = 0; c0 < nb; c0 += SG_CW) {
+      // residual / Z runs of this chunk first (their latency overlaps the MFMAs)
+      uint2 rv[RS][4], zv[RS][4];
+#pragma unroll
+      for (int i = 0; i < RS; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int cc = c0 + j * 16 + 4 * fg;
+          const bool ok = m[i] < M && cc < nb;
+          rv[i][j] = uint2{0u, 0u};
+          zv[i][j] = uint2{0u, 0u};
+          if (ok && res) rv[i][j] = *reinterpret_cast<const uint2*>(res + m[i] * ldo + n0 + cc);
+          if constexpr (ZA != 0) {
+            if (ok) zv[i][j] = *reinterpret_cast<const uint2*>(Z + m[i] * epi.ldz + n0 + cc);
+          }
+        }
+      f32x4 acc[RS][4];
+#pragma unroll
+      for (int i = 0; i < RS; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const bf16x8 w = *reinterpret_cast<const bf16x8*>(Ws + (c0 + j * 16 + fr) * KP + kt * 32 + fg * 8);
+#pragma unroll
+          for (int i = 0; i < RS; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, a[i][kt], acc[i][j], 0, 0, 0);
+        }
+      }
+      // ---- epilogue: lane holds out[m = mp + i*16 + fr][n0 + c0 + j*16 + 4*fg + r], r = 0..3
+      float s1[4][4], s2[4][4];
+      if constexpr (STATS) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) { s1[j][r] = 0.f; s2[j][r] = 0.f; }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int cc = c0 + j * 16 + 4 * fg;
+        const float4 bs = *reinterpret_cast<const float4*>(cvec + cc);
+        const float bias[4] = {bs.x, bs.y, bs.z, bs.w};
+        float shift[4] = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (STATS) {
+          const float4 h = *reinterpret_cast<const float4*>(cvec + nbp + cc);
+          shift[0] = h.x; shift[1] = h.y; shift[2] = h.z; shift[3] = h.w;
+        }
+#pragma unroll
+        for (int i = 0; i < RS; ++i) {
+          if (!(m[i] < M && cc < nb)) continue;
+          const bf16* rb = reinterpret_cast<const bf16*>(&rv[i][j]);
+          const bf16* zb = reinterpret_cast<const bf16*>(&zv[i][j]);
+          uint2 ov;
+          bf16* ob = reinterpret_cast<bf16*>(&ov);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float x = (acc[i][j][r] + bias[r]) * rsc[i] + (float)rb[r];  // rb = 0 without a residual
+            if constexpr (ZA != 0) x *= act_grad(ZA, (float)zb[r]);
+            ob[r] = (bf16)x;
+            if constexpr (STATS) {
+              const float d = (float)ob[r] - shift[r];
+              s1[j][r] += d;
+              s2[j][r] = fmaf(d, d, s2[j][r]);
+            }
+          }
+          *reinterpret_cast<uint2*>(out + m[i] * ldo + n0 + cc) = ov;
+        }
+      }
+      if constexpr (STATS) {
+        // rows are spread over the 16 lanes fr of a group: reduce (xor 1..8), fp32 over <= 32 rows,
+        // then fp64 across panels in the wave's LDS accumulator
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) {
+              s1[j][r] += __shfl_xor(s1[j][r], o, 64);
+              s2[j][r] += __shfl_xor(s2[j][r], o, 64);
+            }
+        if (fr == 0) {
+          double* sa = sacc + wave * 2 * nbp;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int cc = c0 + j * 16 + 4 * fg;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              sa[cc + r] += (double)s1[j][r];
+              sa[nbp + cc + r] += (double)s2[j][r];
+            }
+          }
+        }
+      }
+    }
+  }
+
+  if constexpr (STATS) {  // one partial row per workgroup: stat[blockIdx.x][q][n]
+    __syncthreads();
+    for (int c = tid; c < nb; c += SG_NW * 64) {
+      double t1 = 0.0, t2 = 0.0;
+#pragma unroll
+      for (int w = 0; w < SG_NW; ++w) {
+        t1 += sacc[w * 2 * nbp + c];
+        t2 += sacc[w * 2 * nbp + nbp + c];
+      }
+      epi.stat[((long)blockIdx.x * 2 + 0) * N + n0 + c] = t1;
+      epi.stat[((long)blockIdx.x * 2 + 1) * N + n0 + c] = t2;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// plan + dispatch
+// ------------------------------------------------------------------------------------------------
+static int g_sgemm_mode = -1;  // -1: unset (read OGV_SGEMM once), 0 off, 1 on
+int sgemm_mode() {
+  if (g_sgemm_mode < 0) {
+    const char* e = getenv("OGV_SGEMM");
+    g_sgemm_mode = e ? atoi(e) : 1;
+  }
+  return g_sgemm_mode;
+}
+void set_sgemm_mode(int v) { g_sgemm_mode = v; }
+
+static int device_cus() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  return cus;
+}
+
+struct SgPlan {
+  int ok = 0, KT = 0, RS = 1, NB = 0, ntiles = 1, grid = 0;
+  size_t lds = 0;
+};
+
+static constexpr size_t SG_LDS_CAP = 80 * 1024;  // per workgroup: 2 eight-wave workgroups per CU (the VGPR limit)
+
+static bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+static SgPlan sgemm_plan(int M, int N, int K, bool stats) {
+  SgPlan p;
+  if (M < 32768 || (K & 7) != 0 || (N & 7) != 0) return p;  // small M: the tiled kernel fills the chip better
+  int KT;
+  if (K <= 64) KT = 2;
+  else if (K <= 96) KT = 3;
+  else if (K <= 128) KT = 4;
+  else if (K <= 192) KT = 6;
+  else return p;
+  const int KP = KT * 32 + 8;
+  p.KT = KT;
+  p.RS = KT <= 2 ? 2 : 1;
+  auto lds_of = [&](int nb) {  // nb padded to the chunk
+    return (size_t)nb * KP * 2 + (stats ? (size_t)SG_NW * 2 * nb * 8 : 0) + (size_t)nb * 8;
+  };
+  // widest tile (multiple of the 64-column chunk) whose bf16 copy fits next to the staging slabs
+  int NB = (N + SG_CW - 1) / SG_CW * SG_CW;
+  while (NB > SG_CW && lds_of(NB) > SG_LDS_CAP) NB -= SG_CW;
+  if (lds_of(NB) > SG_LDS_CAP) return p;
+  p.ntiles = (N + NB - 1) / NB;
+  NB = (N + p.ntiles - 1) / p.ntiles;  // balance the tiles
+  NB = (NB + 15) / 16 * 16;
+  p.ntiles = (N + NB - 1) / NB;
+  p.NB = NB;
+  p.lds = lds_of((NB + SG_CW - 1) / SG_CW * SG_CW);
+  const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(2, (160 * 1024) / p.lds));
+  const long panels = ((long)M + 16 * p.RS - 1) / (16 * p.RS);
+  const long want = (panels + SG_NW - 1) / SG_NW;
+  p.grid = (int)std::min<long>(want, (long)device_cus() * per_cu);
+  p.grid = (p.grid + 7) / 8 * 8;  // the N-tiles of one row range share an XCD: x % 8 fixes the XCD
+  if (stats) p.grid = std::min(p.grid, std::max(8, ((M + GEMM_BM - 1) / GEMM_BM) / 8 * 8));  // <= gemm_stat_rows
+  p.ok = 1;
+  return p;
+}
+
+template <int KT, int RS, int PA, int ZA, bool STATS, bool BT>
+static void sg_launch(const SgPlan& p, const bf16* A, int lda, const Pro& pro, const float* W, int ldw,
+                      const Epi& epi, bf16* out, int ldo, int M, int N, int K, hipStream_t s) {
+  auto kern = sgemm_bf16_kernel<KT, RS, PA, ZA, STATS, BT>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)SG_LDS_CAP);
+    attr = true;
+  }
+  dim3 grid((unsigned)p.grid, (unsigned)p.ntiles);
+  kern<<<grid, SG_NW * 64, p.lds, s>>>(A, lda, pro, W, ldw, epi, out, ldo, M, N, K, p.NB);
+}
+
+template <int PA, int ZA, bool STATS, bool BT>
+static void sg_dispatch(const SgPlan& p, const bf16* A, int lda, const Pro& pro, const float* W, int ldw,
+                        const Epi& epi, bf16* out, int ldo, int M, int N, int K, hipStream_t s) {
+  switch (p.KT) {
+    case 2: sg_launch<2, 2, PA, ZA, STATS, BT>(p, A, lda, pro, W, ldw, epi, out, ldo, M, N, K, s); break;
+    case 3: sg_launch<3, 1, PA, ZA, STATS, BT>(p, A, lda, pro, W, ldw, epi, out, ldo, M, N, K, s); break;
+    case 4: sg_launch<4, 1, PA, ZA, STATS, BT>(p, A, lda, pro, W, ldw, epi, out, ldo, M, N, K, s); break;
+    default: sg_launch<6, 1, PA, ZA, STATS, BT>(p, A, lda, pro, W, ldw, epi, out, ldo, M, N, K, s); break;
+  }
+}
+
+static bool epi_ok(const void* out, int ldo, const Epi& e) {
+  return al16(out) && (ldo & 7) == 0 && (!e.res || al16(e.res)) &&
+         (!e.zact || (e.Z && al16(e.Z) && (e.ldz & 7) == 0));
+}
+
+// Returns the number of BatchNorm partial rows written (>= 1) when it handled the call, 0 if the
+// shape / operand combination is not one it covers (the caller falls back to the tiled kernel).
+int sgemm_fwd_try(const void* A, int lda, const Pro& pro, const float* W, int ldw, void* out, int ldo, int M,
+                  int N, int K, const Epi& epi, hipStream_t s) {
+  if (!sgemm_mode() || epi.zact || !al16(A) || (lda & 7) || !epi_ok(out, ldo, epi)) return 0;
+  if (pro.any() && pro.act != OGV_ACT_NONE && pro.act != OGV_ACT_GELU && pro.act != OGV_ACT_SILU) return 0;
+  if (pro.gate && (pro.gld & 3)) return 0;
+  const bool st = epi.stat != nullptr;
+  const SgPlan p = sgemm_plan(M, N, K, st);
+  if (!p.ok) return 0;
+  const bf16* a = static_cast<const bf16*>(A);
+  bf16* o = static_cast<bf16*>(out);
+#define OGV_SG_FWD(PA_)                                                                  \
+  do {                                                                                   \
+    if (st) sg_dispatch<PA_, 0, true, false>(p, a, lda, pro, W, ldw, epi, o, ldo, M, N, K, s);  \
+    else sg_dispatch<PA_, 0, false, false>(p, a, lda, pro, W, ldw, epi, o, ldo, M, N, K, s);    \
+  } while (0)
+  if (!pro.any()) OGV_SG_FWD(-1);
+  else if (pro.act == OGV_ACT_GELU) OGV_SG_FWD(OGV_ACT_GELU);
+  else if (pro.act == OGV_ACT_SILU) OGV_SG_FWD(OGV_ACT_SILU);
+  else OGV_SG_FWD(OGV_ACT_NONE);
+#undef OGV_SG_FWD
+  return st ? p.grid : 1;
+}
+
+// dA[M, Kf] = epi(dOut[M, Nf] . W[Nf, Kf]):  reduction Nf, output columns Kf.
+bool sgemm_dgrad_try(const void* dout, int ldd, const float* W, void* dA, int lda, int M, int Nf, int Kf,
+                     const Epi& epi, hipStream_t s) {
+  if (!sgemm_mode() || epi.stat || !al16(dout) || (ldd & 7) || !epi_ok(dA, lda, epi)) return false;
+  if (epi.zact != OGV_ACT_NONE && epi.zact != OGV_ACT_GELU && epi.zact != OGV_ACT_SILU) return false;
+  const SgPlan p = sgemm_plan(M, Kf, Nf, false);
+  if (!p.ok) return false;
+  const bf16* a = static_cast<const bf16*>(dout);
+  bf16* o = static_cast<bf16*>(dA);
+  if (epi.zact == OGV_ACT_GELU) sg_dispatch<-1, OGV_ACT_GELU, false, true>(p, a, ldd, Pro(), W, Kf, epi, o, lda, M, Kf, Nf, s);
+  else if (epi.zact == OGV_ACT_SILU) sg_dispatch<-1, OGV_ACT_SILU, false, true>(p, a, ldd, Pro(), W, Kf, epi, o, lda, M, Kf, Nf, s);
+  else sg_dispatch<-1, 0, false, true>(p, a, ldd, Pro(), W, Kf, epi, o, lda, M, Kf, Nf, s);
+  return true;
+}
+
+}  // namespace ogv

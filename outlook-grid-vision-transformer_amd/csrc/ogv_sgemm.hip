@@ -21,6 +21,7 @@ namespace ogv {
 
 constexpr int SG_CW = 64;  // output columns per accumulator chunk (4 MFMA n-subtiles)
 constexpr int SG_NW = 8;   // waves per workgroup (they share one weight tile)
+constexpr int SG_WB = 8;   // weight-staging loads in flight per thread
 
 template <int KT>
 __host__ __device__ constexpr int sg_kp() { return KT * 32 + 8; }  // W tile pitch: 16(4KT+1) B, conflict-free
@@ -49,46 +50,75 @@ __global__ __launch_bounds__(SG_NW * 64) void sgemm_bf16_kernel(const bf16* __re
   double* sacc = reinterpret_cast<double*>(smem + (size_t)nbp * KP * 2);
   float* cvec = reinterpret_cast<float*>(sacc + (STATS ? SG_NW * 2 * nbp : 0));  // [bias | stat shift]
 
-  // ---- weight tile -> LDS (bf16), zero outside [0,nb) x [0,K)
+  // ---- weight tile -> LDS (bf16), zero outside [0,nb) x [0,K).  Batches of SG_WB independent
+  // 16-B loads per thread are issued before any is consumed, so staging costs a few L2 round trips
+  // rather than one per loop trip.
+  constexpr int NT = SG_NW * 64;
   if constexpr (!BT) {
     constexpr int QPR = KT * 32 / 4;  // float4 quads per tile row
     const bool wv = ((ldw & 3) == 0) && ((reinterpret_cast<uintptr_t>(W) & 15) == 0);
-    for (int idx = tid; idx < nbp * QPR; idx += SG_NW * 64) {
-      const int r = idx / QPR, k = (idx - r * QPR) * 4;
-      float4 v = float4{0.f, 0.f, 0.f, 0.f};
-      if (r < nb) {
-        const float* src = W + (long)(n0 + r) * ldw + k;
-        if (wv && k + 4 <= K) v = *reinterpret_cast<const float4*>(src);
-        else {
-          v.x = k < K ? src[0] : 0.f;
-          v.y = k + 1 < K ? src[1] : 0.f;
-          v.z = k + 2 < K ? src[2] : 0.f;
-          v.w = k + 3 < K ? src[3] : 0.f;
+    const int total = nbp * QPR;
+    for (int base = tid; base < total; base += SG_WB * NT) {
+      float4 v[SG_WB];
+#pragma unroll
+      for (int b = 0; b < SG_WB; ++b) {
+        const int idx = base + b * NT;
+        const int r = idx / QPR, k = (idx - r * QPR) * 4;
+        v[b] = float4{0.f, 0.f, 0.f, 0.f};
+        if (idx < total && r < nb) {
+          const float* src = W + (long)(n0 + r) * ldw + k;
+          if (wv && k + 4 <= K) v[b] = *reinterpret_cast<const float4*>(src);
+          else if (k < K) {
+            v[b].x = src[0];
+            v[b].y = k + 1 < K ? src[1] : 0.f;
+            v[b].z = k + 2 < K ? src[2] : 0.f;
+            v[b].w = k + 3 < K ? src[3] : 0.f;
+          }
         }
       }
-      bf16x4 b = {(bf16)v.x, (bf16)v.y, (bf16)v.z, (bf16)v.w};
-      *reinterpret_cast<bf16x4*>(Ws + r * KP + k) = b;
+#pragma unroll
+      for (int b = 0; b < SG_WB; ++b) {
+        const int idx = base + b * NT;
+        if (idx < total) {
+          const int r = idx / QPR, k = (idx - r * QPR) * 4;
+          bf16x4 w4 = {(bf16)v[b].x, (bf16)v[b].y, (bf16)v[b].z, (bf16)v[b].w};
+          *reinterpret_cast<bf16x4*>(Ws + r * KP + k) = w4;
+        }
+      }
     }
   } else {  // W is [reduction][output]: 4 consecutive output columns per 16-B load
     const bool wv = ((ldw & 3) == 0) && ((reinterpret_cast<uintptr_t>(W) & 15) == 0) && ((n0 & 3) == 0);
     const int q4 = nbp / 4;
-    for (int idx = tid; idx < q4 * KT * 32; idx += SG_NW * 64) {
-      const int k = idx / q4, r = (idx - k * q4) * 4;
-      float4 v = float4{0.f, 0.f, 0.f, 0.f};
-      if (k < K && r < nb) {
-        const float* src = W + (long)k * ldw + n0 + r;
-        if (wv && r + 4 <= nb) v = *reinterpret_cast<const float4*>(src);
-        else {
-          v.x = src[0];
-          v.y = r + 1 < nb ? src[1] : 0.f;
-          v.z = r + 2 < nb ? src[2] : 0.f;
-          v.w = r + 3 < nb ? src[3] : 0.f;
+    const int total = q4 * KT * 32;
+    for (int base = tid; base < total; base += SG_WB * NT) {
+      float4 v[SG_WB];
+#pragma unroll
+      for (int b = 0; b < SG_WB; ++b) {
+        const int idx = base + b * NT;
+        const int k = idx / q4, r = (idx - k * q4) * 4;
+        v[b] = float4{0.f, 0.f, 0.f, 0.f};
+        if (idx < total && k < K && r < nb) {
+          const float* src = W + (long)k * ldw + n0 + r;
+          if (wv && r + 4 <= nb) v[b] = *reinterpret_cast<const float4*>(src);
+          else {
+            v[b].x = src[0];
+            v[b].y = r + 1 < nb ? src[1] : 0.f;
+            v[b].z = r + 2 < nb ? src[2] : 0.f;
+            v[b].w = r + 3 < nb ? src[3] : 0.f;
+          }
         }
       }
-      Ws[(r + 0) * KP + k] = (bf16)v.x;
-      Ws[(r + 1) * KP + k] = (bf16)v.y;
-      Ws[(r + 2) * KP + k] = (bf16)v.z;
-      Ws[(r + 3) * KP + k] = (bf16)v.w;
+#pragma unroll
+      for (int b = 0; b < SG_WB; ++b) {
+        const int idx = base + b * NT;
+        if (idx < total) {
+          const int k = idx / q4, r = (idx - k * q4) * 4;
+          Ws[(r + 0) * KP + k] = (bf16)v[b].x;
+          Ws[(r + 1) * KP + k] = (bf16)v[b].y;
+          Ws[(r + 2) * KP + k] = (bf16)v[b].z;
+          Ws[(r + 3) * KP + k] = (bf16)v[b].w;
+        }
+      }
     }
   }
   if constexpr (STATS) {
@@ -304,7 +334,10 @@ static constexpr size_t SG_LDS_CAP = 80 * 1024;  // per workgroup: 2 eight-wave 
 
 static bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
-static SgPlan sgemm_plan(int M, int N, int K, bool stats) {
+// Routing (measured, tools/bench_sgemm.py, cold caches, MI355X): the streaming kernel wins for
+// reductions up to 192 everywhere; at 256-384 only when the A prologue (GELU) makes the tiled
+// kernel VALU-bound; a data-gradient whose output needs two weight tiles loses to the tiled kernel.
+static SgPlan sgemm_plan(int M, int N, int K, bool stats, bool prologue, bool dgrad) {
   SgPlan p;
   if (M < 32768 || (K & 7) != 0 || (N & 7) != 0) return p;  // small M: the tiled kernel fills the chip better
   int KT;
@@ -312,7 +345,10 @@ static SgPlan sgemm_plan(int M, int N, int K, bool stats) {
   else if (K <= 96) KT = 3;
   else if (K <= 128) KT = 4;
   else if (K <= 192) KT = 6;
+  else if (K <= 256) KT = 8;
+  else if (K <= 384) KT = 12;
   else return p;
+  if (KT > 6 && !prologue) return p;
   const int KP = KT * 32 + 8;
   p.KT = KT;
   p.RS = KT <= 2 ? 2 : 1;
@@ -324,6 +360,7 @@ static SgPlan sgemm_plan(int M, int N, int K, bool stats) {
   while (NB > SG_CW && lds_of(NB) > SG_LDS_CAP) NB -= SG_CW;
   if (lds_of(NB) > SG_LDS_CAP) return p;
   p.ntiles = (N + NB - 1) / NB;
+  if (dgrad && p.ntiles > 1) return p;
   NB = (N + p.ntiles - 1) / p.ntiles;  // balance the tiles
   NB = (NB + 15) / 16 * 16;
   p.ntiles = (N + NB - 1) / NB;
@@ -360,7 +397,9 @@ static void sg_dispatch(const SgPlan& p, const bf16* A, int lda, const Pro& pro,
     case 2: sg_launch<2, 2, PA, ZA, STATS, BT>(p, A, lda, pro, W, ldw, epi, out, ldo, M, N, K, s); break;
     case 3: sg_launch<3, 1, PA, ZA, STATS, BT>(p, A, lda, pro, W, ldw, epi, out, ldo, M, N, K, s); break;
     case 4: sg_launch<4, 1, PA, ZA, STATS, BT>(p, A, lda, pro, W, ldw, epi, out, ldo, M, N, K, s); break;
-    default: sg_launch<6, 1, PA, ZA, STATS, BT>(p, A, lda, pro, W, ldw, epi, out, ldo, M, N, K, s); break;
+    case 6: sg_launch<6, 1, PA, ZA, STATS, BT>(p, A, lda, pro, W, ldw, epi, out, ldo, M, N, K, s); break;
+    case 8: sg_launch<8, 1, PA, ZA, STATS, BT>(p, A, lda, pro, W, ldw, epi, out, ldo, M, N, K, s); break;
+    default: sg_launch<12, 1, PA, ZA, STATS, BT>(p, A, lda, pro, W, ldw, epi, out, ldo, M, N, K, s); break;
   }
 }
 
@@ -377,7 +416,7 @@ int sgemm_fwd_try(const void* A, int lda, const Pro& pro, const float* W, int ld
   if (pro.any() && pro.act != OGV_ACT_NONE && pro.act != OGV_ACT_GELU && pro.act != OGV_ACT_SILU) return 0;
   if (pro.gate && (pro.gld & 3)) return 0;
   const bool st = epi.stat != nullptr;
-  const SgPlan p = sgemm_plan(M, N, K, st);
+  const SgPlan p = sgemm_plan(M, N, K, st, pro.any(), false);
   if (!p.ok) return 0;
   const bf16* a = static_cast<const bf16*>(A);
   bf16* o = static_cast<bf16*>(out);
@@ -399,7 +438,7 @@ bool sgemm_dgrad_try(const void* dout, int ldd, const float* W, void* dA, int ld
                      const Epi& epi, hipStream_t s) {
   if (!sgemm_mode() || epi.stat || !al16(dout) || (ldd & 7) || !epi_ok(dA, lda, epi)) return false;
   if (epi.zact != OGV_ACT_NONE && epi.zact != OGV_ACT_GELU && epi.zact != OGV_ACT_SILU) return false;
-  const SgPlan p = sgemm_plan(M, Kf, Nf, false);
+  const SgPlan p = sgemm_plan(M, Kf, Nf, false, false, true);
   if (!p.ok) return false;
   const bf16* a = static_cast<const bf16*>(dout);
   bf16* o = static_cast<bf16*>(dA);

@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--batch", type=int, default=512)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--stages", default="48,96,192,256")
+    ap.add_argument("--wgrad", action="store_true")
     a = ap.parse_args()
     import ogv
     from ogv._lib import ACT, load
@@ -96,6 +97,10 @@ def main():
                 assert lib.ogv_set_option(b"sgemm", mode) == 0
                 t[mode] = timeit(fwd)
                 outs[mode] = out.float().clone()
+            if act is None and res is None:  # hipBLASLt reference point (torch.nn.functional.linear, bf16)
+                wb = w.to(bf)
+                tl = timeit(lambda: F.linear(x, wb))
+                print(f"      torch/hipBLASLt linear {tl:7.1f} us {2 * M * (K + N) / tl / 1e3:6.0f} GB/s", flush=True)
             xa = F.gelu(x.float()) if act else x.float()
             ref = xa @ w.t() + b
             if res is not None:
@@ -133,6 +138,20 @@ def main():
             print(f"dgrad s{C:<3d} {name:20s} M={M:7d} N={N:5d} K={K:5d}  tiled {t[0]:7.1f} us "
                   f"{nbytes / t[0] / 1e3:6.0f} GB/s | sgemm {t[1]:7.1f} us {nbytes / t[1] / 1e3:6.0f} GB/s "
                   f"({t[0] / t[1]:4.2f}x)  err {e0:.1e}/{e1:.1e} {'OK' if max(e0, e1) < tol else 'BAD'}", flush=True)
+            # wgrad: dW = dout^T . act(x), dbias (fp32, split-M partials + column reduction)
+            if a.wgrad:
+                dw = torch.empty(N, K, device=dev)
+                db = torch.empty(N, device=dev)
+                wsw = torch.empty(lib.ogv_gemm_wgrad_ws_bytes(M, N, K), dtype=torch.uint8, device=dev)
+                tw = timeit(lambda: lib.ogv_gemm_wgrad(p(dout), N, p(x), K, None, 1, p(dw), p(db), M, N, K, ACT[act],
+                                                       p(wsw), 1, st))
+                xa = F.gelu(x.float()) if act else x.float()
+                refw = dout.float().t() @ xa
+                ew = (dw - refw).abs().max().item() / max(1e-6, refw.abs().max().item())
+                nbytes = 2 * M * (K + N) + 4 * N * K
+                print(f"wgrad s{C:<3d} {name:20s} M={M:7d} N={N:5d} K={K:5d}  {tw:7.1f} us {nbytes / tw / 1e3:6.0f} GB/s"
+                      f"  relerr {ew:.1e} {'OK' if ew < 2e-2 else 'BAD'}", flush=True)
+                del dw, db, wsw
             del x, out, dout, dx, res
         torch.cuda.empty_cache()
     lib.ogv_set_option(b"sgemm", 1)

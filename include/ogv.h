@@ -80,14 +80,15 @@ int ogv_grid_attn_bwd(const void* dout, const void* qkv, const void* out, const 
  * LayerNorm over the contiguous channel dim of [M, C] rows.  Replaces nn.LayerNorm inside
  * LayerNorm2d (src/model/outlook_attention.py:26-31, eps 1e-6) and OutGridBlock.norm2/norm3
  * (src/model/Out_Grid_Block.py:69,84, eps 1e-5).  mean/rstd: fp32 [M] (saved for bwd).
- * bwd: dx [M, C]; dgamma/dbeta fp32 [C] (overwritten); ws >= ogv_layernorm_bwd_ws_bytes(M, C).
+ * bwd: dx [M, C] (+ dres [M, C] when non-null: the gradient of a residual branch that reused x,
+ * summed in the same pass); dgamma/dbeta fp32 [C] (overwritten); ws >= ogv_layernorm_bwd_ws_bytes(M, C).
  * ------------------------------------------------------------------------------------------- */
 int ogv_layernorm_fwd(const void* x, const float* gamma, const float* beta, void* y, float* mean,
                       float* rstd, int M, int C, float eps, ogv_dtype dt, void* stream);
 size_t ogv_layernorm_bwd_ws_bytes(int M, int C);
 int ogv_layernorm_bwd(const void* dy, const void* x, const float* gamma, const float* mean,
-                      const float* rstd, void* dx, float* dgamma, float* dbeta, void* ws, int M, int C,
-                      ogv_dtype dt, void* stream);
+                      const float* rstd, const void* dres, void* dx, float* dgamma, float* dbeta, void* ws,
+                      int M, int C, ogv_dtype dt, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Dense projection GEMMs on MFMA (1x1 Conv2d / nn.Linear of the hot path:

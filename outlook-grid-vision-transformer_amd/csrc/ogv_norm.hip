@@ -80,8 +80,8 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, co
 template <typename T, int G, int NV, int VEC>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                      const float* __restrict__ gamma, const float* __restrict__ mean,
-                                                     const float* __restrict__ rstd, T* __restrict__ dx,
-                                                     float* __restrict__ part, long M, int C) {
+                                                     const float* __restrict__ rstd, const T* __restrict__ dres,
+                                                     T* __restrict__ dx, float* __restrict__ part, long M, int C) {
   constexpr int E = NV * VEC;
   const int lane_g = threadIdx.x % G;
   const long rows_per_block = blockDim.x / G;
@@ -134,6 +134,12 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
         float o[VEC];
 #pragma unroll
         for (int i = 0; i < VEC; ++i) o[i] = rs * (gv[v * VEC + i] - m1 - xh[v * VEC + i] * m2);
+        if (dres) {  // gradient of the residual branch that reused x (one pass instead of an extra add)
+          float r[VEC];
+          load_vec<T, VEC>(dres + row * C + c, r);
+#pragma unroll
+          for (int i = 0; i < VEC; ++i) o[i] += r[i];
+        }
         store_vec<T, VEC>(dx + row * C + c, o);
       }
     }
@@ -219,9 +225,9 @@ static void ln_fwd_launch(const void* x, const float* gamma, const float* beta, 
 
 template <typename T, int G, int NV, int VEC>
 static void ln_bwd_launch(const void* dy, const void* x, const float* gamma, const float* mean, const float* rstd,
-                          void* dx, float* part, long nb, long M, int C, hipStream_t s) {
-  ln_bwd_kernel<T, G, NV, VEC><<<(unsigned)nb, 256, 0, s>>>((const T*)dy, (const T*)x, gamma, mean, rstd, (T*)dx,
-                                                            part, M, C);
+                          const void* dres, void* dx, float* part, long nb, long M, int C, hipStream_t s) {
+  ln_bwd_kernel<T, G, NV, VEC><<<(unsigned)nb, 256, 0, s>>>((const T*)dy, (const T*)x, gamma, mean, rstd,
+                                                            (const T*)dres, (T*)dx, part, M, C);
 }
 
 }  // namespace ogv
@@ -254,8 +260,8 @@ extern "C" size_t ogv_layernorm_bwd_ws_bytes(int M, int C) {
 }
 
 extern "C" int ogv_layernorm_bwd(const void* dy, const void* x, const float* gamma, const float* mean,
-                                 const float* rstd, void* dx, float* dgamma, float* dbeta, void* ws, int M, int C,
-                                 ogv_dtype dt, void* stream) {
+                                 const float* rstd, const void* dres, void* dx, float* dgamma, float* dbeta, void* ws,
+                                 int M, int C, ogv_dtype dt, void* stream) {
   OGV_REQUIRE(dy && x && mean && rstd && dx && ws, "ogv_layernorm_bwd: null pointer");
   OGV_REQUIRE(M > 0 && C > 0, "ogv_layernorm_bwd: bad shape M=%d C=%d", M, C);
   LnPlan p;
@@ -264,7 +270,7 @@ extern "C" int ogv_layernorm_bwd(const void* dy, const void* x, const float* gam
   hipStream_t s = as_stream(stream);
   float* part = (float*)ws;
   float* tmp = part + (size_t)nb * 2 * C;
-  OGV_LN_DISPATCH(ln_bwd_launch, dy, x, gamma, mean, rstd, dx, part, nb, (long)M, C, s);
+  OGV_LN_DISPATCH(ln_bwd_launch, dy, x, gamma, mean, rstd, dres, dx, part, nb, (long)M, C, s);
   // partials are [nb][dgamma(C) | dbeta(C)]: reduced straight into the caller's buffers
   if (dgamma && dbeta) colreduce(part, dgamma, nb, 2L * C, 2L * C, tmp, s, dbeta, C);
   else if (dgamma) colreduce(part, dgamma, nb, C, 2L * C, tmp, s);

@@ -65,7 +65,7 @@ SIGNATURES = {
     "ogv_grid_attn_bwd": (_i, [_p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _f, _i, _p]),
     "ogv_layernorm_fwd": (_i, [_p, _p, _p, _p, _p, _p, _i, _i, _f, _i, _p]),
     "ogv_layernorm_bwd_ws_bytes": (_sz, [_i, _i]),
-    "ogv_layernorm_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _p]),
+    "ogv_layernorm_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _p]),
     "ogv_gemm_fwd": (_i, [_p, _i, _p, _p, _p, _p, _i, _p, _i, _i, _i, _i, _i, _i, _p]),
     "ogv_gemm_dgrad_ws_bytes": (_sz, [_i, _i]),
     "ogv_gemm_dgrad": (_i, [_p, _i, _p, _p, _i, _p, _i, _p, _i, _i, _i, _i, _i, _p, _i, _p]),

@@ -295,8 +295,39 @@ class _LayerNorm(torch.autograd.Function):
         dgamma = torch.empty((C,), dtype=torch.float32, device=x2d.device) if ctx.affine[0] else None
         dbeta = torch.empty((C,), dtype=torch.float32, device=x2d.device) if ctx.affine[1] else None
         ws = _ws(lib.ogv_layernorm_bwd_ws_bytes(M, C), x2d.device)
-        check(lib.ogv_layernorm_bwd(_ptr(dy), _ptr(x2d), _ptr(gamma), _ptr(mean), _ptr(rstd), _ptr(dx), _ptr(dgamma),
-                                    _ptr(dbeta), _ptr(ws), M, C, _dt(x2d), _stream()), "ogv_layernorm_bwd")
+        check(lib.ogv_layernorm_bwd(_ptr(dy), _ptr(x2d), _ptr(gamma), _ptr(mean), _ptr(rstd), None, _ptr(dx),
+                                    _ptr(dgamma), _ptr(dbeta), _ptr(ws), M, C, _dt(x2d), _stream()),
+              "ogv_layernorm_bwd")
+        return dx, dgamma, dbeta, None
+
+
+class _LayerNormPair(torch.autograd.Function):
+    """(LN(x), x) for a pre-norm residual block x + f(LN(x)).  The second output is x itself (a
+    view), used as the block's residual, so its gradient arrives HERE and is summed into dx inside
+    the LN backward kernel instead of by a separate autograd accumulation add."""
+
+    @staticmethod
+    def forward(ctx, x2d, gamma, beta, eps):
+        y = _LayerNorm.forward(ctx, x2d, gamma, beta, eps)
+        return y, x2d.view_as(x2d)
+
+    @staticmethod
+    def backward(ctx, dy, dres):
+        lib = _lib.load()
+        x2d, gamma, mean, rstd = ctx.saved_tensors
+        M, C = x2d.shape
+        if dy is None:
+            return dres, None, None, None
+        dy = dy.to(x2d.dtype).contiguous()
+        if dres is not None:
+            dres = dres.to(x2d.dtype).contiguous()
+        dx = torch.empty_like(x2d)
+        dgamma = torch.empty((C,), dtype=torch.float32, device=x2d.device) if ctx.affine[0] else None
+        dbeta = torch.empty((C,), dtype=torch.float32, device=x2d.device) if ctx.affine[1] else None
+        ws = _ws(lib.ogv_layernorm_bwd_ws_bytes(M, C), x2d.device)
+        check(lib.ogv_layernorm_bwd(_ptr(dy), _ptr(x2d), _ptr(gamma), _ptr(mean), _ptr(rstd), _ptr(dres), _ptr(dx),
+                                    _ptr(dgamma), _ptr(dbeta), _ptr(ws), M, C, _dt(x2d), _stream()),
+              "ogv_layernorm_bwd")
         return dx, dgamma, dbeta, None
 
 
@@ -304,6 +335,13 @@ def layer_norm_rows(x2d, gamma, beta, eps):
     require_device(x2d, gamma, beta, what="ogv.layer_norm")
     x2d = x2d.contiguous()
     return _LayerNorm.apply(x2d, f32(gamma), f32(beta), float(eps))
+
+
+def layer_norm_rows_pair(x2d, gamma, beta, eps):
+    """(LN(x2d), x2d-as-residual): see _LayerNormPair."""
+    require_device(x2d, gamma, beta, what="ogv.layer_norm")
+    x2d = x2d.contiguous()
+    return _LayerNormPair.apply(x2d, f32(gamma), f32(beta), float(eps))
 
 
 # ------------------------------------------------------------------------------------------------

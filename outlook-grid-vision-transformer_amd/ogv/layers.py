@@ -78,6 +78,16 @@ class LayerNorm(nn.LayerNorm):
         y = OF.layer_norm_rows(x2d, self.weight, self.bias, self.eps)
         return y.view(x.shape)
 
+    def forward_pair(self, x):
+        """(LN(x), x as the residual) with the residual's gradient summed in the LN backward.
+        Falls back to (self(x), x) when hooks are registered on this module."""
+        if (self._forward_hooks or self._forward_pre_hooks or not torch.is_grad_enabled()
+                or len(self.normalized_shape) != 1):
+            return self(x), x
+        x2d = x.to(OF.compute_dtype(x)).reshape(-1, x.shape[-1])
+        y, r = OF.layer_norm_rows_pair(x2d, self.weight, self.bias, self.eps)
+        return y.view(x.shape), r.view(x.shape)
+
 
 class BatchNorm2d(nn.BatchNorm2d):
     """nn.BatchNorm2d on the native BN kernels (NHWC rows; train batch statistics with the

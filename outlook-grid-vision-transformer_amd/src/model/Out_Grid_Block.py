@@ -75,6 +75,8 @@ class OutGridBlock(nn.Module):
         xb = x.to(OF.compute_dtype(x)).permute(0, 2, 3, 1)        # BHWC view of channels_last
         if not xb.is_contiguous():
             xb = xb.contiguous()
-        xb = self.grid_attn(self.norm2(xb), residual=xb, row_scale=drop_path_scale(self.dp2, xb))
-        xb = self.mlp(self.norm3(xb), residual=xb, row_scale=drop_path_scale(self.dp3, xb))
+        xn, xr = self.norm2.forward_pair(xb)
+        xb = self.grid_attn(xn, residual=xr, row_scale=drop_path_scale(self.dp2, xb))
+        xn, xr = self.norm3.forward_pair(xb)
+        xb = self.mlp(xn, residual=xr, row_scale=drop_path_scale(self.dp3, xb))
         return xb.permute(0, 3, 1, 2)                              # NCHW (channels_last) view

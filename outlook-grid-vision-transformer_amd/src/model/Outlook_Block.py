@@ -48,7 +48,9 @@ class OutlookerBlock2d(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         x = x.to(OF.compute_dtype(x))
-        x = self.attn(self.norm1(x), residual=x, row_scale=drop_path_scale(self.dp1, x))
-        x = self.mlp(self.norm2(x), residual=x, row_scale=drop_path_scale(self.dp2, x))
+        xn, xr = self.norm1.forward_pair(x)
+        x = self.attn(xn, residual=xr, row_scale=drop_path_scale(self.dp1, x))
+        xn, xr = self.norm2.forward_pair(x)
+        x = self.mlp(xn, residual=xr, row_scale=drop_path_scale(self.dp2, x))
         return x
 

@@ -39,6 +39,16 @@ class LayerNorm2d(nn.Module):
         y = OF.layer_norm_rows(rows, self.ln.weight, self.ln.bias, self.ln.eps)
         return OF.rows_to_nchw(y, B, H, W)
 
+    def forward_pair(self, x: torch.Tensor):
+        """(LN2d(x), x as the residual) with the residual's gradient summed in the LN backward.
+        Falls back to (self(x), x) when hooks are registered on this module."""
+        if self._forward_hooks or self._forward_pre_hooks or not torch.is_grad_enabled():
+            return self(x), x
+        B, C, H, W = x.shape
+        rows = OF.nchw_to_rows(x.to(OF.compute_dtype(x)))
+        y, r = OF.layer_norm_rows_pair(rows, self.ln.weight, self.ln.bias, self.ln.eps)
+        return OF.rows_to_nchw(y, B, H, W), OF.rows_to_nchw(r, B, H, W)
+
 
 class MLP2d(nn.Module):
     """fc1 (1x1) -> act -> drop -> fc2 (1x1) -> drop.  fc1 stores the pre-activation; fc2 applies

@@ -1188,7 +1188,7 @@ size_t wgrad_ws_bytes(int M, int N, int K) {
     const long ld = (long)N * K + N;
     best = std::max(best, ((size_t)p.S * ld + colreduce_tmp_floats(p.S, ld)) * sizeof(float));
   }
-  return best;
+  return std::max(best, swgrad_ws_floats(M > 0 ? M : 1, N, K) * sizeof(float));
 }
 
 template <int BN, int BK>
@@ -1217,9 +1217,16 @@ void gemm_wgrad_launch(ogv_dtype dt, const void* G, int ldg, const void* X, int 
     if (dbias) (void)hipMemsetAsync(dbias, 0, (size_t)N * sizeof(float), s);
     return;
   }
-  const WgradPlan p = wgrad_plan(dt, M, N, K);
   const long ldp = (long)N * K + N;
   float* part = (float*)ws;
+  if (dt == OGV_BF16 && !xc) {
+    const int S = swgrad_try(G, ldg, X, ldx, pro, rs, rps, part, dbias != nullptr, M, N, K, s);
+    if (S > 0) {
+      colreduce(part, dW, S, dbias ? ldp : (long)N * K, ldp, part + (size_t)S * ldp, s, dbias, (long)N * K);
+      return;
+    }
+  }
+  const WgradPlan p = wgrad_plan(dt, M, N, K);
   float* tmp = part + (size_t)p.S * ldp;
   if (dt == OGV_BF16) {
     const bool b = dbias != nullptr;

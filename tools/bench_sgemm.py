@@ -143,14 +143,21 @@ def main():
                 dw = torch.empty(N, K, device=dev)
                 db = torch.empty(N, device=dev)
                 wsw = torch.empty(lib.ogv_gemm_wgrad_ws_bytes(M, N, K), dtype=torch.uint8, device=dev)
-                tw = timeit(lambda: lib.ogv_gemm_wgrad(p(dout), N, p(x), K, None, 1, p(dw), p(db), M, N, K, ACT[act],
-                                                       p(wsw), 1, st))
                 xa = F.gelu(x.float()) if act else x.float()
                 refw = dout.float().t() @ xa
-                ew = (dw - refw).abs().max().item() / max(1e-6, refw.abs().max().item())
+                refb = dout.float().sum(0)
+                tw, ew = {}, {}
+                for mode in (0, 1):
+                    assert lib.ogv_set_option(b"sgemm", mode) == 0
+                    tw[mode] = timeit(lambda: lib.ogv_gemm_wgrad(p(dout), N, p(x), K, None, 1, p(dw), p(db), M, N, K,
+                                                                 ACT[act], p(wsw), 1, st))
+                    ew[mode] = max((dw - refw).abs().max().item() / max(1e-6, refw.abs().max().item()),
+                                   (db - refb).abs().max().item() / max(1e-6, refb.abs().max().item()))
                 nbytes = 2 * M * (K + N) + 4 * N * K
-                print(f"wgrad s{C:<3d} {name:20s} M={M:7d} N={N:5d} K={K:5d}  {tw:7.1f} us {nbytes / tw / 1e3:6.0f} GB/s"
-                      f"  relerr {ew:.1e} {'OK' if ew < 2e-2 else 'BAD'}", flush=True)
+                print(f"wgrad s{C:<3d} {name:20s} M={M:7d} N={N:5d} K={K:5d}  tiled {tw[0]:7.1f} us "
+                      f"{nbytes / tw[0] / 1e3:6.0f} GB/s | stream {tw[1]:7.1f} us {nbytes / tw[1] / 1e3:6.0f} GB/s "
+                      f"({tw[0] / tw[1]:4.2f}x)  relerr {ew[0]:.1e}/{ew[1]:.1e} "
+                      f"{'OK' if max(ew.values()) < 2e-2 else 'BAD'}", flush=True)
                 del dw, db, wsw
             del x, out, dout, dx, res
         torch.cuda.empty_cache()

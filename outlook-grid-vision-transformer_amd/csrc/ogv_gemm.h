@@ -159,5 +159,7 @@ int swgrad_try(const void* G, int ldg, const void* X, int ldx, const Pro& pro, c
 size_t swgrad_ws_floats(int M, int N, int K);
 int sgemm_mode();
 void set_sgemm_mode(int v);
+int sgemm_min_m();
+void set_sgemm_min_m(int v);
 
 }  // namespace ogv

@@ -313,6 +313,9 @@ int sgemm_mode() {
   return g_sgemm_mode;
 }
 void set_sgemm_mode(int v) { g_sgemm_mode = v; }
+static int g_sg_min_m = 65536;  // smallest M routed to the streaming kernels (tuning knob "sgemm_min_m")
+void set_sgemm_min_m(int v) { g_sg_min_m = v; }
+int sgemm_min_m() { return g_sg_min_m; }
 
 static int device_cus() {
   static int cus = 0;
@@ -339,7 +342,7 @@ static bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) =
 // kernel VALU-bound; a data-gradient whose output needs two weight tiles loses to the tiled kernel.
 static SgPlan sgemm_plan(int M, int N, int K, bool stats, bool prologue, bool dgrad) {
   SgPlan p;
-  if (M < 32768 || (K & 7) != 0 || (N & 7) != 0) return p;  // small M: the tiled kernel fills the chip better
+  if (M < g_sg_min_m || (K & 7) != 0 || (N & 7) != 0) return p;  // small M: the tiled kernel fills the chip better
   int KT;
   if (K <= 64) KT = 2;
   else if (K <= 96) KT = 3;

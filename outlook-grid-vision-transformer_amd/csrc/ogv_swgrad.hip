@@ -240,7 +240,7 @@ static int sw_tile(int D) {  // tile edge for an output dim: multiple of 16 in {
 
 static SwPlan swgrad_plan(int M, int N, int K) {
   SwPlan p;
-  if (M < 65536 || (N & 7) || (K & 7)) return p;
+  if (M < sgemm_min_m() || (N & 7) || (K & 7)) return p;
   p.BN = sw_tile(N);
   p.BK = sw_tile(K);
   p.nNt = (N + p.BN - 1) / p.BN;

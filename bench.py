@@ -40,7 +40,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=512, help="per-GPU batch")
     ap.add_argument("--model", default="model_a_7m")
-    ap.add_argument("--probe", default="gemm_fwd", choices=["gemm_fwd", "outlook_fwd", "grid_fwd"],
+    ap.add_argument("--probe", default="sgemm", choices=["sgemm", "gemm_fwd", "outlook_fwd", "grid_fwd"],
                     help="kernel whose launches feed `roofline`")
     ap.add_argument("--eager", action="store_true", help="launch kernels one by one instead of graph replay")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -50,6 +50,8 @@ def parse():
 
 
 PROBE_KERNEL = {  # probe name -> kernel symbol(s) it times (rocprofv3 names)
+    "sgemm": "ogv::sgemm_bf16_kernel<*> (persistent streaming projection GEMM: the Linear / 1x1-conv fwd and dgrad "
+             "launches routed to it)",
     "gemm_fwd": "ogv::gemm_bf16_kernel<{128|64},{128|64},*,false,0,false> (Linear / 1x1-conv forward launches)",
     "outlook_fwd": "ogv::outlook_fwd_kernel",
     "grid_fwd": "ogv::grid_fwd_kernel",
@@ -178,8 +180,10 @@ def main():
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
                     "algorithmic_bytes_per_launch": int(probe["bytes_per_launch"]),
                     "avg_launch_ms": round(probe["avg_ms"], 5), "launches": probe["n"],
-                    "timing": "HIP events around each launch, eager step after the timed graph replays"
-                    if trainer.graphs else "HIP events around each launch, all timed steps"}
+                    "event_overhead_ms": round(probe["event_overhead_ms"], 5),
+                    "timing": ("HIP events around each launch (a 40 us device spin queued ahead of each, so no host "
+                               "launch gap is timed; minus the empty event-pair interval), " + ("eager step after the timed graph replays"
+                                                           if trainer.graphs else "all timed steps"))}
         out = {
             "metric": "training imgs/s Model-A-7M CIFAR-100 32x32 (bf16, bs=512/GPU)",
             "value": round(value, 1), "unit": "imgs/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,

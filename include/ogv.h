@@ -39,9 +39,15 @@ enum {
 const char* ogv_version(void);
 const char* ogv_last_error(void);
 /* Tuning switch (no reference counterpart; process-wide, set before capture):
- *   "sgemm" 1 (default) / 0: persistent streaming kernel for tall-skinny bf16 projections on/off.
+ *   "sgemm" 1 (default) / 0: persistent streaming kernels (projection fwd/dgrad and weight gradient)
+ *   for tall-skinny bf16 shapes on/off;  "sgemm_min_m" (default 65536): smallest M routed to them.
  * Returns OGV_ERR_ARG for an unknown name. */
 int ogv_set_option(const char* name, int value);
+/* Diagnostics (no reference counterpart): 1 if ogv_gemm_fwd (kind 0) / ogv_gemm_dgrad (kind 1) of
+ * this shape runs on the persistent streaming kernel (contiguous 16-B aligned bf16 operands), else 0;
+ * ogv_gpu_sleep queues a ~microseconds device-side spin on the stream (timing harnesses). */
+int ogv_gemm_stream_route(int kind, int M, int N, int K, ogv_act act_in);
+int ogv_gpu_sleep(int microseconds, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Outlook aggregation.  Replaces, for stride 1:

@@ -451,4 +451,37 @@ bool sgemm_dgrad_try(const void* dout, int ldd, const float* W, void* dA, int ld
   return true;
 }
 
+// Spin on the device wall clock (100 MHz class counter) for ~us microseconds: queued in front of a
+// timed launch it keeps the GPU behind the host, so HIP events around the launch time the kernel
+// and not the host's launch latency (bench.py's roofline probe).  Reads the clock only.
+__global__ void gpu_sleep_kernel(unsigned long long ticks) {
+  const unsigned long long t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
+int sgemm_route(int kind, int M, int N, int K, int act) {
+  if (!sgemm_mode()) return 0;
+  if (kind == 0) return sgemm_plan(M, N, K, false, act != OGV_ACT_NONE, false).ok;
+  return sgemm_plan(M, K, N, false, false, true).ok;  // dgrad: output K, reduction N
+}
+
 }  // namespace ogv
+
+using namespace ogv;
+
+extern "C" int ogv_gemm_stream_route(int kind, int M, int N, int K, ogv_act act_in) {
+  return sgemm_route(kind, M, N, K, act_in);
+}
+
+extern "C" int ogv_gpu_sleep(int microseconds, void* stream) {
+  static int khz = 0;
+  if (!khz) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess ||
+        khz <= 0)
+      khz = 100000;
+  }
+  const unsigned long long ticks = (unsigned long long)(microseconds > 0 ? microseconds : 0) * (unsigned long long)khz / 1000ull;
+  gpu_sleep_kernel<<<1, 64, 0, as_stream(stream)>>>(ticks);
+  return check_launch("ogv_gpu_sleep");
+}

@@ -59,6 +59,8 @@ SIGNATURES = {
     "ogv_version": (ctypes.c_char_p, []),
     "ogv_last_error": (ctypes.c_char_p, []),
     "ogv_set_option": (_i, [ctypes.c_char_p, _i]),
+    "ogv_gemm_stream_route": (_i, [_i, _i, _i, _i, _i]),
+    "ogv_gpu_sleep": (_i, [_i, _p]),
     "ogv_outlook_agg_fwd": (_i, [_p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _p]),
     "ogv_outlook_agg_bwd": (_i, [_p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _p]),
     "ogv_grid_attn_fwd": (_i, [_p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _f, _i, _p]),

@@ -101,9 +101,12 @@ def probe_bytes(name: str, u: dict) -> int:
         return e * u["M"] * (2 * u["C"] + u["k"] * u["k"] * u["heads"])
     if name == "grid_fwd":      # read qkv [M,3C], write out [M,C] + fp32 lse [M,h]
         return e * u["M"] * 4 * u["C"] + 4 * u["M"] * u["heads"]
-    if name == "gemm_fwd":      # read A [M,K] (+ residual [M,N]) + fp32 W [N,K] (+ bias), write out [M,N]
+    if name in ("gemm_fwd", "sgemm") and u.get("kind", "fwd") == "fwd":
+        # read A [M,K] (+ residual [M,N]) + fp32 W [N,K] (+ bias), write out [M,N]
         return (e * u["M"] * (u["K"] + u["N"] * (2 if u["res"] else 1)) + 4 * u["N"] * u["K"]
                 + (4 * u["N"] if u["bias"] else 0))
+    if name == "sgemm":         # dgrad: read dOut [M,N] (+ Z [M,K]) + fp32 W [N,K], write dA [M,K]
+        return e * u["M"] * (u["N"] + u["K"] * (2 if u["z"] else 1)) + 4 * u["N"] * u["K"]
     raise KeyError(name)
 
 
@@ -118,8 +121,11 @@ def probe_disarm():
 
 
 class _probe:
-    def __init__(self, name, units):
-        self.on = _PROBE["armed"] and _PROBE["target"] == name
+    """Events bracket the launch on its stream; a ~40 us device-side spin queued in front keeps the
+    GPU behind the host, so the interval is the kernel's own duration, not host launch latency."""
+
+    def __init__(self, name, units, when=True):
+        self.on = _PROBE["armed"] and _PROBE["target"] == name and bool(when)
         if self.on:
             self.e0 = torch.cuda.Event(enable_timing=True)
             self.e1 = torch.cuda.Event(enable_timing=True)
@@ -127,6 +133,7 @@ class _probe:
 
     def __enter__(self):
         if self.on:
+            check(_lib.load().ogv_gpu_sleep(40, _stream()), "ogv_gpu_sleep")
             self.e0.record()
         return self
 
@@ -137,17 +144,35 @@ class _probe:
         return False
 
 
+def _empty_pair_ms(reps: int = 16) -> float:
+    """Median interval of an event pair with nothing between them (same spin in front): the
+    event-recording overhead, subtracted from every probed interval."""
+    lib = _lib.load()
+    pairs = []
+    for _ in range(reps):
+        check(lib.ogv_gpu_sleep(40, _stream()), "ogv_gpu_sleep")
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        b.record()
+        pairs.append((a, b))
+    torch.cuda.synchronize()
+    ms = sorted(a.elapsed_time(b) for a, b in pairs)
+    return ms[len(ms) // 2]
+
+
 def probe_results():
-    """{n, avg_ms, bytes_per_launch, achieved_GBs} over the recorded launches, or None."""
+    """{n, avg_ms, bytes_per_launch, achieved_GBs, event_overhead_ms} over the recorded launches
+    (each interval minus the empty event-pair overhead), or None."""
     recs = _PROBE["recs"]
     if not recs:
         return None
     torch.cuda.synchronize()
-    ms = [a.elapsed_time(b) for a, b, _ in recs]
+    ovh = _empty_pair_ms()
+    ms = [max(a.elapsed_time(b) - ovh, 1e-6) for a, b, _ in recs]
     nbytes = sum(r[2] for r in recs)
     tot = sum(ms)
     return {"n": len(recs), "avg_ms": tot / len(recs), "bytes_per_launch": nbytes / len(recs),
-            "achieved_GBs": nbytes / (tot * 1e-3) / 1e9 if tot > 0 else None}
+            "achieved_GBs": nbytes / (tot * 1e-3) / 1e9 if tot > 0 else None, "event_overhead_ms": ovh}
 
 
 def probe_reset():
@@ -211,8 +236,9 @@ class _Linear(torch.autograd.Function):
         M, K = x2d.shape
         N = w2d.shape[0]
         out = torch.empty((M, N), dtype=x2d.dtype, device=x2d.device)
-        with _probe("gemm_fwd", dict(M=M, N=N, K=K, elem=x2d.element_size(), res=residual is not None,
-                                     bias=bias is not None)):
+        units = dict(M=M, N=N, K=K, elem=x2d.element_size(), res=residual is not None, bias=bias is not None)
+        stream_k = _PROBE["armed"] and lib.ogv_gemm_stream_route(0, M, N, K, ACT[act_in]) == 1
+        with _probe("gemm_fwd", units), _probe("sgemm", units, when=stream_k):
             check(lib.ogv_gemm_fwd(_ptr(x2d), x2d.stride(0), _ptr(w2d), _ptr(bias), _ptr(residual), _ptr(row_scale),
                                    int(rps), _ptr(out), N, M, N, K, ACT[act_in], _dt(x2d), _stream()), "ogv_gemm_fwd")
         ctx.save_for_backward(x2d, w2d, row_scale)
@@ -244,9 +270,12 @@ class _Linear(torch.autograd.Function):
                 check(lib.ogv_gemm_wgrad(_ptr(dout), N, _ptr(x2d), x2d.stride(0), _ptr(rs), rps, _ptr(dw), _ptr(db),
                                          M, N, K, act, _ptr(ws_w), dt, side), "ogv_gemm_wgrad")
             if want_dx:
-                check(lib.ogv_gemm_dgrad(_ptr(dout), N, _ptr(w2d), _ptr(x2d) if act else None, x2d.stride(0),
-                                         _ptr(rs), rps, _ptr(dx), K, M, N, K, act, _ptr(ws_d), dt, _stream()),
-                      "ogv_gemm_dgrad")
+                stream_k = _PROBE["armed"] and lib.ogv_gemm_stream_route(1, M, N, K, act) == 1
+                with _probe("sgemm", dict(kind="dgrad", M=M, N=N, K=K, elem=x2d.element_size(), z=bool(act)),
+                            when=stream_k):
+                    check(lib.ogv_gemm_dgrad(_ptr(dout), N, _ptr(w2d), _ptr(x2d) if act else None, x2d.stride(0),
+                                             _ptr(rs), rps, _ptr(dx), K, M, N, K, act, _ptr(ws_d), dt, _stream()),
+                          "ogv_gemm_dgrad")
         if has_res and ctx.needs_input_grad[3]:
             dres = dout
         return dx, dw, db, dres, None, None, None

@@ -1,0 +1,54 @@
+"""Cross-check bench.py's live roofline probe against the rocprofv3 kernel trace of the same run.
+
+The probed launches are the ones queued right behind an ogv gpu_sleep_kernel (bench.py's eager
+probe step); their rocprof durations are averaged and compared with the probe's `avg_launch_ms`
+(HIP events).  Also prints the average over every launch of the probed kernel family in the
+graph-replayed steps.
+
+    python tools/probe_vs_trace.py bench_kernel_trace.csv bench_stdout.log
+"""
+import csv
+import json
+import re
+import sys
+
+
+def main(trace, log):
+    rows = list(csv.DictReader(open(trace)))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    line = [ln for ln in open(log) if ln.startswith("{")][-1]
+    rec = json.loads(line)
+    roof = rec.get("roofline") or {}
+    fam = "sgemm_bf16_kernel" if "sgemm" in roof.get("kernel", "") else None
+    if fam is None:
+        print("probe kernel is not the streaming GEMM; nothing to compare")
+        return
+    probed, allk = [], []
+    for i, r in enumerate(rows):
+        if fam not in r["Kernel_Name"]:
+            continue
+        d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6  # ms
+        # same queue, the previous launch on it is the sleep kernel
+        prev = next((rows[j] for j in range(i - 1, max(-1, i - 40), -1) if rows[j]["Queue_Id"] == r["Queue_Id"]), None)
+        if prev is not None and "gpu_sleep_kernel" in prev["Kernel_Name"]:
+            probed.append(d)
+        else:
+            allk.append(d)
+    if not probed:
+        print("no probed launches found in the trace")
+        return
+    avg_p = sum(probed) / len(probed)
+    print(f"probe (HIP events): n={roof.get('launches')} avg={roof.get('avg_launch_ms'):.5f} ms "
+          f"achieved={roof.get('achieved')} GB/s")
+    print(f"rocprof, same launches (behind the sleep kernel): n={len(probed)} avg={avg_p:.5f} ms "
+          f"-> ratio events/rocprof = {roof.get('avg_launch_ms') / avg_p:.3f}")
+    if allk:
+        print(f"rocprof, every other {fam} launch (graph replays + MBConv-internal): n={len(allk)} "
+              f"avg={sum(allk) / len(allk):.5f} ms")
+    bpl = roof.get("algorithmic_bytes_per_launch")
+    if bpl:
+        print(f"algorithmic bytes/launch {bpl} -> rocprof-timed achieved {bpl / (avg_p * 1e-3) / 1e9:.1f} GB/s")
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:3])

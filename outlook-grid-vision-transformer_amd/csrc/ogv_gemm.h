@@ -161,5 +161,6 @@ int sgemm_mode();
 void set_sgemm_mode(int v);
 int sgemm_min_m();
 void set_sgemm_min_m(int v);
+void set_bk64_max_m(int v);
 
 }  // namespace ogv

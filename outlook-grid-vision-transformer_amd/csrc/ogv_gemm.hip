@@ -189,18 +189,20 @@ __device__ __forceinline__ void gemm_epilogue_bf16(f32x4 (&acc)[TM][TN], float* 
 // ------------------------------------------------------------------------------------------------
 // fwd / dgrad kernel, bf16
 // ------------------------------------------------------------------------------------------------
-template <int BM, int BN, bool PRO, bool STATS, int AM = 0, bool BT = false>
+// BK = 32 or 64 reduction columns per k-step (64 halves the serial chain of dependent slab loads
+// and barriers: the small-M shapes, whose K loop is latency-bound, use it).
+template <int BM, int BN, bool PRO, bool STATS, int AM = 0, bool BT = false, int BK = 32>
 __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__ A, int lda, Pro pro,
                                                         const float* __restrict__ Wt, int ldw, Epi epi,
                                                         bf16* __restrict__ out, int ldo, int M, int N, int K, int Ka,
                                                         int Kb, int nMt, int nNt, ConvG cv) {
-  constexpr int BK = 32;
-  constexpr int PITCH = BK + 8;  // 80-byte rows: 16-B aligned fragment reads
+  constexpr int PITCH = BK + 8;  // 80 / 144-byte rows: 16-B aligned fragment reads
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
   constexpr int A_VECS = BM * BK / 8 / 256;
   constexpr int B_F4 = BN * BK / 4 / 256;
   constexpr int SP = WN + 4;  // epilogue staging pitch (floats)
-  constexpr int MAIN_BYTES = (BM + BN) * PITCH * 2, EPI_BYTES = 4 * 16 * SP * 4;
+  constexpr int B_ELEMS = (BT && BK * (BN + 16) > BN * PITCH) ? BK * (BN + 16) : BN * PITCH;
+  constexpr int MAIN_BYTES = (BM * PITCH + B_ELEMS) * 2, EPI_BYTES = 4 * 16 * SP * 4;
   __shared__ __attribute__((aligned(16))) char smem[MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES];
   bf16* As = reinterpret_cast<bf16*>(smem);
   bf16* Bs = As + BM * PITCH;
@@ -340,43 +342,47 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
     store_tile(k0);
     __syncthreads();
     if (k0 + BK < K) load_tile(k0 + BK);  // next tile's HBM latency hides under this tile's MFMAs
-    bf16x8 af[TM], bfg[TN];
-    if constexpr (BT) {
-      // B fragments from the [k][n] tile via ds_read_b64_tr_b16: lane (g = lane>>4, c = lane&15) gets
-      // column c at k = {4g..4g+3, 16+4g..16+4g+3}; A fragments are read in that same k order.
-      typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-      typedef __attribute__((ext_vector_type(8))) short s16x8;
-      const int g = lane >> 4, c16 = lane & 15, q = c16 >> 2, p4 = (c16 & 3) * 4;
 #pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const bf16* arow = As + (wm * WM + i * 16 + c16) * PITCH;
-        const s16x4 lo = *reinterpret_cast<const s16x4*>(arow + 4 * g);
-        const s16x4 hi = *reinterpret_cast<const s16x4*>(arow + 16 + 4 * g);
-        const s16x8 a8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        af[i] = __builtin_bit_cast(bf16x8, a8);
-      }
+    for (int ks = 0; ks < BK; ks += 32) {
+      bf16x8 af[TM], bfg[TN];
+      if constexpr (BT) {
+        // B fragments from the [k][n] tile via ds_read_b64_tr_b16: lane (g = lane>>4, c = lane&15) gets
+        // column c at k = {4g..4g+3, 16+4g..16+4g+3}; A fragments are read in that same k order.
+        typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+        typedef __attribute__((ext_vector_type(8))) short s16x8;
+        const int g = lane >> 4, c16 = lane & 15, q = c16 >> 2, p4 = (c16 & 3) * 4;
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int col = wn * WN + j * 16 + p4;
-        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Bs + (4 * g + q) * (BN + 16) + col));
-        const s16x4 hi =
-            __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Bs + (16 + 4 * g + q) * (BN + 16) + col));
-        const s16x8 b8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        bfg[j] = __builtin_bit_cast(bf16x8, b8);
+        for (int i = 0; i < TM; ++i) {
+          const bf16* arow = As + (wm * WM + i * 16 + c16) * PITCH + ks;
+          const s16x4 lo = *reinterpret_cast<const s16x4*>(arow + 4 * g);
+          const s16x4 hi = *reinterpret_cast<const s16x4*>(arow + 16 + 4 * g);
+          const s16x8 a8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          af[i] = __builtin_bit_cast(bf16x8, a8);
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int col = wn * WN + j * 16 + p4;
+          const s16x4 lo =
+              __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Bs + (ks + 4 * g + q) * (BN + 16) + col));
+          const s16x4 hi =
+              __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Bs + (ks + 16 + 4 * g + q) * (BN + 16) + col));
+          const s16x8 b8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          bfg[j] = __builtin_bit_cast(bf16x8, b8);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          af[i] = *reinterpret_cast<const bf16x8*>(As + (wm * WM + i * 16 + (lane & 15)) * PITCH + ks + 8 * (lane >> 4));
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          bfg[j] = *reinterpret_cast<const bf16x8*>(Bs + (wn * WN + j * 16 + (lane & 15)) * PITCH + ks + 8 * (lane >> 4));
       }
-    } else {
 #pragma unroll
       for (int i = 0; i < TM; ++i)
-        af[i] = *reinterpret_cast<const bf16x8*>(As + (wm * WM + i * 16 + (lane & 15)) * PITCH + 8 * (lane >> 4));
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
-        bfg[j] = *reinterpret_cast<const bf16x8*>(Bs + (wn * WN + j * 16 + (lane & 15)) * PITCH + 8 * (lane >> 4));
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfg[j], acc[i][j], 0, 0, 0);
     }
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfg[j], acc[i][j], 0, 0, 0);
     __syncthreads();
   }
 
@@ -931,6 +937,15 @@ __global__ __launch_bounds__(256) void transpose_f32_kernel(const float* __restr
 // ------------------------------------------------------------------------------------------------
 // internal launchers
 // ------------------------------------------------------------------------------------------------
+static int g_bk64_max_m = 32768;  // tuning knob "bk64_max_m": largest M using 64-wide k-steps (0 = off)
+void set_bk64_max_m(int v) { g_bk64_max_m = v; }
+// Measured (tools/bench_sgemm.py, stages 2-3): 64-wide k-steps win for long reductions without a
+// prologue / activation-derivative epilogue, and at the last stage for narrow outputs.
+static bool use_bk64(int M, int K, int ncols, bool pro, bool zact) {
+  if (M > g_bk64_max_m || pro || zact) return false;
+  return K >= 512 || (M <= 8192 && K >= 256 && ncols <= 512);
+}
+
 template <typename T, int BN, bool PRO, bool STATS, int BM = GEMM_BM>
 static void launch_mm(const void* A, int lda, const Pro& pro, const float* Wt, int ldw, void* out, int ldo, int M,
                       int N, int K, int Ka, int Kb, const Epi& epi, hipStream_t s) {
@@ -944,10 +959,17 @@ static void launch_mm(const void* A, int lda, const Pro& pro, const float* Wt, i
   }
   const int nMt = (M + BM - 1) / BM, nNt = (N + BN - 1) / BN;
   const unsigned grid = (unsigned)(((nMt + 7) / 8) * 8 * nNt);
-  if constexpr (sizeof(T) == 2)
-    gemm_bf16_kernel<BM, BN, PRO, STATS><<<grid, 256, 0, s>>>((const bf16*)A, lda, pro, Wt, ldw, epi, (bf16*)out, ldo,
-                                                              M, N, K, Ka, Kb, nMt, nNt, ConvG());
-  else
+  if constexpr (sizeof(T) == 2) {
+    if constexpr (!PRO) {
+      if (use_bk64(M, K, N, false, false)) {
+        gemm_bf16_kernel<BM, BN, PRO, STATS, 0, false, 64><<<grid, 256, 0, s>>>(
+            (const bf16*)A, lda, pro, Wt, ldw, epi, (bf16*)out, ldo, M, N, K, Ka, Kb, nMt, nNt, ConvG());
+        return;
+      }
+    }
+    gemm_bf16_kernel<BM, BN, PRO, STATS><<<grid, 256, 0, s>>>((const bf16*)A, lda, pro, Wt, ldw, epi, (bf16*)out,
+                                                              ldo, M, N, K, Ka, Kb, nMt, nNt, ConvG());
+  } else
     gemm_f32_kernel<BM, BN, PRO, STATS><<<grid, 256, 0, s>>>((const float*)A, lda, pro, Wt, ldw, epi, (float*)out, ldo,
                                                              M, N, K, Ka, Kb, nMt, nNt, ConvG());
 }
@@ -1123,11 +1145,15 @@ static void launch_mm_bt(const void* A, int lda, const float* W, int ldw, void* 
   const int nMt = (M + BM - 1) / BM, nNt = (N + BN - 1) / BN;
   const unsigned grid = (unsigned)(((nMt + 7) / 8) * 8 * nNt);
   const int Kp = (K + 31) / 32 * 32;
-  if constexpr (sizeof(T) == 2)
-    gemm_bf16_kernel<BM, BN, false, false, 0, true><<<grid, 256, 0, s>>>((const bf16*)A, lda, Pro(), W, ldw, epi,
-                                                                         (bf16*)out, ldo, M, N, Kp, K, K, nMt, nNt,
-                                                                         ConvG());
-  else
+  if constexpr (sizeof(T) == 2) {
+    if (use_bk64(M, K, N, false, epi.zact != 0))
+      gemm_bf16_kernel<BM, BN, false, false, 0, true, 64><<<grid, 256, 0, s>>>(
+          (const bf16*)A, lda, Pro(), W, ldw, epi, (bf16*)out, ldo, M, N, (K + 63) / 64 * 64, K, K, nMt, nNt, ConvG());
+    else
+      gemm_bf16_kernel<BM, BN, false, false, 0, true><<<grid, 256, 0, s>>>((const bf16*)A, lda, Pro(), W, ldw, epi,
+                                                                           (bf16*)out, ldo, M, N, Kp, K, K, nMt, nNt,
+                                                                           ConvG());
+  } else
     gemm_f32_kernel<BM, BN, false, false, 0, true><<<grid, 256, 0, s>>>((const float*)A, lda, Pro(), W, ldw, epi,
                                                                         (float*)out, ldo, M, N, Kp, K, K, nMt, nNt,
                                                                         ConvG());

@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--stages", default="48,96,192,256")
     ap.add_argument("--wgrad", action="store_true")
     ap.add_argument("--min-m", type=int, default=0, help="sgemm_min_m option (0: library default)")
+    ap.add_argument("--bk64-max-m", type=int, default=-1, help="bk64_max_m option (-1: library default)")
     a = ap.parse_args()
     import ogv
     from ogv._lib import ACT, load
@@ -40,6 +41,8 @@ def main():
     bf = torch.bfloat16
     # cache flush = a READ of 512 MB (a write would leave dirty lines whose write-back lands inside
     # the timed launch)
+    if a.bk64_max_m >= 0:
+        assert lib.ogv_set_option(b"bk64_max_m", a.bk64_max_m) == 0
     if a.min_m:
         assert lib.ogv_set_option(b"sgemm_min_m", a.min_m) == 0
     flush = torch.ones(128 << 20, dtype=torch.float32, device=dev)

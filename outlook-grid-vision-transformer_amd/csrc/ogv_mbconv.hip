@@ -789,7 +789,9 @@ struct Ops {
   static void dw_fwd(const void* e, const float* w, const float* sc, const float* sh, int act, void* out, double* stat,
                      const float* shift, const DwTile& t, hipStream_t st) {
     const size_t lds = t.lds_bytes(2, V, sizeof(double));
-    if (t.ldq <= 2)
+    if (t.ldq <= 1)
+      dw_fwd_tile_kernel<T, V, 1><<<dw_grid(t), 256, lds, st>>>((const T*)e, w, sc, sh, act, (T*)out, stat, shift, t);
+    else if (t.ldq <= 2)
       dw_fwd_tile_kernel<T, V, 2><<<dw_grid(t), 256, lds, st>>>((const T*)e, w, sc, sh, act, (T*)out, stat, shift, t);
     else
       dw_fwd_tile_kernel<T, V, 3><<<dw_grid(t), 256, lds, st>>>((const T*)e, w, sc, sh, act, (T*)out, stat, shift, t);
@@ -799,7 +801,10 @@ struct Ops {
                        const float* mean, const float* inv, int act, void* out, float* stat, const DwTile& t,
                        hipStream_t st) {
     const size_t lds = t.lds_bytes(2, V, sizeof(float));
-    if (t.ldq <= 2)
+    if (t.ldq <= 1)
+      dw_dgrad_tile_kernel<T, V, 1><<<dw_grid(t), 256, lds, st>>>((const T*)dd, w, (const T*)e, sc, sh, mean, inv, act,
+                                                                  (T*)out, stat, t);
+    else if (t.ldq <= 2)
       dw_dgrad_tile_kernel<T, V, 2><<<dw_grid(t), 256, lds, st>>>((const T*)dd, w, (const T*)e, sc, sh, mean, inv, act,
                                                                   (T*)out, stat, t);
     else
@@ -810,7 +815,9 @@ struct Ops {
   static void dw_wgrad(const void* dd, const void* e, const float* sc, const float* sh, int act, float* part,
                        const DwTile& t, hipStream_t st) {
     const size_t lds = t.lds_bytes(9, V, sizeof(float));
-    if (t.ldq <= 2)
+    if (t.ldq <= 1)
+      dw_wgrad_tile_kernel<T, V, 1><<<dw_grid(t), 256, lds, st>>>((const T*)dd, (const T*)e, sc, sh, act, part, t);
+    else if (t.ldq <= 2)
       dw_wgrad_tile_kernel<T, V, 2><<<dw_grid(t), 256, lds, st>>>((const T*)dd, (const T*)e, sc, sh, act, part, t);
     else
       dw_wgrad_tile_kernel<T, V, 3><<<dw_grid(t), 256, lds, st>>>((const T*)dd, (const T*)e, sc, sh, act, part, t);

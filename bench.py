@@ -49,6 +49,12 @@ def parse():
     return ap.parse_args()
 
 
+METRIC = {  # BASELINE.json configs[1..4]
+    "model_a_7m": "training imgs/s Model-A-7M CIFAR-100 32x32",
+    "model_a_14m_tin64": "training imgs/s Model-A-14M TinyImageNet-200 64x64",
+    "model_a_22m_224": "training imgs/s Model-A-22M synthetic-ImageNet 224x224",
+}
+
 PROBE_KERNEL = {  # probe name -> kernel symbol(s) it times (rocprofv3 names)
     "sgemm": "ogv::sgemm_bf16_kernel<*> (persistent streaming projection GEMM: the Linear / 1x1-conv fwd and dgrad "
              "launches routed to it)",
@@ -185,7 +191,7 @@ def main():
                                "launch gap is timed; minus the empty event-pair interval), " + ("eager step after the timed graph replays"
                                                            if trainer.graphs else "all timed steps"))}
         out = {
-            "metric": "training imgs/s Model-A-7M CIFAR-100 32x32 (bf16, bs=512/GPU)",
+            "metric": METRIC.get(args.model, args.model) + f" (bf16, bs={B}/GPU)",
             "value": round(value, 1), "unit": "imgs/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "bf16", "data": "synthetic (randn images, randint labels; random init)",

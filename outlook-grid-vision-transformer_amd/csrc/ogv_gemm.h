@@ -162,5 +162,6 @@ void set_sgemm_mode(int v);
 int sgemm_min_m();
 void set_sgemm_min_m(int v);
 void set_bk64_max_m(int v);
+void set_grid_mfma(int v);
 
 }  // namespace ogv

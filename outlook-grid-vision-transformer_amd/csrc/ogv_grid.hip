@@ -6,9 +6,11 @@
 //           pixels (ty*g + gi, tx*g + gj), token n = ty*(W/g) + tx
 //   qkv channel = s*C + head*hd + d;  S = (q @ k^T) * hd^-0.5;  P = softmax(S);  O = P @ V
 //   out channel = head*hd + d (transpose(1,2).reshape(B,N,C)), written back at the pixel.
-// Small N (4/16/64 in Model A) is latency/bandwidth bound: one thread per (query, head) walks the
-// group's keys with an online softmax; keys/values of a group are shared through L1/L2 by the
-// N*heads threads of the group, which are adjacent in the launch.
+// bf16 with N >= 16 and head_dim <= 64 runs on the MFMA flash-style kernels of ogv_grid_mfma.hip.
+// The rest (N = 4 groups of Model-A-7M stages 1-3, fp32 parity mode, the probability-capturing
+// analysis path): one thread per (query, head) walks the group's keys with an online softmax;
+// keys/values of a group are shared through L1/L2 by the N*heads threads of the group, which are
+// adjacent in the launch.
 #include "ogv_common.h"
 
 namespace ogv {
@@ -352,6 +354,27 @@ static int make_geom(GridGeom& G, int B, int H, int W, int C, int heads, int g, 
   return OGV_OK;
 }
 
+// MFMA flash-style kernels for N >= 16 (ogv_grid_mfma.hip); false = shape not covered
+bool grid_mfma_fwd(const void* qkv, void* out, float* lse, int B, int H, int W, int C, int heads, int g, float scale,
+                   hipStream_t s);
+bool grid_mfma_bwd(const void* dout, const void* qkv, const float* lse, const float* delta, void* dqkv, int B, int H,
+                   int W, int C, int heads, int g, float scale, hipStream_t s);
+
+template <typename T>
+static void delta_launch(const void* dout, const void* out, float* delta, const GridGeom& G, int vec, hipStream_t s) {
+  const long M = (long)G.B * G.H * G.W;
+  const unsigned grid = cdiv(M * G.heads, 256);
+  switch (vec) {
+    case 8: grid_bwd_delta_kernel<T, 8><<<grid, 256, 0, s>>>((const T*)dout, (const T*)out, delta, M, G.C, G.heads); break;
+    case 4: grid_bwd_delta_kernel<T, 4><<<grid, 256, 0, s>>>((const T*)dout, (const T*)out, delta, M, G.C, G.heads); break;
+    case 2: grid_bwd_delta_kernel<T, 2><<<grid, 256, 0, s>>>((const T*)dout, (const T*)out, delta, M, G.C, G.heads); break;
+    default: grid_bwd_delta_kernel<T, 1><<<grid, 256, 0, s>>>((const T*)dout, (const T*)out, delta, M, G.C, G.heads);
+  }
+}
+
+static int g_grid_mfma = 1;  // tuning knob "grid_mfma"
+void set_grid_mfma(int v) { g_grid_mfma = v; }
+
 }  // namespace ogv
 
 using namespace ogv;
@@ -363,6 +386,9 @@ extern "C" int ogv_grid_attn_fwd(const void* qkv, void* out, float* lse, float* 
   int rc = make_geom(G, B, H, W, C, heads, g, dt, "ogv_grid_attn_fwd");
   if (rc) return rc;
   const int vec = pick_vec(G.hd);
+  if (dt == OGV_BF16 && !probs && g_grid_mfma &&
+      grid_mfma_fwd(qkv, out, lse, B, H, W, C, heads, g, scale, as_stream(stream)))
+    return check_launch("ogv_grid_attn_fwd");
   OGV_GRID_DISPATCH(fwd_launch, qkv, out, lse, probs, G, scale, as_stream(stream));
   return check_launch("ogv_grid_attn_fwd");
 }
@@ -375,6 +401,11 @@ extern "C" int ogv_grid_attn_bwd(const void* dout, const void* qkv, const void* 
   int rc = make_geom(G, B, H, W, C, heads, g, dt, "ogv_grid_attn_bwd");
   if (rc) return rc;
   const int vec = pick_vec(G.hd);
+  if (dt == OGV_BF16 && g_grid_mfma && G.N >= 16 && G.hd % 8 == 0 && G.hd <= 64) {
+    delta_launch<bf16>(dout, out, delta_ws, G, vec, as_stream(stream));
+    if (grid_mfma_bwd(dout, qkv, lse, delta_ws, dqkv, B, H, W, C, heads, g, scale, as_stream(stream)))
+      return check_launch("ogv_grid_attn_bwd");
+  }
   OGV_GRID_DISPATCH(bwd_launch, dout, qkv, out, lse, dqkv, delta_ws, G, scale, as_stream(stream));
   return check_launch("ogv_grid_attn_bwd");
 }

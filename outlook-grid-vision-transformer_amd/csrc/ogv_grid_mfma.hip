@@ -1,0 +1,409 @@
+// Grid multi-head self-attention on MFMA (bf16, N >= 16 tokens per grid group).
+//
+// Same semantics and addressing as ogv_grid.hip (strided grid partition folded into the pixel
+// index, qkv channel s*C + head*hd + d, out channel head*hd + d, fp32 LSE saved per (pixel, head)),
+// but the QK^T / PV products run on v_mfma_f32_16x16x32_bf16 / 16x16x16_bf16 in flash-attention
+// form: one wave owns a 16-row block of one (group, head) and walks the other side in 16-token
+// chunks with an online softmax, so it scales to the N = 196 / 784 groups of the 64^2 / 224^2
+// configurations (the thread-per-query kernel is VALU-bound there).
+//
+// Fragment layouts (lane = 16*fg + fr):
+//   16x16x32 A operand: row fr, k = 8*fg..8*fg+7 (one 16-B load of a token's head slice)
+//   16x16x32 B operand: col fr, k = 8*fg..8*fg+7 (same load shape)
+//   16x16x16 A operand: row fr, k = 4*fg..4*fg+3 -- exactly what a lane holds of a 16x16 C tile
+//            computed TRANSPOSED (C[4*fg+r][fr]), so softmax probabilities feed the next MFMA
+//            from registers
+//   16x16x16 B operand: k = 4*fg..4*fg+3, col fr -- ds_read_b64_tr_b16 of a [token][dim] LDS tile
+//   C / D:   C[4*fg + r][fr], r = 0..3
+// Forward: S^T = K Q^T per key chunk; P^T (registers) -> O += P V (V chunk through LDS).
+// dQ:      S^T, dP^T = V dO^T; dS^T -> dQ += dS K (K chunk through LDS).
+// dK, dV:  S = Q K^T, dP = dO V^T per query chunk; dV += P^T dO, dK += dS^T Q (dO, Q through LDS).
+#include "ogv_common.h"
+
+namespace ogv {
+
+struct GridGeomM {
+  int B, H, W, C, heads, g, Hg, Wg, N, hd;
+  __device__ __forceinline__ long pixel(long grp, int tok) const {
+    const int gj = (int)(grp % g);
+    const long r = grp / g;
+    const int gi = (int)(r % g);
+    const long b = r / g;
+    const int ty = tok / Wg, tx = tok - ty * Wg;
+    return (b * H + (long)ty * g + gi) * W + (long)tx * g + gj;
+  }
+};
+
+typedef __attribute__((ext_vector_type(4))) short gm_s16x4;
+typedef __attribute__((address_space(3))) gm_s16x4 gm_lds_s16x4;
+
+template <int HDP>
+__host__ __device__ constexpr int gm_pitch() { return HDP == 32 ? 48 : 80; }  // 16 * odd elements
+
+// 8 consecutive head dims of one token (zero past hd / for invalid tokens)
+__device__ __forceinline__ bf16x8 gm_load8(const bf16* __restrict__ p, bool ok) {
+  bf16x8 v = {};
+  if (ok) v = *reinterpret_cast<const bf16x8*>(p);
+  return v;
+}
+
+__device__ __forceinline__ gm_s16x4 pack4(const float (&x)[4]) {
+  gm_s16x4 r;
+  bf16* e = reinterpret_cast<bf16*>(&r);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) e[i] = (bf16)x[i];
+  return r;
+}
+
+// Stage 16 tokens x HDP dims (token rows of a chunk) into a wave-private [16][PITCH] LDS tile.
+template <int HDP>
+__device__ __forceinline__ void gm_stage(bf16* tile, const bf16* __restrict__ base, const GridGeomM& G, long grp,
+                                         int tok0, long rowstride, int lane) {
+  constexpr int PIECES = HDP / 8;  // 16-B pieces per token row
+  constexpr int PITCH = gm_pitch<HDP>();
+#pragma unroll
+  for (int t = 0; t < (16 * PIECES + 63) / 64; ++t) {
+    const int idx = lane + 64 * t;
+    if (idx < 16 * PIECES) {
+      const int row = idx / PIECES, pc = idx - row * PIECES;
+      const int tok = tok0 + row;
+      const bool ok = tok < G.N && pc * 8 < G.hd;
+      const bf16x8 v = gm_load8(base + (ok ? G.pixel(grp, tok) : 0) * rowstride + pc * 8, ok);
+      *reinterpret_cast<bf16x8*>(tile + row * PITCH + pc * 8) = v;
+    }
+  }
+}
+
+__device__ __forceinline__ void wave_sync_lds() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Store a 16-token x hd output tile held in C layout (rows 4*fg + r, dim j*16 + fr, times mul[r])
+// through the wave's LDS tile, as 16-B row pieces at base + pixel(tok0 + row) * rowstride.
+template <int HDP>
+__device__ __forceinline__ void gm_store(bf16* tile, const f32x4 (&acc)[HDP / 16], const float (&mul)[4],
+                                         bf16* __restrict__ base, const GridGeomM& G, long grp, int tok0,
+                                         long rowstride, int lane) {
+  constexpr int ND = HDP / 16, PIECES = HDP / 8, PITCH = gm_pitch<HDP>();
+  const int fr = lane & 15, fg = lane >> 4;
+#pragma unroll
+  for (int j = 0; j < ND; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) tile[(4 * fg + r) * PITCH + j * 16 + fr] = (bf16)(acc[j][r] * mul[r]);
+  wave_sync_lds();
+#pragma unroll
+  for (int t = 0; t < (16 * PIECES + 63) / 64; ++t) {
+    const int idx = lane + 64 * t;
+    if (idx < 16 * PIECES) {
+      const int row = idx / PIECES, pc = idx - row * PIECES;
+      const int tok = tok0 + row;
+      if (tok < G.N && pc * 8 < G.hd)
+        *reinterpret_cast<bf16x8*>(base + G.pixel(grp, tok) * rowstride + pc * 8) =
+            *reinterpret_cast<const bf16x8*>(tile + row * PITCH + pc * 8);
+    }
+  }
+  wave_sync_lds();
+}
+
+// ---------------------------------------------------------------------------------------------- fwd
+template <int HDP>
+__global__ __launch_bounds__(256) void grid_mfma_fwd_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
+                                                            float* __restrict__ lse, GridGeomM G, float scale,
+                                                            long units) {
+  constexpr int KK = HDP / 32, ND = HDP / 16, PITCH = gm_pitch<HDP>();
+  __shared__ __attribute__((aligned(16))) bf16 lds[4][16 * PITCH];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const long unit = (long)blockIdx.x * 4 + wave;
+  if (unit >= units) return;
+  const int nqb = (G.N + 15) / 16;
+  const int qb = (int)(unit % nqb);
+  const long gh = unit / nqb;
+  const int h = (int)(gh % G.heads);
+  const long grp = gh / G.heads;
+  const int fr = lane & 15, fg = lane >> 4;
+  const long C3 = 3L * G.C;
+  const bf16* qbase = qkv + h * G.hd;
+  const bf16* kbase = qkv + G.C + h * G.hd;
+  const bf16* vbase = qkv + 2 * G.C + h * G.hd;
+  bf16* tile = lds[wave];
+
+  // Q^T as the B operand: query q0 + fr, dims 8*fg (+32*kk)
+  const int qtok = qb * 16 + fr;
+  const bool qok = qtok < G.N;
+  const long qpix = qok ? G.pixel(grp, qtok) : 0;
+  bf16x8 qf[KK];
+#pragma unroll
+  for (int kk = 0; kk < KK; ++kk) {
+    const int d = kk * 32 + fg * 8;
+    qf[kk] = gm_load8(qbase + qpix * C3 + d, qok && d < G.hd);
+  }
+  f32x4 o[ND];
+#pragma unroll
+  for (int j = 0; j < ND; ++j) o[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, l = 0.f;  // running max / sum of query fr (replicated over fg)
+
+  for (int k0 = 0; k0 < G.N; k0 += 16) {
+    // S^T[key 4fg+r][query fr] = K Q^T
+    const int ktok = k0 + fr;
+    const bool kok = ktok < G.N;
+    const long kpix = kok ? G.pixel(grp, ktok) : 0;
+    f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      const int d = kk * 32 + fg * 8;
+      const bf16x8 kf = gm_load8(kbase + kpix * C3 + d, kok && d < G.hd);
+      s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[kk], s, 0, 0, 0);
+    }
+    // V chunk -> LDS (B operand of P V through transposed reads)
+    gm_stage<HDP>(tile, vbase, G, grp, k0, C3, lane);
+    // online softmax over the chunk's keys for query fr
+    float x[4], mc = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      x[r] = (k0 + 4 * fg + r < G.N) ? s[r] * scale : -INFINITY;
+      mc = fmaxf(mc, x[r]);
+    }
+    mc = fmaxf(mc, __shfl_xor(mc, 16, 64));
+    mc = fmaxf(mc, __shfl_xor(mc, 32, 64));
+    const float mn = fmaxf(m, mc);
+    const float corr = __expf(m - mn);  // 0 on the first chunk (m = -inf)
+    float p[4], ps = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      p[r] = __expf(x[r] - mn);
+      ps += p[r];
+    }
+    ps += __shfl_xor(ps, 16, 64);
+    ps += __shfl_xor(ps, 32, 64);
+    l = l * corr + ps;
+    m = mn;
+    // O rows are queries 4fg+r: their correction factors live in lanes 4fg+r
+    float cr[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) cr[r] = __shfl(corr, 4 * fg + r, 64);
+#pragma unroll
+    for (int j = 0; j < ND; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[j][r] *= cr[r];
+    const gm_s16x4 pa = pack4(p);  // A operand: P[query fr][keys 4fg..4fg+3]
+    wave_sync_lds();
+#pragma unroll
+    for (int j = 0; j < ND; ++j) {
+      const gm_s16x4 vb =
+          __builtin_amdgcn_ds_read_tr16_b64_v4i16((gm_lds_s16x4*)(tile + (4 * fg + (fr >> 2)) * PITCH + j * 16 + (fr & 3) * 4));
+      o[j] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(pa, vb, o[j], 0, 0, 0);
+    }
+    wave_sync_lds();
+  }
+  // normalise rows 4fg+r and store; LSE of query fr
+  float inv[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) inv[r] = 1.f / __shfl(l, 4 * fg + r, 64);
+  gm_store<HDP>(tile, o, inv, out + h * G.hd, G, grp, qb * 16, G.C, lane);
+  if (fg == 0 && qok) lse[qpix * G.heads + h] = m + __logf(l);
+}
+
+// ----------------------------------------------------------------------------------------- dQ
+template <int HDP>
+__global__ __launch_bounds__(256) void grid_mfma_dq_kernel(const bf16* __restrict__ dout, const bf16* __restrict__ qkv,
+                                                           const float* __restrict__ lse,
+                                                           const float* __restrict__ delta, bf16* __restrict__ dqkv,
+                                                           GridGeomM G, float scale, long units) {
+  constexpr int KK = HDP / 32, ND = HDP / 16, PITCH = gm_pitch<HDP>();
+  __shared__ __attribute__((aligned(16))) bf16 lds[4][16 * PITCH];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const long unit = (long)blockIdx.x * 4 + wave;
+  if (unit >= units) return;
+  const int nqb = (G.N + 15) / 16;
+  const int qb = (int)(unit % nqb);
+  const long gh = unit / nqb;
+  const int h = (int)(gh % G.heads);
+  const long grp = gh / G.heads;
+  const int fr = lane & 15, fg = lane >> 4;
+  const long C3 = 3L * G.C;
+  const bf16* qbase = qkv + h * G.hd;
+  const bf16* kbase = qkv + G.C + h * G.hd;
+  const bf16* vbase = qkv + 2 * G.C + h * G.hd;
+  bf16* tile = lds[wave];
+
+  const int qtok = qb * 16 + fr;
+  const bool qok = qtok < G.N;
+  const long qpix = qok ? G.pixel(grp, qtok) : 0;
+  bf16x8 qf[KK], gf[KK];  // Q^T and dO^T as B operands (query fr)
+#pragma unroll
+  for (int kk = 0; kk < KK; ++kk) {
+    const int d = kk * 32 + fg * 8;
+    qf[kk] = gm_load8(qbase + qpix * C3 + d, qok && d < G.hd);
+    gf[kk] = gm_load8(dout + qpix * G.C + h * G.hd + d, qok && d < G.hd);
+  }
+  const float lq = qok ? lse[qpix * G.heads + h] : INFINITY;
+  const float dl = qok ? delta[qpix * G.heads + h] : 0.f;
+  f32x4 dq[ND];
+#pragma unroll
+  for (int j = 0; j < ND; ++j) dq[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int k0 = 0; k0 < G.N; k0 += 16) {
+    const int ktok = k0 + fr;
+    const bool kok = ktok < G.N;
+    const long kpix = kok ? G.pixel(grp, ktok) : 0;
+    f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      const int d = kk * 32 + fg * 8;
+      const bf16x8 kf = gm_load8(kbase + kpix * C3 + d, kok && d < G.hd);
+      const bf16x8 vf = gm_load8(vbase + kpix * C3 + d, kok && d < G.hd);
+      s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[kk], s, 0, 0, 0);    // S^T
+      dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, gf[kk], dp, 0, 0, 0);  // dP^T
+    }
+    gm_stage<HDP>(tile, kbase, G, grp, k0, C3, lane);  // K chunk: B operand of dS K
+    float ds[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const bool ok = k0 + 4 * fg + r < G.N;
+      const float pw = ok ? __expf(s[r] * scale - lq) : 0.f;
+      ds[r] = pw * (dp[r] - dl);
+    }
+    const gm_s16x4 da = pack4(ds);  // A operand: dS[query fr][keys 4fg..]
+    wave_sync_lds();
+#pragma unroll
+    for (int j = 0; j < ND; ++j) {
+      const gm_s16x4 kb =
+          __builtin_amdgcn_ds_read_tr16_b64_v4i16((gm_lds_s16x4*)(tile + (4 * fg + (fr >> 2)) * PITCH + j * 16 + (fr & 3) * 4));
+      dq[j] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(da, kb, dq[j], 0, 0, 0);
+    }
+    wave_sync_lds();
+  }
+  const float sc4[4] = {scale, scale, scale, scale};
+  gm_store<HDP>(tile, dq, sc4, dqkv + h * G.hd, G, grp, qb * 16, C3, lane);
+}
+
+// --------------------------------------------------------------------------------------- dK, dV
+template <int HDP>
+__global__ __launch_bounds__(256) void grid_mfma_dkv_kernel(const bf16* __restrict__ dout, const bf16* __restrict__ qkv,
+                                                            const float* __restrict__ lse,
+                                                            const float* __restrict__ delta, bf16* __restrict__ dqkv,
+                                                            GridGeomM G, float scale, long units) {
+  constexpr int KK = HDP / 32, ND = HDP / 16, PITCH = gm_pitch<HDP>();
+  __shared__ __attribute__((aligned(16))) bf16 lds[4][2][16 * PITCH];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const long unit = (long)blockIdx.x * 4 + wave;
+  if (unit >= units) return;
+  const int nkb = (G.N + 15) / 16;
+  const int kb = (int)(unit % nkb);
+  const long gh = unit / nkb;
+  const int h = (int)(gh % G.heads);
+  const long grp = gh / G.heads;
+  const int fr = lane & 15, fg = lane >> 4;
+  const long C3 = 3L * G.C;
+  const bf16* qbase = qkv + h * G.hd;
+  const bf16* kbase = qkv + G.C + h * G.hd;
+  const bf16* vbase = qkv + 2 * G.C + h * G.hd;
+  bf16* qt = lds[wave][0];
+  bf16* gt = lds[wave][1];
+
+  const int ktok = kb * 16 + fr;
+  const bool kok = ktok < G.N;
+  const long kpix = kok ? G.pixel(grp, ktok) : 0;
+  bf16x8 kf[KK], vf[KK];  // K^T, V^T as B operands (key fr)
+#pragma unroll
+  for (int kk = 0; kk < KK; ++kk) {
+    const int d = kk * 32 + fg * 8;
+    kf[kk] = gm_load8(kbase + kpix * C3 + d, kok && d < G.hd);
+    vf[kk] = gm_load8(vbase + kpix * C3 + d, kok && d < G.hd);
+  }
+  f32x4 dk[ND], dv[ND];
+#pragma unroll
+  for (int j = 0; j < ND; ++j) {
+    dk[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    dv[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  for (int q0 = 0; q0 < G.N; q0 += 16) {
+    // S[query 4fg+r][key fr] = Q K^T ; dP = dO V^T  (query rows of the A operand = q0 + fr)
+    const int qtok = q0 + fr;
+    const bool qok = qtok < G.N;
+    const long qpix = qok ? G.pixel(grp, qtok) : 0;
+    f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      const int d = kk * 32 + fg * 8;
+      const bf16x8 qa = gm_load8(qbase + qpix * C3 + d, qok && d < G.hd);
+      const bf16x8 ga = gm_load8(dout + qpix * G.C + h * G.hd + d, qok && d < G.hd);
+      s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kf[kk], s, 0, 0, 0);
+      dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ga, vf[kk], dp, 0, 0, 0);
+    }
+    gm_stage<HDP>(qt, qbase, G, grp, q0, C3, lane);              // Q chunk  (B operand of dS^T Q)
+    gm_stage<HDP>(gt, dout + h * G.hd, G, grp, q0, G.C, lane);   // dO chunk (B operand of P^T dO)
+    // lse / delta of the C-tile rows (queries 4fg+r)
+    float pw[4], ds[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int tok = q0 + 4 * fg + r;
+      float lq = INFINITY, dl = 0.f;
+      if (tok < G.N) {
+        const long pq = G.pixel(grp, tok);
+        lq = lse[pq * G.heads + h];
+        dl = delta[pq * G.heads + h];
+      }
+      pw[r] = kok ? __expf(s[r] * scale - lq) : 0.f;
+      ds[r] = pw[r] * (dp[r] - dl);
+    }
+    // C layout holds [query 4fg+r][key fr] = the A operand [key fr][queries 4fg..] of the
+    // key-row products below
+    const gm_s16x4 pa = pack4(pw), da = pack4(ds);
+    wave_sync_lds();
+#pragma unroll
+    for (int j = 0; j < ND; ++j) {
+      const int off = (4 * fg + (fr >> 2)) * PITCH + j * 16 + (fr & 3) * 4;
+      const gm_s16x4 gb = __builtin_amdgcn_ds_read_tr16_b64_v4i16((gm_lds_s16x4*)(gt + off));
+      const gm_s16x4 qb2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((gm_lds_s16x4*)(qt + off));
+      dv[j] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(pa, gb, dv[j], 0, 0, 0);
+      dk[j] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(da, qb2, dk[j], 0, 0, 0);
+    }
+    wave_sync_lds();
+  }
+  // rows of dK / dV are keys kb*16 + 4fg + r
+  const float sc4[4] = {scale, scale, scale, scale}, one4[4] = {1.f, 1.f, 1.f, 1.f};
+  gm_store<HDP>(qt, dk, sc4, dqkv + G.C + h * G.hd, G, grp, kb * 16, C3, lane);
+  gm_store<HDP>(gt, dv, one4, dqkv + 2 * G.C + h * G.hd, G, grp, kb * 16, C3, lane);
+}
+
+// ------------------------------------------------------------------------------------------------
+static bool gm_ok(const GridGeomM& G) { return G.N >= 16 && G.hd % 8 == 0 && G.hd <= 64; }
+
+bool grid_mfma_fwd(const void* qkv, void* out, float* lse, int B, int H, int W, int C, int heads, int g, float scale,
+                   hipStream_t s) {
+  GridGeomM G{B, H, W, C, heads, g, H / g, W / g, (H / g) * (W / g), C / heads};
+  if (!gm_ok(G)) return false;
+  const long units = (long)B * g * g * heads * ((G.N + 15) / 16);
+  const unsigned grid = cdiv(units, 4);
+  if (G.hd <= 32)
+    grid_mfma_fwd_kernel<32><<<grid, 256, 0, s>>>((const bf16*)qkv, (bf16*)out, lse, G, scale, units);
+  else
+    grid_mfma_fwd_kernel<64><<<grid, 256, 0, s>>>((const bf16*)qkv, (bf16*)out, lse, G, scale, units);
+  return true;
+}
+
+// delta must already hold rowsum(dO * O) per (pixel, head)
+bool grid_mfma_bwd(const void* dout, const void* qkv, const float* lse, const float* delta, void* dqkv, int B, int H,
+                   int W, int C, int heads, int g, float scale, hipStream_t s) {
+  GridGeomM G{B, H, W, C, heads, g, H / g, W / g, (H / g) * (W / g), C / heads};
+  if (!gm_ok(G)) return false;
+  const long units = (long)B * g * g * heads * ((G.N + 15) / 16);
+  const unsigned grid = cdiv(units, 4);
+  if (G.hd <= 32) {
+    grid_mfma_dq_kernel<32><<<grid, 256, 0, s>>>((const bf16*)dout, (const bf16*)qkv, lse, delta, (bf16*)dqkv, G, scale,
+                                                 units);
+    grid_mfma_dkv_kernel<32><<<grid, 256, 0, s>>>((const bf16*)dout, (const bf16*)qkv, lse, delta, (bf16*)dqkv, G,
+                                                  scale, units);
+  } else {
+    grid_mfma_dq_kernel<64><<<grid, 256, 0, s>>>((const bf16*)dout, (const bf16*)qkv, lse, delta, (bf16*)dqkv, G, scale,
+                                                 units);
+    grid_mfma_dkv_kernel<64><<<grid, 256, 0, s>>>((const bf16*)dout, (const bf16*)qkv, lse, delta, (bf16*)dqkv, G,
+                                                  scale, units);
+  }
+  return true;
+}
+
+}  // namespace ogv

@@ -248,6 +248,47 @@ def test_grid_kernel_vs_oracle(case, dtype):
     assert fx.maxabs(qd.grad.float(), gref) <= (3e-5 if dtype == torch.float32 else 2e-2) * max(1, gref.abs().max().item())
 
 
+GRID_MFMA_CASES = [  # B, H, W, C, heads, g: N >= 16 with head_dim <= 64 runs on the MFMA kernels in bf16
+    (2, 32, 32, 48, 2, 8),    # Model-A-7M stage 0: N = 16, hd = 24
+    (2, 16, 16, 64, 2, 2),    # N = 64, hd = 32
+    (1, 16, 16, 64, 1, 2),    # N = 64, hd = 64
+    (1, 14, 14, 64, 2, 1),    # N = 196 (partial last 16-chunk)
+    (1, 10, 10, 128, 2, 1),   # N = 100, hd = 64
+    (1, 28, 28, 64, 2, 1),    # N = 784 (224^2 stage-0 group size)
+]
+
+
+@pytest.mark.parametrize("case", GRID_MFMA_CASES)
+def test_grid_mfma_vs_oracle(case):
+    """The MFMA flash-style path (bf16, no probability capture) against the fp32 oracle, forward and
+    all of dq / dk / dv, and against the thread-per-query kernel on the same bf16 inputs."""
+    from ogv import functional as OF
+    from ogv._lib import load
+    B, H, W, C, h, g = case
+    gen = torch.Generator().manual_seed(hash(case) & 0xFFFF)
+    qkv = torch.randn(B, H, W, 3 * C, generator=gen).to(torch.bfloat16).float()
+    dy = torch.randn(B, H, W, C, generator=gen).to(torch.bfloat16).float()
+    q_r = qkv.clone().requires_grad_()
+    y_r, _ = orc.grid_core(q_r, h, g, want_probs=True)
+    y_r.backward(dy)
+    outs = {}
+    lib = load()
+    for mode in (1, 0):
+        assert lib.ogv_set_option(b"grid_mfma", mode) == 0
+        qd = qkv.to(DEV, torch.bfloat16).requires_grad_()
+        y, _ = OF.grid_attention_rows(qd.reshape(-1, 3 * C), B, H, W, h, g, (C // h) ** -0.5)
+        y.backward(dy.to(DEV, torch.bfloat16).reshape(-1, C))
+        outs[mode] = (y.float().view(B, H, W, C), qd.grad.float())
+    assert lib.ogv_set_option(b"grid_mfma", 1) == 0
+    y, gq = outs[1]
+    assert fx.maxabs(y, y_r) <= 1e-2 * max(1, y_r.abs().max().item())
+    gref = q_r.grad
+    assert fx.maxabs(gq, gref) <= 2e-2 * max(1, gref.abs().max().item())
+    y0, gq0 = outs[0]
+    assert fx.maxabs(y, y0) <= 1e-2 * max(1, y0.abs().max().item())
+    assert fx.maxabs(gq, gq0) <= 2e-2 * max(1, gq0.abs().max().item())
+
+
 GEMM_CASES = [  # M, N, K, act, bias, residual, rowscale
     (1000, 18, 48, None, True, False, False), (4096, 192, 48, None, False, False, False),
     (777, 96, 96, "gelu", True, True, False), (2048, 48, 192, "silu", True, True, True),

@@ -40,6 +40,52 @@ __global__ __launch_bounds__(256) void colreduce_kernel(const T* __restrict__ sr
   }
 }
 
+// Single-pass form for up to 2048 rows (one launch instead of two): block = 16 column quads
+// (64 columns, 16-B loads) x 16 row groups; each thread keeps 8 rows' loads in flight, then the 16
+// row-group sums are combined in a fixed order through LDS.  Needs n, ld % 4 == 0 and 16-B
+// alignment (fp32 only); split destination as in colreduce_kernel.
+__global__ __launch_bounds__(256) void colreduce4_kernel(const float* __restrict__ src, float* __restrict__ dst, long R,
+                                                         long n, long ld, float* __restrict__ dst2, long n1) {
+  __shared__ float4 red[16][16];
+  const int cq = threadIdx.x & 15, rg = threadIdx.x >> 4;
+  const long j = ((long)blockIdx.x * 16 + cq) * 4;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (j < n) {
+    long r = rg;
+    for (; r + 7 * 16 < R; r += 8 * 16) {
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(src + (r + u * 16) * ld + j);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w;
+      }
+    }
+    for (; r < R; r += 16) {
+      const float4 v = *reinterpret_cast<const float4*>(src + r * ld + j);
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+  }
+  red[rg][cq] = acc;
+  __syncthreads();
+  if (rg == 0 && j < n) {
+    float4 t = red[0][cq];
+#pragma unroll
+    for (int g = 1; g < 16; ++g) {
+      const float4 v = red[g][cq];
+      t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+    }
+    const float o[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const long c = j + q;
+      if (c >= n) break;
+      if (dst2 && c >= n1) dst2[c - n1] = o[q];
+      else dst[c] = o[q];
+    }
+  }
+}
+
 // Sum R rows of a [R, ld] fp32 slab into dst[n].  Two passes when R is large; tmp needs
 // colreduce_tmp_floats(R, n) floats (may be null when that is 0).  Deterministic.
 size_t colreduce_tmp_floats(long R, long n) {
@@ -52,6 +98,12 @@ template <typename T>
 static void colreduce_t(const T* src, T* dst, long R, long n, long ld, T* tmp, hipStream_t s, T* dst2, long n1) {
   const unsigned gx = (unsigned)((n + 63) / 64);
   if (!dst2) n1 = n;
+  if constexpr (sizeof(T) == 4) {
+    if (R > 64 && R <= 2048 && (n & 3) == 0 && (ld & 3) == 0 && (reinterpret_cast<uintptr_t>(src) & 15) == 0) {
+      colreduce4_kernel<<<gx, 256, 0, s>>>(src, dst, R, n, ld, dst2, n1);
+      return;
+    }
+  }
   if (R <= 256) {
     colreduce_kernel<T><<<dim3(gx, 1), 256, 0, s>>>(src, dst, R, n, ld, R, dst2, n1);
     return;

@@ -997,9 +997,21 @@ static bool tiny(int M, int N, ogv_dtype dt, const Epi& epi) {
   return dt == OGV_F32 && epi.stat == nullptr && M <= 2048 && (long)M * N <= (1L << 20);
 }
 
+// OGV_LOG_GEMM=1: one stderr line per GEMM launch (kind, shape, prologue/epilogue flags) for tuning
+static bool log_gemm() {
+  static const int on = [] {
+    const char* e = getenv("OGV_LOG_GEMM");
+    return e && *e == '1' ? 1 : 0;
+  }();
+  return on != 0;
+}
+
 int gemm_fwd_launch(ogv_dtype dt, const void* A, int lda, const Pro& pro, const float* W, int ldw, void* out, int ldo,
                     int M, int N, int K, int Ka, int Kb, const Epi& epi, hipStream_t s) {
   if (M <= 0) return 0;
+  if (log_gemm())
+    fprintf(stderr, "OGVGEMM fwd dt=%d M=%d N=%d K=%d Ka=%d Kb=%d pro=%d stats=%d res=%d\n", (int)dt, M, N, K, Ka, Kb,
+            (int)pro.any(), epi.stat != nullptr, epi.res != nullptr);
   if (dt == OGV_BF16 && Ka == K && Kb == K) {
     const int r = sgemm_fwd_try(A, lda, pro, W, ldw, out, ldo, M, N, K, epi, s);
     if (r > 0) return r;
@@ -1163,6 +1175,8 @@ void gemm_dgrad_launch(ogv_dtype dt, const void* dout, int ldd, const float* W, 
                        const float* rs, int rps, const void* res, void* dA, int lda, int M, int N, int K, void* ws,
                        hipStream_t s) {
   if (M <= 0) return;
+  if (log_gemm())
+    fprintf(stderr, "OGVGEMM dgrad dt=%d M=%d N=%d K=%d zact=%d res=%d\n", (int)dt, M, N, K, zact, res != nullptr);
   Epi e;
   e.rs = rs;
   e.rps = rps;
@@ -1243,6 +1257,9 @@ void gemm_wgrad_launch(ogv_dtype dt, const void* G, int ldg, const void* X, int 
     if (dbias) (void)hipMemsetAsync(dbias, 0, (size_t)N * sizeof(float), s);
     return;
   }
+  if (log_gemm())
+    fprintf(stderr, "OGVGEMM wgrad dt=%d M=%d N=%d K=%d pro=%d conv=%d bias=%d\n", (int)dt, M, N, K, (int)pro.any(),
+            xc != nullptr, dbias != nullptr);
   const long ldp = (long)N * K + N;
   float* part = (float*)ws;
   if (dt == OGV_BF16 && !xc) {

@@ -150,46 +150,68 @@ __device__ __forceinline__ const float* ring_px(const float* ring, const DwTile&
   return ring + ((size_t)ring_slot(r) * (t.TW + 2) + px) * t.PP;
 }
 
-// Up to DW_R input rows (TW+2 pixels incl. halo) of the block's channel tile, in registers.
-template <typename T, int V, int LDQ, bool PRO>
-struct RowPipe {
-  float v[DW_R][LDQ][V];
-  __device__ __forceinline__ void load(const T* __restrict__ src, const DwTile& t, const TileIdx& ti, int y0, int nr,
-                                       int c, bool cok, const float* s, const float* h, int act) {
-    const int n = (ti.tw + 2) * t.chunks;
+// V consecutive elements kept as the raw loaded bits (bf16 pairs / fp32) until they are used, so a
+// prefetch need not retire before the next use of any LATER load (vmcnt retires in issue order).
+template <typename T, int V>
+struct RawVec {
+  static constexpr int NV = (sizeof(T) == 4 && V == 8) ? 2 : 1;
+  typedef typename VecT<T, V>::type VT;
+  VT v[NV];
+  __device__ __forceinline__ void load(const T* __restrict__ p) {
 #pragma unroll
-    for (int r = 0; r < DW_R; ++r)
+    for (int k = 0; k < NV; ++k) v[k] = *reinterpret_cast<const VT*>(p + k * (V / NV));
+  }
+  __device__ __forceinline__ void unpack(float* out) const {
+    const T* e = reinterpret_cast<const T*>(v);
+#pragma unroll
+    for (int i = 0; i < V; ++i) out[i] = to_f(e[i]);
+  }
+};
+
+// Up to DW_R input rows (TW+2 pixels incl. halo) of the block's channel tile, in registers.  The
+// loads are unconditional (addresses clamped into the tensor); the zero padding, the producer's
+// BatchNorm + activation and the conversion to fp32 are applied as the rows enter the LDS ring.
+template <typename T, int V, int LDQ>
+struct RowPipe {
+  RawVec<T, V> raw[DW_R][LDQ];
+  template <int NR>
+  __device__ __forceinline__ void load(const T* __restrict__ src, const DwTile& t, const TileIdx& ti, int y0, int cc) {
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
 #pragma unroll
       for (int j = 0; j < LDQ; ++j) {
-        const int i = threadIdx.x + j * 256, y = y0 + r;
-        const int x = ti.x0 - 1 + i / t.chunks;
-        if (r < nr && i < n && cok && y >= 0 && y < t.H && x >= 0 && x < t.W) {
-          load_vec<T, V>(src + ((ti.b * t.H + y) * t.W + x) * t.C + c, v[r][j]);
-          if constexpr (PRO) {
-#pragma unroll
-            for (int k = 0; k < V; ++k) v[r][j][k] = act_fwd(act, fmaf(v[r][j][k], s[k], h[k]));
-          }
-        } else {
-#pragma unroll
-          for (int k = 0; k < V; ++k) v[r][j][k] = 0.f;
-        }
+        const int i = threadIdx.x + j * 256;
+        const int y = min(max(y0 + r, 0), t.H - 1);
+        const int x = min(max(ti.x0 - 1 + i / t.chunks, 0), t.W - 1);
+        raw[r][j].load(src + ((ti.b * t.H + y) * t.W + x) * t.C + cc);
       }
   }
-  __device__ __forceinline__ void store(float* ring, const DwTile& t, const TileIdx& ti, int y0, int nr,
-                                        int chunk) const {
+  template <bool PRO>
+  __device__ __forceinline__ void store(float* ring, const DwTile& t, const TileIdx& ti, int y0, int nr, int chunk,
+                                        bool cok, const float* s, const float* h, int act) const {
     const int n = (ti.tw + 2) * t.chunks;
 #pragma unroll
     for (int r = 0; r < DW_R; ++r) {
       if (r >= nr) break;
-      float* slot = ring + (size_t)ring_slot(y0 + r) * (t.TW + 2) * t.PP;
+      const int y = y0 + r;
+      float* slot = ring + (size_t)ring_slot(y) * (t.TW + 2) * t.PP;
 #pragma unroll
       for (int j = 0; j < LDQ; ++j) {
         const int i = threadIdx.x + j * 256;
         if (i < n) {
+          const int x = ti.x0 - 1 + i / t.chunks;
+          const bool ok = cok && y >= 0 && y < t.H && x >= 0 && x < t.W;
+          float v[V];
+          raw[r][j].unpack(v);
+#pragma unroll
+          for (int k = 0; k < V; ++k) {
+            if constexpr (PRO) v[k] = act_fwd(act, fmaf(v[k], s[k], h[k]));
+            v[k] = ok ? v[k] : 0.f;
+          }
           float* d = slot + (i / t.chunks) * t.PP + chunk * V;
 #pragma unroll
           for (int k = 0; k < V; k += 4)
-            *reinterpret_cast<float4*>(d + k) = make_float4(v[r][j][k], v[r][j][k + 1], v[r][j][k + 2], v[r][j][k + 3]);
+            *reinterpret_cast<float4*>(d + k) = make_float4(v[k], v[k + 1], v[k + 2], v[k + 3]);
         }
       }
     }
@@ -227,26 +249,31 @@ __device__ __forceinline__ void dw_reduce_store(A (&q)[NQ][V], float* lds_raw, i
 }
 
 // The shared row walk: ring <- rows -1, 0; regs <- rows 1..R; per step: store regs (rows y+1..y+R),
-// prefetch rows y+R+1..y+2R, compute output rows y..y+R-1 through body(y_row, px, it).
-template <typename T, int V, int LDQ, bool PRO, typename Body>
+// pre(y, px) issues the body's own per-pixel loads for output rows y..y+R-1, then the prefetch of
+// rows y+R+1..y+2R is issued (always: past the image it re-reads a clamped row), then output rows
+// y..y+R-1 are computed through body(r, y+r, px), one item (pixel, V channels) per thread and row.
+// Issue order = retire order, so the body waits for its own loads only; the prefetch stays in flight.
+template <typename T, int V, int LDQ, bool PRO, typename Pre, typename Body>
 __device__ __forceinline__ void dw_walk(float* ring, const T* __restrict__ src, const DwTile& t, const TileIdx& ti,
-                                        int c, int chunk, bool cok, const float* s, const float* h, int act,
+                                        int cc, int chunk, bool cok, const float* s, const float* h, int act, Pre&& pre,
                                         Body&& body) {
-  RowPipe<T, V, LDQ, PRO> rp;
-  rp.load(src, t, ti, -1, 2, c, cok, s, h, act);
-  rp.store(ring, t, ti, -1, 2, chunk);
-  rp.load(src, t, ti, 1, DW_R, c, cok, s, h, act);
-  const int nitems = ti.tw * t.chunks;
+  RowPipe<T, V, LDQ> rp;
+  rp.template load<2>(src, t, ti, -1, cc);
+  rp.template store<PRO>(ring, t, ti, -1, 2, chunk, cok, s, h, act);
+  rp.template load<DW_R>(src, t, ti, 1, cc);
+  const int nitems = ti.tw * t.chunks;  // <= 256 (dw_tile_plan)
+  const bool item = cok && (int)threadIdx.x < nitems;
+  const int px = min((int)threadIdx.x, nitems - 1) / t.chunks;
   for (int y = 0; y < t.H; y += DW_R) {
-    rp.store(ring, t, ti, y + 1, DW_R, chunk);
+    rp.template store<PRO>(ring, t, ti, y + 1, DW_R, chunk, cok, s, h, act);
     __syncthreads();
-    if (y + DW_R < t.H) rp.load(src, t, ti, y + DW_R + 1, DW_R, c, cok, s, h, act);
-    if (cok) {
+    pre(y, px);
+    rp.template load<DW_R>(src, t, ti, y + DW_R + 1, cc);
+    if (item) {
 #pragma unroll
       for (int r = 0; r < DW_R; ++r) {
-        const int yy = y + r;
-        if (yy >= t.H) break;
-        for (int it = threadIdx.x; it < nitems; it += 256) body(yy, it / t.chunks);
+        if (y + r >= t.H) break;
+        body(r, y + r, px);
       }
     }
     __syncthreads();
@@ -277,7 +304,8 @@ __global__ __launch_bounds__(256) void dw_fwd_tile_kernel(const T* __restrict__ 
   double q[2][V];  // BN batch statistics in fp64
 #pragma unroll
   for (int i = 0; i < V; ++i) { q[0][i] = 0.0; q[1][i] = 0.0; }
-  dw_walk<T, V, LDQ, true>(ring, e, t, ti, c, chunk, cok, s, h, act, [&](int y, int px) {
+  const int cc = cok ? c : 0;
+  dw_walk<T, V, LDQ, true>(ring, e, t, ti, cc, chunk, cok, s, h, act, [&](int, int) {}, [&](int, int y, int px) {
     float acc[V];
 #pragma unroll
     for (int i = 0; i < V; ++i) acc[i] = 0.f;
@@ -335,10 +363,16 @@ __global__ __launch_bounds__(256) void dw_dgrad_tile_kernel(const T* __restrict_
   float q[2][V];
 #pragma unroll
   for (int i = 0; i < V; ++i) { q[0][i] = 0.f; q[1][i] = 0.f; }
-  dw_walk<T, V, LDQ, false>(ring, dd, t, ti, c, chunk, cok, s, h, 0, [&](int y, int px) {
+  const int cc = cok ? c : 0;
+  RawVec<T, V> ce[DW_R];  // e at this thread's output pixel of the current rows
+  auto pre = [&](int y, int px) {
+#pragma unroll
+    for (int r = 0; r < DW_R; ++r) ce[r].load(e + ((ti.b * t.H + min(y + r, t.H - 1)) * t.W + ti.x0 + px) * t.C + cc);
+  };
+  dw_walk<T, V, LDQ, false>(ring, dd, t, ti, cc, chunk, cok, s, h, 0, pre, [&](int r, int y, int px) {
     const long off = ((ti.b * t.H + y) * t.W + ti.x0 + px) * t.C + c;
     float ev[V];
-    load_vec<T, V>(e + off, ev);
+    ce[r].unpack(ev);
     float acc[V];
 #pragma unroll
     for (int i = 0; i < V; ++i) acc[i] = 0.f;
@@ -391,9 +425,15 @@ __global__ __launch_bounds__(256) void dw_wgrad_tile_kernel(const T* __restrict_
   for (int k = 0; k < 9; ++k)
 #pragma unroll
     for (int i = 0; i < V; ++i) q[k][i] = 0.f;
-  dw_walk<T, V, LDQ, true>(ring, e, t, ti, c, chunk, cok, s, h, act, [&](int y, int px) {
+  const int cc = cok ? c : 0;
+  RawVec<T, V> cg[DW_R];  // dd at this thread's output pixel of the current rows
+  auto pre = [&](int y, int px) {
+#pragma unroll
+    for (int r = 0; r < DW_R; ++r) cg[r].load(dd + ((ti.b * t.H + min(y + r, t.H - 1)) * t.W + ti.x0 + px) * t.C + cc);
+  };
+  dw_walk<T, V, LDQ, true>(ring, e, t, ti, cc, chunk, cok, s, h, act, pre, [&](int r, int y, int px) {
     float g[V];
-    load_vec<T, V>(dd + ((ti.b * t.H + y) * t.W + ti.x0 + px) * t.C + c, g);
+    cg[r].unpack(g);
 #pragma unroll
     for (int ki = 0; ki < 3; ++ki)
 #pragma unroll

@@ -113,9 +113,9 @@ class MBConv(nn.Module):
             buffers = {"bn1_rm": bn1.running_mean, "bn1_rv": bn1.running_var, "bn2_rm": bn2.running_mean,
                        "bn2_rv": bn2.running_var, "bn3_rm": bn3.running_mean, "bn3_rv": bn3.running_var}
             train = bn1.training
-            if train:
-                for b in (bn1, bn2, bn3):
-                    b.num_batches_tracked.add_(1)
+            if train:  # one multi-tensor launch for the three BN counters
+                torch._foreach_add_([bn1.num_batches_tracked, bn2.num_batches_tracked,
+                                     bn3.num_batches_tracked], 1)
             return OF.mbconv_fused(x, B, H, W, e.out_channels, self.se.fc1.out_channels, train, bn1.eps,
                                    bn1.momentum, act_name(self.expand[2]), params, buffers)
         # the stock-op parts (BN, depthwise, SE) follow the activation dtype even outside autocast

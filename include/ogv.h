@@ -40,7 +40,9 @@ const char* ogv_version(void);
 const char* ogv_last_error(void);
 /* Tuning switch (no reference counterpart; process-wide, set before capture):
  *   "sgemm" 1 (default) / 0: persistent streaming kernels (projection fwd/dgrad and weight gradient)
- *   for tall-skinny bf16 shapes on/off;  "sgemm_min_m" (default 65536): smallest M routed to them.
+ *   for tall-skinny bf16 shapes on/off;  "sgemm_min_m" (default 65536): smallest M routed to them;
+ *   "bk64_max_m": largest M using 64-wide k-steps in the tiled GEMM; "grid_mfma" 1/0: MFMA grid
+ *   attention for bf16; "dw_blocks" (default 768): target block count of the depthwise kernels.
  * Returns OGV_ERR_ARG for an unknown name. */
 int ogv_set_option(const char* name, int value);
 /* Diagnostics (no reference counterpart): 1 if ogv_gemm_fwd (kind 0) / ogv_gemm_dgrad (kind 1) of

@@ -163,5 +163,6 @@ int sgemm_min_m();
 void set_sgemm_min_m(int v);
 void set_bk64_max_m(int v);
 void set_grid_mfma(int v);
+void set_dw_blocks(int v);
 
 }  // namespace ogv

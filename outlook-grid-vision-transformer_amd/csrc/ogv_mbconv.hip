@@ -92,19 +92,27 @@ void bn_coeffs_launch(const float* S, int K, float n, const float* gamma, const 
 
 // ------------------------------------------------------------------ depthwise conv with BN fusion
 // ---- row-streaming depthwise kernels -------------------------------------------------------
-// Block = (image b, column strip of TW <= 32 pixels, channel tile of CT = chunks*V channels), XCD-aware
-// order with the channel tile fastest.  The block walks down the image DW_R output rows per step:
-// a (DW_R+2)-row ring in LDS holds input rows y-1 .. y+DW_R (TW+2 pixels with the column halo, zero
-// outside the image, the producer's BatchNorm + activation applied once per element as it is
-// staged) and the next DW_R rows are loaded into registers while the current ones are computed, so
-// every input element is read from HBM once and ~DW_R rows per block are in flight.  chunks is
-// chosen so that one output row is ~256 (pixel, V-channel chunk) items: one per thread per row.
-// Statistics / weight-gradient partials are reduced once per block into row rid = b*ncolt + colt
-// of a [rows][Q][C] slab.
+// Block = (group of G images, column strip of TW <= 32 pixels, channel tile of CT = chunks*V
+// channels), XCD-aware order with the channel tile fastest.  The block walks its images stacked into
+// one tall strip of "virtual rows" (H rows per image plus one zero row between images, so the 3x3
+// halo never mixes images), DW_R output rows per step: a (DW_R+2)-row ring in LDS holds input rows
+// u-1 .. u+DW_R (TW+2 pixels with the column halo, zero outside the image, the producer's BatchNorm
+// + activation applied once per element as it is staged) and the next DW_R rows are loaded into
+// registers while the current ones are computed, so every input element is read from HBM once,
+// ~DW_R rows per block are in flight, and the pipeline runs on across image seams (one prologue and
+// one weight load per block, G chosen for ~one wave of resident blocks).  chunks is chosen so that
+// one output row is ~256 (pixel, V-channel chunk) items: one per thread per row.  Statistics /
+// weight-gradient partials are reduced once per block into row rid = group*ncolt + colt of a
+// [rows][Q][C] slab.
 constexpr int DW_R = 4;
+// tuning knob "dw_blocks": > 0 = target block count of the depthwise kernels; 0 (default) = images
+// per block chosen for ~32 output rows per block (many short blocks balance best over the CUs)
+static int g_dw_blocks = 0;
+void set_dw_blocks(int v) { g_dw_blocks = v > 0 ? v : 0; }
 struct DwTile {
-  int B, H, W, C, TW, ncolt, chunks, CT, nct, PP, ldq;
-  __host__ __device__ long rows() const { return (long)B * ncolt; }
+  int B, H, W, C, TW, ncolt, chunks, CT, nct, PP, ldq, G, ngroups;
+  __host__ __device__ long rows() const { return (long)ngroups * ncolt; }
+  long rows_max() const { return (long)B * ncolt; }  // workspace sizing: any G
   __host__ __device__ long nblocks() const { return rows() * nct; }
   size_t ring_bytes() const { return (size_t)(DW_R + 2) * (TW + 2) * PP * sizeof(float); }
   size_t lds_bytes(int nq, int V, size_t asz) const {
@@ -123,26 +131,57 @@ static DwTile dw_tile_plan(int B, int H, int W, int C, int V) {
   t.chunks = ch;
   t.CT = ch * V;
   t.nct = (C + t.CT - 1) / t.CT;
-  t.PP = t.CT + 4;
+  t.PP = t.CT;  // unpadded: conflict-free ds_read_b128 lane groups for the tap reads (chunks >= 8)
   t.ldq = ((t.TW + 2) * ch + 255) / 256;                      // row-load items per thread (<= 3)
+  long G;
+  if (g_dw_blocks > 0) {
+    const long tiles = (long)B * t.ncolt * t.nct;
+    G = (tiles + g_dw_blocks - 1) / g_dw_blocks;
+  } else {
+    G = 32 / H;
+  }
+  G = G < 1 ? 1 : (G > B ? B : G);
+  t.G = (int)G;
+  t.ngroups = (int)((B + G - 1) / G);
   return t;
 }
 static unsigned dw_grid(const DwTile& t) { return xcd_grid(t.nblocks()); }
 
 struct TileIdx {
-  int ct, colt, x0, tw;
-  long b, rid;
+  int ct, colt, x0, tw, nimg;
+  long b0, rid;
 };
 __device__ __forceinline__ bool tile_idx(const DwTile& t, TileIdx& i) {
   long id;
   if (!xcd_block(t.nblocks(), id)) return false;
   i.ct = (int)(id % t.nct); id /= t.nct;
   i.colt = (int)(id % t.ncolt);
-  i.b = id / t.ncolt;
-  i.rid = i.b * t.ncolt + i.colt;
+  const long g = id / t.ncolt;
+  i.rid = g * t.ncolt + i.colt;
+  i.b0 = g * t.G;
+  i.nimg = (int)(t.B - i.b0 < t.G ? t.B - i.b0 : t.G);
   i.x0 = i.colt * t.TW;
   i.tw = t.W - i.x0 < t.TW ? t.W - i.x0 : t.TW;
   return true;
+}
+// virtual row u (>= -1) = (image im of the block's group, row y); y == H is the zero seam row.
+// Walked one row at a time (no division).
+struct VRow {
+  int u, im, y;
+};
+__device__ __forceinline__ VRow vnext(const DwTile& t, VRow p) {
+  ++p.u;
+  if (++p.y > t.H) {
+    p.y = 0;
+    ++p.im;
+  }
+  return p;
+}
+template <int K>
+__device__ __forceinline__ VRow vadv(const DwTile& t, VRow p) {
+#pragma unroll
+  for (int k = 0; k < K; ++k) p = vnext(t, p);
+  return p;
 }
 
 __device__ __forceinline__ int ring_slot(int r) { return (r + DW_R + 2) % (DW_R + 2); }
@@ -175,37 +214,40 @@ template <typename T, int V, int LDQ>
 struct RowPipe {
   RawVec<T, V> raw[DW_R][LDQ];
   template <int NR>
-  __device__ __forceinline__ void load(const T* __restrict__ src, const DwTile& t, const TileIdx& ti, int y0, int cc) {
+  __device__ __forceinline__ void load(const T* __restrict__ src, const DwTile& t, const TileIdx& ti, VRow p, int cc) {
 #pragma unroll
-    for (int r = 0; r < NR; ++r)
+    for (int r = 0; r < NR; ++r) {
+      const long b = ti.b0 + min(max(p.im, 0), ti.nimg - 1);
+      const int y = min(p.y, t.H - 1);
 #pragma unroll
       for (int j = 0; j < LDQ; ++j) {
         const int i = threadIdx.x + j * 256;
-        const int y = min(max(y0 + r, 0), t.H - 1);
         const int x = min(max(ti.x0 - 1 + i / t.chunks, 0), t.W - 1);
-        raw[r][j].load(src + ((ti.b * t.H + y) * t.W + x) * t.C + cc);
+        raw[r][j].load(src + ((b * t.H + y) * t.W + x) * t.C + cc);
       }
+      p = vnext(t, p);
+    }
   }
-  template <bool PRO>
-  __device__ __forceinline__ void store(float* ring, const DwTile& t, const TileIdx& ti, int y0, int nr, int chunk,
-                                        bool cok, const float* s, const float* h, int act) const {
+  template <bool PRO, int ACT>
+  __device__ __forceinline__ void store(float* ring, const DwTile& t, const TileIdx& ti, VRow p, int nr, int chunk,
+                                        bool cok, const float* s, const float* h) const {
     const int n = (ti.tw + 2) * t.chunks;
 #pragma unroll
-    for (int r = 0; r < DW_R; ++r) {
+    for (int r = 0; r < DW_R; ++r, p = vnext(t, p)) {
       if (r >= nr) break;
-      const int y = y0 + r;
-      float* slot = ring + (size_t)ring_slot(y) * (t.TW + 2) * t.PP;
+      const bool rok = cok && p.im >= 0 && p.im < ti.nimg && p.y < t.H;
+      float* slot = ring + (size_t)ring_slot(p.u) * (t.TW + 2) * t.PP;
 #pragma unroll
       for (int j = 0; j < LDQ; ++j) {
         const int i = threadIdx.x + j * 256;
         if (i < n) {
           const int x = ti.x0 - 1 + i / t.chunks;
-          const bool ok = cok && y >= 0 && y < t.H && x >= 0 && x < t.W;
+          const bool ok = rok && x >= 0 && x < t.W;
           float v[V];
           raw[r][j].unpack(v);
 #pragma unroll
           for (int k = 0; k < V; ++k) {
-            if constexpr (PRO) v[k] = act_fwd(act, fmaf(v[k], s[k], h[k]));
+            if constexpr (PRO) v[k] = act_fwd(ACT, fmaf(v[k], s[k], h[k]));
             v[k] = ok ? v[k] : 0.f;
           }
           float* d = slot + (i / t.chunks) * t.PP + chunk * V;
@@ -248,40 +290,50 @@ __device__ __forceinline__ void dw_reduce_store(A (&q)[NQ][V], float* lds_raw, i
   }
 }
 
-// The shared row walk: ring <- rows -1, 0; regs <- rows 1..R; per step: store regs (rows y+1..y+R),
-// pre(y, px) issues the body's own per-pixel loads for output rows y..y+R-1, then the prefetch of
-// rows y+R+1..y+2R is issued (always: past the image it re-reads a clamped row), then output rows
-// y..y+R-1 are computed through body(r, y+r, px), one item (pixel, V channels) per thread and row.
-// Issue order = retire order, so the body waits for its own loads only; the prefetch stays in flight.
-template <typename T, int V, int LDQ, bool PRO, typename Pre, typename Body>
+// The shared row walk over the block's virtual rows: ring <- rows -1, 0; regs <- rows 1..R; per
+// step: store regs (rows u+1..u+R), pre(u, px) issues the body's own per-pixel loads for output rows
+// u..u+R-1, then the prefetch of rows u+R+1..u+2R is issued (always: past the end it re-reads a
+// clamped row), then the output rows among u..u+R-1 (not seam rows) are computed through
+// body(r, u+r, image, y, px), one item (pixel, V channels) per thread and row.  Issue order = retire
+// order, so the body waits for its own loads only while the prefetch stays in flight.
+template <typename T, int V, int LDQ, bool PRO, int ACT, typename Pre, typename Body>
 __device__ __forceinline__ void dw_walk(float* ring, const T* __restrict__ src, const DwTile& t, const TileIdx& ti,
-                                        int cc, int chunk, bool cok, const float* s, const float* h, int act, Pre&& pre,
+                                        int cc, int chunk, bool cok, const float* s, const float* h, Pre&& pre,
                                         Body&& body) {
   RowPipe<T, V, LDQ> rp;
-  rp.template load<2>(src, t, ti, -1, cc);
-  rp.template store<PRO>(ring, t, ti, -1, 2, chunk, cok, s, h, act);
-  rp.template load<DW_R>(src, t, ti, 1, cc);
+  VRow p = {-1, -1, t.H};
+  rp.template load<2>(src, t, ti, p, cc);
+  rp.template store<PRO, ACT>(ring, t, ti, p, 2, chunk, cok, s, h);
+  rp.template load<DW_R>(src, t, ti, vadv<2>(t, p), cc);
   const int nitems = ti.tw * t.chunks;  // <= 256 (dw_tile_plan)
   const bool item = cok && (int)threadIdx.x < nitems;
   const int px = min((int)threadIdx.x, nitems - 1) / t.chunks;
-  for (int y = 0; y < t.H; y += DW_R) {
-    rp.template store<PRO>(ring, t, ti, y + 1, DW_R, chunk, cok, s, h, act);
+  const int nv = ti.nimg * (t.H + 1) - 1;  // virtual rows incl. the seams between images
+  for (p = vnext(t, p); p.u < nv; p = vadv<DW_R>(t, p)) {
+    rp.template store<PRO, ACT>(ring, t, ti, vnext(t, p), DW_R, chunk, cok, s, h);
     __syncthreads();
-    pre(y, px);
-    rp.template load<DW_R>(src, t, ti, y + DW_R + 1, cc);
+    pre(p, px);
+    rp.template load<DW_R>(src, t, ti, vadv<DW_R + 1>(t, p), cc);
     if (item) {
+      VRow q = p;
 #pragma unroll
-      for (int r = 0; r < DW_R; ++r) {
-        if (y + r >= t.H) break;
-        body(r, y + r, px);
-      }
+      for (int r = 0; r < DW_R; ++r, q = vnext(t, q))
+        if (q.u < nv && q.y < t.H) body(r, q.u, ti.b0 + q.im, q.y, px);
     }
     __syncthreads();
   }
 }
+// pre-load helper: V elements of src at this thread's pixel of virtual row u (clamped into the tensor)
+template <typename T, int V>
+__device__ __forceinline__ void dw_pixel_load(RawVec<T, V>& rv, const T* __restrict__ src, const DwTile& t,
+                                              const TileIdx& ti, VRow q, int px, int cc) {
+  const long b = ti.b0 + min(q.im, ti.nimg - 1);
+  const int y = min(q.y, t.H - 1);
+  rv.load(src + ((b * t.H + y) * t.W + ti.x0 + px) * t.C + cc);
+}
 
 // d = dw3x3(act(e*sc1 + sh1)) (+ fp64 stats of the rounded output minus shift)
-template <typename T, int V, int LDQ>
+template <typename T, int V, int LDQ, int ACT>
 __global__ __launch_bounds__(256) void dw_fwd_tile_kernel(const T* __restrict__ e, const float* __restrict__ wdw,
                                                           const float* __restrict__ sc, const float* __restrict__ sh,
                                                           int act, T* __restrict__ out, double* __restrict__ stat,
@@ -301,11 +353,12 @@ __global__ __launch_bounds__(256) void dw_fwd_tile_kernel(const T* __restrict__ 
     h[i] = cok ? sh[c + i] : 0.f;
     sft[i] = (cok && shift) ? shift[c + i] : 0.f;
   }
-  double q[2][V];  // BN batch statistics in fp64
+  float q[2][V];  // BN batch statistics: fp32 per thread (<= G*H shifted terms), fp64 across threads
 #pragma unroll
-  for (int i = 0; i < V; ++i) { q[0][i] = 0.0; q[1][i] = 0.0; }
+  for (int i = 0; i < V; ++i) { q[0][i] = 0.f; q[1][i] = 0.f; }
   const int cc = cok ? c : 0;
-  dw_walk<T, V, LDQ, true>(ring, e, t, ti, cc, chunk, cok, s, h, act, [&](int, int) {}, [&](int, int y, int px) {
+  dw_walk<T, V, LDQ, true, ACT>(ring, e, t, ti, cc, chunk, cok, s, h, [&](VRow, int) {},
+                           [&](int, int u, long b, int y, int px) {
     float acc[V];
 #pragma unroll
     for (int i = 0; i < V; ++i) acc[i] = 0.f;
@@ -313,7 +366,7 @@ __global__ __launch_bounds__(256) void dw_fwd_tile_kernel(const T* __restrict__ 
     for (int ki = 0; ki < 3; ++ki)
 #pragma unroll
       for (int kj = 0; kj < 3; ++kj) {
-        const float* src = ring_px(ring, t, y - 1 + ki, px + kj) + chunk * V;
+        const float* src = ring_px(ring, t, u - 1 + ki, px + kj) + chunk * V;
 #pragma unroll
         for (int i = 0; i < V; i += 4) {
           const float4 a = *reinterpret_cast<const float4*>(src + i);
@@ -327,17 +380,22 @@ __global__ __launch_bounds__(256) void dw_fwd_tile_kernel(const T* __restrict__ 
 #pragma unroll
     for (int i = 0; i < V; ++i) {
       of[i] = to_f(from_f<T>(acc[i]));
-      const double dl = (double)of[i] - (double)sft[i];
+      const float dl = of[i] - sft[i];
       q[0][i] += dl;
-      q[1][i] = fma(dl, dl, q[1][i]);
+      q[1][i] = fmaf(dl, dl, q[1][i]);
     }
-    store_vec<T, V>(out + ((ti.b * t.H + y) * t.W + ti.x0 + px) * t.C + c, of);
+    store_vec<T, V>(out + ((b * t.H + y) * t.W + ti.x0 + px) * t.C + c, of);
   });
-  if (stat) dw_reduce_store<2, V, double>(q, ring, t.chunks, stat + ti.rid * 2 * t.C, t.C, t.C, ti.ct * t.CT);
+  if (stat) {
+    double qd[2][V];
+#pragma unroll
+    for (int i = 0; i < V; ++i) { qd[0][i] = q[0][i]; qd[1][i] = q[1][i]; }
+    dw_reduce_store<2, V, double>(qd, ring, t.chunks, stat + ti.rid * 2 * t.C, t.C, t.C, ti.ct * t.CT);
+  }
 }
 
 // dy1 = (dw3x3^T dd) * act'(e*sc1 + sh1) -> out; stats: sum dy1, sum dy1*(e - mean1)*invstd1
-template <typename T, int V, int LDQ>
+template <typename T, int V, int LDQ, int ACT>
 __global__ __launch_bounds__(256) void dw_dgrad_tile_kernel(const T* __restrict__ dd, const float* __restrict__ wdw,
                                                             const T* __restrict__ e, const float* __restrict__ sc,
                                                             const float* __restrict__ sh,
@@ -365,12 +423,12 @@ __global__ __launch_bounds__(256) void dw_dgrad_tile_kernel(const T* __restrict_
   for (int i = 0; i < V; ++i) { q[0][i] = 0.f; q[1][i] = 0.f; }
   const int cc = cok ? c : 0;
   RawVec<T, V> ce[DW_R];  // e at this thread's output pixel of the current rows
-  auto pre = [&](int y, int px) {
+  auto pre = [&](VRow q, int px) {
 #pragma unroll
-    for (int r = 0; r < DW_R; ++r) ce[r].load(e + ((ti.b * t.H + min(y + r, t.H - 1)) * t.W + ti.x0 + px) * t.C + cc);
+    for (int r = 0; r < DW_R; ++r, q = vnext(t, q)) dw_pixel_load(ce[r], e, t, ti, q, px, cc);
   };
-  dw_walk<T, V, LDQ, false>(ring, dd, t, ti, cc, chunk, cok, s, h, 0, pre, [&](int r, int y, int px) {
-    const long off = ((ti.b * t.H + y) * t.W + ti.x0 + px) * t.C + c;
+  dw_walk<T, V, LDQ, false, OGV_ACT_NONE>(ring, dd, t, ti, cc, chunk, cok, s, h, pre, [&](int r, int u, long b, int y, int px) {
+    const long off = ((b * t.H + y) * t.W + ti.x0 + px) * t.C + c;
     float ev[V];
     ce[r].unpack(ev);
     float acc[V];
@@ -381,7 +439,7 @@ __global__ __launch_bounds__(256) void dw_dgrad_tile_kernel(const T* __restrict_
 #pragma unroll
       for (int kj = 0; kj < 3; ++kj) {
         // transposed conv: dd row y+1-ki, column x+1-kj  (ring pixel px + 2 - kj)
-        const float* src = ring_px(ring, t, y + 1 - ki, px + 2 - kj) + chunk * V;
+        const float* src = ring_px(ring, t, u + 1 - ki, px + 2 - kj) + chunk * V;
 #pragma unroll
         for (int i = 0; i < V; i += 4) {
           const float4 a = *reinterpret_cast<const float4*>(src + i);
@@ -394,7 +452,7 @@ __global__ __launch_bounds__(256) void dw_dgrad_tile_kernel(const T* __restrict_
     float o2[V];
 #pragma unroll
     for (int i = 0; i < V; ++i) {
-      o2[i] = to_f(from_f<T>(acc[i] * act_grad(act, fmaf(ev[i], s[i], h[i]))));
+      o2[i] = to_f(from_f<T>(acc[i] * act_grad(ACT, fmaf(ev[i], s[i], h[i]))));
       q[0][i] += o2[i];
       q[1][i] = fmaf(o2[i], (ev[i] - mu[i]) * is[i], q[1][i]);
     }
@@ -404,7 +462,7 @@ __global__ __launch_bounds__(256) void dw_dgrad_tile_kernel(const T* __restrict_
 }
 
 // dWdw partials: part[rid][tap][c] = sum over the block's pixels dd[p,c] * act(e*sc1+sh1)[p+tap, c]
-template <typename T, int V, int LDQ>
+template <typename T, int V, int LDQ, int ACT>
 __global__ __launch_bounds__(256) void dw_wgrad_tile_kernel(const T* __restrict__ dd, const T* __restrict__ e,
                                                             const float* __restrict__ sc, const float* __restrict__ sh,
                                                             int act, float* __restrict__ part, DwTile t) {
@@ -427,18 +485,18 @@ __global__ __launch_bounds__(256) void dw_wgrad_tile_kernel(const T* __restrict_
     for (int i = 0; i < V; ++i) q[k][i] = 0.f;
   const int cc = cok ? c : 0;
   RawVec<T, V> cg[DW_R];  // dd at this thread's output pixel of the current rows
-  auto pre = [&](int y, int px) {
+  auto pre = [&](VRow q, int px) {
 #pragma unroll
-    for (int r = 0; r < DW_R; ++r) cg[r].load(dd + ((ti.b * t.H + min(y + r, t.H - 1)) * t.W + ti.x0 + px) * t.C + cc);
+    for (int r = 0; r < DW_R; ++r, q = vnext(t, q)) dw_pixel_load(cg[r], dd, t, ti, q, px, cc);
   };
-  dw_walk<T, V, LDQ, true>(ring, e, t, ti, cc, chunk, cok, s, h, act, pre, [&](int r, int y, int px) {
+  dw_walk<T, V, LDQ, true, ACT>(ring, e, t, ti, cc, chunk, cok, s, h, pre, [&](int r, int u, long, int, int px) {
     float g[V];
     cg[r].unpack(g);
 #pragma unroll
     for (int ki = 0; ki < 3; ++ki)
 #pragma unroll
       for (int kj = 0; kj < 3; ++kj) {
-        const float* src = ring_px(ring, t, y - 1 + ki, px + kj) + chunk * V;
+        const float* src = ring_px(ring, t, u - 1 + ki, px + kj) + chunk * V;
 #pragma unroll
         for (int i = 0; i < V; i += 4) {
           const float4 a = *reinterpret_cast<const float4*>(src + i);
@@ -753,7 +811,7 @@ static FwdWs fwd_ws_layout(void* base, const ogv_mbconv_desc& s, size_t* total) 
   Buf b(base);
   const long M = (long)s.B * s.H * s.W;
   RowPlan rp = row_plan(s.mid);
-  const long S2 = dw_tile_plan(s.B, s.H, s.W, s.mid, 4).rows();
+  const long S2 = dw_tile_plan(s.B, s.H, s.W, s.mid, 4).rows_max();
   const long R1 = gemm_stat_rows((int)M);
   FwdWs w;
   w.stat1 = b.take<double>(R1 * 2 * s.mid);
@@ -779,7 +837,7 @@ static BwdWs bwd_ws_layout(void* base, const ogv_mbconv_desc& s, size_t esz, siz
   Buf b(base);
   const long M = (long)s.B * s.H * s.W;
   RowPlan rp = row_plan(s.mid), rc = row_plan(s.C);
-  const long S2 = dw_tile_plan(s.B, s.H, s.W, s.mid, 4).rows(), S3 = dw_slices(M, rc);
+  const long S2 = dw_tile_plan(s.B, s.H, s.W, s.mid, 4).rows_max(), S3 = dw_slices(M, rc);
   const long K2 = s.mid > s.C ? s.mid : s.C;
   BwdWs w;
   w.dp = b.take<char>(M * s.C * esz);
@@ -825,43 +883,49 @@ static BwdWs bwd_ws_layout(void* base, const ogv_mbconv_desc& s, size_t esz, siz
 
 template <typename T>
 struct Ops {
-  template <int V>
+  // runtime activation -> compile-time ACT (the staging / derivative code is then branch-free)
+#define OGV_DW_ACT(act, ...)                                   \
+  switch (act) {                                               \
+    case OGV_ACT_GELU: { constexpr int A = OGV_ACT_GELU; __VA_ARGS__; } break; \
+    case OGV_ACT_SILU: { constexpr int A = OGV_ACT_SILU; __VA_ARGS__; } break; \
+    case OGV_ACT_RELU: { constexpr int A = OGV_ACT_RELU; __VA_ARGS__; } break; \
+    default: { constexpr int A = OGV_ACT_NONE; __VA_ARGS__; } break;           \
+  }
   static void dw_fwd(const void* e, const float* w, const float* sc, const float* sh, int act, void* out, double* stat,
                      const float* shift, const DwTile& t, hipStream_t st) {
+    constexpr int V = 4;
     const size_t lds = t.lds_bytes(2, V, sizeof(double));
-    if (t.ldq <= 1)
-      dw_fwd_tile_kernel<T, V, 1><<<dw_grid(t), 256, lds, st>>>((const T*)e, w, sc, sh, act, (T*)out, stat, shift, t);
-    else if (t.ldq <= 2)
-      dw_fwd_tile_kernel<T, V, 2><<<dw_grid(t), 256, lds, st>>>((const T*)e, w, sc, sh, act, (T*)out, stat, shift, t);
-    else
-      dw_fwd_tile_kernel<T, V, 3><<<dw_grid(t), 256, lds, st>>>((const T*)e, w, sc, sh, act, (T*)out, stat, shift, t);
+    OGV_DW_ACT(act, if (t.ldq <= 1) dw_fwd_tile_kernel<T, V, 1, A><<<dw_grid(t), 256, lds, st>>>(
+                        (const T*)e, w, sc, sh, act, (T*)out, stat, shift, t);
+               else if (t.ldq <= 2) dw_fwd_tile_kernel<T, V, 2, A><<<dw_grid(t), 256, lds, st>>>(
+                        (const T*)e, w, sc, sh, act, (T*)out, stat, shift, t);
+               else dw_fwd_tile_kernel<T, V, 3, A><<<dw_grid(t), 256, lds, st>>>(
+                        (const T*)e, w, sc, sh, act, (T*)out, stat, shift, t))
   }
-  template <int V>
   static void dw_dgrad(const void* dd, const float* w, const void* e, const float* sc, const float* sh,
                        const float* mean, const float* inv, int act, void* out, float* stat, const DwTile& t,
                        hipStream_t st) {
+    constexpr int V = 4;
     const size_t lds = t.lds_bytes(2, V, sizeof(float));
-    if (t.ldq <= 1)
-      dw_dgrad_tile_kernel<T, V, 1><<<dw_grid(t), 256, lds, st>>>((const T*)dd, w, (const T*)e, sc, sh, mean, inv, act,
-                                                                  (T*)out, stat, t);
-    else if (t.ldq <= 2)
-      dw_dgrad_tile_kernel<T, V, 2><<<dw_grid(t), 256, lds, st>>>((const T*)dd, w, (const T*)e, sc, sh, mean, inv, act,
-                                                                  (T*)out, stat, t);
-    else
-      dw_dgrad_tile_kernel<T, V, 3><<<dw_grid(t), 256, lds, st>>>((const T*)dd, w, (const T*)e, sc, sh, mean, inv, act,
-                                                                  (T*)out, stat, t);
+    OGV_DW_ACT(act, if (t.ldq <= 1) dw_dgrad_tile_kernel<T, V, 1, A><<<dw_grid(t), 256, lds, st>>>(
+                        (const T*)dd, w, (const T*)e, sc, sh, mean, inv, act, (T*)out, stat, t);
+               else if (t.ldq <= 2) dw_dgrad_tile_kernel<T, V, 2, A><<<dw_grid(t), 256, lds, st>>>(
+                        (const T*)dd, w, (const T*)e, sc, sh, mean, inv, act, (T*)out, stat, t);
+               else dw_dgrad_tile_kernel<T, V, 3, A><<<dw_grid(t), 256, lds, st>>>(
+                        (const T*)dd, w, (const T*)e, sc, sh, mean, inv, act, (T*)out, stat, t))
   }
-  template <int V>
   static void dw_wgrad(const void* dd, const void* e, const float* sc, const float* sh, int act, float* part,
                        const DwTile& t, hipStream_t st) {
+    constexpr int V = 4;
     const size_t lds = t.lds_bytes(9, V, sizeof(float));
-    if (t.ldq <= 1)
-      dw_wgrad_tile_kernel<T, V, 1><<<dw_grid(t), 256, lds, st>>>((const T*)dd, (const T*)e, sc, sh, act, part, t);
-    else if (t.ldq <= 2)
-      dw_wgrad_tile_kernel<T, V, 2><<<dw_grid(t), 256, lds, st>>>((const T*)dd, (const T*)e, sc, sh, act, part, t);
-    else
-      dw_wgrad_tile_kernel<T, V, 3><<<dw_grid(t), 256, lds, st>>>((const T*)dd, (const T*)e, sc, sh, act, part, t);
+    OGV_DW_ACT(act, if (t.ldq <= 1) dw_wgrad_tile_kernel<T, V, 1, A><<<dw_grid(t), 256, lds, st>>>(
+                        (const T*)dd, (const T*)e, sc, sh, act, part, t);
+               else if (t.ldq <= 2) dw_wgrad_tile_kernel<T, V, 2, A><<<dw_grid(t), 256, lds, st>>>(
+                        (const T*)dd, (const T*)e, sc, sh, act, part, t);
+               else dw_wgrad_tile_kernel<T, V, 3, A><<<dw_grid(t), 256, lds, st>>>(
+                        (const T*)dd, (const T*)e, sc, sh, act, part, t))
   }
+#undef OGV_DW_ACT
   template <int V>
   static void pool(const void* d, const float* sc, const float* sh, int act, float* pooled, int B, int HW, int K,
                    const RowPlan& rp, hipStream_t st) {
@@ -922,7 +986,7 @@ static void mbconv_fwd_impl(const void* x, void* out, const Saved& sv, const Fwd
   // 2) depthwise conv on act(BN1(e)) (+ BN2 stats)
   {
     const DwTile t = dw_tile_plan(s.B, s.H, s.W, s.mid, 4);
-    OGV_V84_DISPATCH(4, O::template dw_fwd, sv.e, P.w_dw, sv.sc1, sv.sh1, s.act, sv.d, tr ? w.stat2 : nullptr,
+    O::dw_fwd(sv.e, P.w_dw, sv.sc1, sv.sh1, s.act, sv.d, tr ? w.stat2 : nullptr,
                      tr ? P.bn2_rm : nullptr, t, st);
     if (tr) colreduce(w.stat2, w.sums, t.rows(), 2L * s.mid, 2L * s.mid, w.tmp, st);
     bn_finalize_kernel<<<cdiv(s.mid, 256), 256, 0, st>>>(w.sums, s.mid, (double)M, P.bn2_w, P.bn2_b, s.bn_eps,
@@ -1029,10 +1093,10 @@ static void mbconv_bwd_impl(const void* dout, const void* x, const Saved& sv, vo
   // B6) depthwise backward: dy1 = dgrad(dd) * act'(BN1(e)) -> bufA (+ BN1 sums); dWdw from (dd, act(BN1(e)))
   {
     const DwTile t = dw_tile_plan(s.B, s.H, s.W, s.mid, 4);
-    OGV_V84_DISPATCH(4, O::template dw_dgrad, w.bufB, P.w_dw, sv.e, sv.sc1, sv.sh1, sv.mean1, sv.inv1, s.act,
+    O::dw_dgrad(w.bufB, P.w_dw, sv.e, sv.sc1, sv.sh1, sv.mean1, sv.inv1, s.act,
                      w.bufA, w.stat, t, st);
     colreduce(w.stat, w.S, t.rows(), 2L * s.mid, 2L * s.mid, w.tmp, st);
-    OGV_V84_DISPATCH(4, O::template dw_wgrad, w.bufB, sv.e, sv.sc1, sv.sh1, s.act, w.part9, t, st);
+    O::dw_wgrad(w.bufB, sv.e, sv.sc1, sv.sh1, s.act, w.part9, t, st);
     colreduce(w.part9, w.sums9, t.rows(), 9L * s.mid, 9L * s.mid, w.tmp, st);
     tapmajor_to_chan_kernel<<<cdiv(9 * s.mid, 256), 256, 0, st>>>(w.sums9, G.w_dw, s.mid);
   }

@@ -470,3 +470,16 @@ def test_mbconv_fused_vs_unfused(C, H, B, train):
     br, bf = dict(ref.named_buffers()), dict(fused.named_buffers())
     for k in br:
         assert fx.maxabs(bf[k].float(), br[k].float()) <= 1e-4 * max(1, br[k].float().abs().max().item()), k
+
+
+@pytest.mark.parametrize("C,H,B", [(48, 32, 4), (96, 16, 3), (192, 8, 2), (256, 4, 5), (20, 6, 2)])
+def test_mbconv_fused_image_groups(C, H, B):
+    """Depthwise kernels walking several images per block (zero seam rows between them), with a
+    ragged last group: dw_blocks = 10 gives 2-4 images per block at these shapes."""
+    from ogv._lib import load
+    lib = load()
+    assert lib.ogv_set_option(b"dw_blocks", 10) == 0
+    try:
+        test_mbconv_fused_vs_unfused(C, H, B, True)
+    finally:
+        assert lib.ogv_set_option(b"dw_blocks", 0) == 0

@@ -519,9 +519,73 @@ __global__ void tapmajor_to_chan_kernel(const float* __restrict__ s, float* __re
 }
 
 // ------------------------------------------------------------------ Squeeze-Excite
-// pooled[b, c] = mean over the image's pixels of act(d*sc + sh)   (grid = (channel tiles, image))
-template <typename T, int V>
+// Per-image channel reductions over [B, HW, K] rows: block = (image b, group of chunks*V channels),
+// thread = (chunk = tid % chunks, pixel slot = tid / chunks) striding over the image's pixels.
+// chunks is picked per shape so every thread takes >= ~4 pixels (small images: wide channel groups
+// instead of idle slots), then the slots are summed in a fixed order (dw_reduce_store).
+struct ImgPlan {
+  int chunks, ngx;
+};
+static ImgPlan img_plan(int HW, int K, int V) {
+  int slots = 8;
+  while (slots < 64 && slots * 2 * 4 <= HW) slots *= 2;  // >= 4 pixels per slot
+  int ch = 256 / slots;
+  while (ch > 1 && (ch / 2) * V >= K) ch /= 2;
+  ImgPlan p;
+  p.chunks = ch;
+  p.ngx = (K + ch * V - 1) / (ch * V);
+  return p;
+}
+constexpr int IMG_MAX_CHUNKS = 32;  // img_plan: >= 8 slots
+
+// pooled[b, c] = mean over the image's pixels of act(d*sc + sh)
+template <typename T, int V, int ACT>
 __global__ __launch_bounds__(256) void se_pool_kernel(const T* __restrict__ d, const float* __restrict__ sc,
+                                                      const float* __restrict__ sh, float* __restrict__ pooled,
+                                                      int HW, int K, int B, int chunks, int ngx) {
+  __shared__ __attribute__((aligned(16))) float lds[4 * IMG_MAX_CHUNKS * 1 * V];  // dw_reduce_store scratch
+  long lid;
+  if (!xcd_block((long)ngx * B, lid)) return;
+  const int bx = (int)(lid % ngx);
+  const long b = lid / ngx;
+  const int chunk = threadIdx.x % chunks, slot = threadIdx.x / chunks, nslots = 256 / chunks;
+  const int c0 = (bx * chunks + chunk) * V;
+  float q[1][V];
+#pragma unroll
+  for (int i = 0; i < V; ++i) q[0][i] = 0.f;
+  if (c0 < K) {
+    float s[V], h[V];
+    load_vec<float, V>(sc + c0, s);
+    load_vec<float, V>(sh + c0, h);
+#pragma unroll 2
+    for (int p = slot; p < HW; p += nslots) {
+      float v[V];
+      load_vec<T, V>(d + (b * HW + p) * K + c0, v);
+#pragma unroll
+      for (int i = 0; i < V; ++i) q[0][i] += act_fwd(ACT, fmaf(v[i], s[i], h[i]));
+    }
+    const float inv = 1.f / (float)HW;
+#pragma unroll
+    for (int i = 0; i < V; ++i) q[0][i] *= inv;
+  }
+  dw_reduce_store<1, V, float>(q, lds, chunks, pooled + b * K, K, K, bx * chunks * V);
+}
+
+__global__ void sigmoid_kernel(const float* __restrict__ z, float* __restrict__ g, long n) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) g[i] = fast_sigmoid(z[i]);
+}
+
+// dz2 = dgate * g * (1 - g)
+__global__ void sigmoid_bwd_kernel(const float* __restrict__ dgate, const float* __restrict__ g, float* __restrict__ dz,
+                                   long n) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dz[i] = dgate[i] * g[i] * (1.f - g[i]);
+}
+
+// pooled[b, c] = mean over the image's pixels of act(d*sc + sh)   large images: 4 chunks x 64 pixel slots
+template <typename T, int V>
+__global__ __launch_bounds__(256) void se_pool_wide_kernel(const T* __restrict__ d, const float* __restrict__ sc,
                                                       const float* __restrict__ sh, int act, float* __restrict__ pooled,
                                                       int HW, int K, int B) {
   __shared__ float lds[4 * 1 * 4 * 8];
@@ -552,23 +616,8 @@ __global__ __launch_bounds__(256) void se_pool_kernel(const T* __restrict__ d, c
   chunk_reduce_store<1, V>(q, lds, pooled + b * K, K, K, bx * 4 * V);
 }
 
-__global__ void sigmoid_kernel(const float* __restrict__ z, float* __restrict__ g, long n) {
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) g[i] = fast_sigmoid(z[i]);
-}
-
-// dz2 = dgate * g * (1 - g)
-__global__ void sigmoid_bwd_kernel(const float* __restrict__ dgate, const float* __restrict__ g, float* __restrict__ dz,
-                                   long n) {
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) dz[i] = dgate[i] * g[i] * (1.f - g[i]);
-}
-
-// One pass over (dA3, d) per image: R[q][b][c] for
-//   q0 = sum dA3*a2 (-> dgate), q1 = sum dA3*s', q2 = sum s', q3 = sum dA3*s'*dh, q4 = sum s'*dh
-// with y2 = d*sc2+sh2, a2 = act(y2), s' = act'(y2), dh = (d-mean2)*invstd2.
 template <typename T, int V>
-__global__ __launch_bounds__(256) void se_bwd_reduce_kernel(const T* __restrict__ dA3, const T* __restrict__ d,
+__global__ __launch_bounds__(256) void se_bwd_reduce_wide_kernel(const T* __restrict__ dA3, const T* __restrict__ d,
                                                             const float* __restrict__ sc, const float* __restrict__ sh,
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ invstd, int act,
@@ -618,6 +667,62 @@ __global__ __launch_bounds__(256) void se_bwd_reduce_kernel(const T* __restrict_
     }
   }
   chunk_reduce_store<5, V>(q, lds, R + b * K, (long)B * K, K, bx * 4 * V);
+}
+
+// One pass over (dA3, d) per image: R[q][b][c] for
+//   q0 = sum dA3*a2 (-> dgate), q1 = sum dA3*s', q2 = sum s', q3 = sum dA3*s'*dh, q4 = sum s'*dh
+// with y2 = d*sc2+sh2, a2 = act(y2), s' = act'(y2), dh = (d-mean2)*invstd2.
+template <typename T, int V, int ACT>
+__global__ __launch_bounds__(256) void se_bwd_reduce_kernel(const T* __restrict__ dA3, const T* __restrict__ d,
+                                                            const float* __restrict__ sc, const float* __restrict__ sh,
+                                                            const float* __restrict__ mean,
+                                                            const float* __restrict__ invstd, float* __restrict__ R,
+                                                            int B, int HW, int K, int chunks, int ngx) {
+  __shared__ __attribute__((aligned(16))) float lds[4 * IMG_MAX_CHUNKS * 5 * V];  // dw_reduce_store scratch
+  long lid;
+  if (!xcd_block((long)ngx * B, lid)) return;
+  const int bx = (int)(lid % ngx);
+  const long b = lid / ngx;
+  const int chunk = threadIdx.x % chunks, slot = threadIdx.x / chunks, nslots = 256 / chunks;
+  const int c0 = (bx * chunks + chunk) * V;
+  float q[5][V];
+#pragma unroll
+  for (int k = 0; k < 5; ++k)
+#pragma unroll
+    for (int i = 0; i < V; ++i) q[k][i] = 0.f;
+  if (c0 < K) {
+    float s[V], h[V], mu[V], is[V];
+    load_vec<float, V>(sc + c0, s);
+    load_vec<float, V>(sh + c0, h);
+    load_vec<float, V>(mean + c0, mu);
+    load_vec<float, V>(invstd + c0, is);
+#pragma unroll 2
+    for (int p = slot; p < HW; p += nslots) {
+      float ga[V], dv[V];
+      load_vec<T, V>(dA3 + (b * HW + p) * K + c0, ga);
+      load_vec<T, V>(d + (b * HW + p) * K + c0, dv);
+#pragma unroll
+      for (int i = 0; i < V; ++i) {
+        const float y = fmaf(dv[i], s[i], h[i]);
+        float a, sp;
+        if constexpr (ACT == OGV_ACT_SILU) {
+          const float sg = fast_sigmoid(y);
+          a = y * sg;
+          sp = sg * (1.0f + y * (1.0f - sg));
+        } else {
+          a = act_fwd(ACT, y);
+          sp = act_grad(ACT, y);
+        }
+        const float dh = (dv[i] - mu[i]) * is[i];
+        q[0][i] = fmaf(ga[i], a, q[0][i]);
+        q[1][i] = fmaf(ga[i], sp, q[1][i]);
+        q[2][i] += sp;
+        q[3][i] = fmaf(ga[i] * sp, dh, q[3][i]);
+        q[4][i] = fmaf(sp, dh, q[4][i]);
+      }
+    }
+  }
+  dw_reduce_store<5, V, float>(q, lds, chunks, R + b * K, (long)B * K, K, bx * chunks * V);
 }
 
 // BN2 reductions from the per-image sums: dy2 = (dA3*gate + dpool/HW) * s'
@@ -929,14 +1034,47 @@ struct Ops {
   template <int V>
   static void pool(const void* d, const float* sc, const float* sh, int act, float* pooled, int B, int HW, int K,
                    const RowPlan& rp, hipStream_t st) {
-    se_pool_kernel<T, V><<<xcd_grid((long)cdiv(K, 4 * V) * B), 256, 0, st>>>((const T*)d, sc, sh, act, pooled, HW, K,
-                                                                           B);
+    if (HW >= 256) {  // measured: the fixed 4-chunk kernel is faster for large images
+      se_pool_wide_kernel<T, V><<<xcd_grid((long)cdiv(K, 4 * V) * B), 256, 0, st>>>((const T*)d, sc, sh, act, pooled,
+                                                                                   HW, K, B);
+      return;
+    }
+    const ImgPlan ip = img_plan(HW, K, V);
+    const unsigned g = xcd_grid((long)ip.ngx * B);
+    switch (act) {
+      case OGV_ACT_SILU:
+        se_pool_kernel<T, V, OGV_ACT_SILU><<<g, 256, 0, st>>>((const T*)d, sc, sh, pooled, HW, K, B, ip.chunks, ip.ngx);
+        break;
+      case OGV_ACT_GELU:
+        se_pool_kernel<T, V, OGV_ACT_GELU><<<g, 256, 0, st>>>((const T*)d, sc, sh, pooled, HW, K, B, ip.chunks, ip.ngx);
+        break;
+      case OGV_ACT_RELU:
+        se_pool_kernel<T, V, OGV_ACT_RELU><<<g, 256, 0, st>>>((const T*)d, sc, sh, pooled, HW, K, B, ip.chunks, ip.ngx);
+        break;
+      default:
+        se_pool_kernel<T, V, OGV_ACT_NONE><<<g, 256, 0, st>>>((const T*)d, sc, sh, pooled, HW, K, B, ip.chunks, ip.ngx);
+    }
   }
   template <int V>
   static void se_reduce(const void* dA3, const void* d, const float* sc, const float* sh, const float* mean,
                         const float* inv, int act, float* R, int B, int HW, int K, const RowPlan& rp, hipStream_t st) {
-    se_bwd_reduce_kernel<T, V><<<xcd_grid((long)cdiv(K, 4 * V) * B), 256, 0, st>>>((const T*)dA3, (const T*)d, sc, sh, mean, inv,
-                                                                        act, R, B, HW, K);
+    if (HW >= 256) {
+      se_bwd_reduce_wide_kernel<T, V><<<xcd_grid((long)cdiv(K, 4 * V) * B), 256, 0, st>>>(
+          (const T*)dA3, (const T*)d, sc, sh, mean, inv, act, R, B, HW, K);
+      return;
+    }
+    const ImgPlan ip = img_plan(HW, K, V);
+    const unsigned g = xcd_grid((long)ip.ngx * B);
+#define OGV_SE_RED(A)                                                                                            \
+  se_bwd_reduce_kernel<T, V, A><<<g, 256, 0, st>>>((const T*)dA3, (const T*)d, sc, sh, mean, inv, R, B, HW, K, \
+                                                   ip.chunks, ip.ngx)
+    switch (act) {
+      case OGV_ACT_SILU: OGV_SE_RED(OGV_ACT_SILU); break;
+      case OGV_ACT_GELU: OGV_SE_RED(OGV_ACT_GELU); break;
+      case OGV_ACT_RELU: OGV_SE_RED(OGV_ACT_RELU); break;
+      default: OGV_SE_RED(OGV_ACT_NONE);
+    }
+#undef OGV_SE_RED
   }
   template <int V>
   static void bn2_apply(const void* dA3, const void* d, const float* sc, const float* sh, const float* mean,

@@ -739,41 +739,81 @@ __global__ void bn2_terms_kernel(const float* __restrict__ R, const float* __res
   terms[b * 2 * K + K + c] = gg * R[3 * BK + i] + dp * R[4 * BK + i];
 }
 
+// ---- row-tiled elementwise kernels: thread = (channel chunk, row slot), EW_RPT rows per thread, so
+// the per-channel coefficients are loaded once per EW_RPT rows; rows are clamped (loads of all
+// EW_RPT rows are issued up front), stores guarded.
+constexpr int EW_RPT = 4;
+struct EwPlan {
+  int nch, CG, RB, ncg;
+  long nrb;
+  unsigned grid() const { return xcd_grid((long)ncg * nrb); }
+};
+static EwPlan ew_plan(long M, int K, int V) {
+  EwPlan p;
+  p.nch = K / V;
+  p.CG = p.nch < 64 ? p.nch : 64;
+  p.RB = 256 / p.CG;
+  p.ncg = (p.nch + p.CG - 1) / p.CG;
+  p.nrb = (M + (long)p.RB * EW_RPT - 1) / ((long)p.RB * EW_RPT);
+  return p;
+}
+__device__ __forceinline__ bool ew_idx(const EwPlan& p, int V, int& c0, long& m0) {
+  long id;
+  if (!xcd_block((long)p.ncg * p.nrb, id)) return false;
+  const int cg = (int)(id % p.ncg);
+  const long rb = id / p.ncg;
+  const int cc = threadIdx.x % p.CG, rr = threadIdx.x / p.CG;
+  const int ch = cg * p.CG + cc;
+  if (rr >= p.RB || ch >= p.nch) return false;
+  c0 = ch * V;
+  m0 = rb * p.RB * EW_RPT + rr;
+  return true;
+}
+
 // dd = ca*(dy2 - cb - dh*cc), dy2 = (dA3*gate + dpool/HW) * act'(d*sc2+sh2)
-template <typename T, int V>
+template <typename T, int V, int ACT>
 __global__ __launch_bounds__(256) void bn2_apply_kernel(const T* __restrict__ dA3, const T* __restrict__ d,
                                                         const float* __restrict__ sc, const float* __restrict__ sh,
                                                         const float* __restrict__ mean, const float* __restrict__ invstd,
                                                         const float* __restrict__ gate, const float* __restrict__ dpool,
-                                                        const float* __restrict__ coef, int act, T* __restrict__ out,
-                                                        long M, int HW, int K) {
-  const int nch = K / V;
-  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (tid >= M * nch) return;
-  const int c0 = (int)(tid % nch) * V;
-  const long m = tid / nch;
-  const long b = m / HW;
-  const float inv = 1.f / (float)HW;
-  float ga[V], dv[V], o[V], s[V], h[V], mu[V], is[V], gt[V], dp[V], ca[V], cb[V], cc[V];
-  load_vec<T, V>(dA3 + m * K + c0, ga);
-  load_vec<T, V>(d + m * K + c0, dv);
+                                                        const float* __restrict__ coef, T* __restrict__ out,
+                                                        long M, int HW, int K, EwPlan ep) {
+  int c0;
+  long m0;
+  if (!ew_idx(ep, V, c0, m0)) return;
+  float s[V], h[V], mu[V], is[V], ca[V], cb[V], cc[V];
   load_vec<float, V>(sc + c0, s);
   load_vec<float, V>(sh + c0, h);
   load_vec<float, V>(mean + c0, mu);
   load_vec<float, V>(invstd + c0, is);
-  load_vec<float, V>(gate + b * K + c0, gt);
-  load_vec<float, V>(dpool + b * K + c0, dp);
   load_vec<float, V>(coef + c0, ca);
   load_vec<float, V>(coef + K + c0, cb);
   load_vec<float, V>(coef + 2 * K + c0, cc);
+  const float inv = 1.f / (float)HW;
+  float ga[EW_RPT][V], dv[EW_RPT][V];
 #pragma unroll
-  for (int i = 0; i < V; ++i) {
-    const float y = fmaf(dv[i], s[i], h[i]);
-    const float dy2 = fmaf(ga[i], gt[i], dp[i] * inv) * act_grad(act, y);
-    const float dh = (dv[i] - mu[i]) * is[i];
-    o[i] = ca[i] * (dy2 - cb[i] - dh * cc[i]);
+  for (int j = 0; j < EW_RPT; ++j) {
+    const long m = min(m0 + (long)j * ep.RB, M - 1);
+    load_vec<T, V>(dA3 + m * K + c0, ga[j]);
+    load_vec<T, V>(d + m * K + c0, dv[j]);
   }
-  store_vec<T, V>(out + m * K + c0, o);
+#pragma unroll
+  for (int j = 0; j < EW_RPT; ++j) {
+    const long m = m0 + (long)j * ep.RB;
+    if (m >= M) break;
+    const long b = m / HW;
+    float gt[V], dp[V], o[V];
+    load_vec<float, V>(gate + b * K + c0, gt);
+    load_vec<float, V>(dpool + b * K + c0, dp);
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      const float y = fmaf(dv[j][i], s[i], h[i]);
+      const float dy2 = fmaf(ga[j][i], gt[i], dp[i] * inv) * act_grad(ACT, y);
+      const float dh = (dv[j][i] - mu[i]) * is[i];
+      o[i] = ca[i] * (dy2 - cb[i] - dh * cc[i]);
+    }
+    store_vec<T, V>(out + m * K + c0, o);
+  }
 }
 
 // generic BN backward reduction over rows: stat[slice] = [sum dy, sum dy*(x-mean)*invstd]
@@ -819,23 +859,32 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
                                                            const float* __restrict__ mean,
                                                            const float* __restrict__ invstd,
                                                            const float* __restrict__ coef, T* __restrict__ out, long M,
-                                                           int K) {
-  const int nch = K / V;
-  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (tid >= M * nch) return;
-  const int c0 = (int)(tid % nch) * V;
-  const long m = tid / nch;
-  float g[V], xv[V], o[V], mu[V], is[V], ca[V], cb[V], cc[V];
-  load_vec<T, V>(dy + m * K + c0, g);
-  load_vec<T, V>(x + m * K + c0, xv);
+                                                           int K, EwPlan ep) {
+  int c0;
+  long m0;
+  if (!ew_idx(ep, V, c0, m0)) return;
+  float mu[V], is[V], ca[V], cb[V], cc[V];
   load_vec<float, V>(mean + c0, mu);
   load_vec<float, V>(invstd + c0, is);
   load_vec<float, V>(coef + c0, ca);
   load_vec<float, V>(coef + K + c0, cb);
   load_vec<float, V>(coef + 2 * K + c0, cc);
+  float g[EW_RPT][V], xv[EW_RPT][V];
 #pragma unroll
-  for (int i = 0; i < V; ++i) o[i] = ca[i] * (g[i] - cb[i] - (xv[i] - mu[i]) * is[i] * cc[i]);
-  store_vec<T, V>(out + m * K + c0, o);
+  for (int j = 0; j < EW_RPT; ++j) {
+    const long m = min(m0 + (long)j * ep.RB, M - 1);
+    load_vec<T, V>(dy + m * K + c0, g[j]);
+    load_vec<T, V>(x + m * K + c0, xv[j]);
+  }
+#pragma unroll
+  for (int j = 0; j < EW_RPT; ++j) {
+    const long m = m0 + (long)j * ep.RB;
+    if (m >= M) break;
+    float o[V];
+#pragma unroll
+    for (int i = 0; i < V; ++i) o[i] = ca[i] * (g[j][i] - cb[i] - (xv[j][i] - mu[i]) * is[i] * cc[i]);
+    store_vec<T, V>(out + m * K + c0, o);
+  }
 }
 
 // out = res + p*sc + sh
@@ -843,20 +892,28 @@ template <typename T, int V>
 __global__ __launch_bounds__(256) void affine_residual_kernel(const T* __restrict__ res, const T* __restrict__ p,
                                                               const float* __restrict__ sc,
                                                               const float* __restrict__ sh, T* __restrict__ out, long M,
-                                                              int K) {
-  const int nch = K / V;
-  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (tid >= M * nch) return;
-  const int c0 = (int)(tid % nch) * V;
-  const long m = tid / nch;
-  float a[V], b[V], s[V], h[V];
-  load_vec<T, V>(res + m * K + c0, a);
-  load_vec<T, V>(p + m * K + c0, b);
+                                                              int K, EwPlan ep) {
+  int c0;
+  long m0;
+  if (!ew_idx(ep, V, c0, m0)) return;
+  float s[V], h[V];
   load_vec<float, V>(sc + c0, s);
   load_vec<float, V>(sh + c0, h);
+  float a[EW_RPT][V], pv[EW_RPT][V];
 #pragma unroll
-  for (int i = 0; i < V; ++i) a[i] += fmaf(b[i], s[i], h[i]);
-  store_vec<T, V>(out + m * K + c0, a);
+  for (int j = 0; j < EW_RPT; ++j) {
+    const long m = min(m0 + (long)j * ep.RB, M - 1);
+    load_vec<T, V>(res + m * K + c0, a[j]);
+    load_vec<T, V>(p + m * K + c0, pv[j]);
+  }
+#pragma unroll
+  for (int j = 0; j < EW_RPT; ++j) {
+    const long m = m0 + (long)j * ep.RB;
+    if (m >= M) break;
+#pragma unroll
+    for (int i = 0; i < V; ++i) a[j][i] += fmaf(pv[j][i], s[i], h[i]);
+    store_vec<T, V>(out + m * K + c0, a[j]);
+  }
 }
 
 // ------------------------------------------------------------------ orchestration
@@ -1080,8 +1137,17 @@ struct Ops {
   static void bn2_apply(const void* dA3, const void* d, const float* sc, const float* sh, const float* mean,
                         const float* inv, const float* gate, const float* dpool, const float* coef, int act, void* out,
                         long M, int HW, int K, hipStream_t st) {
-    bn2_apply_kernel<T, V><<<cdiv(M * (K / V), 256), 256, 0, st>>>((const T*)dA3, (const T*)d, sc, sh, mean, inv, gate,
-                                                                    dpool, coef, act, (T*)out, M, HW, K);
+    const EwPlan ep = ew_plan(M, K, V);
+#define OGV_BN2(A)                                                                                             \
+  bn2_apply_kernel<T, V, A><<<ep.grid(), 256, 0, st>>>((const T*)dA3, (const T*)d, sc, sh, mean, inv, gate, dpool, \
+                                                       coef, (T*)out, M, HW, K, ep)
+    switch (act) {
+      case OGV_ACT_SILU: OGV_BN2(OGV_ACT_SILU); break;
+      case OGV_ACT_GELU: OGV_BN2(OGV_ACT_GELU); break;
+      case OGV_ACT_RELU: OGV_BN2(OGV_ACT_RELU); break;
+      default: OGV_BN2(OGV_ACT_NONE);
+    }
+#undef OGV_BN2
   }
   template <int V>
   static void bn_reduce(const void* dy, const void* x, const float* mean, const float* inv, float* stat, long M, int K,
@@ -1092,14 +1158,14 @@ struct Ops {
   template <int V>
   static void bn_apply(const void* dy, const void* x, const float* mean, const float* inv, const float* coef, void* out,
                        long M, int K, hipStream_t st) {
-    bn_bwd_apply_kernel<T, V><<<cdiv(M * (K / V), 256), 256, 0, st>>>((const T*)dy, (const T*)x, mean, inv, coef,
-                                                                       (T*)out, M, K);
+    const EwPlan ep = ew_plan(M, K, V);
+    bn_bwd_apply_kernel<T, V><<<ep.grid(), 256, 0, st>>>((const T*)dy, (const T*)x, mean, inv, coef, (T*)out, M, K, ep);
   }
   template <int V>
   static void affine_res(const void* res, const void* p, const float* sc, const float* sh, void* out, long M, int K,
                          hipStream_t st) {
-    affine_residual_kernel<T, V><<<cdiv(M * (K / V), 256), 256, 0, st>>>((const T*)res, (const T*)p, sc, sh, (T*)out, M,
-                                                                          K);
+    const EwPlan ep = ew_plan(M, K, V);
+    affine_residual_kernel<T, V><<<ep.grid(), 256, 0, st>>>((const T*)res, (const T*)p, sc, sh, (T*)out, M, K, ep);
   }
 };
 

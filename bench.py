@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="ogv_set_option tuning switch (repeatable; see include/ogv.h)")
     return ap.parse_args()
 
 
@@ -128,6 +130,10 @@ def main():
     torch.backends.cudnn.benchmark = True   # as the reference (src/training/autocast.py:8-17)
     assert device.type == "cuda", "bench.py needs a HIP device"
     ogv.load()
+    for o in args.opt:
+        name, val = o.split("=")
+        if ogv._lib.load().ogv_set_option(name.encode(), int(val)) != 0:
+            raise SystemExit(f"bench.py: unknown option {name}")
     cfg = MODEL_CONFIGS[args.model]
     torch.manual_seed(7)
     model = build_model(dict(type="model_a", num_classes=cfg["num_classes"], stem_dim=cfg["stem_dim"],

@@ -11,8 +11,10 @@
  *     NCHW tensor is exactly this layout), element type `ogv_dtype` (fp32 or bf16), fp32 math.
  *   - Weights/bias/affine parameters are fp32 (the AMP master copy); bf16 kernels round them
  *     to bf16 when staging.  Weight gradients are produced in fp32.
- *   - The library never allocates, frees or synchronises.  Scratch is passed in by the caller
- *     (sizes from the *_ws_bytes queries).  Every call enqueues on `stream` (a hipStream_t).
+ *   - The library never allocates memory, frees or synchronises.  Scratch is passed in by the caller
+ *     (sizes from the *_ws_bytes queries).  Every call enqueues on `stream` (a hipStream_t); the fused
+ *     MBConv backward also forks independent weight-gradient work onto a library-owned side stream
+ *     (created once per device) and joins it back into `stream` before returning (graph-capturable).
  *   - Return 0 on success; otherwise a non-zero code and ogv_last_error() (thread-local) says why.
  *     Shapes are validated on the host before any launch.
  */
@@ -42,7 +44,8 @@ const char* ogv_last_error(void);
  *   "sgemm" 1 (default) / 0: persistent streaming kernels (projection fwd/dgrad and weight gradient)
  *   for tall-skinny bf16 shapes on/off;  "sgemm_min_m" (default 65536): smallest M routed to them;
  *   "bk64_max_m": largest M using 64-wide k-steps in the tiled GEMM; "grid_mfma" 1/0: MFMA grid
- *   attention for bf16; "dw_blocks" (default 768): target block count of the depthwise kernels.
+ *   attention for bf16; "dw_blocks" (default 0 = ~32 rows per block): target block count of the
+ *   depthwise kernels; "mb_side" 1/0: weight gradients of the fused MBConv backward on a side stream.
  * Returns OGV_ERR_ARG for an unknown name. */
 int ogv_set_option(const char* name, int value);
 /* Diagnostics (no reference counterpart): 1 if ogv_gemm_fwd (kind 0) / ogv_gemm_dgrad (kind 1) of

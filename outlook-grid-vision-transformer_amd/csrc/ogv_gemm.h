@@ -164,5 +164,6 @@ void set_sgemm_min_m(int v);
 void set_bk64_max_m(int v);
 void set_grid_mfma(int v);
 void set_dw_blocks(int v);
+void set_mb_side(int v);
 
 }  // namespace ogv

@@ -353,9 +353,10 @@ __global__ __launch_bounds__(256) void dw_fwd_tile_kernel(const T* __restrict__ 
     h[i] = cok ? sh[c + i] : 0.f;
     sft[i] = (cok && shift) ? shift[c + i] : 0.f;
   }
-  float q[2][V];  // BN batch statistics: fp32 per thread (<= G*H shifted terms), fp64 across threads
+  double q[2][V];  // BN batch statistics in fp64 (shifted sums: fp32 cancels visibly when the
+                   // running-mean shift is far from the batch mean)
 #pragma unroll
-  for (int i = 0; i < V; ++i) { q[0][i] = 0.f; q[1][i] = 0.f; }
+  for (int i = 0; i < V; ++i) { q[0][i] = 0.0; q[1][i] = 0.0; }
   const int cc = cok ? c : 0;
   dw_walk<T, V, LDQ, true, ACT>(ring, e, t, ti, cc, chunk, cok, s, h, [&](VRow, int) {},
                            [&](int, int u, long b, int y, int px) {
@@ -380,18 +381,13 @@ __global__ __launch_bounds__(256) void dw_fwd_tile_kernel(const T* __restrict__ 
 #pragma unroll
     for (int i = 0; i < V; ++i) {
       of[i] = to_f(from_f<T>(acc[i]));
-      const float dl = of[i] - sft[i];
+      const double dl = (double)of[i] - (double)sft[i];
       q[0][i] += dl;
-      q[1][i] = fmaf(dl, dl, q[1][i]);
+      q[1][i] = fma(dl, dl, q[1][i]);
     }
     store_vec<T, V>(out + ((b * t.H + y) * t.W + ti.x0 + px) * t.C + c, of);
   });
-  if (stat) {
-    double qd[2][V];
-#pragma unroll
-    for (int i = 0; i < V; ++i) { qd[0][i] = q[0][i]; qd[1][i] = q[1][i]; }
-    dw_reduce_store<2, V, double>(qd, ring, t.chunks, stat + ti.rid * 2 * t.C, t.C, t.C, ti.ct * t.CT);
-  }
+  if (stat) dw_reduce_store<2, V, double>(q, ring, t.chunks, stat + ti.rid * 2 * t.C, t.C, t.C, ti.ct * t.CT);
 }
 
 // dy1 = (dw3x3^T dd) * act'(e*sc1 + sh1) -> out; stats: sum dy1, sum dy1*(e - mean1)*invstd1
@@ -992,7 +988,8 @@ struct BwdWs {
   void *dp, *bufA, *bufB;
   float *stat, *S, *coef, *R, *dgate, *dz2, *dh, *dz1, *dpool, *part9, *tmp, *sums9, *terms;
   float *wtse, *split;  // transposed SE weight, split-K partials
-  char* gemm;
+  float* tmp2;          // colreduce scratch of the side stream
+  char *gemm, *gemm2;   // GEMM workspaces: current stream, side stream
 };
 static size_t max3(size_t a, size_t b, size_t c) { return a > b ? (a > c ? a : c) : (b > c ? b : c); }
 static BwdWs bwd_ws_layout(void* base, const ogv_mbconv_desc& s, size_t esz, size_t* total) {
@@ -1027,8 +1024,46 @@ static BwdWs bwd_ws_layout(void* base, const ogv_mbconv_desc& s, size_t esz, siz
                              wgrad_ws_bytes(s.B, s.se, s.mid)),
                         max3(dgrad_ws_bytes(s.mid, s.se), dgrad_ws_bytes(s.se, s.mid), 64));
   w.gemm = b.take<char>(g);
+  w.tmp2 = b.take<float>(colreduce_tmp_floats(S2, 9L * s.mid) + 16);
+  w.gemm2 = b.take<char>(g);
   if (total) *total = b.off + 256;
   return w;
+}
+
+// Side stream for the weight-gradient work of the fused backward (independent of the data-gradient
+// chain): forked from / joined back into the caller's stream with events, which also works inside a
+// captured hipGraph (the side stream joins the capture).  Knob "mb_side" (default 1).
+static int g_mb_side = 1;
+void set_mb_side(int v) { g_mb_side = v; }
+struct SideStream {
+  hipStream_t s = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+};
+static SideStream* side_stream() {
+  static SideStream ss[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  SideStream& x = ss[dev];
+  if (!x.s) {
+    if (hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    (void)hipEventCreateWithFlags(&x.fork, hipEventDisableTiming);
+    (void)hipEventCreateWithFlags(&x.join, hipEventDisableTiming);
+  }
+  return &x;
+}
+// returns the stream side work goes to (the caller's when the side stream is off / unavailable)
+static hipStream_t fork_side(hipStream_t st) {
+  SideStream* x = g_mb_side ? side_stream() : nullptr;
+  if (!x) return st;
+  (void)hipEventRecord(x->fork, st);
+  (void)hipStreamWaitEvent(x->s, x->fork, 0);
+  return x->s;
+}
+static void join_side(hipStream_t st, hipStream_t side) {
+  if (side == st) return;
+  SideStream* x = side_stream();
+  (void)hipEventRecord(x->join, side);
+  (void)hipStreamWaitEvent(st, x->join, 0);
 }
 
 #define OGV_V_DISPATCH(V, FN, ...)      \
@@ -1247,7 +1282,8 @@ static void mbconv_bwd_impl(const void* dout, const void* x, const Saved& sv, vo
                                                      s.train);
     OGV_V_DISPATCH(rc.V, O::template bn_apply, dout, sv.p, sv.mean3, sv.inv3, w.coef, w.dp, M, s.C, st);
   }
-  // B2) project: dA3 = dp . Wp ; dWp = dp^T . (act(BN2(d)) * gate)
+  // B2) project: dA3 = dp . Wp ; dWp = dp^T . (act(BN2(d)) * gate)   (dWp on the side stream)
+  hipStream_t sd = fork_side(st);
   {
     gemm_dgrad_launch(dt, w.dp, s.C, P.w_proj, nullptr, 0, 0, nullptr, 1, nullptr, w.bufA, s.mid, (int)M, s.C, s.mid,
                       w.gemm, st);
@@ -1258,7 +1294,7 @@ static void mbconv_bwd_impl(const void* dout, const void* x, const Saved& sv, vo
     pr.gate = sv.gate;
     pr.rps = HW;
     pr.gld = s.mid;
-    gemm_wgrad_launch(dt, w.dp, s.C, sv.d, s.mid, pr, nullptr, 1, G.w_proj, nullptr, (int)M, s.C, s.mid, w.gemm, st);
+    gemm_wgrad_launch(dt, w.dp, s.C, sv.d, s.mid, pr, nullptr, 1, G.w_proj, nullptr, (int)M, s.C, s.mid, w.gemm2, sd);
   }
   // B3) one pass over (dA3, d): SE gate grads + BN2 partial sums per image
   OGV_V_DISPATCH(rp.V, O::template se_reduce, w.bufA, sv.d, sv.sc2, sv.sh2, sv.mean2, sv.inv2, s.act, w.R, s.B, HW,
@@ -1297,21 +1333,26 @@ static void mbconv_bwd_impl(const void* dout, const void* x, const Saved& sv, vo
   // B6) depthwise backward: dy1 = dgrad(dd) * act'(BN1(e)) -> bufA (+ BN1 sums); dWdw from (dd, act(BN1(e)))
   {
     const DwTile t = dw_tile_plan(s.B, s.H, s.W, s.mid, 4);
+    join_side(st, sd);
+    sd = fork_side(st);  // bufB (dd) complete: dWdw on the side stream overlaps the data gradient
+    O::dw_wgrad(w.bufB, sv.e, sv.sc1, sv.sh1, s.act, w.part9, t, sd);
+    colreduce(w.part9, w.sums9, t.rows(), 9L * s.mid, 9L * s.mid, w.tmp2, sd);
+    tapmajor_to_chan_kernel<<<cdiv(9 * s.mid, 256), 256, 0, sd>>>(w.sums9, G.w_dw, s.mid);
     O::dw_dgrad(w.bufB, P.w_dw, sv.e, sv.sc1, sv.sh1, sv.mean1, sv.inv1, s.act,
                      w.bufA, w.stat, t, st);
     colreduce(w.stat, w.S, t.rows(), 2L * s.mid, 2L * s.mid, w.tmp, st);
-    O::dw_wgrad(w.bufB, sv.e, sv.sc1, sv.sh1, s.act, w.part9, t, st);
-    colreduce(w.part9, w.sums9, t.rows(), 9L * s.mid, 9L * s.mid, w.tmp, st);
-    tapmajor_to_chan_kernel<<<cdiv(9 * s.mid, 256), 256, 0, st>>>(w.sums9, G.w_dw, s.mid);
   }
+  join_side(st, sd);  // B7 overwrites bufB
   // B7) BN1 backward: de = ca*(dy1 - cb - ehat*cc) -> bufB
   bn_coeffs_kernel<<<cdiv(s.mid, 256), 256, 0, st>>>(w.S, s.mid, (float)M, P.bn1_w, sv.inv1, G.bn1_w, G.bn1_b, w.coef,
                                                      s.train);
   OGV_V_DISPATCH(rp.V, O::template bn_apply, w.bufA, sv.e, sv.mean1, sv.inv1, w.coef, w.bufB, M, s.mid, st);
   // B8) expand: dx = de . We + dout (residual) ; dWe = de^T . x
+  sd = fork_side(st);  // dWe on the side stream, overlapping dx
+  gemm_wgrad_launch(dt, w.bufB, s.mid, x, s.C, Pro(), nullptr, 1, G.w_expand, nullptr, (int)M, s.mid, s.C, w.gemm2, sd);
   gemm_dgrad_launch(dt, w.bufB, s.mid, P.w_expand, nullptr, 0, 0, nullptr, 1, dout, dx, s.C, (int)M, s.mid, s.C,
                     w.gemm, st);
-  gemm_wgrad_launch(dt, w.bufB, s.mid, x, s.C, Pro(), nullptr, 1, G.w_expand, nullptr, (int)M, s.mid, s.C, w.gemm, st);
+  join_side(st, sd);
 }
 
 static int mb_check(const ogv_mbconv_desc* s, ogv_dtype dt, const char* who) {

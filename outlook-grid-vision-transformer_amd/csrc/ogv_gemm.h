@@ -165,5 +165,6 @@ void set_bk64_max_m(int v);
 void set_grid_mfma(int v);
 void set_dw_blocks(int v);
 void set_mb_side(int v);
+void set_ln_bwd_blocks(int v);
 
 }  // namespace ogv

@@ -99,48 +99,58 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
     }
   }
   const float invC = 1.f / (float)C;
-  for (long row = blockIdx.x * rows_per_block + threadIdx.x / G; row < M; row += (long)gridDim.x * rows_per_block) {
-    const float mu = mean[row], rs = rstd[row];
-    float xh[E], gv[E];
-    float s1 = 0.f, s2 = 0.f;
+  // two rows per iteration, every load of both (x, dy, dres, mean, rstd) issued before any use
+  constexpr int RPI = 2;
+  const long stride = (long)gridDim.x * rows_per_block;
+  for (long row0 = blockIdx.x * rows_per_block + threadIdx.x / G; row0 < M; row0 += RPI * stride) {
+    float xv[RPI][E], dv[RPI][E], rv[RPI][E], mu[RPI], rs[RPI];
 #pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      const int c = (v * G + lane_g) * VEC;
-      if (valid[v]) {
-        float xv[VEC], dv[VEC];
-        load_vec<T, VEC>(x + row * C + c, xv);
-        load_vec<T, VEC>(dy + row * C + c, dv);
+    for (int q = 0; q < RPI; ++q) {
+      const long row = min(row0 + q * stride, M - 1);
+      mu[q] = mean[row];
+      rs[q] = rstd[row];
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        const int c = min((v * G + lane_g) * VEC, C - VEC);
+        load_vec<T, VEC>(x + row * C + c, xv[q] + v * VEC);
+        load_vec<T, VEC>(dy + row * C + c, dv[q] + v * VEC);
+        if (dres) load_vec<T, VEC>(dres + row * C + c, rv[q] + v * VEC);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < RPI; ++q) {
+      const long row = row0 + q * stride;
+      if (row >= M) break;
+      float xh[E], gv[E];
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
 #pragma unroll
         for (int i = 0; i < VEC; ++i) {
           const int e = v * VEC + i;
-          xh[e] = (xv[i] - mu) * rs;
-          gv[e] = dv[i] * gw[e];
+          const float d = valid[v] ? dv[q][e] : 0.f;
+          xh[e] = valid[v] ? (xv[q][e] - mu[q]) * rs[q] : 0.f;
+          gv[e] = d * gw[e];
           s1 += gv[e];
           s2 = fmaf(gv[e], xh[e], s2);
-          dgam[e] = fmaf(dv[i], xh[e], dgam[e]);
-          dbet[e] += dv[i];
+          dgam[e] = fmaf(d, xh[e], dgam[e]);
+          dbet[e] += d;
         }
-      } else {
-#pragma unroll
-        for (int i = 0; i < VEC; ++i) { xh[v * VEC + i] = 0.f; gv[v * VEC + i] = 0.f; }
       }
-    }
-    const float m1 = group_sum<G>(s1) * invC;
-    const float m2 = group_sum<G>(s2) * invC;
+      const float m1 = group_sum<G>(s1) * invC;
+      const float m2 = group_sum<G>(s2) * invC;
 #pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      const int c = (v * G + lane_g) * VEC;
-      if (valid[v]) {
-        float o[VEC];
+      for (int v = 0; v < NV; ++v) {
+        const int c = (v * G + lane_g) * VEC;
+        if (valid[v]) {
+          float o[VEC];
 #pragma unroll
-        for (int i = 0; i < VEC; ++i) o[i] = rs * (gv[v * VEC + i] - m1 - xh[v * VEC + i] * m2);
-        if (dres) {  // gradient of the residual branch that reused x (one pass instead of an extra add)
-          float r[VEC];
-          load_vec<T, VEC>(dres + row * C + c, r);
-#pragma unroll
-          for (int i = 0; i < VEC; ++i) o[i] += r[i];
+          for (int i = 0; i < VEC; ++i) {
+            o[i] = rs[q] * (gv[v * VEC + i] - m1 - xh[v * VEC + i] * m2);
+            if (dres) o[i] += rv[q][v * VEC + i];  // gradient of the residual branch that reused x
+          }
+          store_vec<T, VEC>(dx + row * C + c, o);
         }
-        store_vec<T, VEC>(dx + row * C + c, o);
       }
     }
   }
@@ -245,11 +255,16 @@ extern "C" int ogv_layernorm_fwd(const void* x, const float* gamma, const float*
   return check_launch("ogv_layernorm_fwd");
 }
 
+// tuning knob "ln_bwd_blocks": grid cap of the backward (each block's dgamma/dbeta partial is a row
+// of the slab, summed by one colreduce pass up to 2048 rows)
+static long g_ln_bwd_cap = 1024;
+namespace ogv {
+void set_ln_bwd_blocks(int v) { g_ln_bwd_cap = v > 0 ? v : 1024; }
+}
 static long ln_bwd_blocks(long M, int G) {
-  // fewer, fatter blocks than the forward: each block's dgamma/dbeta partial is a row of the slab
   const long rows_per_block = 256 / G;
   long nb = (M + rows_per_block - 1) / rows_per_block;
-  return nb < 512 ? nb : 512;
+  return nb < g_ln_bwd_cap ? nb : g_ln_bwd_cap;
 }
 
 extern "C" size_t ogv_layernorm_bwd_ws_bytes(int M, int C) {

@@ -11,6 +11,7 @@ exactly that layout, so the reference's `.permute(...).contiguous()` copies
 from __future__ import annotations
 
 import ctypes
+import os
 import warnings
 
 import torch
@@ -38,6 +39,8 @@ def _dt(t: torch.Tensor) -> int:
 
 
 _SIDE = {}
+# smallest M*(N+K) of a Linear backward whose weight gradient is forked onto the side stream
+_FORK_MIN_WORK = int(os.environ.get("OGV_FORK_MIN_WORK", "0"))
 
 
 def _side_stream(device):
@@ -265,7 +268,9 @@ class _Linear(torch.autograd.Function):
         # dgrad and wgrad are independent: the weight gradient runs on a side stream (forked from and
         # joined back into the current one, also inside a captured graph) so the two latency-bound
         # GEMMs overlap.
-        with _fork(want_dx and want_dw, dout, x2d, rs, dw, db, ws_w if want_dw else None) as side:
+        # (below ~_FORK_MIN_WORK the fork/join latency (~10 us per cross-stream edge) outweighs the overlap)
+        fork = want_dx and want_dw and M * (N + K) >= _FORK_MIN_WORK
+        with _fork(fork, dout, x2d, rs, dw, db, ws_w if want_dw else None) as side:
             if want_dw:
                 check(lib.ogv_gemm_wgrad(_ptr(dout), N, _ptr(x2d), x2d.stride(0), _ptr(rs), rps, _ptr(dw), _ptr(db),
                                          M, N, K, act, _ptr(ws_w), dt, side), "ogv_gemm_wgrad")

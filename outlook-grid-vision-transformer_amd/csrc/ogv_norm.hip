@@ -28,49 +28,51 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, co
     }
   }
   const float invC = 1.f / (float)C;
-  for (long row = blockIdx.x * rows_per_block + threadIdx.x / G; row < M; row += (long)gridDim.x * rows_per_block) {
-    const T* xr = x + row * C;
-    float xv[E];
-    float s = 0.f;
+  // two rows per iteration, both loads issued before any use
+  constexpr int RPI = 2;
+  const long stride = (long)gridDim.x * rows_per_block;
+  for (long row0 = blockIdx.x * rows_per_block + threadIdx.x / G; row0 < M; row0 += RPI * stride) {
+    float xv[RPI][E];
 #pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      const int c = (v * G + lane_g) * VEC;
-      if (valid[v]) {
-        load_vec<T, VEC>(xr + c, xv + v * VEC);
-      } else {
+    for (int q = 0; q < RPI; ++q) {
+      const long row = min(row0 + q * stride, M - 1);
 #pragma unroll
-        for (int i = 0; i < VEC; ++i) xv[v * VEC + i] = 0.f;
-      }
-#pragma unroll
-      for (int i = 0; i < VEC; ++i) s += xv[v * VEC + i];
+      for (int v = 0; v < NV; ++v) load_vec<T, VEC>(x + row * C + min((v * G + lane_g) * VEC, C - VEC), xv[q] + v * VEC);
     }
-    const float mu = group_sum<G>(s) * invC;
-    float ss = 0.f;
 #pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      if (valid[v]) {
+    for (int q = 0; q < RPI; ++q) {
+      const long row = row0 + q * stride;
+      if (row >= M) break;
+      float s = 0.f;
+#pragma unroll
+      for (int v = 0; v < NV; ++v)
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) s += valid[v] ? xv[q][v * VEC + i] : 0.f;
+      const float mu = group_sum<G>(s) * invC;
+      float ss = 0.f;
+#pragma unroll
+      for (int v = 0; v < NV; ++v)
 #pragma unroll
         for (int i = 0; i < VEC; ++i) {
-          const float d = xv[v * VEC + i] - mu;
+          const float d = valid[v] ? xv[q][v * VEC + i] - mu : 0.f;
           ss = fmaf(d, d, ss);
         }
-      }
-    }
-    const float rs = rsqrtf(group_sum<G>(ss) * invC + eps);
-    T* yr = y + row * C;
+      const float rs = rsqrtf(group_sum<G>(ss) * invC + eps);
+      T* yr = y + row * C;
 #pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      const int c = (v * G + lane_g) * VEC;
-      if (valid[v]) {
-        float o[VEC];
+      for (int v = 0; v < NV; ++v) {
+        const int c = (v * G + lane_g) * VEC;
+        if (valid[v]) {
+          float o[VEC];
 #pragma unroll
-        for (int i = 0; i < VEC; ++i) o[i] = (xv[v * VEC + i] - mu) * rs * gw[v * VEC + i] + bw[v * VEC + i];
-        store_vec<T, VEC>(yr + c, o);
+          for (int i = 0; i < VEC; ++i) o[i] = (xv[q][v * VEC + i] - mu) * rs * gw[v * VEC + i] + bw[v * VEC + i];
+          store_vec<T, VEC>(yr + c, o);
+        }
       }
-    }
-    if (lane_g == 0) {
-      if (mean_out) mean_out[row] = mu;
-      if (rstd_out) rstd_out[row] = rs;
+      if (lane_g == 0) {
+        if (mean_out) mean_out[row] = mu;
+        if (rstd_out) rstd_out[row] = rs;
+      }
     }
   }
 }

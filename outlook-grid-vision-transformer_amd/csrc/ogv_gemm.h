@@ -166,5 +166,6 @@ void set_grid_mfma(int v);
 void set_dw_blocks(int v);
 void set_mb_side(int v);
 void set_ln_bwd_blocks(int v);
+void set_gemm_bn64(int v);
 
 }  // namespace ogv

@@ -974,10 +974,16 @@ static void launch_mm(const void* A, int lda, const Pro& pro, const float* Wt, i
                                                              M, N, K, Ka, Kb, nMt, nNt, ConvG());
 }
 
+// 128-wide column tiles unless that leaves a half-empty last tile (N = 192, 576: 64-wide tiles
+// waste nothing and give more blocks).  Knob "gemm_bn64" (default 1) turns the rule off.
+static int g_gemm_bn64 = 1;
+void set_gemm_bn64(int v) { g_gemm_bn64 = v; }
+static bool wide_cols(int N) { return N > 64 && !(g_gemm_bn64 && N % 128 != 0 && N % 128 <= 64); }
+
 template <typename T, bool PRO, bool STATS>
 static void launch_mm_bn(const void* A, int lda, const Pro& pro, const float* Wt, int ldw, void* out, int ldo, int M,
                          int N, int K, int Ka, int Kb, const Epi& epi, hipStream_t s) {
-  if (N > 64)
+  if (wide_cols(N))
     launch_mm<T, 128, PRO, STATS>(A, lda, pro, Wt, ldw, out, ldo, M, N, K, Ka, Kb, epi, s);
   else
     launch_mm<T, 64, PRO, STATS>(A, lda, pro, Wt, ldw, out, ldo, M, N, K, Ka, Kb, epi, s);
@@ -1187,10 +1193,10 @@ void gemm_dgrad_launch(ogv_dtype dt, const void* dout, int ldd, const float* W, 
   // dA[M,K] = dout[M,N] . W[N,K]: W read as [reduction N][output K] (no transposed copy)
   if (dt == OGV_BF16 && sgemm_dgrad_try(dout, ldd, W, dA, lda, M, N, K, e, s)) return;
   if (dt == OGV_BF16) {
-    if (K > 64) launch_mm_bt<bf16, 128>(dout, ldd, W, K, dA, lda, M, K, N, e, s);
+    if (wide_cols(K)) launch_mm_bt<bf16, 128>(dout, ldd, W, K, dA, lda, M, K, N, e, s);
     else launch_mm_bt<bf16, 64>(dout, ldd, W, K, dA, lda, M, K, N, e, s);
   } else {
-    if (K > 64) launch_mm_bt<float, 128>(dout, ldd, W, K, dA, lda, M, K, N, e, s);
+    if (wide_cols(K)) launch_mm_bt<float, 128>(dout, ldd, W, K, dA, lda, M, K, N, e, s);
     else launch_mm_bt<float, 64>(dout, ldd, W, K, dA, lda, M, K, N, e, s);
   }
 }

@@ -223,6 +223,12 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
 
   uint4 ra[A_VECS];
   float4 rb[B_F4];
+  // prologue parameters of the staged A chunks, fetched with the tile (not by the staging pass,
+  // whose own loads would wait behind the next tile's prefetch): this thread's k chunk is the same
+  // for all its A_VECS rows (256 % (BK/8) == 0)
+  constexpr bool PV = PRO && AM == 0;
+  float psc[PV ? 8 : 1], psh[PV ? 8 : 1], pgt[PV ? A_VECS : 1][8];
+  bool pvec = false;
   const bool a_vec = ((lda & 7) == 0) && ((reinterpret_cast<uintptr_t>(A) & 15) == 0);
   const bool b_vec = ((ldw & 3) == 0) && ((reinterpret_cast<uintptr_t>(Wt) & 15) == 0);
   ConvRow crow[AM ? A_VECS : 1];
@@ -257,6 +263,16 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
           }
         }
         continue;
+      }
+      if constexpr (PV) {
+        if (i == 0) {
+          pvec = gk + 8 <= Ka && (gk & 3) == 0 && (pro.gld & 3) == 0;
+#pragma unroll
+          for (int t = 0; t < 8; ++t) { psc[t] = 1.f; psh[t] = 0.f; }
+          if (pvec && pro.sc) load_vec<float, 8>(pro.sc + gk, psc);
+          if (pvec && pro.sh) load_vec<float, 8>(pro.sh + gk, psh);
+        }
+        if (pvec && pro.gate && gm < M) load_vec<float, 8>(pro.gate + (long)(gm / pro.rps) * pro.gld + gk, pgt[i]);
       }
       if (gm < M) {
         const bf16* src = A + (long)gm * lda + gk;
@@ -316,7 +332,19 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
           float f[8];
 #pragma unroll
           for (int q = 0; q < 8; ++q) f[q] = (float)e[q];
-          pro_apply_run<8>(pro, f, gm, gk, Ka);
+          if constexpr (PV) {
+            if (pvec) {
+#pragma unroll
+              for (int q = 0; q < 8; ++q) {
+                f[q] = act_fwd(pro.act, fmaf(f[q], psc[q], psh[q]));
+                if (pro.gate) f[q] *= pgt[i][q];
+              }
+            } else {
+              pro_apply_run<8>(pro, f, gm, gk, Ka);
+            }
+          } else {
+            pro_apply_run<8>(pro, f, gm, gk, Ka);
+          }
 #pragma unroll
           for (int q = 0; q < 8; ++q) e[q] = gk + q < Ka ? (bf16)f[q] : (bf16)0.f;
         }
@@ -627,11 +655,26 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(const bf16* __restrict_
   const bool g_vec = ((ldg & 7) == 0) && ((reinterpret_cast<uintptr_t>(G) & 15) == 0) && n0 + gc8 + 8 <= N;
   const bool x_vec = ((ldx & 7) == 0) && ((reinterpret_cast<uintptr_t>(X) & 15) == 0) && k0 + xc8 + 8 <= K;
   uint4 gr[GV], xr[XV];
+  // Everything the staging pass multiplies in is fetched with the tile (row scales, SE gate) or once
+  // per block (per-column BN scale / shift): the staging pass issues no global load of its own, which
+  // would otherwise wait behind the next tile's prefetch (vmcnt retires in issue order).
+  float rsv[GV];
+  const int pk = k0 + xc8;
+  const bool pvec = PRO && pk + 8 <= K && (pk & 3) == 0 && (pro.gld & 3) == 0;
+  float psc[8], psh[8], gtv[PRO ? XV : 1][8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) { psc[t] = 1.f; psh[t] = 0.f; }
+  if constexpr (PRO) {
+    if (pvec && pro.sc) load_vec<float, 8>(pro.sc + pk, psc);
+    if (pvec && pro.sh) load_vec<float, 8>(pro.sh + pk, psh);
+  }
   auto load = [&](int m0) {
 #pragma unroll
     for (int i = 0; i < GV; ++i) {
       const int gm = m0 + grow + i * (256 / GC);
       gr[i] = uint4{0u, 0u, 0u, 0u};
+      rsv[i] = 1.f;
+      if (rs && gm < mend) rsv[i] = rs[gm / rps];
       if (gm < mend) {
         const bf16* src = G + (long)gm * ldg + n0 + gc8;
         if (g_vec) gr[i] = *reinterpret_cast<const uint4*>(src);
@@ -666,6 +709,9 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(const bf16* __restrict_
         }
         continue;
       }
+      if constexpr (PRO) {
+        if (pvec && pro.gate && gm < mend) load_vec<float, 8>(pro.gate + (long)(gm / pro.rps) * pro.gld + pk, gtv[i]);
+      }
       if (gm < mend) {
         const bf16* src = X + (long)gm * ldx + k0 + xc8;
         if (x_vec) xr[i] = *reinterpret_cast<const uint4*>(src);
@@ -684,9 +730,8 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(const bf16* __restrict_
       uint4 v = gr[i];
       bf16* e = reinterpret_cast<bf16*>(&v);
       if (rs && m0 + r < mend) {
-        const float sc = rs[(m0 + r) / rps];
 #pragma unroll
-        for (int t = 0; t < 8; ++t) e[t] = (bf16)((float)e[t] * sc);
+        for (int t = 0; t < 8; ++t) e[t] = (bf16)((float)e[t] * rsv[i]);
       }
       if (do_bias) {
 #pragma unroll
@@ -705,7 +750,15 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(const bf16* __restrict_
           float f[8];
 #pragma unroll
           for (int t = 0; t < 8; ++t) f[t] = (float)e[t];
-          pro_apply_run<8>(pro, f, gm, k0 + xc8, K);
+          if (pvec) {
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+              f[t] = act_fwd(pro.act, fmaf(f[t], psc[t], psh[t]));
+              if (pro.gate) f[t] *= gtv[i][t];
+            }
+          } else {
+            pro_apply_run<8>(pro, f, gm, k0 + xc8, K);
+          }
 #pragma unroll
           for (int t = 0; t < 8; ++t) e[t] = k0 + xc8 + t < K ? (bf16)f[t] : (bf16)0.f;
         }

@@ -7,7 +7,8 @@ import collections
 import csv
 import sys
 
-KEYS = ("dw_fwd", "dw_dgrad", "dw_wgrad", "se_bwd_reduce", "se_pool", "bn2_apply", "bn_bwd_apply", "sgemm", "gemm_bf16")
+KEYS = ("dw_fwd", "dw_dgrad", "dw_wgrad", "se_bwd_reduce", "se_pool", "se_mlp_fwd", "se_mlp_bwd", "wgrad_f32", "bn2_apply",
+        "bn_bwd_apply", "sgemm", "gemm_bf16")
 
 
 def main(path):

@@ -104,6 +104,31 @@ def drop_path_scale(dp: nn.Module, x: torch.Tensor):
     p = float(getattr(dp, "drop_prob", 0.0))
     if p <= 0.0 or not dp.training:
         return None
+    pre = getattr(dp, "_ogv_scale", None)  # drawn for the whole forward by draw_drop_path_scales
+    if pre is not None and pre.shape[0] == x.shape[0]:
+        dp._ogv_scale = None
+        return pre
     keep = 1.0 - p
     mask = torch.empty((x.shape[0],), device=x.device, dtype=torch.float32).bernoulli_(keep)
     return mask / keep
+
+
+_KEEP_CACHE = {}
+
+
+def draw_drop_path_scales(modules, batch: int, device) -> None:
+    """One draw for every live DropPath of a forward pass: row i of (floor(U + keep_i) / keep_i),
+    U ~ Uniform[0,1)^(n x B), is module i's per-sample factor — the same Bernoulli(keep) / keep law
+    as each module drawing its own mask (src/model/Outlook_Block.py:15-22), in four launches per
+    step instead of two per module.  Each row is consumed by that module's next drop_path_scale."""
+    live = [m for m in modules if float(getattr(m, "drop_prob", 0.0)) > 0.0 and m.training]
+    if len(live) < 2:
+        return
+    key = (str(device), tuple(float(m.drop_prob) for m in live))
+    keep = _KEEP_CACHE.get(key)
+    if keep is None:  # built on the first (eager) step, reused inside captured graphs
+        keep = _KEEP_CACHE[key] = torch.tensor([[1.0 - p] for p in key[1]], dtype=torch.float32, device=device)
+    u = torch.rand((len(live), batch), dtype=torch.float32, device=device)
+    scales = u.add_(keep).floor_().div_(keep)
+    for i, m in enumerate(live):
+        m._ogv_scale = scales[i]

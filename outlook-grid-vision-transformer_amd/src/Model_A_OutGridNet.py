@@ -15,7 +15,7 @@ from src.model.downsampling import Downsample, DownsampleConfig
 from src.model.stem_head import ConvStem, List, make_dpr
 from src.stage_config import StageCfg
 import torch.nn as nn
-from ogv.layers import BatchNorm2d, Conv1x1
+from ogv.layers import BatchNorm2d, Conv1x1, draw_drop_path_scales
 
 
 class MaxOutNet(nn.Module):
@@ -39,6 +39,12 @@ class MaxOutNet(nn.Module):
         self.classifier = nn.Linear(stages[-1].dim, num_classes)
 
     def forward(self, x):
+        if self.training:  # every block's DropPath factors in one draw (ogv.layers.draw_drop_path_scales)
+            dps = getattr(self, "_ogv_droppaths", None)
+            if dps is None:
+                from src.model.Outlook_Block import DropPath
+                dps = self._ogv_droppaths = [m for m in self.modules() if isinstance(m, DropPath)]
+            draw_drop_path_scales(dps, x.shape[0], x.device)
         x = self.proj_in(self.stem(x))
         for si, blocks in enumerate(self.stages):
             for blk in blocks:

@@ -623,7 +623,7 @@ def conv3x3_bn_act(x, conv, bn=None, act=None):
     geom = (int(B), int(H), int(W), int(Cin), int(Cout), int(stride), has_bn, train, eps, mom, ACT[act])
     y = _ConvBN.apply(x2d, geom, rm, rv, f32(conv.weight).contiguous(), f32(conv.bias),
                       f32(bn.weight) if has_bn else None, f32(bn.bias) if has_bn else None)
-    if has_bn and train:
+    if has_bn and train and not getattr(bn, "_ogv_nbt_pooled", False):
         bn.num_batches_tracked.add_(1)
     return rows_to_nchw(y, B, (H - 1) // stride + 1, (W - 1) // stride + 1)
 
@@ -669,6 +669,6 @@ def batchnorm_act_nchw(x, bn, act=None):
     x2d = _rows_contig(nchw_to_rows(x.to(compute_dtype(x))))
     y = _BNAct.apply(x2d, (train, eps, mom, ACT[act]), rm, rv, f32(bn.weight) if bn.affine else None,
                      f32(bn.bias) if bn.affine else None)
-    if train:
+    if train and not getattr(bn, "_ogv_nbt_pooled", False):
         bn.num_batches_tracked.add_(1)
     return rows_to_nchw(y, B, H, W)

@@ -14,6 +14,7 @@ from src.model.Out_Grid_Block import OutGridBlock
 from src.model.downsampling import Downsample, DownsampleConfig
 from src.model.stem_head import ConvStem, List, make_dpr
 from src.stage_config import StageCfg
+import torch
 import torch.nn as nn
 from ogv.layers import BatchNorm2d, Conv1x1, draw_drop_path_scales
 
@@ -45,6 +46,15 @@ class MaxOutNet(nn.Module):
                 from src.model.Outlook_Block import DropPath
                 dps = self._ogv_droppaths = [m for m in self.modules() if isinstance(m, DropPath)]
             draw_drop_path_scales(dps, x.shape[0], x.device)
+            # every BatchNorm counter of the model in one multi-tensor add (the modules skip theirs)
+            bns = getattr(self, "_ogv_bns", None)
+            if bns is None:
+                bns = self._ogv_bns = [m for m in self.modules() if isinstance(m, nn.modules.batchnorm._BatchNorm)
+                                       and m.track_running_stats and m.num_batches_tracked is not None]
+                for m in bns:
+                    m._ogv_nbt_pooled = True
+            if bns and bns[0].training:
+                torch._foreach_add_([m.num_batches_tracked for m in bns], 1)
         x = self.proj_in(self.stem(x))
         for si, blocks in enumerate(self.stages):
             for blk in blocks:

@@ -113,7 +113,7 @@ class MBConv(nn.Module):
             buffers = {"bn1_rm": bn1.running_mean, "bn1_rv": bn1.running_var, "bn2_rm": bn2.running_mean,
                        "bn2_rv": bn2.running_var, "bn3_rm": bn3.running_mean, "bn3_rv": bn3.running_var}
             train = bn1.training
-            if train:  # one multi-tensor launch for the three BN counters
+            if train and not getattr(bn1, "_ogv_nbt_pooled", False):  # one multi-tensor launch
                 torch._foreach_add_([bn1.num_batches_tracked, bn2.num_batches_tracked,
                                      bn3.num_batches_tracked], 1)
             return OF.mbconv_fused(x, B, H, W, e.out_channels, self.se.fc1.out_channels, train, bn1.eps,
@@ -121,4 +121,8 @@ class MBConv(nn.Module):
         # the stock-op parts (BN, depthwise, SE) follow the activation dtype even outside autocast
         with torch.autocast("cuda", dtype=torch.bfloat16, enabled=(dt == torch.bfloat16 and x.is_cuda)):
             h = self.project(self.se(self.depthwise(self.expand(x))))
+        bns = (self.expand[1], self.depthwise[1], self.project[1])
+        if bns[0].training and getattr(bns[0], "_ogv_nbt_pooled", False):
+            # stock BatchNorm2d counted itself; the model-level pooled add counted it too
+            torch._foreach_add_([b.num_batches_tracked for b in bns if isinstance(b, nn.BatchNorm2d)], -1)
         return x + self.drop_path(h) if self.use_res else h

@@ -79,6 +79,80 @@ __global__ void bn_coeffs_kernel(const float* __restrict__ S, int K, float n, co
   coef[2 * K + c] = train ? sdyx / n : 0.f;
 }
 
+// Fused column reduction + finalize / coefficients: a block owns 16 channels, its 16 row groups walk
+// the [R][ld] partial rows (columns c and K + c) in a fixed order, combined in a fixed order in LDS;
+// one launch instead of colreduce + bn_finalize / bn_coeffs.
+__global__ __launch_bounds__(256) void bn_reduce_finalize_kernel(const double* __restrict__ part, long R, long ld, int K,
+                                                                 double n, const float* __restrict__ gamma,
+                                                                 const float* __restrict__ beta, float eps,
+                                                                 float momentum, float* rm, float* rv,
+                                                                 float* __restrict__ mean_out,
+                                                                 float* __restrict__ invstd_out, float* __restrict__ sc,
+                                                                 float* __restrict__ sh) {
+  __shared__ double red[2][16][16];
+  const int cl = threadIdx.x & 15, rg = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
+  double s1 = 0.0, s2 = 0.0;
+  if (c < K)
+    for (long r = rg; r < R; r += 16) {
+      s1 += part[r * ld + c];
+      s2 += part[r * ld + K + c];
+    }
+  red[0][rg][cl] = s1;
+  red[1][rg][cl] = s2;
+  __syncthreads();
+  if (rg != 0 || c >= K) return;
+  double t1 = 0.0, t2 = 0.0;
+#pragma unroll
+  for (int g = 0; g < 16; ++g) {
+    t1 += red[0][g][cl];
+    t2 += red[1][g][cl];
+  }
+  const double m1 = t1 / n, m2 = t2 / n;
+  const float mean = (float)((double)rm[c] + m1);
+  const double v = m2 - m1 * m1;
+  const float var = (float)(v > 0.0 ? v : 0.0);
+  rm[c] = (1.f - momentum) * rm[c] + momentum * mean;
+  rv[c] = (1.f - momentum) * rv[c] + momentum * (float)(var * (n / (n > 1.0 ? n - 1.0 : 1.0)));
+  const float is = rsqrtf(var + eps);
+  const float gm = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+  mean_out[c] = mean;
+  invstd_out[c] = is;
+  sc[c] = gm * is;
+  sh[c] = bt - mean * gm * is;
+}
+
+__global__ __launch_bounds__(256) void bn_reduce_coeffs_kernel(const float* __restrict__ part, long R, long ld, int K,
+                                                               float n, const float* __restrict__ gamma,
+                                                               const float* __restrict__ invstd,
+                                                               float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                               float* __restrict__ coef, int train) {
+  __shared__ float red[2][16][16];
+  const int cl = threadIdx.x & 15, rg = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
+  float s1 = 0.f, s2 = 0.f;
+  if (c < K)
+    for (long r = rg; r < R; r += 16) {
+      s1 += part[r * ld + c];
+      s2 += part[r * ld + K + c];
+    }
+  red[0][rg][cl] = s1;
+  red[1][rg][cl] = s2;
+  __syncthreads();
+  if (rg != 0 || c >= K) return;
+  float sdy = 0.f, sdyx = 0.f;
+#pragma unroll
+  for (int g = 0; g < 16; ++g) {
+    sdy += red[0][g][cl];
+    sdyx += red[1][g][cl];
+  }
+  if (dgamma) dgamma[c] = sdyx;
+  if (dbeta) dbeta[c] = sdy;
+  coef[c] = (gamma ? gamma[c] : 1.f) * invstd[c];
+  coef[K + c] = train ? sdy / n : 0.f;
+  coef[2 * K + c] = train ? sdyx / n : 0.f;
+}
+
 void bn_finalize_launch(const double* sums, int K, double n, const float* gamma, const float* beta, float eps,
                         float momentum, float* rm, float* rv, float* mean, float* invstd, float* sc, float* sh, int train,
                         hipStream_t s) {
@@ -1217,20 +1291,24 @@ static void mbconv_fwd_impl(const void* x, void* out, const Saved& sv, const Fwd
     Epi e;
     if (tr) { e.stat = w.stat1; e.stat_shift = P.bn1_rm; }
     const int R = gemm_fwd_launch(dt, x, s.C, Pro(), P.w_expand, s.C, sv.e, s.mid, (int)M, s.mid, s.C, s.C, s.C, e, st);
-    if (tr) colreduce(w.stat1, w.sums, R, 2L * s.mid, 2L * s.mid, w.tmp, st);
-    bn_finalize_kernel<<<cdiv(s.mid, 256), 256, 0, st>>>(w.sums, s.mid, (double)M, P.bn1_w, P.bn1_b, s.bn_eps,
-                                                         s.bn_momentum, P.bn1_rm, P.bn1_rv, sv.mean1, sv.inv1, sv.sc1,
-                                                         sv.sh1, s.train);
+    if (tr)
+      bn_reduce_finalize_kernel<<<cdiv(s.mid, 16), 256, 0, st>>>(w.stat1, R, 2L * s.mid, s.mid, (double)M, P.bn1_w, P.bn1_b,
+                                                        s.bn_eps, s.bn_momentum, P.bn1_rm, P.bn1_rv, sv.mean1, sv.inv1, sv.sc1, sv.sh1);
+    else
+      bn_finalize_kernel<<<cdiv(s.mid, 256), 256, 0, st>>>(w.sums, s.mid, (double)M, P.bn1_w, P.bn1_b, s.bn_eps, s.bn_momentum,
+                                                         P.bn1_rm, P.bn1_rv, sv.mean1, sv.inv1, sv.sc1, sv.sh1, 0);
   }
   // 2) depthwise conv on act(BN1(e)) (+ BN2 stats)
   {
     const DwTile t = dw_tile_plan(s.B, s.H, s.W, s.mid, 4);
     O::dw_fwd(sv.e, P.w_dw, sv.sc1, sv.sh1, s.act, sv.d, tr ? w.stat2 : nullptr,
                      tr ? P.bn2_rm : nullptr, t, st);
-    if (tr) colreduce(w.stat2, w.sums, t.rows(), 2L * s.mid, 2L * s.mid, w.tmp, st);
-    bn_finalize_kernel<<<cdiv(s.mid, 256), 256, 0, st>>>(w.sums, s.mid, (double)M, P.bn2_w, P.bn2_b, s.bn_eps,
-                                                         s.bn_momentum, P.bn2_rm, P.bn2_rv, sv.mean2, sv.inv2, sv.sc2,
-                                                         sv.sh2, s.train);
+    if (tr)
+      bn_reduce_finalize_kernel<<<cdiv(s.mid, 16), 256, 0, st>>>(w.stat2, t.rows(), 2L * s.mid, s.mid, (double)M, P.bn2_w, P.bn2_b,
+                                                        s.bn_eps, s.bn_momentum, P.bn2_rm, P.bn2_rv, sv.mean2, sv.inv2, sv.sc2, sv.sh2);
+    else
+      bn_finalize_kernel<<<cdiv(s.mid, 256), 256, 0, st>>>(w.sums, s.mid, (double)M, P.bn2_w, P.bn2_b, s.bn_eps, s.bn_momentum,
+                                                         P.bn2_rm, P.bn2_rv, sv.mean2, sv.inv2, sv.sc2, sv.sh2, 0);
   }
   // 3) Squeeze-Excite gate (B rows)
   {
@@ -1257,10 +1335,12 @@ static void mbconv_fwd_impl(const void* x, void* out, const Saved& sv, const Fwd
     Epi e;
     if (tr) { e.stat = w.stat3; e.stat_shift = P.bn3_rm; }
     const int R = gemm_fwd_launch(dt, sv.d, s.mid, pr, P.w_proj, s.mid, sv.p, s.C, (int)M, s.C, s.mid, s.mid, s.mid, e, st);
-    if (tr) colreduce(w.stat3, w.sums, R, 2L * s.C, 2L * s.C, w.tmp, st);
-    bn_finalize_kernel<<<cdiv(s.C, 256), 256, 0, st>>>(w.sums, s.C, (double)M, P.bn3_w, P.bn3_b, s.bn_eps,
-                                                       s.bn_momentum, P.bn3_rm, P.bn3_rv, sv.mean3, sv.inv3, sv.sc3,
-                                                       sv.sh3, s.train);
+    if (tr)
+      bn_reduce_finalize_kernel<<<cdiv(s.C, 16), 256, 0, st>>>(w.stat3, R, 2L * s.C, s.C, (double)M, P.bn3_w, P.bn3_b,
+                                                        s.bn_eps, s.bn_momentum, P.bn3_rm, P.bn3_rv, sv.mean3, sv.inv3, sv.sc3, sv.sh3);
+    else
+      bn_finalize_kernel<<<cdiv(s.C, 256), 256, 0, st>>>(w.sums, s.C, (double)M, P.bn3_w, P.bn3_b, s.bn_eps, s.bn_momentum,
+                                                         P.bn3_rm, P.bn3_rv, sv.mean3, sv.inv3, sv.sc3, sv.sh3, 0);
     OGV_V_DISPATCH(rc.V, O::template affine_res, x, sv.p, sv.sc3, sv.sh3, out, M, s.C, st);
   }
 }
@@ -1277,9 +1357,8 @@ static void mbconv_bwd_impl(const void* dout, const void* x, const Saved& sv, vo
   {
     const long S = dw_slices(M, rc), per = (M + S - 1) / S;
     OGV_V_DISPATCH(rc.V, O::template bn_reduce, dout, sv.p, sv.mean3, sv.inv3, w.stat, M, s.C, rc, S, per, st);
-    colreduce(w.stat, w.S, S, 2L * s.C, 2L * s.C, w.tmp, st);
-    bn_coeffs_kernel<<<cdiv(s.C, 256), 256, 0, st>>>(w.S, s.C, (float)M, P.bn3_w, sv.inv3, G.bn3_w, G.bn3_b, w.coef,
-                                                     s.train);
+    bn_reduce_coeffs_kernel<<<cdiv(s.C, 16), 256, 0, st>>>(w.stat, S, 2L * s.C, s.C, (float)M, P.bn3_w, sv.inv3, G.bn3_w,
+                                                          G.bn3_b, w.coef, s.train);
     OGV_V_DISPATCH(rc.V, O::template bn_apply, dout, sv.p, sv.mean3, sv.inv3, w.coef, w.dp, M, s.C, st);
   }
   // B2) project: dA3 = dp . Wp ; dWp = dp^T . (act(BN2(d)) * gate)   (dWp on the side stream)
@@ -1324,9 +1403,8 @@ static void mbconv_bwd_impl(const void* dout, const void* x, const Saved& sv, vo
   // B5) BN2 backward: dd = ca*(dy2 - cb - dhat*cc)  -> bufB
   {
     bn2_terms_kernel<<<cdiv((long)s.B * s.mid, 256), 256, 0, st>>>(w.R, sv.gate, w.dpool, w.terms, s.B, HW, s.mid);
-    colreduce(w.terms, w.S, s.B, 2L * s.mid, 2L * s.mid, w.tmp, st);
-    bn_coeffs_kernel<<<cdiv(s.mid, 256), 256, 0, st>>>(w.S, s.mid, (float)M, P.bn2_w, sv.inv2, G.bn2_w, G.bn2_b,
-                                                       w.coef, s.train);
+    bn_reduce_coeffs_kernel<<<cdiv(s.mid, 16), 256, 0, st>>>(w.terms, s.B, 2L * s.mid, s.mid, (float)M, P.bn2_w, sv.inv2,
+                                                            G.bn2_w, G.bn2_b, w.coef, s.train);
     OGV_V_DISPATCH(rp.V, O::template bn2_apply, w.bufA, sv.d, sv.sc2, sv.sh2, sv.mean2, sv.inv2, sv.gate, w.dpool,
                    w.coef, s.act, w.bufB, M, HW, s.mid, st);
   }
@@ -1340,12 +1418,14 @@ static void mbconv_bwd_impl(const void* dout, const void* x, const Saved& sv, vo
     tapmajor_to_chan_kernel<<<cdiv(9 * s.mid, 256), 256, 0, sd>>>(w.sums9, G.w_dw, s.mid);
     O::dw_dgrad(w.bufB, P.w_dw, sv.e, sv.sc1, sv.sh1, sv.mean1, sv.inv1, s.act,
                      w.bufA, w.stat, t, st);
-    colreduce(w.stat, w.S, t.rows(), 2L * s.mid, 2L * s.mid, w.tmp, st);
   }
   join_side(st, sd);  // B7 overwrites bufB
   // B7) BN1 backward: de = ca*(dy1 - cb - ehat*cc) -> bufB
-  bn_coeffs_kernel<<<cdiv(s.mid, 256), 256, 0, st>>>(w.S, s.mid, (float)M, P.bn1_w, sv.inv1, G.bn1_w, G.bn1_b, w.coef,
-                                                     s.train);
+  {
+    const long R1 = dw_tile_plan(s.B, s.H, s.W, s.mid, 4).rows();
+    bn_reduce_coeffs_kernel<<<cdiv(s.mid, 16), 256, 0, st>>>(w.stat, R1, 2L * s.mid, s.mid, (float)M, P.bn1_w, sv.inv1,
+                                                            G.bn1_w, G.bn1_b, w.coef, s.train);
+  }
   OGV_V_DISPATCH(rp.V, O::template bn_apply, w.bufA, sv.e, sv.mean1, sv.inv1, w.coef, w.bufB, M, s.mid, st);
   // B8) expand: dx = de . We + dout (residual) ; dWe = de^T . x
   sd = fork_side(st);  // dWe on the side stream, overlapping dx

@@ -167,5 +167,6 @@ void set_dw_blocks(int v);
 void set_mb_side(int v);
 void set_ln_bwd_blocks(int v);
 void set_gemm_bn64(int v);
+void set_grid_lds(int v);
 
 }  // namespace ogv

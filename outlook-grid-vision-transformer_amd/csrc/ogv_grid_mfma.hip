@@ -370,12 +370,327 @@ __global__ __launch_bounds__(256) void grid_mfma_dkv_kernel(const bf16* __restri
 }
 
 // ------------------------------------------------------------------------------------------------
+// LDS-resident variants: a block owns PP (group, head) pairs and first stages the pair's whole
+// K/V (fwd, dQ) or Q/dO (+ lse, delta: dK/dV) into LDS once; its 4 waves then walk the pair's
+// 16-row blocks against it.  The per-row-block kernels above re-read those operands from global
+// memory for every row block and every 16-token chunk (a global-latency chain per chunk); here the
+// chunk loop runs entirely out of LDS.  Used when the tiles fit in 64 KB (N <= ~300 for hd <= 32).
+struct GmLds {
+  int PP, nrb, Np;      // pairs per block, 16-row blocks per pair, padded tokens
+  long pairs, blocks;
+  size_t tile_elems;    // one [Np][PITCH] tile
+};
+template <int HDP>
+static GmLds gm_lds_plan(const GridGeomM& G) {
+  GmLds p;
+  p.nrb = (G.N + 15) / 16;
+  p.Np = p.nrb * 16;
+  p.PP = p.nrb >= 4 ? 1 : 4 / p.nrb;
+  p.pairs = (long)G.B * G.g * G.g * G.heads;
+  p.blocks = (p.pairs + p.PP - 1) / p.PP;
+  p.tile_elems = (size_t)p.Np * gm_pitch<HDP>();
+  return p;
+}
+template <int HDP>
+static size_t gm_lds_bytes(const GmLds& p, bool stats) {
+  return (size_t)p.PP * (2 * p.tile_elems * sizeof(bf16) + (stats ? 2 * p.Np * sizeof(float) : 0)) +
+         4 * 16 * gm_pitch<HDP>() * sizeof(bf16);
+}
+
+// all 256 threads: tokens [0, Np) x head dims of one pair from base (row stride ld) into tile
+template <int HDP>
+__device__ __forceinline__ void gm_stage_pair(bf16* tile, const bf16* __restrict__ base, long ld, const GridGeomM& G,
+                                              long grp, int Np) {
+  constexpr int PIECES = HDP / 8, PITCH = gm_pitch<HDP>();
+  for (int idx = threadIdx.x; idx < Np * PIECES; idx += 256) {
+    const int row = idx / PIECES, pc = idx - row * PIECES;
+    const bool ok = row < G.N && pc * 8 < G.hd;
+    const bf16x8 v = gm_load8(base + (ok ? G.pixel(grp, row) : 0) * ld + pc * 8, ok);
+    *reinterpret_cast<bf16x8*>(tile + row * PITCH + pc * 8) = v;
+  }
+}
+
+template <int HDP>
+__global__ __launch_bounds__(256) void grid_lds_fwd_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
+                                                           float* __restrict__ lse, GridGeomM G, float scale, GmLds L) {
+  constexpr int KK = HDP / 32, ND = HDP / 16, PITCH = gm_pitch<HDP>();
+  extern __shared__ __attribute__((aligned(16))) bf16 gsm[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const long C3 = 3L * G.C;
+  const long pair0 = (long)blockIdx.x * L.PP;
+  for (int p = 0; p < L.PP; ++p) {
+    const long pr = pair0 + p;
+    if (pr >= L.pairs) break;
+    const int h = (int)(pr % G.heads);
+    const long grp = pr / G.heads;
+    bf16* Ks = gsm + (size_t)p * 2 * L.tile_elems;
+    gm_stage_pair<HDP>(Ks, qkv + G.C + h * G.hd, C3, G, grp, L.Np);
+    gm_stage_pair<HDP>(Ks + L.tile_elems, qkv + 2 * G.C + h * G.hd, C3, G, grp, L.Np);
+  }
+  __syncthreads();
+  bf16* tile = gsm + (size_t)L.PP * 2 * L.tile_elems + wave * 16 * PITCH;
+  for (int it = wave; it < L.PP * L.nrb; it += 4) {
+    const int p = it / L.nrb, qb = it - p * L.nrb;
+    const long pr = pair0 + p;
+    if (pr >= L.pairs) break;
+    const int h = (int)(pr % G.heads);
+    const long grp = pr / G.heads;
+    const bf16* Ks = gsm + (size_t)p * 2 * L.tile_elems;
+    const bf16* Vs = Ks + L.tile_elems;
+    const int qtok = qb * 16 + fr;
+    const bool qok = qtok < G.N;
+    const long qpix = qok ? G.pixel(grp, qtok) : 0;
+    bf16x8 qf[KK];
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      const int d = kk * 32 + fg * 8;
+      qf[kk] = gm_load8(qkv + h * G.hd + qpix * C3 + d, qok && d < G.hd);
+    }
+    f32x4 o[ND];
+#pragma unroll
+    for (int j = 0; j < ND; ++j) o[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float m = -INFINITY, l = 0.f;
+    for (int k0 = 0; k0 < G.N; k0 += 16) {
+      f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) {
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks + (k0 + fr) * PITCH + kk * 32 + fg * 8);
+        s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[kk], s, 0, 0, 0);
+      }
+      float x[4], mc = -INFINITY;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        x[r] = (k0 + 4 * fg + r < G.N) ? s[r] * scale : -INFINITY;
+        mc = fmaxf(mc, x[r]);
+      }
+      mc = fmaxf(mc, __shfl_xor(mc, 16, 64));
+      mc = fmaxf(mc, __shfl_xor(mc, 32, 64));
+      const float mn = fmaxf(m, mc);
+      const float corr = __expf(m - mn);
+      float pw[4], ps = 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        pw[r] = __expf(x[r] - mn);
+        ps += pw[r];
+      }
+      ps += __shfl_xor(ps, 16, 64);
+      ps += __shfl_xor(ps, 32, 64);
+      l = l * corr + ps;
+      m = mn;
+      float cr[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) cr[r] = __shfl(corr, 4 * fg + r, 64);
+#pragma unroll
+      for (int j = 0; j < ND; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[j][r] *= cr[r];
+      const gm_s16x4 pa = pack4(pw);
+#pragma unroll
+      for (int j = 0; j < ND; ++j) {
+        const gm_s16x4 vb = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (gm_lds_s16x4*)(Vs + (k0 + 4 * fg + (fr >> 2)) * PITCH + j * 16 + (fr & 3) * 4));
+        o[j] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(pa, vb, o[j], 0, 0, 0);
+      }
+    }
+    float inv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) inv[r] = 1.f / __shfl(l, 4 * fg + r, 64);
+    gm_store<HDP>(tile, o, inv, out + h * G.hd, G, grp, qb * 16, G.C, lane);
+    if (fg == 0 && qok) lse[qpix * G.heads + h] = m + __logf(l);
+  }
+}
+
+template <int HDP>
+__global__ __launch_bounds__(256) void grid_lds_dq_kernel(const bf16* __restrict__ dout, const bf16* __restrict__ qkv,
+                                                          const float* __restrict__ lse, const float* __restrict__ delta,
+                                                          bf16* __restrict__ dqkv, GridGeomM G, float scale, GmLds L) {
+  constexpr int KK = HDP / 32, ND = HDP / 16, PITCH = gm_pitch<HDP>();
+  extern __shared__ __attribute__((aligned(16))) bf16 gsm[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const long C3 = 3L * G.C;
+  const long pair0 = (long)blockIdx.x * L.PP;
+  for (int p = 0; p < L.PP; ++p) {
+    const long pr = pair0 + p;
+    if (pr >= L.pairs) break;
+    const int h = (int)(pr % G.heads);
+    const long grp = pr / G.heads;
+    bf16* Ks = gsm + (size_t)p * 2 * L.tile_elems;
+    gm_stage_pair<HDP>(Ks, qkv + G.C + h * G.hd, C3, G, grp, L.Np);
+    gm_stage_pair<HDP>(Ks + L.tile_elems, qkv + 2 * G.C + h * G.hd, C3, G, grp, L.Np);
+  }
+  __syncthreads();
+  bf16* tile = gsm + (size_t)L.PP * 2 * L.tile_elems + wave * 16 * PITCH;
+  for (int it = wave; it < L.PP * L.nrb; it += 4) {
+    const int p = it / L.nrb, qb = it - p * L.nrb;
+    const long pr = pair0 + p;
+    if (pr >= L.pairs) break;
+    const int h = (int)(pr % G.heads);
+    const long grp = pr / G.heads;
+    const bf16* Ks = gsm + (size_t)p * 2 * L.tile_elems;
+    const bf16* Vs = Ks + L.tile_elems;
+    const int qtok = qb * 16 + fr;
+    const bool qok = qtok < G.N;
+    const long qpix = qok ? G.pixel(grp, qtok) : 0;
+    bf16x8 qf[KK], gf[KK];
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      const int d = kk * 32 + fg * 8;
+      qf[kk] = gm_load8(qkv + h * G.hd + qpix * C3 + d, qok && d < G.hd);
+      gf[kk] = gm_load8(dout + qpix * G.C + h * G.hd + d, qok && d < G.hd);
+    }
+    const float lq = qok ? lse[qpix * G.heads + h] : INFINITY;
+    const float dl = qok ? delta[qpix * G.heads + h] : 0.f;
+    f32x4 dq[ND];
+#pragma unroll
+    for (int j = 0; j < ND; ++j) dq[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int k0 = 0; k0 < G.N; k0 += 16) {
+      f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) {
+        const int off = (k0 + fr) * PITCH + kk * 32 + fg * 8;
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks + off);
+        const bf16x8 vf = *reinterpret_cast<const bf16x8*>(Vs + off);
+        s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[kk], s, 0, 0, 0);
+        dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, gf[kk], dp, 0, 0, 0);
+      }
+      float ds[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const bool ok = k0 + 4 * fg + r < G.N;
+        const float pw = ok ? __expf(s[r] * scale - lq) : 0.f;
+        ds[r] = pw * (dp[r] - dl);
+      }
+      const gm_s16x4 da = pack4(ds);
+#pragma unroll
+      for (int j = 0; j < ND; ++j) {
+        const gm_s16x4 kb = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (gm_lds_s16x4*)(Ks + (k0 + 4 * fg + (fr >> 2)) * PITCH + j * 16 + (fr & 3) * 4));
+        dq[j] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(da, kb, dq[j], 0, 0, 0);
+      }
+    }
+    const float sc4[4] = {scale, scale, scale, scale};
+    gm_store<HDP>(tile, dq, sc4, dqkv + h * G.hd, G, grp, qb * 16, C3, lane);
+  }
+}
+
+template <int HDP>
+__global__ __launch_bounds__(256) void grid_lds_dkv_kernel(const bf16* __restrict__ dout, const bf16* __restrict__ qkv,
+                                                           const float* __restrict__ lse,
+                                                           const float* __restrict__ delta, bf16* __restrict__ dqkv,
+                                                           GridGeomM G, float scale, GmLds L) {
+  constexpr int KK = HDP / 32, ND = HDP / 16, PITCH = gm_pitch<HDP>();
+  extern __shared__ __attribute__((aligned(16))) bf16 gsm[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const long C3 = 3L * G.C;
+  const long pair0 = (long)blockIdx.x * L.PP;
+  float* stats = reinterpret_cast<float*>(gsm + (size_t)L.PP * 2 * L.tile_elems);  // [PP][2][Np]
+  for (int p = 0; p < L.PP; ++p) {
+    const long pr = pair0 + p;
+    if (pr >= L.pairs) break;
+    const int h = (int)(pr % G.heads);
+    const long grp = pr / G.heads;
+    bf16* Qs = gsm + (size_t)p * 2 * L.tile_elems;
+    gm_stage_pair<HDP>(Qs, qkv + h * G.hd, C3, G, grp, L.Np);
+    gm_stage_pair<HDP>(Qs + L.tile_elems, dout + h * G.hd, G.C, G, grp, L.Np);
+    for (int t = threadIdx.x; t < L.Np; t += 256) {
+      const bool ok = t < G.N;
+      const long pq = ok ? G.pixel(grp, t) : 0;
+      stats[(p * 2 + 0) * L.Np + t] = ok ? lse[pq * G.heads + h] : INFINITY;
+      stats[(p * 2 + 1) * L.Np + t] = ok ? delta[pq * G.heads + h] : 0.f;
+    }
+  }
+  __syncthreads();
+  bf16* tile = reinterpret_cast<bf16*>(stats + (size_t)L.PP * 2 * L.Np) + wave * 16 * PITCH;
+  for (int it = wave; it < L.PP * L.nrb; it += 4) {
+    const int p = it / L.nrb, kb = it - p * L.nrb;
+    const long pr = pair0 + p;
+    if (pr >= L.pairs) break;
+    const int h = (int)(pr % G.heads);
+    const long grp = pr / G.heads;
+    const bf16* Qs = gsm + (size_t)p * 2 * L.tile_elems;
+    const bf16* Gs = Qs + L.tile_elems;
+    const float* lq_s = stats + (p * 2 + 0) * L.Np;
+    const float* dl_s = stats + (p * 2 + 1) * L.Np;
+    const int ktok = kb * 16 + fr;
+    const bool kok = ktok < G.N;
+    const long kpix = kok ? G.pixel(grp, ktok) : 0;
+    bf16x8 kf[KK], vf[KK];
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      const int d = kk * 32 + fg * 8;
+      kf[kk] = gm_load8(qkv + G.C + h * G.hd + kpix * C3 + d, kok && d < G.hd);
+      vf[kk] = gm_load8(qkv + 2 * G.C + h * G.hd + kpix * C3 + d, kok && d < G.hd);
+    }
+    f32x4 dk[ND], dv[ND];
+#pragma unroll
+    for (int j = 0; j < ND; ++j) {
+      dk[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      dv[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    for (int q0 = 0; q0 < G.N; q0 += 16) {
+      f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) {
+        const int off = (q0 + fr) * PITCH + kk * 32 + fg * 8;
+        const bf16x8 qa = *reinterpret_cast<const bf16x8*>(Qs + off);
+        const bf16x8 ga = *reinterpret_cast<const bf16x8*>(Gs + off);
+        s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kf[kk], s, 0, 0, 0);
+        dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ga, vf[kk], dp, 0, 0, 0);
+      }
+      float pw[4], ds[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int tok = q0 + 4 * fg + r;  // < Np: padded rows hold lse = inf -> pw = 0
+        pw[r] = kok ? __expf(s[r] * scale - lq_s[tok]) : 0.f;
+        ds[r] = pw[r] * (dp[r] - dl_s[tok]);
+      }
+      const gm_s16x4 pa = pack4(pw), da = pack4(ds);
+#pragma unroll
+      for (int j = 0; j < ND; ++j) {
+        const int off = (q0 + 4 * fg + (fr >> 2)) * PITCH + j * 16 + (fr & 3) * 4;
+        const gm_s16x4 gb = __builtin_amdgcn_ds_read_tr16_b64_v4i16((gm_lds_s16x4*)(Gs + off));
+        const gm_s16x4 qb2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((gm_lds_s16x4*)(Qs + off));
+        dv[j] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(pa, gb, dv[j], 0, 0, 0);
+        dk[j] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(da, qb2, dk[j], 0, 0, 0);
+      }
+    }
+    const float sc4[4] = {scale, scale, scale, scale}, one4[4] = {1.f, 1.f, 1.f, 1.f};
+    gm_store<HDP>(tile, dk, sc4, dqkv + G.C + h * G.hd, G, grp, kb * 16, C3, lane);
+    gm_store<HDP>(tile, dv, one4, dqkv + 2 * G.C + h * G.hd, G, grp, kb * 16, C3, lane);
+  }
+}
+
+static int g_grid_lds = 1;  // tuning knob "grid_lds": LDS-resident pairs when they fit
+void set_grid_lds(int v) { g_grid_lds = v; }
+constexpr size_t GM_LDS_MAX = 64 * 1024;
+
+// ------------------------------------------------------------------------------------------------
 static bool gm_ok(const GridGeomM& G) { return G.N >= 16 && G.hd % 8 == 0 && G.hd <= 64; }
 
 bool grid_mfma_fwd(const void* qkv, void* out, float* lse, int B, int H, int W, int C, int heads, int g, float scale,
                    hipStream_t s) {
   GridGeomM G{B, H, W, C, heads, g, H / g, W / g, (H / g) * (W / g), C / heads};
   if (!gm_ok(G)) return false;
+  if (g_grid_lds && G.N > 16) {
+    if (G.hd <= 32) {
+      const GmLds L = gm_lds_plan<32>(G);
+      const size_t lds = gm_lds_bytes<32>(L, false);
+      if (lds <= GM_LDS_MAX) {
+        grid_lds_fwd_kernel<32><<<(unsigned)L.blocks, 256, lds, s>>>((const bf16*)qkv, (bf16*)out, lse, G, scale, L);
+        return true;
+      }
+    } else {
+      const GmLds L = gm_lds_plan<64>(G);
+      const size_t lds = gm_lds_bytes<64>(L, false);
+      if (lds <= GM_LDS_MAX) {
+        grid_lds_fwd_kernel<64><<<(unsigned)L.blocks, 256, lds, s>>>((const bf16*)qkv, (bf16*)out, lse, G, scale, L);
+        return true;
+      }
+    }
+  }
   const long units = (long)B * g * g * heads * ((G.N + 15) / 16);
   const unsigned grid = cdiv(units, 4);
   if (G.hd <= 32)
@@ -390,6 +705,22 @@ bool grid_mfma_bwd(const void* dout, const void* qkv, const float* lse, const fl
                    int W, int C, int heads, int g, float scale, hipStream_t s) {
   GridGeomM G{B, H, W, C, heads, g, H / g, W / g, (H / g) * (W / g), C / heads};
   if (!gm_ok(G)) return false;
+  if (g_grid_lds && G.N > 16) {
+#define OGV_GRID_LDS_BWD(HD)                                                                                          \
+  {                                                                                                                   \
+    const GmLds L = gm_lds_plan<HD>(G);                                                                               \
+    const size_t l1 = gm_lds_bytes<HD>(L, false), l2 = gm_lds_bytes<HD>(L, true);                                     \
+    if (l2 <= GM_LDS_MAX) {                                                                                           \
+      grid_lds_dq_kernel<HD><<<(unsigned)L.blocks, 256, l1, s>>>((const bf16*)dout, (const bf16*)qkv, lse, delta,     \
+                                                                 (bf16*)dqkv, G, scale, L);                          \
+      grid_lds_dkv_kernel<HD><<<(unsigned)L.blocks, 256, l2, s>>>((const bf16*)dout, (const bf16*)qkv, lse, delta,    \
+                                                                  (bf16*)dqkv, G, scale, L);                         \
+      return true;                                                                                                    \
+    }                                                                                                                 \
+  }
+    if (G.hd <= 32) OGV_GRID_LDS_BWD(32) else OGV_GRID_LDS_BWD(64)
+#undef OGV_GRID_LDS_BWD
+  }
   const long units = (long)B * g * g * heads * ((G.N + 15) / 16);
   const unsigned grid = cdiv(units, 4);
   if (G.hd <= 32) {

@@ -42,6 +42,10 @@ extern "C" int ogv_set_option(const char* name, int value) {
     set_sgemm_mode(value ? 1 : 0);
     return OGV_OK;
   }
+  if (!strcmp(name, "grid_lds")) {
+    set_grid_lds(value ? 1 : 0);
+    return OGV_OK;
+  }
   if (!strcmp(name, "gemm_bn64")) {
     set_gemm_bn64(value ? 1 : 0);
     return OGV_OK;

@@ -254,7 +254,10 @@ GRID_MFMA_CASES = [  # B, H, W, C, heads, g: N >= 16 with head_dim <= 64 runs on
     (1, 16, 16, 64, 1, 2),    # N = 64, hd = 64
     (1, 14, 14, 64, 2, 1),    # N = 196 (partial last 16-chunk)
     (1, 10, 10, 128, 2, 1),   # N = 100, hd = 64
-    (1, 28, 28, 64, 2, 1),    # N = 784 (224^2 stage-0 group size)
+    (1, 28, 28, 64, 2, 1),    # N = 784 (224^2 stage-0 group size: global-chunk kernels)
+    (3, 10, 10, 48, 2, 2),    # N = 25: two (group, head) pairs per LDS-resident block
+    (3, 5, 5, 32, 1, 1),      # N = 25, 3 pairs: ragged last block
+    (2, 12, 12, 48, 2, 2),    # N = 36: 3 row blocks on 4 waves
 ]
 
 

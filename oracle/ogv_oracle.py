@@ -19,6 +19,9 @@ parameter dict keyed like the reference state_dict, so the same deterministic pa
   mhsa                src/model/grid_attention.py:62-89
   grid_attention      src/model/grid_attention.py:112-131
   outgrid_block       src/model/Out_Grid_Block.py:88-107 (MLP :24-32)
+  gridonly_block      src/model/Grid_Only_Block.py:47-59
+  stage_out_then_grid src/model/Grid_Only_Block.py:103-108
+  model_b             src/Model_B_OutGridNet.py:10-104
   model_a             src/Model_A_OutGridNet.py:14-67, stem_head.py:17-32, downsampling.py:50-65
 
 Parity: pinned against golden vectors produced by running the reference itself in the build
@@ -47,44 +50,58 @@ def _bn(pre, c):
             pre + "num_batches_tracked": ()}
 
 
-def block_shapes(pre: str, cfg: dict) -> Dict[str, tuple]:
-    """Parameter/buffer shapes of one OutGridBlock, keys as in the reference state_dict."""
+def outlooker_shapes(pre: str, cfg: dict) -> Dict[str, tuple]:
+    """OutlookerBlock2d (Outlook_Block.py:26-64): norm1.ln, attn.{attn,v,proj}, norm2.ln, mlp.fc1/fc2."""
     C = cfg["dim"]
     ho, k = cfg.get("outlook_heads", 6), cfg.get("outlook_kernel", 3)
     s = {}
-    s.update(_ln(pre + "outlook.norm1.ln.", C))
-    s[pre + "outlook.attn.attn.weight"] = (ho * k * k, C, 1, 1)
-    s[pre + "outlook.attn.attn.bias"] = (ho * k * k,)
+    s.update(_ln(pre + "norm1.ln.", C))
+    s[pre + "attn.attn.weight"] = (ho * k * k, C, 1, 1)
+    s[pre + "attn.attn.bias"] = (ho * k * k,)
     for n in ("v", "proj"):
-        s[pre + f"outlook.attn.{n}.weight"] = (C, C, 1, 1)
-        s[pre + f"outlook.attn.{n}.bias"] = (C,)
-    s.update(_ln(pre + "outlook.norm2.ln.", C))
+        s[pre + f"attn.{n}.weight"] = (C, C, 1, 1)
+        s[pre + f"attn.{n}.bias"] = (C,)
+    s.update(_ln(pre + "norm2.ln.", C))
     hid = max(1, int(C * cfg.get("outlook_mlp_ratio", 2.0)))
-    s[pre + "outlook.mlp.fc1.weight"], s[pre + "outlook.mlp.fc1.bias"] = (hid, C, 1, 1), (hid,)
-    s[pre + "outlook.mlp.fc2.weight"], s[pre + "outlook.mlp.fc2.bias"] = (C, hid, 1, 1), (C,)
+    s[pre + "mlp.fc1.weight"], s[pre + "mlp.fc1.bias"] = (hid, C, 1, 1), (hid,)
+    s[pre + "mlp.fc2.weight"], s[pre + "mlp.fc2.bias"] = (C, hid, 1, 1), (C,)
+    return s
+
+
+def mbconv_shapes(pre: str, cfg: dict) -> Dict[str, tuple]:
+    """MBConv (mbc_conv.py:44-89): expand.0/1, depthwise.0/1, se.fc1/fc2, project.0/1."""
+    C = cfg["dim"]
+    s = {}
     mid = max(1, int(round(C * cfg.get("mbconv_expand_ratio", 4.0))))
     use_bn = cfg.get("use_bn", True)
     if mid != C:
-        s[pre + "mbconv.expand.0.weight"] = (mid, C, 1, 1)
+        s[pre + "expand.0.weight"] = (mid, C, 1, 1)
         if use_bn:
-            s.update(_bn(pre + "mbconv.expand.1.", mid))
+            s.update(_bn(pre + "expand.1.", mid))
         else:
-            s[pre + "mbconv.expand.0.bias"] = (mid,)
-    s[pre + "mbconv.depthwise.0.weight"] = (mid, 1, 3, 3)
+            s[pre + "expand.0.bias"] = (mid,)
+    s[pre + "depthwise.0.weight"] = (mid, 1, 3, 3)
     if use_bn:
-        s.update(_bn(pre + "mbconv.depthwise.1.", mid))
+        s.update(_bn(pre + "depthwise.1.", mid))
     else:
-        s[pre + "mbconv.depthwise.0.bias"] = (mid,)
+        s[pre + "depthwise.0.bias"] = (mid,)
     se_ratio = cfg.get("mbconv_se_ratio", 0.25)
     if se_ratio > 0:
         sq = max(1, int(mid * se_ratio))
-        s[pre + "mbconv.se.fc1.weight"], s[pre + "mbconv.se.fc1.bias"] = (sq, mid, 1, 1), (sq,)
-        s[pre + "mbconv.se.fc2.weight"], s[pre + "mbconv.se.fc2.bias"] = (mid, sq, 1, 1), (mid,)
-    s[pre + "mbconv.project.0.weight"] = (C, mid, 1, 1)
+        s[pre + "se.fc1.weight"], s[pre + "se.fc1.bias"] = (sq, mid, 1, 1), (sq,)
+        s[pre + "se.fc2.weight"], s[pre + "se.fc2.bias"] = (mid, sq, 1, 1), (mid,)
+    s[pre + "project.0.weight"] = (C, mid, 1, 1)
     if use_bn:
-        s.update(_bn(pre + "mbconv.project.1.", C))
+        s.update(_bn(pre + "project.1.", C))
     else:
-        s[pre + "mbconv.project.0.bias"] = (C,)
+        s[pre + "project.0.bias"] = (C,)
+    return s
+
+
+def grid_tail_shapes(pre: str, cfg: dict) -> Dict[str, tuple]:
+    """norm2, grid_attn.mhsa.{qkv,proj}, norm3, mlp.fc1/fc2 (Out_Grid_Block.py:74-86)."""
+    C = cfg["dim"]
+    s = {}
     s.update(_ln(pre + "norm2.", C))
     s[pre + "grid_attn.mhsa.qkv.weight"], s[pre + "grid_attn.mhsa.qkv.bias"] = (3 * C, C), (3 * C,)
     s[pre + "grid_attn.mhsa.proj.weight"], s[pre + "grid_attn.mhsa.proj.bias"] = (C, C), (C,)
@@ -92,6 +109,50 @@ def block_shapes(pre: str, cfg: dict) -> Dict[str, tuple]:
     hid = max(1, int(C * cfg.get("mlp_ratio", 4.0)))
     s[pre + "mlp.fc1.weight"], s[pre + "mlp.fc1.bias"] = (hid, C), (hid,)
     s[pre + "mlp.fc2.weight"], s[pre + "mlp.fc2.bias"] = (C, hid), (C,)
+    return s
+
+
+def block_shapes(pre: str, cfg: dict) -> Dict[str, tuple]:
+    """Parameter/buffer shapes of one OutGridBlock, keys as in the reference state_dict."""
+    s = outlooker_shapes(pre + "outlook.", cfg)
+    s.update(mbconv_shapes(pre + "mbconv.", cfg))
+    s.update(grid_tail_shapes(pre, cfg))
+    return s
+
+
+def gridonly_block_shapes(pre: str, cfg: dict) -> Dict[str, tuple]:
+    """GridOnlyBlock (Grid_Only_Block.py:21-59): mbconv, norm2, grid_attn, norm3, mlp."""
+    s = mbconv_shapes(pre + "mbconv.", cfg)
+    s.update(grid_tail_shapes(pre, cfg))
+    return s
+
+
+def stage_out_then_grid_shapes(pre: str, cfg: dict, depth: int, out_depth: int = 1) -> Dict[str, tuple]:
+    """StageOutThenGrid (Grid_Only_Block.py:75-108): outlookers.<i>, blocks.<j>."""
+    s = {}
+    for i in range(out_depth):
+        s.update(outlooker_shapes(f"{pre}outlookers.{i}.", cfg))
+    for j in range(depth):
+        s.update(gridonly_block_shapes(f"{pre}blocks.{j}.", cfg))
+    return s
+
+
+def model_b_shapes(stages: List[dict], num_classes=100, in_ch=3, stem_dim=64, front_depth=2) -> Dict[str, tuple]:
+    """OutlookerFrontGridNet (Model_B_OutGridNet.py:10-82): stem, proj_in, front, stages, downs, head."""
+    s = {"stem.stem.0.weight": (stem_dim, in_ch, 3, 3)}
+    s.update(_bn("stem.stem.1.", stem_dim))
+    if stem_dim != stages[0]["dim"]:
+        s["proj_in.weight"], s["proj_in.bias"] = (stages[0]["dim"], stem_dim, 1, 1), (stages[0]["dim"],)
+    for i in range(front_depth):
+        s.update(outlooker_shapes(f"front.{i}.", stages[0]))
+    for si, st in enumerate(stages):
+        for b in range(st["depth"]):
+            s.update(gridonly_block_shapes(f"stages.{si}.{b}.", st))
+    for si in range(len(stages) - 1):
+        s[f"downs.{si}.op.0.weight"] = (stages[si + 1]["dim"], stages[si]["dim"], 3, 3)
+        s.update(_bn(f"downs.{si}.op.1.", stages[si + 1]["dim"]))
+    s.update(_bn("head_norm.", stages[-1]["dim"]))
+    s["classifier.weight"], s["classifier.bias"] = (num_classes, stages[-1]["dim"]), (num_classes,)
     return s
 
 
@@ -215,10 +276,9 @@ def grid_attention(x, p, pre, heads, g, want_probs=False):
     return (y, att) if want_probs else y
 
 
-def outgrid_block(x, p, pre, cfg, train=False):
-    x = outlooker_block(x, p, pre + "outlook.", cfg.get("outlook_heads", 6), cfg.get("outlook_kernel", 3),
-                        cfg.get("mlp_act", "gelu"))
-    x = mbconv(x, p, pre + "mbconv.", train, cfg.get("mbconv_act", "silu"))
+def grid_tail(x, p, pre, cfg):
+    """permute -> x + Grid(LN(x)) -> x + MLP(LN(x)) -> permute (Out_Grid_Block.py:96-107,
+    Grid_Only_Block.py:47-59)."""
     xb = x.permute(0, 2, 3, 1).contiguous()
     C = xb.shape[-1]
     y = F.layer_norm(xb, (C,), p[pre + "norm2.weight"], p[pre + "norm2.bias"], 1e-5)
@@ -227,6 +287,48 @@ def outgrid_block(x, p, pre, cfg, train=False):
     y = F.linear(_act(cfg.get("mlp_act", "gelu"), F.linear(y, p[pre + "mlp.fc1.weight"], p[pre + "mlp.fc1.bias"])),
                  p[pre + "mlp.fc2.weight"], p[pre + "mlp.fc2.bias"])
     return (xb + y).permute(0, 3, 1, 2).contiguous()
+
+
+def outgrid_block(x, p, pre, cfg, train=False):
+    x = outlooker_block(x, p, pre + "outlook.", cfg.get("outlook_heads", 6), cfg.get("outlook_kernel", 3),
+                        cfg.get("mlp_act", "gelu"))
+    x = mbconv(x, p, pre + "mbconv.", train, cfg.get("mbconv_act", "silu"))
+    return grid_tail(x, p, pre, cfg)
+
+
+def gridonly_block(x, p, pre, cfg, train=False):
+    """GridOnlyBlock.forward (Grid_Only_Block.py:47-59): MBConv -> grid tail."""
+    return grid_tail(mbconv(x, p, pre + "mbconv.", train, cfg.get("mbconv_act", "silu")), p, pre, cfg)
+
+
+def stage_out_then_grid(x, p, pre, cfg, depth, out_depth=1, train=False):
+    """StageOutThenGrid.forward (Grid_Only_Block.py:103-108)."""
+    for i in range(out_depth):
+        x = outlooker_block(x, p, f"{pre}outlookers.{i}.", cfg.get("outlook_heads", 6),
+                            cfg.get("outlook_kernel", 3), cfg.get("mlp_act", "gelu"))
+    for j in range(depth):
+        x = gridonly_block(x, p, f"{pre}blocks.{j}.", cfg, train)
+    return x
+
+
+def model_b(x, p, stages, front_depth=2, train=False):
+    """OutlookerFrontGridNet.forward (Model_B_OutGridNet.py:84-104)."""
+    h = F.conv2d(x, p["stem.stem.0.weight"], None, padding=1)
+    h = F.silu(_bn_apply(h, p, "stem.stem.1.", train))
+    if "proj_in.weight" in p:
+        h = F.conv2d(h, p["proj_in.weight"], p["proj_in.bias"])
+    s0 = stages[0]
+    for i in range(front_depth):
+        h = outlooker_block(h, p, f"front.{i}.", s0.get("outlook_heads", 6), s0.get("outlook_kernel", 3),
+                            s0.get("mlp_act", "gelu"))
+    for si, st in enumerate(stages):
+        for b in range(st["depth"]):
+            h = gridonly_block(h, p, f"stages.{si}.{b}.", st, train)
+        if si + 1 < len(stages):
+            h = F.conv2d(h, p[f"downs.{si}.op.0.weight"], None, stride=2, padding=1)
+            h = F.silu(_bn_apply(h, p, f"downs.{si}.op.1.", train))
+    h = _bn_apply(h, p, "head_norm.", train).mean(dim=(2, 3))
+    return F.linear(h, p["classifier.weight"], p["classifier.bias"])
 
 
 def model_a(x, p, stages, train=False):

@@ -51,25 +51,37 @@ MODEL_CONFIGS = {
         dict(dim=128, depth=3, num_heads=4, grid_size=8, outlook_heads=4),
         dict(dim=256, depth=4, num_heads=8, grid_size=4, outlook_heads=8),
         dict(dim=384, depth=2, num_heads=6, grid_size=2, outlook_heads=6)]),
+    # Model B (OutlookerFrontGridNet), configs/cifar100_model_b.yaml:1-29
+    "model_b_cifar100": dict(type="model_b", num_classes=100, stem_dim=64, dpr_max=0.1, img=32,
+                             outlooker_front_depth=3, stages=[
+        dict(dim=64, depth=2, num_heads=2, grid_size=8, outlook_heads=2),
+        dict(dim=128, depth=2, num_heads=4, grid_size=8, outlook_heads=4),
+        dict(dim=256, depth=3, num_heads=8, grid_size=4, outlook_heads=8),
+        dict(dim=384, depth=1, num_heads=6, grid_size=2, outlook_heads=6)]),
 }
 
 
 def build_model(model_cfg: dict) -> nn.Module:
-    """YAML `model:` section -> MaxOutNet (only Model A is on the hot path)."""
+    """YAML `model:` section -> MaxOutNet (Model A) or OutlookerFrontGridNet (Model B), the
+    dispatch of scripts/train.py:33-60 (same type aliases, same errors)."""
     from src.Model_A_OutGridNet import MaxOutNet
+    from src.Model_B_OutGridNet import OutlookerFrontGridNet
     from src.model.downsampling import DownsampleConfig
     from src.stage_config import StageCfg
 
     kind = str(model_cfg.get("type", "model_a")).lower()
-    if kind not in ("a", "model_a", "maxout", "outgrid"):
-        raise ValueError(f"model.type '{kind}' is not built by this framework (Model A only)")
     stages = [StageCfg(**s) for s in model_cfg.get("stages", [])]
     if not stages:
         raise ValueError("model.stages must have at least one stage config")
-    return MaxOutNet(num_classes=int(model_cfg.get("num_classes", 100)), stages=stages,
-                     in_ch=int(model_cfg.get("in_ch", 3)), stem_dim=int(model_cfg.get("stem_dim", 64)),
-                     dpr_max=float(model_cfg.get("dpr_max", 0.1)),
-                     down_cfg=DownsampleConfig(**model_cfg.get("downsample", {})))
+    common = dict(num_classes=int(model_cfg.get("num_classes", 100)), stages=stages,
+                  in_ch=int(model_cfg.get("in_ch", 3)), stem_dim=int(model_cfg.get("stem_dim", 64)),
+                  dpr_max=float(model_cfg.get("dpr_max", 0.1)),
+                  down_cfg=DownsampleConfig(**model_cfg.get("downsample", {})))
+    if kind in ("a", "model_a", "maxout", "outgrid"):
+        return MaxOutNet(**common)
+    if kind in ("b", "model_b", "outlooker_front", "front"):
+        return OutlookerFrontGridNet(outlooker_front_depth=int(model_cfg.get("outlooker_front_depth", 2)), **common)
+    raise ValueError(f"Unknown model.type '{kind}'. Use 'model_a' (MaxOutNet) or 'model_b' (OutlookerFrontGridNet)")
 
 
 def param_groups_no_wd(model: nn.Module, weight_decay: float):

@@ -40,21 +40,7 @@ class MaxOutNet(nn.Module):
         self.classifier = nn.Linear(stages[-1].dim, num_classes)
 
     def forward(self, x):
-        if self.training:  # every block's DropPath factors in one draw (ogv.layers.draw_drop_path_scales)
-            dps = getattr(self, "_ogv_droppaths", None)
-            if dps is None:
-                from src.model.Outlook_Block import DropPath
-                dps = self._ogv_droppaths = [m for m in self.modules() if isinstance(m, DropPath)]
-            draw_drop_path_scales(dps, x.shape[0], x.device)
-            # every BatchNorm counter of the model in one multi-tensor add (the modules skip theirs)
-            bns = getattr(self, "_ogv_bns", None)
-            if bns is None:
-                bns = self._ogv_bns = [m for m in self.modules() if isinstance(m, nn.modules.batchnorm._BatchNorm)
-                                       and m.track_running_stats and m.num_batches_tracked is not None]
-                for m in bns:
-                    m._ogv_nbt_pooled = True
-            if bns and bns[0].training:
-                torch._foreach_add_([m.num_batches_tracked for m in bns], 1)
+        train_prologue(self, x)
         x = self.proj_in(self.stem(x))
         for si, blocks in enumerate(self.stages):
             for blk in blocks:
@@ -63,3 +49,24 @@ class MaxOutNet(nn.Module):
                 x = self.downs[si](x)
         pooled = self.head_norm(x).mean(dim=(2, 3))
         return self.classifier(pooled)
+
+
+def train_prologue(model: nn.Module, x):
+    """Per-forward work shared by Model A and Model B in training mode: every block's DropPath
+    factors in one draw (ogv.layers.draw_drop_path_scales) and every BatchNorm counter of the model
+    in one multi-tensor add (the modules skip theirs)."""
+    if not model.training:
+        return
+    dps = getattr(model, "_ogv_droppaths", None)
+    if dps is None:
+        from src.model.Outlook_Block import DropPath
+        dps = model._ogv_droppaths = [m for m in model.modules() if isinstance(m, DropPath)]
+    draw_drop_path_scales(dps, x.shape[0], x.device)
+    bns = getattr(model, "_ogv_bns", None)
+    if bns is None:
+        bns = model._ogv_bns = [m for m in model.modules() if isinstance(m, nn.modules.batchnorm._BatchNorm)
+                                and m.track_running_stats and m.num_batches_tracked is not None]
+        for m in bns:
+            m._ogv_nbt_pooled = True
+    if bns and bns[0].training:
+        torch._foreach_add_([m.num_batches_tracked for m in bns], 1)

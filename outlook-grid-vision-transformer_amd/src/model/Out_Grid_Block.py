@@ -71,12 +71,18 @@ class OutGridBlock(nn.Module):
         self.dp3 = DropPath(cfg.drop_path) if cfg.drop_path > 0 else nn.Identity()
 
     def forward(self, x):
-        x = self.mbconv(self.outlook(x))
-        xb = x.to(OF.compute_dtype(x)).permute(0, 2, 3, 1)        # BHWC view of channels_last
-        if not xb.is_contiguous():
-            xb = xb.contiguous()
-        xn, xr = self.norm2.forward_pair(xb)
-        xb = self.grid_attn(xn, residual=xr, row_scale=drop_path_scale(self.dp2, xb))
-        xn, xr = self.norm3.forward_pair(xb)
-        xb = self.mlp(xn, residual=xr, row_scale=drop_path_scale(self.dp3, xb))
-        return xb.permute(0, 3, 1, 2)                              # NCHW (channels_last) view
+        return grid_tail(self, self.mbconv(self.outlook(x)))
+
+
+def grid_tail(blk, x):
+    """permute -> x + DP(Grid(LN(x))) -> x + DP(MLP(LN(x))) -> permute back, shared by OutGridBlock
+    (Out_Grid_Block.py:96-107) and GridOnlyBlock (Grid_Only_Block.py:50-59).  `blk` holds norm2,
+    grid_attn, dp2, norm3, mlp, dp3; the residual adds / DropPath run in the proj and fc2 epilogues."""
+    xb = x.to(OF.compute_dtype(x)).permute(0, 2, 3, 1)            # BHWC view of channels_last
+    if not xb.is_contiguous():
+        xb = xb.contiguous()
+    xn, xr = blk.norm2.forward_pair(xb)
+    xb = blk.grid_attn(xn, residual=xr, row_scale=drop_path_scale(blk.dp2, xb))
+    xn, xr = blk.norm3.forward_pair(xb)
+    xb = blk.mlp(xn, residual=xr, row_scale=drop_path_scale(blk.dp3, xb))
+    return xb.permute(0, 3, 1, 2)                                  # NCHW (channels_last) view

@@ -50,6 +50,13 @@ def shapes_for(meta) -> dict:
         return {k[len("mbconv."):]: v for k, v in full.items() if k.startswith("mbconv.")}
     if kind == "outgrid_block":
         return orc.block_shapes("", meta["stage"])
+    if kind == "gridonly_block":
+        return orc.gridonly_block_shapes("", meta["stage"])
+    if kind == "stage_out_then_grid":
+        return orc.stage_out_then_grid_shapes("", meta["stage"], meta["depth"], meta["out_depth"])
+    if kind == "model_b":
+        return orc.model_b_shapes(meta["stages"], meta["num_classes"], 3, meta["stem_dim"],
+                                  meta["outlooker_front_depth"])
     if kind == "model_a":
         return orc.model_a_shapes(meta["stages"], meta["num_classes"], 3, meta["stem_dim"])
     raise KeyError(kind)

@@ -63,7 +63,8 @@ def test_cpu_tensors_are_refused():
 
 @pytest.mark.parametrize("name", ["outlook_attn_s0", "grid_attn_s1", "layernorm2d_s0", "outlooker_block_s1",
                                   "mbconv_s0_train", "outgrid_block_s2_eval", "outgrid_block_tiny_eval",
-                                  "model_a_7m_eval_b2"])
+                                  "model_a_7m_eval_b2", "gridonly_block_b1_eval", "stage_out_then_grid_eval",
+                                  "model_b_eval_b2"])
 def test_state_dict_matches_reference_layout(name):
     import test_gpu_parity as tg
     meta, _ = fx.load(name)
@@ -72,7 +73,7 @@ def test_state_dict_matches_reference_layout(name):
     ref = {k: tuple(s) for k, s in fx.shapes_for(meta).items()}
     assert list(ours) == list(ref)
     assert ours == ref
-    if meta["kind"] == "model_a":
+    if meta["kind"] in ("model_a", "model_b"):
         assert [k for k, _ in mod.named_parameters()] == meta["param_names"]
         assert sum(p.numel() for p in mod.parameters()) == meta["n_params"]
 

@@ -56,6 +56,16 @@ def _module(meta):
                                                      grid_size=meta["g"]))
     if k == "outgrid_block":
         return OutGridBlock(StageCfg(**meta["stage"]))
+    if k == "gridonly_block":
+        from src.model.Grid_Only_Block import GridOnlyBlock
+        return GridOnlyBlock(StageCfg(**meta["stage"]))
+    if k == "stage_out_then_grid":
+        from src.model.Grid_Only_Block import StageOutThenGrid
+        return StageOutThenGrid(StageCfg(**meta["stage"]), meta["depth"], meta["out_depth"])
+    if k == "model_b":
+        from src.Model_B_OutGridNet import OutlookerFrontGridNet
+        return OutlookerFrontGridNet(meta["num_classes"], [StageCfg(**s) for s in meta["stages"]], 3,
+                                     meta["stem_dim"], meta["outlooker_front_depth"], meta["dpr_max"])
     if k == "model_a":
         return MaxOutNet(meta["num_classes"], [StageCfg(**s) for s in meta["stages"]], 3, meta["stem_dim"],
                          meta["dpr_max"])
@@ -81,7 +91,8 @@ def _tol(ref, t):
 GOLDEN_MODULES = (fx.fixture_names("outlook_attn_") + fx.fixture_names("grid_attn_s") + fx.fixture_names("grid_attn_rect")
                   + fx.fixture_names("grid_attn_g3") + fx.fixture_names("grid_attn_14m") + fx.fixture_names("grid_attn_n784")
                   + ["layernorm2d_s0", "outlooker_block_s1"] + fx.fixture_names("mbconv_")
-                  + fx.fixture_names("outgrid_block_"))
+                  + fx.fixture_names("outgrid_block_") + fx.fixture_names("gridonly_block_")
+                  + fx.fixture_names("stage_out_then_grid_"))
 
 
 @pytest.mark.parametrize("name", GOLDEN_MODULES)
@@ -112,7 +123,10 @@ def _torch_bf16_error(meta, arr):
           "layernorm2d": lambda: orc.ln2d(xt, p["ln.weight"], p["ln.bias"], meta["eps"]),
           "outlooker_block": lambda: orc.outlooker_block(xt, p, "", meta["heads"]),
           "mbconv": lambda: orc.mbconv(xt, p, "", meta["train"]),
-          "outgrid_block": lambda: orc.outgrid_block(xt, p, "", meta["stage"], meta["train"])}[kind]
+          "outgrid_block": lambda: orc.outgrid_block(xt, p, "", meta["stage"], meta["train"]),
+          "gridonly_block": lambda: orc.gridonly_block(xt, p, "", meta["stage"], meta["train"]),
+          "stage_out_then_grid": lambda: orc.stage_out_then_grid(xt, p, "", meta["stage"], meta["depth"],
+                                                                 meta["out_depth"], meta["train"])}[kind]
     with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
         y = fn()
     return fx.maxabs(y.float(), arr["y"])
@@ -157,10 +171,15 @@ def test_outlook_attn_forward_hook_sees_logits():
     assert seen == [torch.Size([2, 36, 8, 8])]
 
 
+@pytest.mark.parametrize("fixture", ["model_a_7m", "model_b"])
 @pytest.mark.parametrize("mode", ["eval", "train"])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_model_a_logits(mode, dtype):
-    meta, arr = fx.load(f"model_a_7m_{mode}_b2")
+def test_model_logits(fixture, mode, dtype):
+    """Model A (MaxOutNet) and Model B (OutlookerFrontGridNet) logits / loss / grad norms vs the
+    reference's recorded values."""
+    meta, arr = fx.load(f"{fixture}_{mode}_b2")
+    ref_fn = (lambda x, p: orc.model_a(x, p, meta["stages"], train=(mode == "train"))) if meta["kind"] == "model_a" \
+        else (lambda x, p: orc.model_b(x, p, meta["stages"], meta["outlooker_front_depth"], train=(mode == "train")))
     mod = _module(meta)
     gp.fill_module(mod, meta["seed"])
     mod = mod.to(DEV).train(mode == "train")
@@ -171,16 +190,16 @@ def test_model_a_logits(mode, dtype):
                                              label_smoothing=0.1)
     e = fx.maxabs(logits.detach().float(), arr["logits"])
     if dtype == torch.float32:
-        assert e <= 1e-3, f"model A {mode} fp32 logits max|d| {e:.3e}"
+        assert e <= 1e-3, f"{fixture} {mode} fp32 logits max|d| {e:.3e}"
     else:
         # stock PyTorch bf16 autocast of the same model (oracle functions on the GPU)
         p = {k: v.to(DEV) for k, v in fx.oracle_params(meta, requires_grad=False).items()}
         with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
-            lt = orc.model_a(x, p, meta["stages"], train=(mode == "train"))
+            lt = ref_fn(x, p)
         e_t = fx.maxabs(lt.float(), arr["logits"])
-        print(f"model A {mode}: bf16 logits max|d| ours {e:.3e} torch-autocast {e_t:.3e}")
+        print(f"{fixture} {mode}: bf16 logits max|d| ours {e:.3e} torch-autocast {e_t:.3e}")
         assert e <= max(1e-2 * max(1.0, float(np.abs(arr['logits']).max())), 1.25 * e_t), \
-            f"model A {mode} bf16 logits max|d| {e:.3e} (torch autocast {e_t:.3e})"
+            f"{fixture} {mode} bf16 logits max|d| {e:.3e} (torch autocast {e_t:.3e})"
     loss.backward()
     names = meta["param_names"]
     params = dict(mod.named_parameters())

@@ -97,3 +97,33 @@ def test_model_a(mode):
     np.testing.assert_allclose(gn, arr["grad_norms"], rtol=2e-4, atol=1e-7)
     n_params = sum(p[k].numel() for k in names)
     assert n_params == meta["n_params"] == 7518102
+
+
+# ---------------------------------------------------------------- Model B family (Grid_Only_Block.py,
+# Model_B_OutGridNet.py), recorded by `make_golden.py model_b`
+@pytest.mark.parametrize("name", fx.fixture_names("gridonly_block_"))
+def test_gridonly_block(name):
+    _check(name, lambda x, p, m: orc.gridonly_block(x, p, "", m["stage"], m["train"]))
+
+
+@pytest.mark.parametrize("name", fx.fixture_names("stage_out_then_grid_"))
+def test_stage_out_then_grid(name):
+    _check(name, lambda x, p, m: orc.stage_out_then_grid(x, p, "", m["stage"], m["depth"], m["out_depth"],
+                                                         m["train"]))
+
+
+@pytest.mark.parametrize("mode", ["eval", "train"])
+def test_model_b(mode):
+    meta, arr = fx.load(f"model_b_{mode}_b2")
+    p = fx.oracle_params(meta)
+    names = [k for k in p if p[k].requires_grad]
+    assert names == meta["param_names"], "state_dict parameter order differs from the reference"
+    x = torch.from_numpy(gp.input_from_spec(meta["x"]))
+    logits = orc.model_b(x, p, meta["stages"], meta["outlooker_front_depth"], train=(mode == "train"))
+    assert fx.maxabs(logits.detach(), arr["logits"]) < 2e-5
+    loss = torch.nn.functional.cross_entropy(logits, torch.from_numpy(arr["targets"]), label_smoothing=0.1)
+    assert abs(loss.item() - arr["loss"][0]) < 2e-6
+    loss.backward()
+    gn = np.array([p[k].grad.norm().item() if p[k].grad is not None else 0.0 for k in names])
+    np.testing.assert_allclose(gn, arr["grad_norms"], rtol=2e-4, atol=1e-7)
+    assert sum(p[k].numel() for k in names) == meta["n_params"]

@@ -229,6 +229,23 @@ int ogv_bn_act_bwd(const void* dout, const void* x, const float* saved, void* dx
                    void* ws, const float* bn_w, int M, int C, int train, int act, ogv_dtype dt,
                    void* stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * Batch mixing (training-loop input side).  Replaces apply_mixup_cutmix's tensor work
+ * (src/training/cutmix_mixup_aug.py:17-64: clone + images[perm] box paste, or
+ * images*lam + images[perm]*(1-lam), and the one_hot(targets)*lam + one_hot(targets[perm])*(1-lam)
+ * blend, :6-7 and :64); the host draws perm / lam / box exactly as the reference does.
+ *   x, out  [B, C, H, W] contiguous NCHW (channels_last = 0) or NHWC (channels_last = 1), dtype dt;
+ *           out must not alias x.  perm [B] int64 device indices in [0, B).
+ *   mode    0 = MixUp: out = x*lam_a + x[perm]*lam_b (fp32 math, ATen's rounding points)
+ *           1 = CutMix: out = x with rows y1..y2-1, columns x1..x2-1 taken from x[perm].
+ * ogv_mix_targets: out [B, K] fp32 = onehot(t)*lam_a + onehot(t[perm])*lam_b; perm == NULL writes
+ * onehot(t) (the no-mix branch, :30-34).  Labels outside [0, K) give an all-zero row (F.one_hot
+ * would raise; checking needs a device sync, so the Python wrapper documents it instead). */
+int ogv_mix_images(const void* x, void* out, const int64_t* perm, int B, int C, int H, int W, int channels_last,
+                   int mode, float lam_a, float lam_b, int y1, int y2, int x1, int x2, ogv_dtype dt, void* stream);
+int ogv_mix_targets(const int64_t* targets, const int64_t* perm, float* out, int B, int K, float lam_a, float lam_b,
+                    void* stream);
+
 /* Elementwise helpers used by the autograd glue. */
 int ogv_cast(const void* src, ogv_dtype src_dt, void* dst, ogv_dtype dst_dt, size_t n, void* stream);
 

@@ -22,6 +22,7 @@ parameter dict keyed like the reference state_dict, so the same deterministic pa
   gridonly_block      src/model/Grid_Only_Block.py:47-59
   stage_out_then_grid src/model/Grid_Only_Block.py:103-108
   model_b             src/Model_B_OutGridNet.py:10-104
+  mix_apply           src/training/cutmix_mixup_aug.py:6-7, 36-64 (given the drawn perm/lam/box)
   model_a             src/Model_A_OutGridNet.py:14-67, stem_head.py:17-32, downsampling.py:50-65
 
 Parity: pinned against golden vectors produced by running the reference itself in the build
@@ -398,3 +399,20 @@ def grid_core(qkv, heads: int, g: int, want_probs=False):
     o = (att @ v).transpose(1, 2).reshape(Bg, H // g, W // g, C)
     y = grid_unpartition(o, B, H, W, g)
     return (y, att) if want_probs else y
+
+
+# ---------------------------------------------------------------------------- batch mixing
+def mix_apply(images, targets, num_classes, mix, cutmix=False, perm=None, lam=1.0, box=(0, 0, 0, 0)):
+    """apply_mixup_cutmix's tensor work once its random draws are known (cutmix_mixup_aug.py:36-64;
+    the no-mix returns :30-34).  box = (y1, y2, x1, x2)."""
+    y1h = F.one_hot(targets, num_classes=num_classes).float()
+    if not mix:
+        return images, y1h
+    y2h = F.one_hot(targets[perm], num_classes=num_classes).float()
+    if cutmix:
+        yb1, yb2, xb1, xb2 = box
+        out = images.clone()
+        out[:, :, yb1:yb2, xb1:xb2] = images[perm, :, yb1:yb2, xb1:xb2]
+    else:
+        out = images * lam + images[perm] * (1.0 - lam)
+    return out, y1h * lam + y2h * (1.0 - lam)

@@ -201,7 +201,11 @@ class Trainer:
         with torch.autocast("cuda", dtype=self.amp_dtype or torch.float32, enabled=self.amp_dtype is not None,
                             cache_enabled=not self.graphs):
             logits = self.model(x)
-        loss = F.cross_entropy(logits.float(), y, label_smoothing=self.ls)
+        if y.is_floating_point():   # soft targets from MixUp/CutMix (one_epoch_train.py:89-92)
+            from .mix import soft_target_cross_entropy
+            loss = soft_target_cross_entropy(logits.float(), y)
+        else:
+            loss = F.cross_entropy(logits.float(), y, label_smoothing=self.ls)
         loss.backward()
         return loss.detach()
 

@@ -10,7 +10,18 @@
 // (separate products, then the sum; no fused multiply-add), so results are bit-identical.
 #include "ogv_common.h"
 
+// hipcc contracts a*b + c*d into an FMA by default; ATen's CPU MixUp rounds each product.
+// (The pragma must cover the expression itself: __fmul_rn/__fadd_rn are header inlines compiled
+// with contraction on.)
+#pragma clang fp contract(off)
+
 namespace ogv {
+
+__device__ __forceinline__ float blend(float a, float la, float b, float lb) {
+  const float pa = a * la;
+  const float pb = b * lb;
+  return pa + pb;
+}
 
 // out[b, e] for e in one image (n = C*H*W elements).  mode 0: MixUp, 1: CutMix.
 // CutMix: an element (c, y, x) comes from image perm[b] when y1 <= y < y2 and x1 <= x < x2.
@@ -33,7 +44,7 @@ __global__ void __launch_bounds__(256) mix_images_kernel(const T* __restrict__ x
       load_vec<T, V>(xa + e0, a);
       load_vec<T, V>(xb + e0, r);
 #pragma unroll
-      for (int i = 0; i < V; ++i) r[i] = __fadd_rn(__fmul_rn(a[i], lam_a), __fmul_rn(r[i], lam_b));
+      for (int i = 0; i < V; ++i) r[i] = blend(a[i], lam_a, r[i], lam_b);
       store_vec<T, V>(o + e0, r);
     } else {
       bool in[V];
@@ -75,7 +86,7 @@ __global__ void __launch_bounds__(256) mix_images_scalar_kernel(const T* __restr
     const float r = to_f(x[pb * n + e]);
     float v;
     if (mode == 0) {
-      v = __fadd_rn(__fmul_rn(a, lam_a), __fmul_rn(r, lam_b));
+      v = blend(a, lam_a, r, lam_b);
     } else {
       int yy, xx;
       if (CL) { const long p = e / C; yy = (int)(p / W); xx = (int)(p % W); }
@@ -96,7 +107,7 @@ __global__ void __launch_bounds__(256) mix_targets_kernel(const int64_t* __restr
     const float y1 = t[b] == k ? 1.f : 0.f;
     if (perm == nullptr) { out[i] = y1; continue; }
     const float y2 = t[perm[b]] == k ? 1.f : 0.f;
-    out[i] = __fadd_rn(__fmul_rn(y1, lam_a), __fmul_rn(y2, lam_b));
+    out[i] = blend(y1, lam_a, y2, lam_b);
   }
 }
 

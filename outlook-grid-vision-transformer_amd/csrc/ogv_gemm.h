@@ -161,6 +161,8 @@ int sgemm_mode();
 void set_sgemm_mode(int v);
 int sgemm_min_m();
 void set_sgemm_min_m(int v);
+void set_sg_per_cu(int v);
+void set_sg_prefetch(int v);
 void set_bk64_max_m(int v);
 void set_grid_mfma(int v);
 void set_dw_blocks(int v);

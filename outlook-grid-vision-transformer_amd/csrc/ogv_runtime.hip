@@ -70,6 +70,14 @@ extern "C" int ogv_set_option(const char* name, int value) {
     set_bk64_max_m(value);
     return OGV_OK;
   }
+  if (!strcmp(name, "sg_prefetch")) {
+    set_sg_prefetch(value);
+    return OGV_OK;
+  }
+  if (!strcmp(name, "sg_per_cu")) {
+    set_sg_per_cu(value);
+    return OGV_OK;
+  }
   if (!strcmp(name, "sgemm_min_m")) {
     set_sgemm_min_m(value);
     return OGV_OK;

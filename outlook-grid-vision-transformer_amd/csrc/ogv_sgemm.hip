@@ -39,7 +39,7 @@ template <int KT, int RS, int PA, int ZA, bool STATS, bool BT>
 __global__ __launch_bounds__(SG_NW * 64) void sgemm_bf16_kernel(const bf16* __restrict__ A, int lda, Pro pro,
                                                                 const float* __restrict__ W, int ldw, Epi epi,
                                                                 bf16* __restrict__ out, int ldo, int M, int N, int K,
-                                                                int NB) {
+                                                                int NB, int pf) {
   constexpr int KP = sg_kp<KT>();
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -136,22 +136,47 @@ __global__ __launch_bounds__(SG_NW * 64) void sgemm_bf16_kernel(const bf16* __re
   const bf16* res = static_cast<const bf16*>(epi.res);
   const bf16* Z = static_cast<const bf16*>(epi.Z);
 
+  // A fragments (+ row scales) of panel pp, raw
+  auto fetch = [&](long pp, bf16x8 (&dst)[RS][KT], float (&rs)[RS]) {
+#pragma unroll
+    for (int i = 0; i < RS; ++i) {
+      const long mi = pp * 16 * RS + i * 16 + fr;
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt) {
+        const int k = kt * 32 + fg * 8;
+        bf16x8 v = {};
+        if (mi < M && k < K) v = *reinterpret_cast<const bf16x8*>(A + mi * lda + k);
+        dst[i][kt] = v;
+      }
+      rs[i] = (epi.rs && mi < M) ? epi.rs[mi / epi.rps] : 1.f;
+    }
+  };
+  // Without an A prologue the next panel's fragments are fetched right after the current ones are
+  // taken, so a wave keeps two panels of loads in flight across its MFMAs and stores (knob
+  // "sg_prefetch").  With a prologue its sc / sh / gate loads would wait on that prefetch
+  // (in-order vmcnt), so those variants fetch each panel when they reach it.
+  const bool pipe = PA < 0 && pf;
+  bf16x8 an[RS][KT];
+  float rsn[RS];
+  if (pipe && (long)blockIdx.x * SG_NW + wave < P) fetch((long)blockIdx.x * SG_NW + wave, an, rsn);
+
   for (long p = (long)blockIdx.x * SG_NW + wave; p < P; p += GW) {
     const long mp = p * 16 * RS;
     bf16x8 a[RS][KT];
     long m[RS];
     float rsc[RS];
 #pragma unroll
-    for (int i = 0; i < RS; ++i) {
-      m[i] = mp + i * 16 + fr;
+    for (int i = 0; i < RS; ++i) m[i] = mp + i * 16 + fr;
+    if (pipe) {
 #pragma unroll
-      for (int kt = 0; kt < KT; ++kt) {
-        const int k = kt * 32 + fg * 8;
-        bf16x8 v = {};
-        if (m[i] < M && k < K) v = *reinterpret_cast<const bf16x8*>(A + m[i] * lda + k);
-        a[i][kt] = v;
+      for (int i = 0; i < RS; ++i) {
+        rsc[i] = rsn[i];
+#pragma unroll
+        for (int kt = 0; kt < KT; ++kt) a[i][kt] = an[i][kt];
       }
-      rsc[i] = (epi.rs && m[i] < M) ? epi.rs[m[i] / epi.rps] : 1.f;
+      if (p + GW < P) fetch(p + GW, an, rsn);
+    } else {
+      fetch(p, a, rsc);
     }
     if constexpr (PA >= 0) {
 #pragma unroll
@@ -313,6 +338,11 @@ int sgemm_mode() {
   return g_sgemm_mode;
 }
 void set_sgemm_mode(int v) { g_sgemm_mode = v; }
+static int g_sg_per_cu = 2;     // workgroups per CU the planner asks for (tuning knob "sg_per_cu"),
+                                // clamped at launch to the kernel's real occupancy
+void set_sg_per_cu(int v) { g_sg_per_cu = v < 1 ? 1 : (v > 4 ? 4 : v); }
+static int g_sg_prefetch = 1;   // knob "sg_prefetch": next-panel register prefetch (no-prologue variants)
+void set_sg_prefetch(int v) { g_sg_prefetch = v ? 1 : 0; }
 static int g_sg_min_m = 65536;  // smallest M routed to the streaming kernels (tuning knob "sgemm_min_m")
 void set_sgemm_min_m(int v) { g_sg_min_m = v; }
 int sgemm_min_m() { return g_sg_min_m; }
@@ -369,7 +399,7 @@ static SgPlan sgemm_plan(int M, int N, int K, bool stats, bool prologue, bool dg
   p.ntiles = (N + NB - 1) / NB;
   p.NB = NB;
   p.lds = lds_of((NB + SG_CW - 1) / SG_CW * SG_CW);
-  const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(2, (160 * 1024) / p.lds));
+  const int per_cu = (int)std::max<size_t>(1, std::min<size_t>((size_t)g_sg_per_cu, (160 * 1024) / p.lds));
   const long panels = ((long)M + 16 * p.RS - 1) / (16 * p.RS);
   const long want = (panels + SG_NW - 1) / SG_NW;
   p.grid = (int)std::min<long>(want, (long)device_cus() * per_cu);
@@ -379,9 +409,13 @@ static SgPlan sgemm_plan(int M, int N, int K, bool stats, bool prologue, bool dg
   return p;
 }
 
+// Returns the workgroup count launched along x (= BatchNorm partial rows with STATS).  Panels are
+// dealt to waves statically, so every workgroup must be resident at once: above 2 per CU the
+// planner's grid is clamped to the occupancy the runtime reports for this instantiation
+// (VGPRs / LDS), never raised above the plan (the partial-row buffer is sized for the plan).
 template <int KT, int RS, int PA, int ZA, bool STATS, bool BT>
-static void sg_launch(const SgPlan& p, const bf16* A, int lda, const Pro& pro, const float* W, int ldw,
-                      const Epi& epi, bf16* out, int ldo, int M, int N, int K, hipStream_t s) {
+static int sg_launch(const SgPlan& p, const bf16* A, int lda, const Pro& pro, const float* W, int ldw,
+                     const Epi& epi, bf16* out, int ldo, int M, int N, int K, hipStream_t s) {
   auto kern = sgemm_bf16_kernel<KT, RS, PA, ZA, STATS, BT>;
   static bool attr = false;
   if (!attr) {
@@ -389,20 +423,30 @@ static void sg_launch(const SgPlan& p, const bf16* A, int lda, const Pro& pro, c
                               (int)SG_LDS_CAP);
     attr = true;
   }
-  dim3 grid((unsigned)p.grid, (unsigned)p.ntiles);
-  kern<<<grid, SG_NW * 64, p.lds, s>>>(A, lda, pro, W, ldw, epi, out, ldo, M, N, K, p.NB);
+  int gx = p.grid;
+  if (g_sg_per_cu > 2) {
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(kern), SG_NW * 64,
+                                                     p.lds) != hipSuccess || occ < 1)
+      occ = 2;
+    const long cap = (long)device_cus() * std::min(occ, g_sg_per_cu);
+    if (gx > cap) gx = (int)std::max(8L, cap / 8 * 8);
+  }
+  dim3 grid((unsigned)gx, (unsigned)p.ntiles);
+  kern<<<grid, SG_NW * 64, p.lds, s>>>(A, lda, pro, W, ldw, epi, out, ldo, M, N, K, p.NB, g_sg_prefetch);
+  return gx;
 }
 
 template <int PA, int ZA, bool STATS, bool BT>
-static void sg_dispatch(const SgPlan& p, const bf16* A, int lda, const Pro& pro, const float* W, int ldw,
+static int sg_dispatch(const SgPlan& p, const bf16* A, int lda, const Pro& pro, const float* W, int ldw,
                         const Epi& epi, bf16* out, int ldo, int M, int N, int K, hipStream_t s) {
   switch (p.KT) {
-    case 2: sg_launch<2, 2, PA, ZA, STATS, BT>(p, A, lda, pro, W, ldw, epi, out, ldo, M, N, K, s); break;
-    case 3: sg_launch<3, 1, PA, ZA, STATS, BT>(p, A, lda, pro, W, ldw, epi, out, ldo, M, N, K, s); break;
-    case 4: sg_launch<4, 1, PA, ZA, STATS, BT>(p, A, lda, pro, W, ldw, epi, out, ldo, M, N, K, s); break;
-    case 6: sg_launch<6, 1, PA, ZA, STATS, BT>(p, A, lda, pro, W, ldw, epi, out, ldo, M, N, K, s); break;
-    case 8: sg_launch<8, 1, PA, ZA, STATS, BT>(p, A, lda, pro, W, ldw, epi, out, ldo, M, N, K, s); break;
-    default: sg_launch<12, 1, PA, ZA, STATS, BT>(p, A, lda, pro, W, ldw, epi, out, ldo, M, N, K, s); break;
+    case 2: return sg_launch<2, 2, PA, ZA, STATS, BT>(p, A, lda, pro, W, ldw, epi, out, ldo, M, N, K, s);
+    case 3: return sg_launch<3, 1, PA, ZA, STATS, BT>(p, A, lda, pro, W, ldw, epi, out, ldo, M, N, K, s);
+    case 4: return sg_launch<4, 1, PA, ZA, STATS, BT>(p, A, lda, pro, W, ldw, epi, out, ldo, M, N, K, s);
+    case 6: return sg_launch<6, 1, PA, ZA, STATS, BT>(p, A, lda, pro, W, ldw, epi, out, ldo, M, N, K, s);
+    case 8: return sg_launch<8, 1, PA, ZA, STATS, BT>(p, A, lda, pro, W, ldw, epi, out, ldo, M, N, K, s);
+    default: return sg_launch<12, 1, PA, ZA, STATS, BT>(p, A, lda, pro, W, ldw, epi, out, ldo, M, N, K, s);
   }
 }
 
@@ -423,17 +467,18 @@ int sgemm_fwd_try(const void* A, int lda, const Pro& pro, const float* W, int ld
   if (!p.ok) return 0;
   const bf16* a = static_cast<const bf16*>(A);
   bf16* o = static_cast<bf16*>(out);
-#define OGV_SG_FWD(PA_)                                                                  \
-  do {                                                                                   \
-    if (st) sg_dispatch<PA_, 0, true, false>(p, a, lda, pro, W, ldw, epi, o, ldo, M, N, K, s);  \
-    else sg_dispatch<PA_, 0, false, false>(p, a, lda, pro, W, ldw, epi, o, ldo, M, N, K, s);    \
+  int gx = p.grid;
+#define OGV_SG_FWD(PA_)                                                                       \
+  do {                                                                                        \
+    if (st) gx = sg_dispatch<PA_, 0, true, false>(p, a, lda, pro, W, ldw, epi, o, ldo, M, N, K, s); \
+    else gx = sg_dispatch<PA_, 0, false, false>(p, a, lda, pro, W, ldw, epi, o, ldo, M, N, K, s);   \
   } while (0)
   if (!pro.any()) OGV_SG_FWD(-1);
   else if (pro.act == OGV_ACT_GELU) OGV_SG_FWD(OGV_ACT_GELU);
   else if (pro.act == OGV_ACT_SILU) OGV_SG_FWD(OGV_ACT_SILU);
   else OGV_SG_FWD(OGV_ACT_NONE);
 #undef OGV_SG_FWD
-  return st ? p.grid : 1;
+  return st ? gx : 1;
 }
 
 // dA[M, Kf] = epi(dOut[M, Nf] . W[Nf, Kf]):  reduction Nf, output columns Kf.

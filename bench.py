@@ -31,6 +31,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+MFMA_PEAK_TFLOPS = 2500.0   # MI355X_MICROARCH.md: dense bf16 MFMA peak (no 2:1 sparsity)
 
 
 def parse():
@@ -198,6 +199,11 @@ def main():
                     "algorithmic_bytes_per_launch": int(probe["bytes_per_launch"]),
                     "avg_launch_ms": round(probe["avg_ms"], 5), "launches": probe["n"],
                     "event_overhead_ms": round(probe["event_overhead_ms"], 5),
+                    # the same launches against the dense bf16 MFMA peak (these GEMMs sit far below
+                    # the ~310 flop/B ridge, so this fraction is small by construction)
+                    "mfma": {"achieved": round(probe["achieved_TFLOPs"], 2), "peak": MFMA_PEAK_TFLOPS,
+                             "unit": "TFLOP/s", "frac": round(probe["achieved_TFLOPs"] / MFMA_PEAK_TFLOPS, 4),
+                             "algorithmic_flops_per_launch": int(probe["flops_per_launch"])},
                     "timing": ("HIP events around each launch (a 40 us device spin queued ahead of each, so no host "
                                "launch gap is timed; minus the empty event-pair interval), " + ("eager step after the timed graph replays"
                                                            if trainer.graphs else "all timed steps"))}

@@ -113,6 +113,15 @@ def probe_bytes(name: str, u: dict) -> int:
     raise KeyError(name)
 
 
+def probe_flops(name: str, u: dict) -> int:
+    """Algorithmic flops of one launch: the GEMMs 2*M*N*K (the MFMA work)."""
+    if name == "outlook_fwd":
+        return 18 * u["M"] * u["C"] + 45 * u["M"] * u["heads"]
+    if name == "grid_fwd":
+        return 4 * u["M"] * u["N"] * u["C"]
+    return 2 * u["M"] * u["N"] * u["K"]
+
+
 def probe_arm(target: str):
     if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
         raise RuntimeError("ogv probe: timing events cannot be recorded into a ROCm graph")
@@ -133,6 +142,7 @@ class _probe:
             self.e0 = torch.cuda.Event(enable_timing=True)
             self.e1 = torch.cuda.Event(enable_timing=True)
             self.nbytes = probe_bytes(name, units)
+            self.nflops = probe_flops(name, units)
 
     def __enter__(self):
         if self.on:
@@ -143,7 +153,7 @@ class _probe:
     def __exit__(self, *a):
         if self.on:
             self.e1.record()
-            _PROBE["recs"].append((self.e0, self.e1, self.nbytes))
+            _PROBE["recs"].append((self.e0, self.e1, self.nbytes, self.nflops))
         return False
 
 
@@ -171,11 +181,14 @@ def probe_results():
         return None
     torch.cuda.synchronize()
     ovh = _empty_pair_ms()
-    ms = [max(a.elapsed_time(b) - ovh, 1e-6) for a, b, _ in recs]
+    ms = [max(a.elapsed_time(b) - ovh, 1e-6) for a, b, _, _ in recs]
     nbytes = sum(r[2] for r in recs)
+    nflops = sum(r[3] for r in recs)
     tot = sum(ms)
     return {"n": len(recs), "avg_ms": tot / len(recs), "bytes_per_launch": nbytes / len(recs),
-            "achieved_GBs": nbytes / (tot * 1e-3) / 1e9 if tot > 0 else None, "event_overhead_ms": ovh}
+            "achieved_GBs": nbytes / (tot * 1e-3) / 1e9 if tot > 0 else None, "event_overhead_ms": ovh,
+            "flops_per_launch": nflops / len(recs),
+            "achieved_TFLOPs": nflops / (tot * 1e-3) / 1e12 if tot > 0 else None}
 
 
 def probe_reset():

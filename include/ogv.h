@@ -46,7 +46,9 @@ const char* ogv_last_error(void);
  *   "bk64_max_m": largest M using 64-wide k-steps in the tiled GEMM; "grid_mfma" 1/0: MFMA grid
  *   attention for bf16; "dw_blocks" (default 0 = ~32 rows per block): target block count of the
  *   depthwise kernels; "mb_side" 1/0: weight gradients of the fused MBConv backward on a side stream;
- *   "ln_bwd_blocks" (default 1024): grid cap of the LayerNorm backward.
+ *   "ln_bwd_blocks" (default 1024): grid cap of the LayerNorm backward; "sg_prefetch" 1/0: next-panel
+ *   register prefetch in the streaming GEMM; "sg_per_cu" (default 2): streaming-GEMM workgroups per CU;
+ *   "splitk_max" (default 32): K-slab cap of the fp32 split-K GEMM (SE MLP).
  * Returns OGV_ERR_ARG for an unknown name. */
 int ogv_set_option(const char* name, int value);
 /* Diagnostics (no reference counterpart): 1 if ogv_gemm_fwd (kind 0) / ogv_gemm_dgrad (kind 1) of

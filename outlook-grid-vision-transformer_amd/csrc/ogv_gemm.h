@@ -163,6 +163,7 @@ int sgemm_min_m();
 void set_sgemm_min_m(int v);
 void set_sg_per_cu(int v);
 void set_sg_prefetch(int v);
+void set_splitk_max(int v);
 void set_bk64_max_m(int v);
 void set_grid_mfma(int v);
 void set_dw_blocks(int v);

@@ -1142,6 +1142,9 @@ void conv_gemm_launch(ogv_dtype dt, const void* A, const ConvG& cv, const float*
 struct SplitPlan {
   int S, kc, nNt, BN;
 };
+static int g_splitk_max = 32;  // knob "splitk_max": cap on the K slabs of the fp32 split-K GEMM (SE MLP)
+void set_splitk_max(int v) { g_splitk_max = v < 1 ? 1 : (v > 32 ? 32 : v); }
+
 static SplitPlan splitk_plan(int M, int N, int K) {
   SplitPlan p;
   p.BN = N > 64 ? 128 : 64;
@@ -1150,7 +1153,7 @@ static SplitPlan splitk_plan(int M, int N, int K) {
   long S = (256 + tiles - 1) / tiles;
   S = std::min(S, (long)((K + 31) / 32));                          // >= 2 MFMA K-steps per chunk
   S = std::min(S, std::max(1L, (4L << 20) / ((long)M * N)));       // partials <= 16 MB
-  S = std::max(1L, std::min(S, 32L));
+  S = std::max(1L, std::min(S, (long)g_splitk_max));
   p.kc = (int)(((K + S - 1) / S + 15) / 16 * 16);
   p.S = (K + p.kc - 1) / p.kc;
   return p;

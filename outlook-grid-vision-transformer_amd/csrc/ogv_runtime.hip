@@ -70,6 +70,10 @@ extern "C" int ogv_set_option(const char* name, int value) {
     set_bk64_max_m(value);
     return OGV_OK;
   }
+  if (!strcmp(name, "splitk_max")) {
+    set_splitk_max(value);
+    return OGV_OK;
+  }
   if (!strcmp(name, "sg_prefetch")) {
     set_sg_prefetch(value);
     return OGV_OK;

@@ -429,6 +429,8 @@ static int sg_launch(const SgPlan& p, const bf16* A, int lda, const Pro& pro, co
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(kern), SG_NW * 64,
                                                      p.lds) != hipSuccess || occ < 1)
       occ = 2;
+    // (the API reads one block per CU high for SGPR counts 81-112 on ROCm 7.2 — MI355X_MICROARCH.md;
+    // harmless here: a non-resident workgroup only delays the tail, nothing waits on it)
     const long cap = (long)device_cus() * std::min(occ, g_sg_per_cu);
     if (gx > cap) gx = (int)std::max(8L, cap / 8 * 8);
   }

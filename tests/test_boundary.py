@@ -131,3 +131,20 @@ def test_make_dpr_matches_reference_formula():
     from src.model.stem_head import make_dpr
     assert make_dpr(1, 0.3) == [0.3]
     assert make_dpr(7, 0.07) == [0.07 * i / 6 for i in range(7)]
+
+
+def test_build_model_dispatch_matches_reference_aliases():
+    """scripts/train.py:33-60: model.type aliases and the unknown-type error (constructed on the host)."""
+    from ogv.train import MODEL_CONFIGS, build_model
+    from src.Model_A_OutGridNet import MaxOutNet
+    from src.Model_B_OutGridNet import OutlookerFrontGridNet
+    stages = MODEL_CONFIGS["model_a_7m"]["stages"]
+    for t in ("a", "model_a", "maxout", "outgrid"):
+        assert isinstance(build_model(dict(type=t, stages=stages)), MaxOutNet)
+    for t in ("b", "model_b", "outlooker_front", "front"):
+        m = build_model(dict(type=t, stages=stages, outlooker_front_depth=1))
+        assert isinstance(m, OutlookerFrontGridNet) and len(m.front) == 1
+    with pytest.raises(ValueError, match="Unknown model.type"):
+        build_model(dict(type="model_c", stages=stages))
+    with pytest.raises(ValueError, match="at least one stage"):
+        build_model(dict(type="model_b", stages=[]))

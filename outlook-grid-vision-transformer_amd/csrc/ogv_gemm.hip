@@ -429,7 +429,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
   if (kc > 0) {  // split-K: blockIdx.y owns columns [y*kc, y*kc + kc); raw partial to out[y]
     const int ofs = blockIdx.y * kc;
     A += ofs;
-    Wt += ofs;
+    Wt += BT ? (long)ofs * ldw : ofs;  // BT: the reduction index is W's row
     Ka = min(Ka - ofs, kc);
     Kb = min(Kb - ofs, kc);
     if (pro.sc) pro.sc += ofs;
@@ -1179,14 +1179,21 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 }
 
 void gemm_fwd_splitk_f32(const float* A, int lda, const Pro& pro, const float* W, int ldw, float* out, int ldo, int M,
-                         int N, int K, const Epi& epi, void* ws, hipStream_t s) {
+                         int N, int K, const Epi& epi, void* ws, hipStream_t s, bool bt) {
   if (M <= 0) return;
   const SplitPlan p = splitk_plan(M, N, K);
   float* part = (float*)ws;
   const int nMt = (M + GEMM_BM - 1) / GEMM_BM;
   dim3 grid((unsigned)(((nMt + 7) / 8) * 8 * p.nNt), (unsigned)p.S);
   const bool pr = pro.any();
-  if (p.BN == 128) {
+  if (bt) {  // W stored [K][ldw] (reduction-major): the data-gradient of a [N'][K'] weight, no transpose
+    if (p.BN == 128)
+      gemm_f32_kernel<GEMM_BM, 128, false, false, 0, true><<<grid, 256, 0, s>>>(A, lda, pro, W, ldw, Epi(), part, N, M,
+                                                                                N, p.kc, K, K, nMt, p.nNt, ConvG(), p.kc);
+    else
+      gemm_f32_kernel<GEMM_BM, 64, false, false, 0, true><<<grid, 256, 0, s>>>(A, lda, pro, W, ldw, Epi(), part, N, M,
+                                                                               N, p.kc, K, K, nMt, p.nNt, ConvG(), p.kc);
+  } else if (p.BN == 128) {
     if (pr) gemm_f32_kernel<GEMM_BM, 128, true, false><<<grid, 256, 0, s>>>(A, lda, pro, W, ldw, Epi(), part, N, M, N,
                                                                            p.kc, K, K, nMt, p.nNt, ConvG(), p.kc);
     else gemm_f32_kernel<GEMM_BM, 128, false, false><<<grid, 256, 0, s>>>(A, lda, pro, W, ldw, Epi(), part, N, M, N,

@@ -1385,19 +1385,18 @@ static void mbconv_bwd_impl(const void* dout, const void* x, const Saved& sv, vo
     Pro p2;
     p2.act = s.act;
     gemm_wgrad_launch(OGV_F32, w.dz2, s.mid, sv.z1, s.se, p2, nullptr, 1, G.se_w2, G.se_b2, s.B, s.mid, s.se, w.gemm, st);
-    {  // dz1 = act'(z1) * (dz2 . W2):  W2 [mid, se] -> W2^T [se, mid]
-      transpose_f32_launch(P.se_w2, w.wtse, s.mid, s.se, s.mid, st);
+    {  // dz1 = act'(z1) * (dz2 . W2):  W2 [mid, se] read reduction-major (no transpose launch)
       Epi e;
       e.Z = sv.z1;
       e.ldz = s.se;
       e.zact = s.act;
-      gemm_fwd_splitk_f32(w.dz2, s.mid, Pro(), w.wtse, s.mid, w.dz1, s.se, s.B, s.se, s.mid, e, w.split, st);
+      gemm_fwd_splitk_f32(w.dz2, s.mid, Pro(), P.se_w2, s.se, w.dz1, s.se, s.B, s.se, s.mid, e, w.split, st, true);
     }
     gemm_wgrad_launch(OGV_F32, w.dz1, s.se, sv.pooled, s.mid, Pro(), nullptr, 1, G.se_w1, G.se_b1, s.B, s.se, s.mid,
                       w.gemm, st);
-    {  // dpool = dz1 . W1:  W1 [se, mid] -> W1^T [mid, se]
-      transpose_f32_launch(P.se_w1, w.wtse, s.se, s.mid, s.se, st);
-      gemm_fwd_splitk_f32(w.dz1, s.se, Pro(), w.wtse, s.se, w.dpool, s.mid, s.B, s.mid, s.se, Epi(), w.split, st);
+    {  // dpool = dz1 . W1:  W1 [se, mid] read reduction-major
+      gemm_fwd_splitk_f32(w.dz1, s.se, Pro(), P.se_w1, s.mid, w.dpool, s.mid, s.B, s.mid, s.se, Epi(), w.split, st,
+                          true);
     }
   }
   // B5) BN2 backward: dd = ca*(dy2 - cb - dhat*cc)  -> bufB

@@ -137,7 +137,8 @@ void gemm_wgrad_launch(ogv_dtype dt, const void* G, int ldg, const void* X, int 
 // ws >= splitk_ws_bytes(M, N, K).  Epilogue: bias, rs, res, zact (no stats).
 size_t splitk_ws_bytes(int M, int N, int K);
 void gemm_fwd_splitk_f32(const float* A, int lda, const Pro& pro, const float* W, int ldw, float* out, int ldo, int M,
-                         int N, int K, const Epi& epi, void* ws, hipStream_t s, bool bt = false);
+                         int N, int K, const Epi& epi, void* ws, hipStream_t s, bool bt = false,
+                         float* sig_out = nullptr);
 // WT[k][n] = W[n][k] (fp32), zero for n in [N, ldt)
 void transpose_f32_launch(const float* W, float* WT, int N, int K, int ldt, hipStream_t s);
 

@@ -1165,7 +1165,8 @@ size_t splitk_ws_bytes(int M, int N, int K) {
 }
 
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ part, int S, int M, int N,
-                                                            Epi epi, float* __restrict__ out, int ldo) {
+                                                            Epi epi, float* __restrict__ out, int ldo,
+                                                            float* __restrict__ sig_out) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (long)M * N) return;
   const int m = (int)(i / N), n = (int)(i - (long)m * N);
@@ -1176,10 +1177,11 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   if (epi.res) v += static_cast<const float*>(epi.res)[(long)m * ldo + n];
   if (epi.zact) v *= act_grad(epi.zact, static_cast<const float*>(epi.Z)[(long)m * epi.ldz + n]);
   out[(long)m * ldo + n] = v;
+  if (sig_out) sig_out[(long)m * ldo + n] = fast_sigmoid(v);  // the SE gate, fused (was its own launch)
 }
 
 void gemm_fwd_splitk_f32(const float* A, int lda, const Pro& pro, const float* W, int ldw, float* out, int ldo, int M,
-                         int N, int K, const Epi& epi, void* ws, hipStream_t s, bool bt) {
+                         int N, int K, const Epi& epi, void* ws, hipStream_t s, bool bt, float* sig_out) {
   if (M <= 0) return;
   const SplitPlan p = splitk_plan(M, N, K);
   float* part = (float*)ws;
@@ -1204,7 +1206,7 @@ void gemm_fwd_splitk_f32(const float* A, int lda, const Pro& pro, const float* W
     else gemm_f32_kernel<GEMM_BM, 64, false, false><<<grid, 256, 0, s>>>(A, lda, pro, W, ldw, Epi(), part, N, M, N,
                                                                          p.kc, K, K, nMt, p.nNt, ConvG(), p.kc);
   }
-  splitk_reduce_kernel<<<cdiv((long)M * N, 256), 256, 0, s>>>(part, p.S, M, N, epi, out, ldo);
+  splitk_reduce_kernel<<<cdiv((long)M * N, 256), 256, 0, s>>>(part, p.S, M, N, epi, out, ldo, sig_out);
 }
 
 void transpose_f32_launch(const float* W, float* WT, int N, int K, int ldt, hipStream_t s) {

@@ -1320,8 +1320,8 @@ static void mbconv_fwd_impl(const void* x, void* out, const Saved& sv, const Fwd
     p2.act = s.act;
     Epi e2;
     e2.bias = P.se_b2;
-    gemm_fwd_splitk_f32(sv.z1, s.se, p2, P.se_w2, s.se, sv.z2, s.mid, s.B, s.mid, s.se, e2, w.split, st);
-    sigmoid_kernel<<<cdiv((long)s.B * s.mid, 256), 256, 0, st>>>(sv.z2, sv.gate, (long)s.B * s.mid);
+    gemm_fwd_splitk_f32(sv.z1, s.se, p2, P.se_w2, s.se, sv.z2, s.mid, s.B, s.mid, s.se, e2, w.split, st, false,
+                        sv.gate);  // gate = sigmoid(z2) written by the split-K reduce
   }
   // 4) project GEMM on act(BN2(d)) * gate (+ BN3 stats), then out = x + BN3(p)
   {

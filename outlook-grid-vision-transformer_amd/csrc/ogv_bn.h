@@ -8,7 +8,8 @@ namespace ogv {
 // slot = tid >> 2): xor-shuffles over lane bits 2..5 inside each wave, then the 4 waves through
 // LDS (4*NQ*4*V floats; the LDS may be reused).  out[k*qstride + c], c = cbase + chunk*V + i < C.
 template <int NQ, int V, typename A = float>
-__device__ __forceinline__ void chunk_reduce_store(A (&q)[NQ][V], A* lds, A* out, long qstride, int C, int cbase) {
+__device__ __forceinline__ void chunk_reduce_store(A (&q)[NQ][V], A* lds, A* out, long qstride, int C, int cbase,
+                                                   const float* gate = nullptr, float* dz = nullptr) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
   for (int k = 0; k < NQ; ++k)
@@ -36,7 +37,11 @@ __device__ __forceinline__ void chunk_reduce_store(A (&q)[NQ][V], A* lds, A* out
 #pragma unroll
     for (int w = 0; w < 4; ++w) sum += lds[((w * NQ + k) * 4 + ch) * V + i];
     const int c = cbase + ch * V + i;
-    if (c < C) out[(long)k * qstride + c] = sum;
+    if (c < C) {
+      out[(long)k * qstride + c] = sum;
+      // SE: quantity 0 is dgate; dz2 = dgate * g * (1 - g) (the sigmoid backward, fused)
+      if (dz && k == 0) dz[c] = (float)sum * gate[c] * (1.f - gate[c]);
+    }
   }
 }
 

@@ -338,7 +338,7 @@ struct RowPipe {
 // xor-shuffles inside each wave, then the 4 waves through LDS (reused ring).  out[k*qstride + c].
 template <int NQ, int V, typename A>
 __device__ __forceinline__ void dw_reduce_store(A (&q)[NQ][V], float* lds_raw, int chunks, A* out, long qstride,
-                                                int C, int c0) {
+                                                int C, int c0, const float* gate = nullptr, float* dz = nullptr) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
   for (int k = 0; k < NQ; ++k)
@@ -360,7 +360,10 @@ __device__ __forceinline__ void dw_reduce_store(A (&q)[NQ][V], float* lds_raw, i
 #pragma unroll
     for (int w = 0; w < 4; ++w) sum += lds[((w * chunks + ch) * NQ + k) * V + i];
     const int c = c0 + ch * V + i;
-    if (c < C) out[(long)k * qstride + c] = sum;
+    if (c < C) {
+      out[(long)k * qstride + c] = sum;
+      if (dz && k == 0) dz[c] = (float)sum * gate[c] * (1.f - gate[c]);  // SE sigmoid backward, fused
+    }
   }
 }
 
@@ -691,7 +694,8 @@ __global__ __launch_bounds__(256) void se_bwd_reduce_wide_kernel(const T* __rest
                                                             const float* __restrict__ sc, const float* __restrict__ sh,
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ invstd, int act,
-                                                            float* __restrict__ R, int B, int HW, int K) {
+                                                            float* __restrict__ R, int B, int HW, int K,
+                                                            const float* __restrict__ gate, float* __restrict__ dz2) {
   __shared__ float lds[4 * 5 * 4 * 8];
   const int gx = (K + 4 * V - 1) / (4 * V);
   long lid;
@@ -736,7 +740,7 @@ __global__ __launch_bounds__(256) void se_bwd_reduce_wide_kernel(const T* __rest
       }
     }
   }
-  chunk_reduce_store<5, V>(q, lds, R + b * K, (long)B * K, K, bx * 4 * V);
+  chunk_reduce_store<5, V>(q, lds, R + b * K, (long)B * K, K, bx * 4 * V, gate + b * K, dz2 + b * K);
 }
 
 // One pass over (dA3, d) per image: R[q][b][c] for
@@ -747,7 +751,8 @@ __global__ __launch_bounds__(256) void se_bwd_reduce_kernel(const T* __restrict_
                                                             const float* __restrict__ sc, const float* __restrict__ sh,
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ invstd, float* __restrict__ R,
-                                                            int B, int HW, int K, int chunks, int ngx) {
+                                                            int B, int HW, int K, int chunks, int ngx,
+                                                            const float* __restrict__ gate, float* __restrict__ dz2) {
   __shared__ __attribute__((aligned(16))) float lds[4 * IMG_MAX_CHUNKS * 5 * V];  // dw_reduce_store scratch
   long lid;
   if (!xcd_block((long)ngx * B, lid)) return;
@@ -792,7 +797,7 @@ __global__ __launch_bounds__(256) void se_bwd_reduce_kernel(const T* __restrict_
       }
     }
   }
-  dw_reduce_store<5, V, float>(q, lds, chunks, R + b * K, (long)B * K, K, bx * chunks * V);
+  dw_reduce_store<5, V, float>(q, lds, chunks, R + b * K, (long)B * K, K, bx * chunks * V, gate + b * K, dz2 + b * K);
 }
 
 // BN2 reductions from the per-image sums: dy2 = (dA3*gate + dpool/HW) * s'
@@ -1223,17 +1228,18 @@ struct Ops {
   }
   template <int V>
   static void se_reduce(const void* dA3, const void* d, const float* sc, const float* sh, const float* mean,
-                        const float* inv, int act, float* R, int B, int HW, int K, const RowPlan& rp, hipStream_t st) {
+                        const float* inv, int act, float* R, int B, int HW, int K, const RowPlan& rp, hipStream_t st,
+                        const float* gate, float* dz2) {
     if (HW >= 256) {
       se_bwd_reduce_wide_kernel<T, V><<<xcd_grid((long)cdiv(K, 4 * V) * B), 256, 0, st>>>(
-          (const T*)dA3, (const T*)d, sc, sh, mean, inv, act, R, B, HW, K);
+          (const T*)dA3, (const T*)d, sc, sh, mean, inv, act, R, B, HW, K, gate, dz2);
       return;
     }
     const ImgPlan ip = img_plan(HW, K, V);
     const unsigned g = xcd_grid((long)ip.ngx * B);
 #define OGV_SE_RED(A)                                                                                            \
   se_bwd_reduce_kernel<T, V, A><<<g, 256, 0, st>>>((const T*)dA3, (const T*)d, sc, sh, mean, inv, R, B, HW, K, \
-                                                   ip.chunks, ip.ngx)
+                                                   ip.chunks, ip.ngx, gate, dz2)
     switch (act) {
       case OGV_ACT_SILU: OGV_SE_RED(OGV_ACT_SILU); break;
       case OGV_ACT_GELU: OGV_SE_RED(OGV_ACT_GELU); break;
@@ -1376,12 +1382,11 @@ static void mbconv_bwd_impl(const void* dout, const void* x, const Saved& sv, vo
     gemm_wgrad_launch(dt, w.dp, s.C, sv.d, s.mid, pr, nullptr, 1, G.w_proj, nullptr, (int)M, s.C, s.mid, w.gemm2, sd);
   }
   // B3) one pass over (dA3, d): SE gate grads + BN2 partial sums per image
+  // (+ dz2 = dgate * g * (1 - g), the gate's sigmoid backward, written by the same reduce)
   OGV_V_DISPATCH(rp.V, O::template se_reduce, w.bufA, sv.d, sv.sc2, sv.sh2, sv.mean2, sv.inv2, s.act, w.R, s.B, HW,
-                 s.mid, rp, st);
+                 s.mid, rp, st, sv.gate, w.dz2);
   // B4) SE MLP backward (fp32, B rows): dgate = R0 -> dz2 -> (W2, b2) -> dz1 (act') -> (W1, b1) -> dpooled
   {
-    const long n2 = (long)s.B * s.mid;
-    sigmoid_bwd_kernel<<<cdiv(n2, 256), 256, 0, st>>>(w.R, sv.gate, w.dz2, n2);
     Pro p2;
     p2.act = s.act;
     gemm_wgrad_launch(OGV_F32, w.dz2, s.mid, sv.z1, s.se, p2, nullptr, 1, G.se_w2, G.se_b2, s.B, s.mid, s.se, w.gemm, st);

@@ -199,9 +199,9 @@ def main():
                     "algorithmic_bytes_per_launch": int(probe["bytes_per_launch"]),
                     "avg_launch_ms": round(probe["avg_ms"], 5), "launches": probe["n"],
                     "event_overhead_ms": round(probe["event_overhead_ms"], 5),
-                    # the same launches against the dense bf16 MFMA peak (these GEMMs sit far below
-                    # the ~310 flop/B ridge, so this fraction is small by construction)
-                    "mfma": {"achieved": round(probe["achieved_TFLOPs"], 2), "peak": MFMA_PEAK_TFLOPS,
+                    # the same launches' algorithmic flops against the dense bf16 MFMA peak (all the
+                    # probed kernels sit far below the ~310 flop/B ridge, so this is small by construction)
+                    "compute": {"achieved": round(probe["achieved_TFLOPs"], 2), "peak": MFMA_PEAK_TFLOPS,
                              "unit": "TFLOP/s", "frac": round(probe["achieved_TFLOPs"] / MFMA_PEAK_TFLOPS, 4),
                              "algorithmic_flops_per_launch": int(probe["flops_per_launch"])},
                     "timing": ("HIP events around each launch (a 40 us device spin queued ahead of each, so no host "

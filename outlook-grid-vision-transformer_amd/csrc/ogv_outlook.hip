@@ -34,6 +34,54 @@ __global__ __launch_bounds__(256) void outlook_fwd_kernel(const T* __restrict__ 
   const long rowbase = (t / H) * H;  // b * H
 
   const T* lg = logits + p * ldl + head * KK;
+  if constexpr (sizeof(T) == 2 && V == 8 && KS == 3) {
+    // bf16 x 8 channels: every neighbour row is fetched up front (clamped addresses, so the loads
+    // are unconditional and independent of the softmax), then the logits — one memory round trip
+    // per thread instead of logits -> softmax -> neighbours.  Out-of-image neighbours keep their
+    // softmax mass and contribute zero (the reference's zero padding); same summation order.
+    uint4 raw[KK];
+    bool inb[KK];
+#pragma unroll
+    for (int ki = 0; ki < KS; ++ki) {
+      const int y2 = yy + ki - PAD;
+      const int y2c = min(max(y2, 0), H - 1);
+#pragma unroll
+      for (int kj = 0; kj < KS; ++kj) {
+        const int x2 = x + kj - PAD;
+        const int x2c = min(max(x2, 0), W - 1);
+        inb[ki * KS + kj] = y2 >= 0 && y2 < H && x2 >= 0 && x2 < W;
+        raw[ki * KS + kj] = *reinterpret_cast<const uint4*>(v + ((rowbase + y2c) * W + x2c) * C + c0);
+      }
+    }
+    float a[KK];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < KK; ++j) {
+      a[j] = to_f(lg[j]);
+      mx = fmaxf(mx, a[j]);
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < KK; ++j) {
+      a[j] = __expf(a[j] - mx);
+      s += a[j];
+    }
+    const float inv = 1.0f / s;
+    float acc[V];
+#pragma unroll
+    for (int i = 0; i < V; ++i) acc[i] = 0.f;
+#pragma unroll
+    for (int j = 0; j < KK; ++j) {
+      if (!inb[j]) continue;
+      const bf16* e = reinterpret_cast<const bf16*>(&raw[j]);
+#pragma unroll
+      for (int i = 0; i < V; ++i) acc[i] = fmaf(a[j], (float)e[i], acc[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < V; ++i) acc[i] *= inv;
+    store_vec<T, V>(y + p * C + c0, acc);
+    return;
+  }
   float a[KK];
   float mx = -INFINITY;
 #pragma unroll

@@ -162,6 +162,35 @@ __global__ __launch_bounds__(256) void outlook_bwd_logits_kernel(const T* __rest
 #pragma unroll
   for (int j = 0; j < KK; ++j) dp[j] = 0.f;
   const int cb = head * hd;
+  if constexpr (sizeof(T) == 2 && V == 8 && KS == 3) {
+    // per 8-channel slice: dy and all neighbour v rows issued together (clamped, unconditional)
+    bool inb[KK];
+    long nb[KK];
+#pragma unroll
+    for (int ki = 0; ki < KS; ++ki)
+#pragma unroll
+      for (int kj = 0; kj < KS; ++kj) {
+        const int y2 = yy + ki - PAD, x2 = x + kj - PAD;
+        inb[ki * KS + kj] = y2 >= 0 && y2 < H && x2 >= 0 && x2 < W;
+        nb[ki * KS + kj] = ((rowbase + min(max(y2, 0), H - 1)) * W + min(max(x2, 0), W - 1)) * C + cb;
+      }
+    for (int d = 0; d < hd; d += V) {
+      const uint4 graw = *reinterpret_cast<const uint4*>(dy + p * C + cb + d);
+      uint4 raw[KK];
+#pragma unroll
+      for (int j = 0; j < KK; ++j) raw[j] = *reinterpret_cast<const uint4*>(v + nb[j] + d);
+      const bf16* ge = reinterpret_cast<const bf16*>(&graw);
+#pragma unroll
+      for (int j = 0; j < KK; ++j) {
+        if (!inb[j]) continue;
+        const bf16* e = reinterpret_cast<const bf16*>(&raw[j]);
+        float acc = dp[j];
+#pragma unroll
+        for (int i = 0; i < V; ++i) acc = fmaf((float)ge[i], (float)e[i], acc);
+        dp[j] = acc;
+      }
+    }
+  } else
   for (int d = 0; d < hd; d += V) {
     float g[V];
     load_vec<T, V>(dy + p * C + cb + d, g);
@@ -218,6 +247,36 @@ __global__ __launch_bounds__(256) void outlook_bwd_v_kernel(const T* __restrict_
   float acc[V];
 #pragma unroll
   for (int i = 0; i < V; ++i) acc[i] = 0.f;
+  if constexpr (sizeof(T) == 2 && V == 8 && KS == 3) {
+    // every neighbour's dy row and probability fetched up front (clamped, unconditional), then
+    // accumulated in the same order with out-of-image neighbours skipped
+    uint4 raw[KK];
+    float wv[KK];
+    bool inb[KK];
+#pragma unroll
+    for (int ki = 0; ki < KS; ++ki) {
+      const int y2 = yy - (ki - PAD);
+      const int y2c = min(max(y2, 0), H - 1);
+#pragma unroll
+      for (int kj = 0; kj < KS; ++kj) {
+        const int x2 = x - (kj - PAD);
+        const int x2c = min(max(x2, 0), W - 1);
+        const long pp = (rowbase + y2c) * W + x2c;
+        inb[ki * KS + kj] = y2 >= 0 && y2 < H && x2 >= 0 && x2 < W;
+        wv[ki * KS + kj] = probs[(pp * heads + head) * KK + ki * KS + kj];
+        raw[ki * KS + kj] = *reinterpret_cast<const uint4*>(dy + pp * C + c0);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < KK; ++j) {
+      if (!inb[j]) continue;
+      const bf16* e = reinterpret_cast<const bf16*>(&raw[j]);
+#pragma unroll
+      for (int i = 0; i < V; ++i) acc[i] = fmaf(wv[j], (float)e[i], acc[i]);
+    }
+    store_vec<T, V>(dv + q * C + c0, acc);
+    return;
+  }
 #pragma unroll
   for (int ki = 0; ki < KS; ++ki) {
     const int y2 = yy - (ki - PAD);

@@ -10,7 +10,7 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT"
   -- python3 bench.py --steps ${STEPS:-4} --warmup ${WARMUP:-3} --no-cpu-baseline --no-parity ${BENCH_ARGS:-} > "$OUT/bench_prof.log" 2>&1
 rc=$?
 echo "== rocprof rc=$rc"; grep -E '^\{' "$OUT/bench_prof.log" | tail -1
-python3 tools/trace_steps.py "$OUT/bench_kernel_trace.csv" --top 60 > "$OUT/step_breakdown.txt" 2>&1
+python3 tools/trace_steps.py "$OUT/bench_kernel_trace.csv" --top 60 --step -2 > "$OUT/step_breakdown.txt" 2>&1
 head -45 "$OUT/step_breakdown.txt"
 gzip -f "$OUT/bench_kernel_trace.csv"
 exit $rc

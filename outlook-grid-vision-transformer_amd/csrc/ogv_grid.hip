@@ -74,6 +74,45 @@ __global__ __launch_bounds__(256) void grid_fwd_kernel(const T* __restrict__ qkv
     const long pk = G.pixel(grp, u);
     const T* kp = qkv + pk * C3 + G.C + h * hd;
     float s = 0.f;
+    if constexpr (sizeof(T) == 2 && V == 8) {
+      // bf16: this key's k AND v rows are issued together (v does not depend on the score), so a
+      // key costs one memory round trip instead of two; same arithmetic order as below
+      uint4 rk[HDMAX / 8], rv[HDMAX / 8];
+#pragma unroll
+      for (int c = 0; c < HDMAX / 8; ++c) {
+        rk[c] = c * 8 < hd ? *reinterpret_cast<const uint4*>(kp + c * 8) : uint4{0u, 0u, 0u, 0u};
+        rv[c] = c * 8 < hd ? *reinterpret_cast<const uint4*>(kp + G.C + c * 8) : uint4{0u, 0u, 0u, 0u};
+      }
+#pragma unroll
+      for (int c = 0; c < HDMAX / 8; ++c) {
+        if (c * 8 < hd) {
+          const bf16* e = reinterpret_cast<const bf16*>(&rk[c]);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) s = fmaf(q[c * 8 + i], (float)e[i], s);
+        }
+      }
+      float pw;
+      if (s > m) {
+        const float corr = __expf(m - s);
+        l *= corr;
+#pragma unroll
+        for (int d = 0; d < HDMAX; ++d) o[d] *= corr;
+        m = s;
+        pw = 1.f;
+      } else {
+        pw = __expf(s - m);
+      }
+      l += pw;
+#pragma unroll
+      for (int c = 0; c < HDMAX / 8; ++c) {
+        if (c * 8 < hd) {
+          const bf16* e = reinterpret_cast<const bf16*>(&rv[c]);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) o[c * 8 + i] = fmaf(pw, (float)e[i], o[c * 8 + i]);
+        }
+      }
+      continue;
+    }
 #pragma unroll
     for (int d0 = 0; d0 < HDMAX; d0 += V) {
       if (d0 < hd) {

@@ -45,7 +45,7 @@ def parse():
                     help="kernel whose launches feed `roofline`")
     ap.add_argument("--eager", action="store_true", help="launch kernels one by one instead of graph replay")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=24.0)
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="ogv_set_option tuning switch (repeatable; see include/ogv.h)")
@@ -96,35 +96,56 @@ def fwd_parity(device):
     return out
 
 
+def _host_threads():
+    """Threads for the CPU baseline: the CPUs this process may run on (the box's CPU share:
+    sched_getaffinity), capped by OMP_NUM_THREADS when the launcher sets it."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
 def cpu_baseline(seconds):
-    """The oracle's fwd+CE+bwd+clip+AdamW at bs=8, fp32, NCHW on the host cores (bounded)."""
+    """The oracle's fwd+CE+bwd+clip+AdamW, fp32, NCHW on the host cores (bounded), at the two
+    batch sizes SURVEY §8d times the reference at (bs=8: config 1; bs=64: the host's best
+    throughput); `value` is the better of the two."""
     sys.path.insert(0, str(ROOT / "oracle"))
     sys.path.insert(0, str(ROOT / "tests" / "golden"))
     import gen_params as gp
     import ogv_oracle as orc
     from ogv.train import MODEL_CONFIGS
     cfg = MODEL_CONFIGS["model_a_7m"]
-    threads = min(16, os.cpu_count() or 1)
+    threads = _host_threads()
     torch.set_num_threads(threads)
-    p = orc.make_params(orc.model_a_shapes(cfg["stages"], cfg["num_classes"], 3, cfg["stem_dim"]),
-                        lambda k, s: gp.param_value(k, s, 7))
-    opt = orc.make_optimizer(p)
-    bs = 8
-    g = torch.Generator().manual_seed(7)
-    x = torch.randn(bs, 3, 32, 32, generator=g)
-    y = torch.randint(0, 100, (bs,), generator=g)
-    for _ in range(2):
-        orc.train_step(x, y, p, cfg["stages"], opt)
-    n, t0 = 0, time.perf_counter()
-    while True:
-        orc.train_step(x, y, p, cfg["stages"], opt)
-        n += 1
-        if time.perf_counter() - t0 > seconds:
-            break
-    dt = time.perf_counter() - t0
-    return {"value": round(n * bs / dt, 2), "unit": "imgs/s", "cores": threads, "kind": "port",
-            "sample": f"{n} steps x bs={bs} Model-A-7M 32x32 fp32 fwd+CE+bwd+clip+AdamW (oracle restatement, "
-                      f"{dt:.1f}s after 2 warmup steps)"}
+    samples = []
+    for bs in (8, 64):
+        p = orc.make_params(orc.model_a_shapes(cfg["stages"], cfg["num_classes"], 3, cfg["stem_dim"]),
+                            lambda k, s: gp.param_value(k, s, 7))
+        opt = orc.make_optimizer(p)
+        g = torch.Generator().manual_seed(7)
+        x = torch.randn(bs, 3, 32, 32, generator=g)
+        y = torch.randint(0, 100, (bs,), generator=g)
+        for _ in range(2):
+            orc.train_step(x, y, p, cfg["stages"], opt)
+        n, t0 = 0, time.perf_counter()
+        while True:
+            orc.train_step(x, y, p, cfg["stages"], opt)
+            n += 1
+            if time.perf_counter() - t0 > seconds / 2:
+                break
+        dt = time.perf_counter() - t0
+        samples.append({"bs": bs, "steps": n, "seconds": round(dt, 2), "imgs_per_s": round(n * bs / dt, 2)})
+    best = max(samples, key=lambda d: d["imgs_per_s"])
+    return {"value": best["imgs_per_s"], "unit": "imgs/s", "cores": threads, "kind": "port",
+            "host_cpus": os.cpu_count(),
+            "sample": f"Model-A-7M 32x32 fp32 fwd+CE+bwd+clip+AdamW (oracle restatement of the reference), "
+                      f"bs=8 and bs=64, ~{seconds / 2:.0f}s each after 2 warmup steps, {threads} threads "
+                      f"(this process's CPU affinity / OMP_NUM_THREADS); value = bs={best['bs']}",
+            "samples": samples}
 
 
 def main():

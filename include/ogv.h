@@ -241,8 +241,9 @@ int ogv_bn_act_bwd(const void* dout, const void* x, const float* saved, void* dx
  *   mode    0 = MixUp: out = x*lam_a + x[perm]*lam_b (fp32 math, ATen's rounding points)
  *           1 = CutMix: out = x with rows y1..y2-1, columns x1..x2-1 taken from x[perm].
  * ogv_mix_targets: out [B, K] fp32 = onehot(t)*lam_a + onehot(t[perm])*lam_b; perm == NULL writes
- * onehot(t) (the no-mix branch, :30-34).  Labels outside [0, K) give an all-zero row (F.one_hot
- * would raise; checking needs a device sync, so the Python wrapper documents it instead). */
+ * onehot(t) (the no-mix branch, :30-34).  A label outside [0, K) (F.one_hot raises on it; raising
+ * needs a device sync) gives a NaN row, so the loss is non-finite and the training step's device
+ * guard (ogv_step_flag) skips the update and counts it. */
 int ogv_mix_images(const void* x, void* out, const int64_t* perm, int B, int C, int H, int W, int channels_last,
                    int mode, float lam_a, float lam_b, int y1, int y2, int x1, int x2, ogv_dtype dt, void* stream);
 int ogv_mix_targets(const int64_t* targets, const int64_t* perm, float* out, int B, int K, float lam_a, float lam_b,
@@ -250,6 +251,20 @@ int ogv_mix_targets(const int64_t* targets, const int64_t* perm, float* out, int
 
 /* Elementwise helpers used by the autograd glue. */
 int ogv_cast(const void* src, ogv_dtype src_dt, void* dst, ogv_dtype dst_dt, size_t n, void* stream);
+
+/* Training-step guard and schedule (src/training/one_epoch_train.py:98-108, :152-153;
+ * src/training/warmup.py:38-52), one single-thread launch each, capturable, no host sync:
+ * ogv_step_flag: *found = 1.0f when the fp32 scalar *x is not finite (mode 0: x = the loss) or
+ *   when *x > 0 (mode 1: x = the all-reduced count of ranks with a non-finite loss), else 0.0f.
+ *   *found is the found_inf the fused AdamW reads (1 = the whole update is skipped).
+ * ogv_schedule_step: after the optimizer: *nonfinite += *found; *counter += 1 - *found (the
+ *   reference does not step its scheduler on a skipped step); then every group's lr tensor
+ *   lr[g][0] = warmup-cosine(counter, base_lr[g]) computed in fp64 as warmup.py does.
+ *   n_groups <= OGV_MAX_LR_GROUPS. */
+#define OGV_MAX_LR_GROUPS 8
+int ogv_step_flag(const float* x, int mode, float* found, void* stream);
+int ogv_schedule_step(const float* found, float* counter, float* nonfinite, float* const* lr, const float* base_lr,
+                      int n_groups, int warmup_steps, int total_steps, float min_lr, void* stream);
 
 #ifdef __cplusplus
 }

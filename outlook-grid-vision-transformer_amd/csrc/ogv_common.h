@@ -17,6 +17,11 @@ typedef __attribute__((ext_vector_type(4))) short s16x4;
 
 namespace ogv {
 
+// BatchNorm batch statistics are accumulated as sums shifted by the running mean (fp64).  A
+// non-finite running mean (a NaN batch poisons it, exactly as in torch's BatchNorm2d) must not
+// leak into the train-mode output, which torch computes from the batch alone: such a shift is 0.
+__device__ __forceinline__ float bn_shift(float v) { return __builtin_isfinite(v) ? v : 0.f; }
+
 // ---------------------------------------------------------------- host-side error plumbing
 void set_error(const char* fmt, ...);
 int check_launch(const char* what);

@@ -76,6 +76,8 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const T* __restrict__ x, 
   if (c0 < C) {
     float sf[V];
     load_vec<float, V>(shift + c0, sf);
+#pragma unroll
+    for (int i = 0; i < V; ++i) sf[i] = bn_shift(sf[i]);
     for (long r = r0 + slot; r < r1; r += 64) {
       float v[V];
       load_vec<T, V>(x + r * C + c0, v);

@@ -80,7 +80,7 @@ __device__ __forceinline__ void gemm_epilogue_bf16(f32x4 (&acc)[TM][TN], float* 
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     bias[q] = (epi.bias && n + q < N) ? epi.bias[n + q] : 0.f;
-    shift[q] = (STATS && epi.stat_shift && n + q < N) ? epi.stat_shift[n + q] : 0.f;
+    shift[q] = (STATS && epi.stat_shift && n + q < N) ? bn_shift(epi.stat_shift[n + q]) : 0.f;
     s1[q] = 0.0;
     s2[q] = 0.0;
   }
@@ -598,7 +598,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
         if (epi.zact) v *= act_grad(epi.zact, Z[(long)m * epi.ldz + n]);
         out[(long)m * ldo + n] = v;
         if constexpr (STATS) {
-          const double d = (double)v - (double)(epi.stat_shift ? epi.stat_shift[n] : 0.f);
+          const double d = (double)v - (double)(epi.stat_shift ? bn_shift(epi.stat_shift[n]) : 0.f);
           s1[j] += d;
           s2[j] = fma(d, d, s2[j]);
         }

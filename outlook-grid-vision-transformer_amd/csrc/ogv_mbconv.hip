@@ -46,7 +46,7 @@ __global__ void bn_finalize_kernel(const double* __restrict__ sums, int K, doubl
   float mean, var;
   if (train) {
     const double s1 = sums[c] / n, s2 = sums[K + c] / n;
-    const double shift = rm[c];
+    const double shift = bn_shift(rm[c]);
     mean = (float)(shift + s1);
     double v = s2 - s1 * s1;
     var = (float)(v > 0.0 ? v : 0.0);
@@ -109,7 +109,7 @@ __global__ __launch_bounds__(256) void bn_reduce_finalize_kernel(const double* _
     t2 += red[1][g][cl];
   }
   const double m1 = t1 / n, m2 = t2 / n;
-  const float mean = (float)((double)rm[c] + m1);
+  const float mean = (float)((double)bn_shift(rm[c]) + m1);
   const double v = m2 - m1 * m1;
   const float var = (float)(v > 0.0 ? v : 0.0);
   rm[c] = (1.f - momentum) * rm[c] + momentum * mean;
@@ -428,7 +428,7 @@ __global__ __launch_bounds__(256) void dw_fwd_tile_kernel(const T* __restrict__ 
     for (int k = 0; k < 9; ++k) w[k][i] = cok ? wdw[(c + i) * 9 + k] : 0.f;
     s[i] = cok ? sc[c + i] : 0.f;
     h[i] = cok ? sh[c + i] : 0.f;
-    sft[i] = (cok && shift) ? shift[c + i] : 0.f;
+    sft[i] = (cok && shift) ? bn_shift(shift[c + i]) : 0.f;
   }
   double q[2][V];  // BN batch statistics in fp64 (shifted sums: fp32 cancels visibly when the
                    // running-mean shift is far from the batch mean)

@@ -7,7 +7,8 @@
 // batch (reads x and x[perm] once, writes out once) and one launch writes the [B, K] soft targets.
 // HBM-bound elementwise work: 16-B vector accesses, one image row-slab per block so the perm
 // lookup is a single scalar load.  Arithmetic follows ATen's rounding points exactly
-// (separate products, then the sum; no fused multiply-add), so results are bit-identical.
+// (separate products, then the sum; no fused multiply-add), so fp32 results are bit-identical;
+// for bf16 images the blend is computed in fp32 and rounded once (ATen rounds each bf16 op).
 #include "ogv_common.h"
 
 // hipcc contracts a*b + c*d into an FMA by default; ATen's CPU MixUp rounds each product.
@@ -104,9 +105,14 @@ __global__ void __launch_bounds__(256) mix_targets_kernel(const int64_t* __restr
   const long total = (long)B * K;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     const int b = (int)(i / K), k = (int)(i % K);
-    const float y1 = t[b] == k ? 1.f : 0.f;
+    // a label outside [0, K) (F.one_hot raises on it) makes its row NaN: the loss turns
+    // non-finite and the training step's device guard skips the update and counts it
+    const int64_t ta = t[b];
+    const int64_t tb = perm ? t[perm[b]] : 0;
+    if (ta < 0 || ta >= K || tb < 0 || tb >= K) { out[i] = __builtin_nanf(""); continue; }
+    const float y1 = ta == k ? 1.f : 0.f;
     if (perm == nullptr) { out[i] = y1; continue; }
-    const float y2 = t[perm[b]] == k ? 1.f : 0.f;
+    const float y2 = tb == k ? 1.f : 0.f;
     out[i] = blend(y1, lam_a, y2, lam_b);
   }
 }

@@ -29,9 +29,65 @@ __global__ void cast_kernel(const S* __restrict__ src, D* __restrict__ dst, size
   for (; i < n; i += stride) dst[i] = from_f<D>(to_f(src[i]));
 }
 
+__global__ void step_flag_kernel(const float* __restrict__ x, int mode, float* __restrict__ found) {
+  const float v = *x;
+  *found = (mode == 0 ? !__builtin_isfinite(v) : v > 0.f) ? 1.f : 0.f;
+}
+
+struct LrGroups {
+  float* lr[OGV_MAX_LR_GROUPS];
+  float base[OGV_MAX_LR_GROUPS];
+};
+
+// warmup.py:38-52 in fp64 (the host formula), one thread
+__global__ void schedule_step_kernel(const float* __restrict__ found, float* counter, float* nonfinite, LrGroups g,
+                                     int n, int warmup, int total, float min_lr) {
+  const float f = *found;
+  *nonfinite += f;
+  const float t = *counter + (1.f - f);
+  *counter = t;
+  const double td = (double)t;
+  for (int i = 0; i < n; ++i) {
+    const double base = g.base[i];
+    double lr;
+    if (warmup > 0 && td <= (double)warmup) {
+      lr = base * (td / (double)warmup);
+    } else {
+      const double tt = td < (double)total ? td : (double)total;
+      const double prog = (tt - (double)warmup) / (double)(total - warmup > 1 ? total - warmup : 1);
+      lr = (double)min_lr + (base - (double)min_lr) * 0.5 * (1.0 + cos(3.14159265358979323846 * prog));
+    }
+    *g.lr[i] = (float)lr;
+  }
+}
+
 }  // namespace ogv
 
 using namespace ogv;
+
+extern "C" int ogv_step_flag(const float* x, int mode, float* found, void* stream) {
+  OGV_REQUIRE(x && found, "ogv_step_flag: null pointer");
+  OGV_REQUIRE(mode == 0 || mode == 1, "ogv_step_flag: mode %d (0 = non-finite, 1 = positive)", mode);
+  step_flag_kernel<<<1, 1, 0, as_stream(stream)>>>(x, mode, found);
+  return check_launch("ogv_step_flag");
+}
+
+extern "C" int ogv_schedule_step(const float* found, float* counter, float* nonfinite, float* const* lr,
+                                 const float* base_lr, int n_groups, int warmup_steps, int total_steps, float min_lr,
+                                 void* stream) {
+  OGV_REQUIRE(found && counter && nonfinite && lr && base_lr, "ogv_schedule_step: null pointer");
+  OGV_REQUIRE(n_groups >= 0 && n_groups <= OGV_MAX_LR_GROUPS, "ogv_schedule_step: %d groups (max %d)", n_groups,
+              OGV_MAX_LR_GROUPS);
+  LrGroups g;
+  for (int i = 0; i < OGV_MAX_LR_GROUPS; ++i) {
+    g.lr[i] = i < n_groups ? lr[i] : nullptr;
+    g.base[i] = i < n_groups ? base_lr[i] : 0.f;
+  }
+  for (int i = 0; i < n_groups; ++i) OGV_REQUIRE(g.lr[i], "ogv_schedule_step: null lr pointer %d", i);
+  schedule_step_kernel<<<1, 1, 0, as_stream(stream)>>>(found, counter, nonfinite, g, n_groups, warmup_steps,
+                                                      total_steps, min_lr);
+  return check_launch("ogv_schedule_step");
+}
 
 extern "C" const char* ogv_version(void) { return "ogv-hip 0.1.0 (gfx950)"; }
 extern "C" const char* ogv_last_error(void) { return g_err; }

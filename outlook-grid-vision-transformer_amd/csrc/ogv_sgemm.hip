@@ -126,7 +126,7 @@ __global__ __launch_bounds__(SG_NW * 64) void sgemm_bf16_kernel(const bf16* __re
   }
   for (int c = tid; c < nbp; c += SG_NW * 64) {
     cvec[c] = (epi.bias && c < nb) ? epi.bias[n0 + c] : 0.f;
-    if (STATS) cvec[nbp + c] = (epi.stat_shift && c < nb) ? epi.stat_shift[n0 + c] : 0.f;
+    if (STATS) cvec[nbp + c] = (epi.stat_shift && c < nb) ? bn_shift(epi.stat_shift[n0 + c]) : 0.f;
   }
   __syncthreads();
 

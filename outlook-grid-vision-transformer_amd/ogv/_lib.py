@@ -92,6 +92,8 @@ SIGNATURES = {
     "ogv_mix_images": (_i, [_p, _p, _p, _i, _i, _i, _i, _i, _i, _f, _f, _i, _i, _i, _i, _i, _p]),
     "ogv_mix_targets": (_i, [_p, _p, _p, _i, _i, _f, _f, _p]),
     "ogv_cast": (_i, [_p, _i, _p, _i, _sz, _p]),
+    "ogv_step_flag": (_i, [_p, _i, _p, _p]),
+    "ogv_schedule_step": (_i, [_p, _p, _p, ctypes.POINTER(_p), ctypes.POINTER(_f), _i, _i, _i, _f, _p]),
 }
 
 OGV_F32, OGV_BF16 = 0, 1

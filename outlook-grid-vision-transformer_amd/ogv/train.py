@@ -25,6 +25,7 @@ once at start; each rank keeps its own BatchNorm batch statistics.
 """
 from __future__ import annotations
 
+import ctypes
 import math
 import os
 from typing import List, Optional
@@ -96,26 +97,71 @@ def param_groups_no_wd(model: nn.Module, weight_decay: float):
 
 
 class WarmupCosineLR:
-    """Linear warmup for warmup_steps, then cosine from the base lr down to min_lr."""
+    """Linear warmup for warmup_steps, then cosine from the base lr down to min_lr
+    (src/training/warmup.py:29-59: the same formula, step-based, state_dict = step_num).
+
+    ``bind_device(counter)``: the step count lives in a device tensor that the Trainer advances
+    inside its (captured) step only when the step was applied (non-finite steps are skipped like
+    the reference's ``continue`` before ``scheduler.step()``, one_epoch_train.py:98-108), and the
+    groups' lr tensors are recomputed on the device from it -- no host sync per step."""
 
     def __init__(self, optimizer, total_steps: int, warmup_steps: int, min_lr: float = 0.0):
         self.optimizer = optimizer
         self.total_steps, self.warmup_steps, self.min_lr = int(total_steps), int(warmup_steps), float(min_lr)
         self.base_lrs = [float(g["lr"]) for g in optimizer.param_groups]
-        self.step_num = 0
+        self._step_num = 0
+        self._dev = None
 
+    # host formula (warmup.py:38-52)
     def lr_at(self, t: int, base: float) -> float:
         if self.warmup_steps > 0 and t <= self.warmup_steps:
             return base * t / self.warmup_steps
         prog = (min(t, self.total_steps) - self.warmup_steps) / max(1, self.total_steps - self.warmup_steps)
         return self.min_lr + (base - self.min_lr) * 0.5 * (1.0 + math.cos(math.pi * prog))
 
-    def step(self):
-        self.step_num += 1
+    def bind_device(self, counter: torch.Tensor):
+        counter.fill_(float(self._step_num))
+        self._dev = counter
+
+    def device_step(self, found: torch.Tensor, nonfinite: torch.Tensor):
+        """counter += 1 - found, nonfinite += found, every group's lr tensor = lr(counter): one
+        native single-thread launch (ogv_schedule_step), capturable, no host sync."""
+        from . import _lib
+        lib = _lib.load()
+        groups = self.optimizer.param_groups
+        ptrs = (ctypes.c_void_p * len(groups))(*[g["lr"].data_ptr() for g in groups])
+        base = (ctypes.c_float * len(groups))(*self.base_lrs)
+        _lib.check(lib.ogv_schedule_step(found.data_ptr(), self._dev.data_ptr(), nonfinite.data_ptr(), ptrs, base,
+                                         len(groups), self.warmup_steps, self.total_steps, self.min_lr,
+                                         torch.cuda.current_stream().cuda_stream), "ogv_schedule_step")
+
+    def apply_device(self):
+        """Write lr(step_num) into every group's device lr tensor (reads the counter: a sync;
+        used on resume / a manual scheduler.step(), never inside the training step)."""
+        t = self.step_num
         for g, base in zip(self.optimizer.param_groups, self.base_lrs):
-            v = self.lr_at(self.step_num, base)
+            g["lr"].fill_(self.lr_at(t, base))
+
+    @property
+    def step_num(self) -> int:
+        return int(self._dev.item()) if self._dev is not None else self._step_num
+
+    @step_num.setter
+    def step_num(self, v: int):
+        self._step_num = int(v)
+        if self._dev is not None:
+            self._dev.fill_(float(v))
+
+    def step(self):
+        if self._dev is not None:
+            self.step_num = self.step_num + 1
+            self.apply_device()
+            return
+        self._step_num += 1
+        for g, base in zip(self.optimizer.param_groups, self.base_lrs):
+            v = self.lr_at(self._step_num, base)
             if isinstance(g["lr"], torch.Tensor):
-                g["lr"].fill_(v)      # device-resident lr read by the captured AdamW
+                g["lr"].fill_(v)
             else:
                 g["lr"] = v
 
@@ -124,6 +170,32 @@ class WarmupCosineLR:
 
     def load_state_dict(self, d):
         self.step_num = int(d.get("step_num", 0))
+        if self._dev is not None:
+            self.apply_device()
+
+
+def load_optimizer_state(optimizer: torch.optim.Optimizer, state_dict: dict):
+    """optimizer.load_state_dict that keeps a capturable/fused optimizer usable and any hipGraph
+    recorded over it valid: the runtime flags (fused, capturable, foreach) and the device lr
+    tensors of the groups are kept (a saved float / CPU lr is copied INTO the existing device
+    tensor), and state tensors that already exist are overwritten in place instead of replaced."""
+    old_groups = [dict(g) for g in optimizer.param_groups]
+    old_state = {p: dict(st) for p, st in optimizer.state.items()}
+    optimizer.load_state_dict(state_dict)
+    for g, og in zip(optimizer.param_groups, old_groups):
+        for k in ("fused", "capturable", "foreach", "differentiable"):
+            if k in og:
+                g[k] = og[k]
+        if isinstance(og["lr"], torch.Tensor):
+            og["lr"].fill_(float(g["lr"]))
+            g["lr"] = og["lr"]
+    for p, st in optimizer.state.items():
+        old = old_state.get(p, {})
+        for k, v in list(st.items()):
+            o = old.get(k)
+            if isinstance(v, torch.Tensor) and isinstance(o, torch.Tensor) and o.shape == v.shape:
+                o.copy_(v)
+                st[k] = o
 
 
 # ------------------------------------------------------------------------------- distributed
@@ -160,88 +232,244 @@ def _dist_world():
     return 1
 
 
+class _Bucket:
+    """A run of parameters (reverse registration order ~ the order backward produces their
+    gradients) whose gradients are all-reduced together as soon as the last one is accumulated."""
+
+    def __init__(self, params, device):
+        self.params = params
+        self.sizes = [p.numel() for p in params]
+        self.flat = torch.zeros(sum(self.sizes), device=device, dtype=torch.float32)
+        self.ready = 0
+        self.work = None
+
+
 class Trainer:
-    """Holds model/optimizer/schedule; ``step(x, y)`` is one full training iteration.
+    """Holds model/optimizer/schedule; ``step(x, y)`` is one full training iteration
+    (src/training/one_epoch_train.py:85-153 without its host syncs).
 
     ``graphs=True`` (HIP device only): the first ``capture_warmup`` calls run eagerly, the next one
-    runs eagerly on a side stream and records the step into hipGraphs, every later call replays
-    them (inputs are copied into the recorded x / y tensors when other tensors are passed).
-    With world_size > 1 gradients are averaged by one all_reduce of a flat bucket (see module doc);
-    pass the bare model (not DDP-wrapped)."""
+    runs eagerly on a side stream and records the step into hipGraphs, every later call copies its
+    batch into trainer-owned input buffers and replays them.  A batch of another shape / dtype (a
+    ragged last batch) runs as an eager step instead.
+
+    Non-finite loss (one_epoch_train.py:98-108): on a HIP device the guard is a device flag, no host
+    sync -- the fused AdamW skips the update when it is set (``found_inf``: parameters, moments and
+    step counts unchanged), and the device step counter that drives the warmup-cosine schedule is
+    not advanced, exactly as the reference ``continue``s before ``optimizer.step()`` /
+    ``scheduler.step()``.  ``nonfinite_steps`` counts them (reading it syncs).  On the CPU the check
+    is the reference's host ``if``.
+
+    With world_size > 1 (pass the bare model, not DDP): parameters and buffers are broadcast from
+    rank 0 at start; every step all-reduces the gradients (pre-divided by world size), the float
+    buffers (BatchNorm running statistics: rank 0 contributes them, the others zeros, so the sum IS
+    rank 0's values -- DDP's ``broadcast_buffers`` riding in the same collective) and the
+    non-finite flag (so every rank takes the same skip decision).  Graph mode: graph A (fwd + bwd +
+    flatten into one bucket) -> one all_reduce -> graph B (unflatten + clip + AdamW); eager mode:
+    ``bucket_mb`` buckets all-reduced asynchronously as backward produces them."""
 
     def __init__(self, model: nn.Module, lr=5e-4, weight_decay=0.05, clip=1.0, label_smoothing=0.1,
                  total_steps=10_000, warmup_ratio=0.05, min_lr=1e-6, amp_dtype: Optional[torch.dtype] = torch.bfloat16,
-                 graphs: bool = False, capture_warmup: int = 3, capture_hook=None):
+                 graphs: bool = False, capture_warmup: int = 3, capture_hook=None, bucket_mb: float = 8.0,
+                 broadcast_buffers: bool = True):
         self.model = model
         core = model.module if hasattr(model, "module") else model
+        self.core = core
         self.ddp = core is not model
         dev = next(core.parameters()).device
-        fused = dev.type == "cuda"
-        self.graphs = bool(graphs) and fused
-        lr0 = torch.tensor(float(lr), device=dev) if self.graphs else lr
-        self.opt = torch.optim.AdamW(param_groups_no_wd(core, weight_decay), lr=lr0, fused=fused,
-                                     capturable=self.graphs)
+        self.device_side = dev.type == "cuda"      # fused AdamW, device guard + schedule
+        self.graphs = bool(graphs) and self.device_side
+        lr0 = torch.tensor(float(lr), device=dev) if self.device_side else lr
+        self.opt = torch.optim.AdamW(param_groups_no_wd(core, weight_decay), lr=lr0, fused=self.device_side,
+                                     capturable=self.device_side)
+        if self.device_side:
+            for g in self.opt.param_groups:     # one device lr tensor per group
+                g["lr"] = g["lr"].clone()
         self.sched = WarmupCosineLR(self.opt, total_steps, int(warmup_ratio * total_steps), min_lr)
         self.params = [p for p in core.parameters() if p.requires_grad]
         self.clip, self.ls, self.amp_dtype = clip, label_smoothing, amp_dtype
-        self.world = 1 if self.ddp else _dist_world()
         self.capture_warmup = int(capture_warmup)
         self.capture_hook = capture_hook          # called right before recording starts
         self._eager_steps = 0
+        self.eager_fallbacks = 0
         self._g = None
+        self._nonfinite_host = 0
+        if self.device_side:
+            self._found = torch.zeros((), dtype=torch.float32, device=dev)
+            self.opt.found_inf = self._found       # read by the fused AdamW kernel (1 = skip)
+            self._nonfinite = torch.zeros((), dtype=torch.float32, device=dev)
+            self.sched.bind_device(torch.zeros((), dtype=torch.float32, device=dev))
+        self.world = 1 if self.ddp else _dist_world()
+        self.rank = torch.distributed.get_rank() if self.world > 1 else 0
         if self.world > 1:
-            self._sizes = [p.numel() for p in self.params]
-            self.flat = torch.zeros(sum(self._sizes), device=dev, dtype=torch.float32)
             with torch.no_grad():   # identical start on every rank (what DDP's constructor does)
                 for t in list(core.parameters()) + list(core.buffers()):
                     torch.distributed.broadcast(t.data, 0)
+            self._bufs = [b for b in core.buffers() if b.is_floating_point()] if broadcast_buffers else []
+            self._sizes = [p.numel() for p in self.params]
+            self._bsizes = [b.numel() for b in self._bufs]
+            self._ng, self._nb = sum(self._sizes), sum(self._bsizes)
+            self.flat = torch.zeros(self._ng + self._nb + 1, device=dev, dtype=torch.float32)
+            self.meta = torch.zeros(self._nb + 1, device=dev, dtype=torch.float32)
+            self._buckets = []
+            self._overlap = False
+            if bucket_mb and bucket_mb > 0 and not self.graphs:
+                self._make_buckets(float(bucket_mb), dev)
+
+    # -- data-parallel buckets (eager mode) ----------------------------------------------------
+    def _make_buckets(self, bucket_mb, dev):
+        cap = int(bucket_mb * 2 ** 20) // 4
+        cur, n = [], 0
+        for p in reversed(self.params):
+            if cur and n + p.numel() > cap:
+                self._buckets.append(_Bucket(cur, dev))
+                cur, n = [], 0
+            cur.append(p)
+            n += p.numel()
+        if cur:
+            self._buckets.append(_Bucket(cur, dev))
+        self._bucket_of = {}
+        for b in self._buckets:
+            for p in b.params:
+                self._bucket_of[p] = b
+                p.register_post_accumulate_grad_hook(self._grad_ready)
+
+    def _launch_bucket(self, b):
+        grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in b.params]
+        torch.cat([g.reshape(-1).float() for g in grads], out=b.flat)
+        b.flat.mul_(1.0 / self.world)
+        b.work = torch.distributed.all_reduce(b.flat, async_op=True)
+
+    def _grad_ready(self, p):
+        if not self._overlap:
+            return
+        b = self._bucket_of[p]
+        b.ready += 1
+        if b.ready == len(b.params):
+            self._launch_bucket(b)
 
     # -- pieces of one step -------------------------------------------------------------------
-    def _fwd_bwd(self, x, y):
+    def _loss(self, x, y):
         with torch.autocast("cuda", dtype=self.amp_dtype or torch.float32, enabled=self.amp_dtype is not None,
                             cache_enabled=not self.graphs):
             logits = self.model(x)
         if y.is_floating_point():   # soft targets from MixUp/CutMix (one_epoch_train.py:89-92)
             from .mix import soft_target_cross_entropy
-            loss = soft_target_cross_entropy(logits.float(), y)
-        else:
-            loss = F.cross_entropy(logits.float(), y, label_smoothing=self.ls)
+            return soft_target_cross_entropy(logits.float(), y)
+        return F.cross_entropy(logits.float(), y, label_smoothing=self.ls)
+
+    def _fwd_bwd(self, x, y):
+        loss = self._loss(x, y)
+        if self.device_side:
+            self._flag(loss.detach(), 0)
+        if self.world > 1 and self._overlap:
+            self._launch_meta(loss)
         loss.backward()
         return loss.detach()
 
-    def _flatten(self):
+    def _meta_values(self, loss):
+        bscale = 1.0 if self.rank == 0 else 0.0
+        flag = self._found.view(1) if self.device_side else \
+            torch.tensor([0.0 if bool(torch.isfinite(loss)) else 1.0], device=self.flat.device)
+        parts = [b.detach().reshape(-1).float() * bscale for b in self._bufs] + [flag]
+        return parts
+
+    def _launch_meta(self, loss):
+        torch.cat(self._meta_values(loss), out=self.meta)
+        self._meta_work = torch.distributed.all_reduce(self.meta, async_op=True)
+
+    def _flatten(self, loss):
         grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in self.params]
-        torch.cat([g.reshape(-1) for g in grads], out=self.flat)
-        self.flat.mul_(1.0 / self.world)
+        torch.cat([g.reshape(-1) for g in grads] + self._meta_values(loss), out=self.flat)
+        self.flat[:self._ng].mul_(1.0 / self.world)
+
+    def _apply_meta(self, meta):
+        """Copy the all-reduced buffers (= rank 0's) back; returns the all-reduced non-finite count."""
+        if self._bufs:
+            views = meta[:self._nb].split(self._bsizes)
+            with torch.no_grad():
+                torch._foreach_copy_(self._bufs, [v.view_as(b) for v, b in zip(views, self._bufs)])
+        return meta[self._nb:]
 
     def _unflatten(self):
-        views = [v.view_as(p) for v, p in zip(self.flat.split(self._sizes), self.params)]
+        views = [v.view_as(p) for v, p in zip(self.flat[:self._ng].split(self._sizes), self.params)]
         for p, v in zip(self.params, views):
             if p.grad is None:
                 p.grad = torch.empty_like(p)
         torch._foreach_copy_([p.grad for p in self.params], views)
+        return self._apply_meta(self.flat[self._ng:])
 
-    def _update(self):
+    def _finish_buckets(self):
+        for b in self._buckets:
+            if b.work is None:          # parameters that got no gradient this step
+                self._launch_bucket(b)
+        for b in self._buckets:
+            b.work.wait()
+            views = b.flat.split(b.sizes)
+            for p, v in zip(b.params, views):
+                if p.grad is None:
+                    p.grad = torch.empty_like(p)
+            torch._foreach_copy_([p.grad for p in b.params], [v.view_as(p) for v, p in zip(views, b.params)])
+            b.ready, b.work = 0, None
+        self._meta_work.wait()
+        return self._apply_meta(self.meta)
+
+    def _flag(self, x, mode):
+        """_found = !isfinite(x) (mode 0, x = the fp32 loss) or x > 0 (mode 1, x = the all-reduced
+        count of non-finite ranks): one native launch, no host sync."""
+        from . import _lib
+        x = x.reshape(1).float().contiguous()
+        _lib.check(_lib.load().ogv_step_flag(x.data_ptr(), mode, self._found.data_ptr(),
+                                             torch.cuda.current_stream().cuda_stream), "ogv_step_flag")
+
+    def _update(self, flag=None):
+        """clip + AdamW + schedule.  Device side: gated by the found_inf flag with no host sync."""
+        if self.device_side:
+            if flag is not None:
+                self._flag(flag, 1)
+            if self.clip is not None:
+                torch.nn.utils.clip_grad_norm_(self.params, self.clip, foreach=True)
+            self.opt.step()                                   # skipped entirely when _found == 1
+            # nonfinite += found; the schedule's step counter advances on applied steps only
+            self.sched.device_step(self._found, self._nonfinite)
+            return
+        if flag is not None and float(flag.view(())) > 0:   # host check: CPU only (no device to sync)
+            self._nonfinite_host += 1
+            self.opt.zero_grad(set_to_none=True)
+            return
         if self.clip is not None:
             torch.nn.utils.clip_grad_norm_(self.params, self.clip, foreach=True)
         self.opt.step()
+        self.sched.step()
 
     def _allreduce(self):
         torch.distributed.all_reduce(self.flat)
 
     def _eager(self, x, y):
         self.opt.zero_grad(set_to_none=True)
+        if self.world > 1 and self._buckets:
+            self._overlap = True
+            try:
+                loss = self._fwd_bwd(x, y)
+            finally:
+                self._overlap = False
+            self._update(self._finish_buckets())
+            return loss
         loss = self._fwd_bwd(x, y)
+        flag = None
         if self.world > 1:
-            self._flatten()
+            self._flatten(loss)
             self._allreduce()
-            self._unflatten()
-        self._update()
+            flag = self._unflatten()
+        elif not self.device_side:
+            flag = torch.tensor([0.0 if bool(torch.isfinite(loss)) else 1.0])
+        self._update(flag)
         return loss
 
     def _capture(self, x, y):
         """This call's update runs eagerly on a side stream (allocator / library warm-up, as graph
-        capture requires); then the step is recorded — recording executes nothing."""
+        capture requires); then the step is recorded on trainer-owned copies of the batch --
+        recording executes nothing."""
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
@@ -249,39 +477,59 @@ class Trainer:
         torch.cuda.current_stream().wait_stream(side)
         loss = loss.clone()
         self.opt.zero_grad(set_to_none=True)
-        self._x, self._y = x, y
+        self._x = x.detach().clone(memory_format=torch.preserve_format)
+        self._y = y.detach().clone()
         if self.capture_hook is not None:
             self.capture_hook()
         pool = torch.cuda.graph_pool_handle()
         self._g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self._g, pool=pool):
-            self._loss = self._fwd_bwd(x, y)
+            self._loss_static = self._fwd_bwd(self._x, self._y)
             if self.world > 1:
-                self._flatten()
+                self._flatten(self._loss_static)
             else:
                 self._update()
         self.graph_grads = [p.grad for p in self.params]   # the tensors the replays write
         if self.world > 1:
             self._g2 = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self._g2, pool=pool):
-                self._unflatten()
-                self._update()
+                self._update(self._unflatten())
         return loss
+
+    def _replayable(self, x, y) -> bool:
+        return (x.shape == self._x.shape and x.dtype == self._x.dtype and x.device == self._x.device
+                and y.shape == self._y.shape and y.dtype == self._y.dtype and y.device == self._y.device)
 
     def step(self, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
         if not self.graphs or (self._g is None and self._eager_steps < self.capture_warmup):
             self._eager_steps += 1
-            loss = self._eager(x, y)
-        elif self._g is None:
-            loss = self._capture(x, y)
-        else:
-            if x is not self._x or y is not self._y:
-                self._x.copy_(x)
-                self._y.copy_(y)
-            self._g.replay()
-            if self.world > 1:
-                self._allreduce()
-                self._g2.replay()
-            loss = self._loss
-        self.sched.step()
-        return loss
+            return self._eager(x, y)
+        if self._g is None:
+            return self._capture(x, y)
+        if not self._replayable(x, y):      # e.g. a ragged last batch: same state, plain launches
+            self.eager_fallbacks += 1
+            return self._eager(x, y)
+        self._x.copy_(x)
+        self._y.copy_(y)
+        self._g.replay()
+        if self.world > 1:
+            self._allreduce()
+            self._g2.replay()
+        return self._loss_static.clone()
+
+    @property
+    def nonfinite_steps(self) -> int:
+        return int(self._nonfinite.item()) if self.device_side else self._nonfinite_host
+
+    # -- checkpoint / resume (src/training/chekpoints.py dict keys) -----------------------------
+    def state_dict(self):
+        return {"model": self.core.state_dict(), "optimizer": self.opt.state_dict(),
+                "scheduler": self.sched.state_dict()}
+
+    def load_state_dict(self, sd):
+        """In place: a recorded graph keeps reading the same parameter / moment / lr tensors."""
+        self.core.load_state_dict(sd["model"])
+        if sd.get("optimizer") is not None:
+            load_optimizer_state(self.opt, sd["optimizer"])
+        if sd.get("scheduler") is not None:
+            self.sched.load_state_dict(sd["scheduler"])

@@ -4,7 +4,10 @@ the reference load here and vice versa (parameter/buffer names match the referen
 
 Loading uses torch.load(weights_only=True): a checkpoint holds tensors, numbers, strings and
 containers only, and nothing in it is executed.  Tensors are mapped to `map_location` and then
-copied into the (device-resident) modules by load_state_dict.
+copied into the (device-resident) modules by load_state_dict.  The optimizer state goes through
+ogv.train.load_optimizer_state: a fused / capturable AdamW keeps its flags and its device lr
+tensors (a saved float lr is copied into them), and existing moment tensors are overwritten in
+place, so a hipGraph recorded over the optimizer stays valid after a resume.
 """
 import torch
 
@@ -30,7 +33,8 @@ def load_checkpoint(path: str, model, optimizer=None, scheduler=None, scaler=Non
     core = model.module if hasattr(model, "module") else model
     core.load_state_dict(ckpt["model"], strict=strict)
     if optimizer is not None and ckpt.get("optimizer") is not None:
-        optimizer.load_state_dict(ckpt["optimizer"])
+        from ogv.train import load_optimizer_state
+        load_optimizer_state(optimizer, ckpt["optimizer"])
     if scheduler is not None and ckpt.get("scheduler") is not None:
         scheduler.load_state_dict(ckpt["scheduler"])
     if scaler is not None and ckpt.get("scaler") is not None:

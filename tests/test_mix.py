@@ -85,6 +85,21 @@ def test_kernel_bf16_and_full_size_properties():
     assert (out.float() - ref.float()).abs().max().item() <= 2 ** -7 * ref.float().abs().max().item()
 
 
+@pytest.mark.gpu
+def test_out_of_range_label_gives_nan_row():
+    """F.one_hot raises on a label outside [0, K); the kernel cannot raise without a sync, so the
+    row turns NaN (the loss goes non-finite and the Trainer's device guard skips the step)."""
+    from ogv.mix import MixPlan, apply_plan
+    x = torch.randn(4, 3, 8, 8, device="cuda")
+    t = torch.tensor([1, -100, 3, 10], device="cuda")
+    perm = torch.tensor([1, 0, 3, 2], device="cuda")
+    _, soft = apply_plan(x, t, 10, MixPlan(True, False, perm, 0.6))
+    bad = ~torch.isfinite(soft).all(1)
+    assert bad.tolist() == [True, True, True, True]     # every row touches label -100 or 10
+    _, soft = apply_plan(x, torch.tensor([1, 2, 3, 10], device="cuda"), 10, MixPlan(False, False, None, 1.0))
+    assert (~torch.isfinite(soft).all(1)).tolist() == [False, False, False, True]
+
+
 def test_cpu_tensor_refused():
     from ogv.mix import MixPlan, apply_plan
     with pytest.raises(RuntimeError, match="HIP device"):

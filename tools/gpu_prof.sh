@@ -4,7 +4,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
-OUT=gpurun_out/prof
+OUT=${OUT:-gpurun_out/prof}
 rm -rf "$OUT"; mkdir -p "$OUT"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT" -o bench \
   -- python3 bench.py --steps ${STEPS:-4} --warmup ${WARMUP:-3} --no-cpu-baseline --no-parity ${BENCH_ARGS:-} > "$OUT/bench_prof.log" 2>&1

@@ -191,7 +191,12 @@ __device__ __forceinline__ void gemm_epilogue_bf16(f32x4 (&acc)[TM][TN], float* 
 // ------------------------------------------------------------------------------------------------
 // BK = 32 or 64 reduction columns per k-step (64 halves the serial chain of dependent slab loads
 // and barriers: the small-M shapes, whose K loop is latency-bound, use it).
-template <int BM, int BN, bool PRO, bool STATS, int AM = 0, bool BT = false, int BK = 32>
+// SW (split weights): the fp32 weight w is staged as two bf16 tiles, hi = bf16(w) and
+// lo = bf16(w - hi), and every A fragment meets both (two MFMAs): the product carries ~16
+// mantissa bits of the weight instead of 8, so the only bf16 rounding left on a projection is
+// the activation's own storage.  The GEMMs are far below the MFMA ridge (HBM-bound), so the
+// doubled matrix work is nearly free; it halves the bf16 model's logit error.
+template <int BM, int BN, bool PRO, bool STATS, int AM = 0, bool BT = false, int BK = 32, bool SW = false>
 __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__ A, int lda, Pro pro,
                                                         const float* __restrict__ Wt, int ldw, Epi epi,
                                                         bf16* __restrict__ out, int ldo, int M, int N, int K, int Ka,
@@ -202,10 +207,11 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
   constexpr int B_F4 = BN * BK / 4 / 256;
   constexpr int SP = WN + 4;  // epilogue staging pitch (floats)
   constexpr int B_ELEMS = (BT && BK * (BN + 16) > BN * PITCH) ? BK * (BN + 16) : BN * PITCH;
-  constexpr int MAIN_BYTES = (BM * PITCH + B_ELEMS) * 2, EPI_BYTES = 4 * 16 * SP * 4;
+  constexpr int MAIN_BYTES = (BM * PITCH + B_ELEMS * (SW ? 2 : 1)) * 2, EPI_BYTES = 4 * 16 * SP * 4;
   __shared__ __attribute__((aligned(16))) char smem[MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES];
   bf16* As = reinterpret_cast<bf16*>(smem);
   bf16* Bs = As + BM * PITCH;
+  bf16* Bl = Bs + B_ELEMS;  // SW: the lo tile, same layout
 
   const int bid = blockIdx.x;
   const int xcd = bid & 7, local = bid >> 3;
@@ -353,15 +359,17 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
     }
 #pragma unroll
     for (int i = 0; i < B_F4; ++i) {
-      if constexpr (BT) {  // stage as loaded: Bs[kr][n] (pitch BN+16), read back with transposed LDS reads
-        const int idx = tid + i * 256, kr = idx / (BN / 4), nq = idx % (BN / 4);
-        bf16x4 b = {(bf16)rb[i].x, (bf16)rb[i].y, (bf16)rb[i].z, (bf16)rb[i].w};
-        *reinterpret_cast<bf16x4*>(Bs + kr * (BN + 16) + nq * 4) = b;
-        continue;
-      }
-      const int idx = tid + i * 256, row = idx / (BK / 4), kq = idx % (BK / 4);
+      const int idx = tid + i * 256;
+      // BT: stage as loaded, Bs[kr][n] (pitch BN+16), read back with transposed LDS reads
+      const int off = BT ? (idx / (BN / 4)) * (BN + 16) + (idx % (BN / 4)) * 4
+                         : (idx / (BK / 4)) * PITCH + (idx % (BK / 4)) * 4;
       bf16x4 b = {(bf16)rb[i].x, (bf16)rb[i].y, (bf16)rb[i].z, (bf16)rb[i].w};
-      *reinterpret_cast<bf16x4*>(Bs + row * PITCH + kq * 4) = b;
+      *reinterpret_cast<bf16x4*>(Bs + off) = b;
+      if constexpr (SW) {
+        bf16x4 l = {(bf16)(rb[i].x - (float)b[0]), (bf16)(rb[i].y - (float)b[1]), (bf16)(rb[i].z - (float)b[2]),
+                    (bf16)(rb[i].w - (float)b[3])};
+        *reinterpret_cast<bf16x4*>(Bl + off) = l;
+      }
     }
   };
 
@@ -410,6 +418,30 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
 #pragma unroll
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfg[j], acc[i][j], 0, 0, 0);
+      if constexpr (SW) {  // the lo tile: same fragment addresses, second MFMA per (i, j)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          if constexpr (BT) {
+            typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+            typedef __attribute__((ext_vector_type(8))) short s16x8;
+            const int g = lane >> 4, c16 = lane & 15, q = c16 >> 2, p4 = (c16 & 3) * 4;
+            const int col = wn * WN + j * 16 + p4;
+            const s16x4 lo =
+                __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Bl + (ks + 4 * g + q) * (BN + 16) + col));
+            const s16x4 hi =
+                __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Bl + (ks + 16 + 4 * g + q) * (BN + 16) + col));
+            const s16x8 b8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            bfg[j] = __builtin_bit_cast(bf16x8, b8);
+          } else {
+            bfg[j] = *reinterpret_cast<const bf16x8*>(Bl + (wn * WN + j * 16 + (lane & 15)) * PITCH + ks + 8 * (lane >> 4));
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfg[j], acc[i][j], 0, 0, 0);
+      }
     }
     __syncthreads();
   }
@@ -999,6 +1031,25 @@ static bool use_bk64(int M, int K, int ncols, bool pro, bool zact) {
   return K >= 512 || (M <= 8192 && K >= 256 && ncols <= 512);
 }
 
+// knob "split_w" (bit mask, default 1): bf16 GEMMs multiply by the weight's hi + lo bf16 halves
+// (SW above) in the forward products (bit 0: projections, implicit-GEMM convs) and / or the data
+// gradients (bit 1)
+static int g_split_w = 1;
+void set_split_w(int v) { g_split_w = v & 3; }
+int split_w() { return g_split_w; }
+#define OGV_SW_LAUNCH(COND, KERN, grid, s, ...)  \
+  do {                                           \
+    if (COND) {                                  \
+      constexpr bool SW_ = true;                 \
+      auto k_ = KERN;                            \
+      k_<<<(grid), 256, 0, (s)>>>(__VA_ARGS__);  \
+    } else {                                     \
+      constexpr bool SW_ = false;                \
+      auto k_ = KERN;                            \
+      k_<<<(grid), 256, 0, (s)>>>(__VA_ARGS__);  \
+    }                                            \
+  } while (0)
+
 template <typename T, int BN, bool PRO, bool STATS, int BM = GEMM_BM>
 static void launch_mm(const void* A, int lda, const Pro& pro, const float* Wt, int ldw, void* out, int ldo, int M,
                       int N, int K, int Ka, int Kb, const Epi& epi, hipStream_t s) {
@@ -1015,13 +1066,13 @@ static void launch_mm(const void* A, int lda, const Pro& pro, const float* Wt, i
   if constexpr (sizeof(T) == 2) {
     if constexpr (!PRO) {
       if (use_bk64(M, K, N, false, false)) {
-        gemm_bf16_kernel<BM, BN, PRO, STATS, 0, false, 64><<<grid, 256, 0, s>>>(
-            (const bf16*)A, lda, pro, Wt, ldw, epi, (bf16*)out, ldo, M, N, K, Ka, Kb, nMt, nNt, ConvG());
+        OGV_SW_LAUNCH(g_split_w & 1, (gemm_bf16_kernel<BM, BN, PRO, STATS, 0, false, 64, SW_>), grid, s,
+                      (const bf16*)A, lda, pro, Wt, ldw, epi, (bf16*)out, ldo, M, N, K, Ka, Kb, nMt, nNt, ConvG());
         return;
       }
     }
-    gemm_bf16_kernel<BM, BN, PRO, STATS><<<grid, 256, 0, s>>>((const bf16*)A, lda, pro, Wt, ldw, epi, (bf16*)out,
-                                                              ldo, M, N, K, Ka, Kb, nMt, nNt, ConvG());
+    OGV_SW_LAUNCH(g_split_w & 1, (gemm_bf16_kernel<BM, BN, PRO, STATS, 0, false, 32, SW_>), grid, s, (const bf16*)A, lda, pro, Wt, ldw,
+                  epi, (bf16*)out, ldo, M, N, K, Ka, Kb, nMt, nNt, ConvG());
   } else
     gemm_f32_kernel<BM, BN, PRO, STATS><<<grid, 256, 0, s>>>((const float*)A, lda, pro, Wt, ldw, epi, (float*)out, ldo,
                                                              M, N, K, Ka, Kb, nMt, nNt, ConvG());
@@ -1104,8 +1155,8 @@ static void launch_conv_mm(const void* A, const ConvG& cv, const float* Wt, void
     const int nNt = (N + 127) / 128;
     const unsigned grid = (unsigned)(((nMt + 7) / 8) * 8 * nNt);
     if constexpr (sizeof(T) == 2)
-      gemm_bf16_kernel<BM, 128, false, STATS, 1><<<grid, 256, 0, s>>>((const bf16*)A, 0, Pro(), Wt, K, epi, (bf16*)out,
-                                                                      N, M, N, Kp, K, K, nMt, nNt, cv);
+      OGV_SW_LAUNCH(g_split_w & (cv.transposed ? 2 : 1), (gemm_bf16_kernel<BM, 128, false, STATS, 1, false, 32, SW_>), grid, s, (const bf16*)A, 0, Pro(), Wt,
+                    K, epi, (bf16*)out, N, M, N, Kp, K, K, nMt, nNt, cv);
     else
       gemm_f32_kernel<BM, 128, false, STATS, 1><<<grid, 256, 0, s>>>((const float*)A, 0, Pro(), Wt, K, epi,
                                                                      (float*)out, N, M, N, Kp, K, K, nMt, nNt, cv);
@@ -1113,8 +1164,8 @@ static void launch_conv_mm(const void* A, const ConvG& cv, const float* Wt, void
     const int nNt = (N + 63) / 64;
     const unsigned grid = (unsigned)(((nMt + 7) / 8) * 8 * nNt);
     if constexpr (sizeof(T) == 2)
-      gemm_bf16_kernel<BM, 64, false, STATS, 1><<<grid, 256, 0, s>>>((const bf16*)A, 0, Pro(), Wt, K, epi, (bf16*)out,
-                                                                     N, M, N, Kp, K, K, nMt, nNt, cv);
+      OGV_SW_LAUNCH(g_split_w & (cv.transposed ? 2 : 1), (gemm_bf16_kernel<BM, 64, false, STATS, 1, false, 32, SW_>), grid, s, (const bf16*)A, 0, Pro(), Wt,
+                    K, epi, (bf16*)out, N, M, N, Kp, K, K, nMt, nNt, cv);
     else
       gemm_f32_kernel<BM, 64, false, STATS, 1><<<grid, 256, 0, s>>>((const float*)A, 0, Pro(), Wt, K, epi,
                                                                     (float*)out, N, M, N, Kp, K, K, nMt, nNt, cv);
@@ -1230,12 +1281,11 @@ static void launch_mm_bt(const void* A, int lda, const float* W, int ldw, void* 
   const int Kp = (K + 31) / 32 * 32;
   if constexpr (sizeof(T) == 2) {
     if (use_bk64(M, K, N, false, epi.zact != 0))
-      gemm_bf16_kernel<BM, BN, false, false, 0, true, 64><<<grid, 256, 0, s>>>(
-          (const bf16*)A, lda, Pro(), W, ldw, epi, (bf16*)out, ldo, M, N, (K + 63) / 64 * 64, K, K, nMt, nNt, ConvG());
+      OGV_SW_LAUNCH(g_split_w & 2, (gemm_bf16_kernel<BM, BN, false, false, 0, true, 64, SW_>), grid, s, (const bf16*)A, lda, Pro(), W,
+                    ldw, epi, (bf16*)out, ldo, M, N, (K + 63) / 64 * 64, K, K, nMt, nNt, ConvG());
     else
-      gemm_bf16_kernel<BM, BN, false, false, 0, true><<<grid, 256, 0, s>>>((const bf16*)A, lda, Pro(), W, ldw, epi,
-                                                                           (bf16*)out, ldo, M, N, Kp, K, K, nMt, nNt,
-                                                                           ConvG());
+      OGV_SW_LAUNCH(g_split_w & 2, (gemm_bf16_kernel<BM, BN, false, false, 0, true, 32, SW_>), grid, s, (const bf16*)A, lda, Pro(), W,
+                    ldw, epi, (bf16*)out, ldo, M, N, Kp, K, K, nMt, nNt, ConvG());
   } else
     gemm_f32_kernel<BM, BN, false, false, 0, true><<<grid, 256, 0, s>>>((const float*)A, lda, Pro(), W, ldw, epi,
                                                                         (float*)out, ldo, M, N, Kp, K, K, nMt, nNt,

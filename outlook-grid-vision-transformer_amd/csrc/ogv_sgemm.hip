@@ -35,7 +35,10 @@ __host__ __device__ constexpr int sg_kp() { return KT * 32 + 8; }  // W tile pit
 // columns of one row: bias / residual / Z are read and out is written as 8-byte runs straight
 // from registers (the four lanes of a row group cover 32 contiguous bytes per instruction, the
 // four n-subtiles of a chunk the whole 128-byte line), with no LDS staging and no wave barrier.
-template <int KT, int RS, int PA, int ZA, bool STATS, bool BT>
+//
+// SW: the weight is staged as two bf16 tiles (hi = bf16(w), lo = bf16(w - hi)) and every A
+// fragment meets both, as in the tiled kernel (ogv_gemm.hip, knob "split_w").
+template <int KT, int RS, int PA, int ZA, bool STATS, bool BT, bool SW>
 __global__ __launch_bounds__(SG_NW * 64) void sgemm_bf16_kernel(const bf16* __restrict__ A, int lda, Pro pro,
                                                                 const float* __restrict__ W, int ldw, Epi epi,
                                                                 bf16* __restrict__ out, int ldo, int M, int N, int K,
@@ -47,7 +50,8 @@ __global__ __launch_bounds__(SG_NW * 64) void sgemm_bf16_kernel(const bf16* __re
   const int nb = min(NB, N - n0);  // multiple of 8
   const int nbp = (nb + SG_CW - 1) / SG_CW * SG_CW;
   bf16* Ws = reinterpret_cast<bf16*>(smem);
-  double* sacc = reinterpret_cast<double*>(smem + (size_t)nbp * KP * 2);
+  bf16* Wl = Ws + (size_t)nbp * KP;  // SW: lo tile
+  double* sacc = reinterpret_cast<double*>(smem + (size_t)nbp * KP * 2 * (SW ? 2 : 1));
   float* cvec = reinterpret_cast<float*>(sacc + (STATS ? SG_NW * 2 * nbp : 0));  // [bias | stat shift]
 
   // ---- weight tile -> LDS (bf16), zero outside [0,nb) x [0,K).  Batches of SG_WB independent
@@ -83,6 +87,11 @@ __global__ __launch_bounds__(SG_NW * 64) void sgemm_bf16_kernel(const bf16* __re
           const int r = idx / QPR, k = (idx - r * QPR) * 4;
           bf16x4 w4 = {(bf16)v[b].x, (bf16)v[b].y, (bf16)v[b].z, (bf16)v[b].w};
           *reinterpret_cast<bf16x4*>(Ws + r * KP + k) = w4;
+          if constexpr (SW) {
+            bf16x4 l4 = {(bf16)(v[b].x - (float)w4[0]), (bf16)(v[b].y - (float)w4[1]), (bf16)(v[b].z - (float)w4[2]),
+                         (bf16)(v[b].w - (float)w4[3])};
+            *reinterpret_cast<bf16x4*>(Wl + r * KP + k) = l4;
+          }
         }
       }
     }
@@ -113,10 +122,13 @@ __global__ __launch_bounds__(SG_NW * 64) void sgemm_bf16_kernel(const bf16* __re
         const int idx = base + b * NT;
         if (idx < total) {
           const int k = idx / q4, r = (idx - k * q4) * 4;
-          Ws[(r + 0) * KP + k] = (bf16)v[b].x;
-          Ws[(r + 1) * KP + k] = (bf16)v[b].y;
-          Ws[(r + 2) * KP + k] = (bf16)v[b].z;
-          Ws[(r + 3) * KP + k] = (bf16)v[b].w;
+          const float vv[4] = {v[b].x, v[b].y, v[b].z, v[b].w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const bf16 h = (bf16)vv[e];
+            Ws[(r + e) * KP + k] = h;
+            if constexpr (SW) Wl[(r + e) * KP + k] = (bf16)(vv[e] - (float)h);
+          }
         }
       }
     }
@@ -242,6 +254,12 @@ __global__ __launch_bounds__(SG_NW * 64) void sgemm_bf16_kernel(const bf16* __re
           const bf16x8 w = *reinterpret_cast<const bf16x8*>(Ws + (c0 + j * 16 + fr) * KP + kt * 32 + fg * 8);
 #pragma unroll
           for (int i = 0; i < RS; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, a[i][kt], acc[i][j], 0, 0, 0);
+          if constexpr (SW) {
+            const bf16x8 wl = *reinterpret_cast<const bf16x8*>(Wl + (c0 + j * 16 + fr) * KP + kt * 32 + fg * 8);
+#pragma unroll
+            for (int i = 0; i < RS; ++i)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl, a[i][kt], acc[i][j], 0, 0, 0);
+          }
         }
       }
       // ---- epilogue: lane holds out[m = mp + i*16 + fr][n0 + c0 + j*16 + 4*fg + r], r = 0..3
@@ -359,7 +377,7 @@ static int device_cus() {
 }
 
 struct SgPlan {
-  int ok = 0, KT = 0, RS = 1, NB = 0, ntiles = 1, grid = 0;
+  int ok = 0, KT = 0, RS = 1, NB = 0, ntiles = 1, grid = 0, sw = 0;
   size_t lds = 0;
 };
 
@@ -370,8 +388,20 @@ static bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) =
 // Routing (measured, tools/bench_sgemm.py, cold caches, MI355X): the streaming kernel wins for
 // reductions up to 192 everywhere; at 256-384 only when the A prologue (GELU) makes the tiled
 // kernel VALU-bound; a data-gradient whose output needs two weight tiles loses to the tiled kernel.
+// split weights (knob "split_w") double the weight tile; a shape whose split tiles do not fit
+// runs unsplit on this kernel rather than moving to the tiled one
+static SgPlan sgemm_plan_w(int M, int N, int K, bool stats, bool prologue, bool dgrad, int wtiles);
 static SgPlan sgemm_plan(int M, int N, int K, bool stats, bool prologue, bool dgrad) {
+  if (split_w() & (dgrad ? 2 : 1)) {
+    SgPlan p = sgemm_plan_w(M, N, K, stats, prologue, dgrad, 2);
+    if (p.ok) return p;
+  }
+  return sgemm_plan_w(M, N, K, stats, prologue, dgrad, 1);
+}
+
+static SgPlan sgemm_plan_w(int M, int N, int K, bool stats, bool prologue, bool dgrad, int wtiles) {
   SgPlan p;
+  p.sw = wtiles == 2;
   if (M < g_sg_min_m || (K & 7) != 0 || (N & 7) != 0) return p;  // small M: the tiled kernel fills the chip better
   int KT;
   if (K <= 64) KT = 2;
@@ -386,7 +416,7 @@ static SgPlan sgemm_plan(int M, int N, int K, bool stats, bool prologue, bool dg
   p.KT = KT;
   p.RS = KT <= 2 ? 2 : 1;
   auto lds_of = [&](int nb) {  // nb padded to the chunk
-    return (size_t)nb * KP * 2 + (stats ? (size_t)SG_NW * 2 * nb * 8 : 0) + (size_t)nb * 8;
+    return (size_t)nb * KP * 2 * wtiles + (stats ? (size_t)SG_NW * 2 * nb * 8 : 0) + (size_t)nb * 8;
   };
   // widest tile (multiple of the 64-column chunk) whose bf16 copy fits next to the staging slabs
   int NB = (N + SG_CW - 1) / SG_CW * SG_CW;
@@ -416,12 +446,13 @@ static SgPlan sgemm_plan(int M, int N, int K, bool stats, bool prologue, bool dg
 template <int KT, int RS, int PA, int ZA, bool STATS, bool BT>
 static int sg_launch(const SgPlan& p, const bf16* A, int lda, const Pro& pro, const float* W, int ldw,
                      const Epi& epi, bf16* out, int ldo, int M, int N, int K, hipStream_t s) {
-  auto kern = sgemm_bf16_kernel<KT, RS, PA, ZA, STATS, BT>;
-  static bool attr = false;
-  if (!attr) {
+  const int sw = p.sw;
+  auto kern = sw ? sgemm_bf16_kernel<KT, RS, PA, ZA, STATS, BT, true> : sgemm_bf16_kernel<KT, RS, PA, ZA, STATS, BT, false>;
+  static bool attr[2] = {false, false};
+  if (!attr[sw]) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)SG_LDS_CAP);
-    attr = true;
+    attr[sw] = true;
   }
   int gx = p.grid;
   if (g_sg_per_cu > 2) {

@@ -47,8 +47,16 @@ class MaxOutNet(nn.Module):
                 x = blk(x)
             if si < len(self.downs):
                 x = self.downs[si](x)
-        pooled = self.head_norm(x).mean(dim=(2, 3))
-        return self.classifier(pooled)
+        return classifier_head(self.head_norm(x), self.classifier)
+
+
+def classifier_head(x, classifier: nn.Linear):
+    """GAP -> Linear (Model_A_OutGridNet.py:65-67) in fp32 even under bf16 autocast: the pooled
+    features are averaged in fp32 and the classifier keeps its fp32 weights ([B, C] x [C, K]: no
+    measurable cost), so the logits carry no bf16 rounding of their own."""
+    pooled = x.mean(dim=(2, 3), dtype=torch.float32)
+    with torch.autocast("cuda", enabled=False):
+        return classifier(pooled)
 
 
 def train_prologue(model: nn.Module, x):

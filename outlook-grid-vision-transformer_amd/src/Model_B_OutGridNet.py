@@ -19,7 +19,7 @@ from src.model.Grid_Only_Block import GridOnlyBlock, OutlookerBlock2d
 from src.model.downsampling import Downsample, DownsampleConfig
 from src.model.stem_head import ConvStem, make_dpr
 from src.stage_config import StageCfg
-from src.Model_A_OutGridNet import train_prologue
+from src.Model_A_OutGridNet import classifier_head, train_prologue
 from ogv.layers import BatchNorm2d, Conv1x1
 
 
@@ -58,5 +58,4 @@ class OutlookerFrontGridNet(nn.Module):
                 x = blk(x)
             if si < len(self.downs):
                 x = self.downs[si](x)
-        pooled = self.head_norm(x).mean(dim=(2, 3))
-        return self.classifier(pooled)
+        return classifier_head(self.head_norm(x), self.classifier)

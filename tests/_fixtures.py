@@ -6,6 +6,8 @@ import pathlib
 
 import numpy as np
 import torch
+import torch.utils._python_dispatch
+import torch.utils._pytree
 
 import gen_params as gp
 import ogv_oracle as orc
@@ -102,3 +104,27 @@ def maxrel(a, b):
 
 def maxabs(a, b):
     return (torch.as_tensor(a).double().cpu() - torch.as_tensor(b).double().cpu()).abs().max().item()
+
+
+class Bf16Storage(torch.utils._python_dispatch.TorchDispatchMode):
+    """fp32 emulation of bf16 activation storage (test infrastructure): every floating-point
+    tensor an op produces is rounded to bf16 and carried on in fp32.  Parameters enter unrounded
+    (the kernels multiply by hi + lo weight halves: split_w), arithmetic is fp32.  Run the CPU
+    oracle's functions under it (on any device) to get the error that storing every intermediate
+    activation in bf16 costs a forward -- a superset of the fused kernels' own rounding points."""
+
+    def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+        out = func(*args, **(kwargs or {}))
+
+        def rnd(t):
+            if isinstance(t, torch.Tensor) and t.dtype == torch.float32 and t.ndim >= 1 and t.numel() > 1:
+                return t.to(torch.bfloat16).to(torch.float32)
+            return t
+        return torch.utils._pytree.tree_map(rnd, out)
+
+
+def bf16_storage_error(fn, x, ref):
+    """max|fn(bf16(x)) - ref| with fn run under Bf16Storage (fn: oracle forward of x)."""
+    with torch.no_grad(), Bf16Storage():
+        y = fn(x.to(torch.bfloat16).to(torch.float32))
+    return maxabs(y.float(), ref)

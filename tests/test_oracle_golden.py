@@ -81,8 +81,10 @@ def test_grid_capture_golden():
 
 
 @pytest.mark.parametrize("mode", ["eval", "train"])
-def test_model_a(mode):
-    meta, arr = fx.load(f"model_a_7m_{mode}_b2")
+@pytest.mark.parametrize("size", ["7m", "14m"])
+def test_model_a(mode, size):
+    """Model-A-7M (CIFAR 32x32) and Model-A-14M (200 classes, 64x64: BASELINE configs[3])."""
+    meta, arr = fx.load(f"model_a_{size}_{mode}_b2")
     p = fx.oracle_params(meta)
     assert list(p.keys()) == list(fx.shapes_for(meta).keys())
     names = [k for k in p if p[k].requires_grad]
@@ -96,7 +98,7 @@ def test_model_a(mode):
     gn = np.array([p[k].grad.norm().item() if p[k].grad is not None else 0.0 for k in names])
     np.testing.assert_allclose(gn, arr["grad_norms"], rtol=2e-4, atol=1e-7)
     n_params = sum(p[k].numel() for k in names)
-    assert n_params == meta["n_params"] == 7518102
+    assert n_params == meta["n_params"] == {"7m": 7518102, "14m": 14637698}[size]
 
 
 # ---------------------------------------------------------------- Model B family (Grid_Only_Block.py,

@@ -61,16 +61,23 @@ int ogv_gpu_sleep(int microseconds, void* stream);
  * Outlook aggregation.  Replaces, for stride 1:
  *   softmax over the k*k logits per (pixel, head)   src/model/outlook_attention.py:106-107
  *   F.unfold(v, k, padding=k//2) + mul + sum(-1)    src/model/outlook_attention.py:111-120
- * logits: [M, heads*k*k] (channel = head*k*k + ki*k + kj, unscaled), v/y: [M, C], M = B*H*W.
- * Zero-padded neighbours keep their softmax mass (reference semantics).
- * bwd writes dv [M, C] and dlogits [M, heads*k*k]; probs_ws is fp32 [M, heads*k*k] scratch.
- * ld_logits is the row stride of logits/dlogits in elements (>= heads*k*k).
+ * logits: [M, heads*k*k] (channel = head*k*k + ki*k + kj, unscaled), v: [M, C], y/dy: [M, C]
+ * contiguous, M = B*H*W.  Zero-padded neighbours keep their softmax mass (reference semantics).
+ * Row strides in elements: ld_logits (>= heads*k*k) for logits, ld_v (>= C) for v, ld_dv for dv,
+ * ld_dlogits for dlogits -- so v and the logits may be the two column ranges of ONE [M, ld]
+ * projection output (the fused v / attn 1x1 GEMM, OutlookAttention2d with no hooks on .attn/.v),
+ * and dv / dlogits the matching column ranges of one gradient buffer.
+ * bwd writes dv [M, C] and dlogits [M, heads*k*k]; columns [heads*k*k, dl_cols) of every dlogits
+ * row are written with zeros (the padding columns of a concatenated gradient).  probs_ws is fp32
+ * scratch of ogv_outlook_bwd_ws_bytes(...) bytes (0 = may be NULL: the LDS-tiled bf16 kernels,
+ * k = 3 and head_dim % 8 == 0, <= 64, keep the probabilities in LDS).
  * ------------------------------------------------------------------------------------------- */
 int ogv_outlook_agg_fwd(const void* v, const void* logits, void* y, int B, int H, int W, int C,
-                        int heads, int k, int ld_logits, ogv_dtype dt, void* stream);
+                        int heads, int k, int ld_logits, int ld_v, ogv_dtype dt, void* stream);
+size_t ogv_outlook_bwd_ws_bytes(int B, int H, int W, int C, int heads, int k, ogv_dtype dt);
 int ogv_outlook_agg_bwd(const void* dy, const void* v, const void* logits, void* dv, void* dlogits,
                         float* probs_ws, int B, int H, int W, int C, int heads, int k, int ld_logits,
-                        ogv_dtype dt, void* stream);
+                        int ld_v, int ld_dv, int ld_dlogits, int dl_cols, ogv_dtype dt, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Grid multi-head self-attention core.  Replaces

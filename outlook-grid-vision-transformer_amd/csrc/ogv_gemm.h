@@ -173,6 +173,7 @@ void set_ln_bwd_blocks(int v);
 void set_gemm_bn64(int v);
 void set_grid_lds(int v);
 void set_split_w(int v);
+void set_outlook_tile(int v);
 int split_w();
 
 }  // namespace ogv

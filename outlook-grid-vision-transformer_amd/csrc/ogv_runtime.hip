@@ -138,6 +138,10 @@ extern "C" int ogv_set_option(const char* name, int value) {
     set_sg_per_cu(value);
     return OGV_OK;
   }
+  if (!strcmp(name, "outlook_tile")) {
+    set_outlook_tile(value);
+    return OGV_OK;
+  }
   if (!strcmp(name, "split_w")) {
     set_split_w(value);
     return OGV_OK;

@@ -394,34 +394,77 @@ def layer_norm_rows_pair(x2d, gamma, beta, eps):
 # ------------------------------------------------------------------------------------------------
 # Outlook aggregation (softmax over k*k + zero-padded neighbourhood gather)
 # ------------------------------------------------------------------------------------------------
+def _outlook_bwd(dy, v2d, ldv, logits2d, ldl, dv, lddv, dlogits, lddl, dl_cols, B, H, W, C, heads, k):
+    lib = _lib.load()
+    M = B * H * W
+    dt = _dt(dy)
+    nws = lib.ogv_outlook_bwd_ws_bytes(B, H, W, C, heads, k, dt)
+    probs = torch.empty(max(nws // 4, 1), dtype=torch.float32, device=dy.device) if nws else None
+    check(lib.ogv_outlook_agg_bwd(_ptr(dy), _vp(v2d), _vp(logits2d), _vp(dv), _vp(dlogits), _ptr(probs), B, H, W, C,
+                                  heads, k, ldl, ldv, lddv, lddl, dl_cols, dt, _stream()), "ogv_outlook_agg_bwd")
+
+
 class _OutlookAgg(torch.autograd.Function):
+    """v [M, C] (row stride >= C) and logits [M, heads*k*k] as separate tensors."""
+
     @staticmethod
     def forward(ctx, v2d, logits2d, B, H, W, heads, k):
         lib = _lib.load()
         M, C = v2d.shape
-        y = torch.empty_like(v2d)
+        y = torch.empty((M, C), dtype=v2d.dtype, device=v2d.device)
         with _probe("outlook_fwd", dict(M=M, C=C, heads=heads, k=k, elem=v2d.element_size())):
             check(lib.ogv_outlook_agg_fwd(_ptr(v2d), _ptr(logits2d), _ptr(y), B, H, W, C, heads, k,
-                                          logits2d.stride(0), _dt(v2d), _stream()), "ogv_outlook_agg_fwd")
+                                          logits2d.stride(0), v2d.stride(0), _dt(v2d), _stream()),
+                  "ogv_outlook_agg_fwd")
         ctx.save_for_backward(v2d, logits2d)
         ctx.meta = (B, H, W, C, heads, k)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        lib = _lib.load()
         v2d, logits2d = ctx.saved_tensors
         B, H, W, C, heads, k = ctx.meta
         kk = k * k
         dy = dy.to(v2d.dtype).contiguous()
-        dv = torch.empty_like(v2d)
         M = v2d.shape[0]
+        dv = torch.empty((M, C), dtype=v2d.dtype, device=v2d.device)
         ld = logits2d.stride(0)
         dlogits = torch.empty((M, ld), dtype=v2d.dtype, device=v2d.device)[:, : heads * kk]
-        probs = torch.empty((M, heads * kk), dtype=torch.float32, device=v2d.device)
-        check(lib.ogv_outlook_agg_bwd(_ptr(dy), _ptr(v2d), _ptr(logits2d), _ptr(dv), _ptr(dlogits), _ptr(probs), B, H,
-                                      W, C, heads, k, ld, _dt(v2d), _stream()), "ogv_outlook_agg_bwd")
+        _outlook_bwd(dy, v2d.data_ptr(), v2d.stride(0), logits2d.data_ptr(), ld, dv.data_ptr(), C, dlogits.data_ptr(),
+                     ld, heads * kk, B, H, W, C, heads, k)
         return dv, dlogits, None, None, None, None, None
+
+
+class _OutlookAggCat(torch.autograd.Function):
+    """The fused v / attn projection output cat = [v | logits | zero pad] of shape [M, ld]
+    (OutlookAttention2d with no hooks): the kernels read both column ranges in place, and the
+    backward writes ONE gradient [dv | dlogits | 0] of the same layout, which the single
+    concatenated GEMM's backward consumes (one dgrad + one wgrad, no autograd add)."""
+
+    @staticmethod
+    def forward(ctx, cat, C, B, H, W, heads, k):
+        lib = _lib.load()
+        M, ld = cat.shape
+        y = torch.empty((M, C), dtype=cat.dtype, device=cat.device)
+        es = cat.element_size()
+        with _probe("outlook_fwd", dict(M=M, C=C, heads=heads, k=k, elem=es)):
+            check(lib.ogv_outlook_agg_fwd(_ptr(cat), _vp(cat.data_ptr() + C * es), _ptr(y), B, H, W, C, heads, k, ld, ld,
+                                          _dt(cat), _stream()), "ogv_outlook_agg_fwd")
+        ctx.save_for_backward(cat)
+        ctx.meta = (B, H, W, C, heads, k)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        cat, = ctx.saved_tensors
+        B, H, W, C, heads, k = ctx.meta
+        M, ld = cat.shape
+        es = cat.element_size()
+        dy = dy.to(cat.dtype).contiguous()
+        dcat = torch.empty_like(cat)
+        _outlook_bwd(dy, cat.data_ptr(), ld, cat.data_ptr() + C * es, ld, dcat.data_ptr(), ld, dcat.data_ptr() + C * es,
+                     ld, ld - C, B, H, W, C, heads, k)
+        return dcat, None, None, None, None, None, None
 
 
 def outlook_aggregate_rows(v2d, logits2d, B, H, W, heads, k):
@@ -432,6 +475,14 @@ def outlook_aggregate_rows(v2d, logits2d, B, H, W, heads, k):
     if logits2d.dtype != v2d.dtype:
         logits2d = logits2d.to(v2d.dtype)
     return _OutlookAgg.apply(v2d, logits2d, int(B), int(H), int(W), int(heads), int(k))
+
+
+def outlook_aggregate_cat(cat, C, B, H, W, heads, k):
+    """cat [M, ld] = [v (C columns) | logits (heads*k*k) | padding] -> y [M, C]."""
+    require_device(cat, what="ogv.outlook_aggregate")
+    if cat.stride(-1) != 1 or cat.stride(0) != cat.shape[1] or cat.shape[1] < C + heads * k * k:
+        raise ValueError("ogv.outlook_aggregate_cat: expects a contiguous [M, >= C + heads*k*k] tensor")
+    return _OutlookAggCat.apply(cat, int(C), int(B), int(H), int(W), int(heads), int(k))
 
 
 # ------------------------------------------------------------------------------------------------

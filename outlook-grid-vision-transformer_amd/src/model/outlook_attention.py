@@ -6,7 +6,12 @@ Drop-in for src/model/outlook_attention.py of the reference:
   MLP2d                      :33-49    (1x1 C->hidden, act, 1x1 hidden->C) -> two MFMA GEMMs,
                                         the activation applied in the second GEMM's prologue
   OutlookAttention2d         :52-124   logits/v/proj 1x1 convs -> MFMA GEMMs; softmax over k*k +
-                                        unfold-gather (:100-120) -> ogv_outlook_agg_{fwd,bwd}
+                                        unfold-gather (:100-120) -> ogv_outlook_agg_{fwd,bwd}.
+                                        With no hooks on .attn / .v the two projections of the same
+                                        input run as ONE GEMM over [Wv; Wattn; 0] (v and the logits
+                                        are column ranges of its output, read in place by the
+                                        LDS-tiled gather; the backward is one gradient buffer,
+                                        one dgrad and one wgrad)
 Parameters and their names/shapes are unchanged (attn.weight [heads*k*k, C, 1, 1], v.*, proj.*).
 Tensors are NCHW logically and channels_last physically.
 """
@@ -101,16 +106,42 @@ class OutlookAttention2d(nn.Module):
         self.proj = Conv1x1(dim, dim, bias=True)
         self.proj_drop = nn.Dropout(proj_drop)
 
+    def _hooked(self) -> bool:
+        return any(m._forward_hooks or m._forward_pre_hooks for m in (self.attn, self.v))
+
+    def _cat_params(self):
+        """[Wv; Wattn; 0] ([ld, C], ld = C + heads*k*k rounded up to 8 so every row of the GEMM
+        output is 16-B aligned) and the matching bias, differentiable w.r.t. both convs."""
+        C, n = self.dim, self.attn.out_channels
+        ld = (C + n + 7) // 8 * 8
+        wv, wa = self.v.weight.reshape(C, C), self.attn.weight.reshape(n, C)
+        parts = [wv.float(), wa.float()]
+        if ld > C + n:
+            parts.append(wv.new_zeros(ld - C - n, C, dtype=torch.float32))
+        w = torch.cat(parts)
+        if self.v.bias is None and self.attn.bias is None:
+            return w, None
+        bv = self.v.bias if self.v.bias is not None else wv.new_zeros(C)
+        ba = self.attn.bias if self.attn.bias is not None else wa.new_zeros(n)
+        bparts = [bv.float(), ba.float()] + ([bv.new_zeros(ld - C - n, dtype=torch.float32)] if ld > C + n else [])
+        return w, torch.cat(bparts)
+
     def forward(self, x: torch.Tensor, residual=None, row_scale=None) -> torch.Tensor:
         if self.stride != 1:
             raise NotImplementedError("ogv OutlookAttention2d implements stride=1 (the OutGridBlock path)")
         if self.training and self.attn_drop.p > 0:
             raise NotImplementedError("ogv OutlookAttention2d: attn_drop > 0 in training is not implemented")
         B, C, H, W = x.shape
-        a = self.attn(x)                     # [B, heads*k*k, H, W]
-        v = self.v(x)                        # [B, C, H, W]
-        y = OF.outlook_aggregate_rows(OF.nchw_to_rows(v), OF.nchw_to_rows(a), B, H, W,
-                                      self.num_heads, self.kernel_size)
+        if self._hooked():
+            a = self.attn(x)                     # [B, heads*k*k, H, W]  (analysis hooks read this)
+            v = self.v(x)                        # [B, C, H, W]
+            y = OF.outlook_aggregate_rows(OF.nchw_to_rows(v), OF.nchw_to_rows(a), B, H, W,
+                                          self.num_heads, self.kernel_size)
+        else:
+            dt = OF.compute_dtype(x)
+            w, b = self._cat_params()
+            cat = OF.linear_rows(OF.nchw_to_rows(x.to(dt)), w, b)     # [M, v | logits | 0]
+            y = OF.outlook_aggregate_cat(cat, C, B, H, W, self.num_heads, self.kernel_size)
         y = OF.rows_to_nchw(y, B, H, W)
         if self.training and self.proj_drop.p > 0:
             y = self.proj_drop(self.proj(y))

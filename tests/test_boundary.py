@@ -35,13 +35,17 @@ def test_host_validation_without_gpu():
     import ogv._lib as L
     lib = L.load()
     # null pointers / bad shapes are rejected before any launch
-    rc = lib.ogv_outlook_agg_fwd(None, None, None, 1, 4, 4, 16, 3, 3, 27, 0, None)
+    rc = lib.ogv_outlook_agg_fwd(None, None, None, 1, 4, 4, 16, 3, 3, 27, 16, 0, None)
     assert rc == 1 and b"null" in lib.ogv_last_error()
     x = ctypes.c_void_p(16)
-    rc = lib.ogv_outlook_agg_fwd(x, x, x, 1, 4, 4, 16, 3, 3, 27, 0, None)     # 16 % 3 != 0
+    rc = lib.ogv_outlook_agg_fwd(x, x, x, 1, 4, 4, 16, 3, 3, 27, 16, 0, None)     # 16 % 3 != 0
     assert rc == 1 and b"divisible" in lib.ogv_last_error()
-    rc = lib.ogv_outlook_agg_fwd(x, x, x, 1, 4, 4, 18, 3, 4, 27, 0, None)     # even kernel
+    rc = lib.ogv_outlook_agg_fwd(x, x, x, 1, 4, 4, 18, 3, 4, 27, 18, 0, None)     # even kernel
     assert rc == 1
+    rc = lib.ogv_outlook_agg_fwd(x, x, x, 1, 4, 4, 18, 3, 3, 27, 16, 0, None)     # ld_v < C
+    assert rc == 1 and b"ld_v" in lib.ogv_last_error()
+    rc = lib.ogv_outlook_agg_bwd(x, x, x, x, x, None, 1, 4, 4, 18, 3, 3, 27, 18, 18, 27, 20, 0, None)  # dl_cols < 27
+    assert rc == 1 and b"dl_cols" in lib.ogv_last_error()
     rc = lib.ogv_grid_attn_fwd(x, x, x, None, 1, 6, 6, 16, 2, 4, 1.0, 0, None)  # 6 % 4
     assert rc == 1 and b"divisible" in lib.ogv_last_error()
     rc = lib.ogv_layernorm_fwd(x, None, None, x, None, None, 4, 6, 1e-5, 0, None)  # C % 4

@@ -233,12 +233,26 @@ def test_model_logits(fixture, mode, dtype):
 OUTLOOK_CASES = [  # B, C, heads, k, H, W
     (1, 48, 2, 3, 32, 32), (3, 96, 3, 3, 16, 16), (2, 16, 4, 3, 5, 7), (2, 24, 2, 5, 9, 6),
     (1, 64, 2, 7, 8, 8), (2, 12, 3, 1, 4, 4), (2, 32, 8, 3, 1, 1), (1, 256, 8, 3, 4, 4),
+    # LDS-tiled bf16 kernels (k = 3, head_dim % 8 == 0, <= 64): partial tiles, several images per
+    # block with a ragged last group, head_dim 8 / 64, 1x1 images
+    (1, 64, 1, 3, 7, 13), (3, 128, 2, 3, 4, 4), (5, 384, 6, 3, 8, 8), (2, 16, 2, 3, 1, 1), (1, 48, 2, 3, 9, 33),
+    (2, 192, 6, 3, 8, 8), (1, 64, 2, 3, 56, 56),
 ]
+
+
+@pytest.fixture(params=[2, 3], ids=["tile_bwd", "tile_fwd_bwd"])
+def outlook_tile_mode(request):
+    """Default kernel selection (tiled backward) and the knob's tiled forward as well."""
+    from ogv._lib import load
+    lib = load()
+    assert lib.ogv_set_option(b"outlook_tile", request.param) == 0
+    yield request.param
+    assert lib.ogv_set_option(b"outlook_tile", 2) == 0
 
 
 @pytest.mark.parametrize("case", OUTLOOK_CASES)
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_outlook_kernel_vs_oracle(case, dtype):
+def test_outlook_kernel_vs_oracle(case, dtype, outlook_tile_mode):
     from ogv import functional as OF
     B, C, h, k, H, W = case
     g = torch.Generator().manual_seed(hash(case) & 0xFFFF)
@@ -257,6 +271,63 @@ def test_outlook_kernel_vs_oracle(case, dtype):
     assert fx.maxabs(y.float(), y_r) <= tol * max(1, y_r.abs().max().item())
     assert fx.maxabs(vd.grad.float(), v_r.grad) <= tol * max(1, v_r.grad.abs().max().item())
     assert fx.maxabs(ld.grad.float(), l_r.grad) <= tol * max(1, l_r.grad.abs().max().item())
+
+
+@pytest.mark.parametrize("case", [(1, 48, 2, 32, 32), (3, 96, 3, 16, 16), (2, 256, 8, 4, 4), (1, 64, 2, 7, 13)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_outlook_cat_layout_vs_oracle(case, dtype):
+    """The fused-projection layout: v and the logits are column ranges of one [M, ld] buffer
+    (ld = C + 9h rounded up to 8), read in place; the backward writes [dv | dlogits | 0]."""
+    from ogv import functional as OF
+    B, C, h, H, W = case
+    kk = 9
+    ld = (C + h * kk + 7) // 8 * 8
+    g = torch.Generator().manual_seed(C * 31 + H)
+    v = torch.randn(B, C, H, W, generator=g).to(dtype).float()
+    lg = (2 * torch.randn(B, h * kk, H, W, generator=g)).to(dtype).float()
+    dy = torch.randn(B, C, H, W, generator=g).to(dtype).float()
+    v_r, l_r = v.clone().requires_grad_(), lg.clone().requires_grad_()
+    y_r = orc.outlook_aggregate(v_r, l_r, h, 3)
+    y_r.backward(dy)
+    cat = torch.zeros(B * H * W, ld, dtype=dtype)
+    cat[:, :C] = v.permute(0, 2, 3, 1).reshape(-1, C).to(dtype)
+    cat[:, C:C + h * kk] = lg.permute(0, 2, 3, 1).reshape(-1, h * kk).to(dtype)
+    cat = cat.to(DEV).requires_grad_()
+    y = OF.outlook_aggregate_cat(cat, C, B, H, W, h, 3)
+    y.backward(dy.permute(0, 2, 3, 1).reshape(-1, C).to(DEV, dtype))
+    tol = 2e-5 if dtype == torch.float32 else 1e-2
+    yr = y_r.permute(0, 2, 3, 1).reshape(-1, C)
+    assert fx.maxabs(y.float(), yr) <= tol * max(1, yr.abs().max().item())
+    gv = v_r.grad.permute(0, 2, 3, 1).reshape(-1, C)
+    gl = l_r.grad.permute(0, 2, 3, 1).reshape(-1, h * kk)
+    d = cat.grad.float()
+    assert fx.maxabs(d[:, :C], gv) <= tol * max(1, gv.abs().max().item())
+    assert fx.maxabs(d[:, C:C + h * kk], gl) <= tol * max(1, gl.abs().max().item())
+    assert torch.equal(d[:, C + h * kk:], torch.zeros_like(d[:, C + h * kk:])), "padding columns must be zero"
+
+
+@pytest.mark.parametrize("case", [(2, 48, 2, 32, 32), (3, 256, 8, 4, 4), (1, 64, 2, 7, 13), (2, 384, 6, 8, 8)])
+def test_outlook_tile_matches_thread_kernels(case):
+    """LDS-tiled bf16 kernels (knob outlook_tile=3) vs the thread-per-chunk kernels (0) on the same
+    inputs: same math, different summation grouping -> within bf16 output rounding."""
+    from ogv import functional as OF
+    from ogv._lib import load
+    lib = load()
+    B, C, h, H, W = case
+    g = torch.Generator(device=DEV).manual_seed(7)
+    v = torch.randn(B * H * W, C, device=DEV, generator=g).to(torch.bfloat16)
+    lg = (2 * torch.randn(B * H * W, h * 9, device=DEV, generator=g)).to(torch.bfloat16)
+    dy = torch.randn(B * H * W, C, device=DEV, generator=g).to(torch.bfloat16)
+    outs = []
+    for mode in (3, 0):     # both tiled kernels / neither
+        assert lib.ogv_set_option(b"outlook_tile", mode) == 0
+        vd, ld_ = v.clone().requires_grad_(), lg.clone().requires_grad_()
+        y = OF.outlook_aggregate_rows(vd, ld_, B, H, W, h, 3)
+        y.backward(dy)
+        outs.append((y.float(), vd.grad.float(), ld_.grad.float()))
+    assert lib.ogv_set_option(b"outlook_tile", 2) == 0
+    for a, b in zip(*outs):
+        assert fx.maxabs(a, b) <= 1e-2 * max(1.0, b.abs().max().item())
 
 
 GRID_CASES = [  # B, H, W, C, heads, g
@@ -407,6 +478,28 @@ def test_layernorm_vs_fp64(case, dtype):
 
 
 # ------------------------------------------------------------------ full-size properties
+def test_outlook_border_mass_224_full_size():
+    """The 224x224 stage-0 layout at its full BASELINE configs[4] size (bs=128, C=64, 2 heads;
+    6.4 M pixels): uniform logits, v == 1 -> 4/9 corner, 6/9 edge, 1 inside; and the backward of
+    y.sum() gives dv = (#windows covering the pixel)/9 with the same border pattern."""
+    from ogv import functional as OF
+    B, C, H, W, h = 128, 64, 224, 224, 2
+    v = torch.ones(B * H * W, C, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    lg = torch.zeros(B * H * W, h * 9, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    y = OF.outlook_aggregate_rows(v, lg, B, H, W, h, 3)
+    y4 = y.detach().view(B, H, W, C).float()
+    for (yy, xx), want in (((0, 0), 4 / 9), ((0, 100), 6 / 9), ((223, 223), 4 / 9), ((150, 0), 6 / 9)):
+        assert torch.allclose(y4[:, yy, xx], torch.full_like(y4[:, yy, xx], want), atol=4e-3)
+    assert torch.allclose(y4[:, 1:-1, 1:-1], torch.ones_like(y4[:, 1:-1, 1:-1]), atol=4e-3)
+    y.backward(torch.ones_like(y))
+    g4 = v.grad.view(B, H, W, C).float()
+    assert torch.allclose(g4[:, 0, 0], torch.full_like(g4[:, 0, 0], 4 / 9), atol=4e-3)
+    assert torch.allclose(g4[:, 5:-5, 5:-5], torch.ones_like(g4[:, 5:-5, 5:-5]), atol=4e-3)
+    # uniform softmax and v == 1: dP is equal across the in-image taps, so dlogits are 0 inside
+    gl = lg.grad.view(B, H, W, h * 9).float()
+    assert gl[:, 1:-1, 1:-1].abs().max().item() <= 1e-3
+
+
 def test_outlook_border_mass_full_size():
     """Uniform logits, v == 1: output = (#in-image neighbours)/9 — 4/9 corner, 6/9 edge, 1 inside
     (zero-padded neighbours keep softmax mass), at the bs=512 stage-0 shape."""

@@ -41,8 +41,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=512, help="per-GPU batch")
     ap.add_argument("--model", default="model_a_7m")
-    ap.add_argument("--probe", default="sgemm", choices=["sgemm", "gemm_fwd", "outlook_fwd", "grid_fwd"],
-                    help="kernel whose launches feed `roofline`")
+    ap.add_argument("--probe", default="gemm_tiled",
+                    choices=["gemm_tiled", "sgemm", "wgrad", "gemm_fwd", "outlook_fwd", "outlook_bwd", "grid_fwd"],
+                    help="kernel family whose launches feed `roofline`")
     ap.add_argument("--eager", action="store_true", help="launch kernels one by one instead of graph replay")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=24.0)
@@ -60,6 +61,11 @@ METRIC = {  # BASELINE.json configs[1..4]
 }
 
 PROBE_KERNEL = {  # probe name -> kernel symbol(s) it times (rocprofv3 names)
+    "gemm_tiled": "ogv::gemm_bf16_kernel<*> (tiled MFMA GEMM: the Linear / 1x1-conv forward and data-gradient "
+                  "launches NOT routed to the streaming kernel -- stages 2-3 of 7M, M <= 32768; the largest-time "
+                  "kernel family of the step)",
+    "wgrad": "ogv::wgrad_bf16_kernel<*> / ogv::swgrad_bf16_kernel<*> + colreduce (Linear / 1x1-conv weight gradients)",
+    "outlook_bwd": "ogv::outlook_bwd_tile_kernel<*> (LDS-tiled outlook backward: the col2im fold as a gather + dlogits)",
     "sgemm": "ogv::sgemm_bf16_kernel<*> (persistent streaming projection GEMM: the Linear / 1x1-conv fwd and dgrad "
              "launches routed to it)",
     "gemm_fwd": "ogv::gemm_bf16_kernel<{128|64},{128|64},*,false,0,false> (Linear / 1x1-conv forward launches)",
@@ -215,7 +221,7 @@ def main():
             if tf.exists() and args.model == "model_a_7m" and B == 512:   # the PMC passes ran on this workload
                 traffic = json.loads(tf.read_text()).get(args.probe, {}).get("hbm_bytes_per_launch")
             ach = probe["achieved_GBs"]
-            roof = {"kernel": PROBE_KERNEL[args.probe], "bound": "hbm", "achieved": round(ach, 1),
+            roof = {"probe": args.probe, "kernel": PROBE_KERNEL[args.probe], "bound": "hbm", "achieved": round(ach, 1),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
                     "algorithmic_bytes_per_launch": int(probe["bytes_per_launch"]),
                     "avg_launch_ms": round(probe["avg_ms"], 5), "launches": probe["n"],

@@ -104,11 +104,15 @@ def probe_bytes(name: str, u: dict) -> int:
         return e * u["M"] * (2 * u["C"] + u["k"] * u["k"] * u["heads"])
     if name == "grid_fwd":      # read qkv [M,3C], write out [M,C] + fp32 lse [M,h]
         return e * u["M"] * 4 * u["C"] + 4 * u["M"] * u["heads"]
-    if name in ("gemm_fwd", "sgemm") and u.get("kind", "fwd") == "fwd":
+    if name == "outlook_bwd":   # read dy, v, logits; write dv, dlogits
+        return e * u["M"] * (3 * u["C"] + 2 * u["k"] * u["k"] * u["heads"])
+    if name == "wgrad":         # read G [M,N], X [M,K]; write fp32 dW [N,K] (+ dbias)
+        return e * u["M"] * (u["N"] + u["K"]) + 4 * u["N"] * u["K"] + (4 * u["N"] if u["bias"] else 0)
+    if name in ("gemm_fwd", "sgemm", "gemm_tiled") and u.get("kind", "fwd") == "fwd":
         # read A [M,K] (+ residual [M,N]) + fp32 W [N,K] (+ bias), write out [M,N]
         return (e * u["M"] * (u["K"] + u["N"] * (2 if u["res"] else 1)) + 4 * u["N"] * u["K"]
                 + (4 * u["N"] if u["bias"] else 0))
-    if name == "sgemm":         # dgrad: read dOut [M,N] (+ Z [M,K]) + fp32 W [N,K], write dA [M,K]
+    if name in ("sgemm", "gemm_tiled"):   # dgrad: read dOut [M,N] (+ Z [M,K]) + fp32 W [N,K], write dA [M,K]
         return e * u["M"] * (u["N"] + u["K"] * (2 if u["z"] else 1)) + 4 * u["N"] * u["K"]
     raise KeyError(name)
 
@@ -117,6 +121,8 @@ def probe_flops(name: str, u: dict) -> int:
     """Algorithmic flops of one launch: the GEMMs 2*M*N*K (the MFMA work)."""
     if name == "outlook_fwd":
         return 18 * u["M"] * u["C"] + 45 * u["M"] * u["heads"]
+    if name == "outlook_bwd":
+        return 36 * u["M"] * u["C"]
     if name == "grid_fwd":
         return 4 * u["M"] * u["N"] * u["C"]
     return 2 * u["M"] * u["N"] * u["K"]
@@ -254,7 +260,9 @@ class _Linear(torch.autograd.Function):
         out = torch.empty((M, N), dtype=x2d.dtype, device=x2d.device)
         units = dict(M=M, N=N, K=K, elem=x2d.element_size(), res=residual is not None, bias=bias is not None)
         stream_k = _PROBE["armed"] and lib.ogv_gemm_stream_route(0, M, N, K, ACT[act_in]) == 1
-        with _probe("gemm_fwd", units), _probe("sgemm", units, when=stream_k):
+        tiled = x2d.dtype == torch.bfloat16 and not stream_k
+        with _probe("gemm_fwd", units), _probe("sgemm", units, when=stream_k), \
+                _probe("gemm_tiled", units, when=tiled):
             check(lib.ogv_gemm_fwd(_ptr(x2d), x2d.stride(0), _ptr(w2d), _ptr(bias), _ptr(residual), _ptr(row_scale),
                                    int(rps), _ptr(out), N, M, N, K, ACT[act_in], _dt(x2d), _stream()), "ogv_gemm_fwd")
         ctx.save_for_backward(x2d, w2d, row_scale)
@@ -282,15 +290,19 @@ class _Linear(torch.autograd.Function):
         # joined back into the current one, also inside a captured graph) so the two latency-bound
         # GEMMs overlap.
         # (below ~_FORK_MIN_WORK the fork/join latency (~10 us per cross-stream edge) outweighs the overlap)
-        fork = want_dx and want_dw and M * (N + K) >= _FORK_MIN_WORK
+        # (while a probe is armed everything stays on the current stream, where its events are)
+        fork = want_dx and want_dw and M * (N + K) >= _FORK_MIN_WORK and not _PROBE["armed"]
         with _fork(fork, dout, x2d, rs, dw, db, ws_w if want_dw else None) as side:
             if want_dw:
-                check(lib.ogv_gemm_wgrad(_ptr(dout), N, _ptr(x2d), x2d.stride(0), _ptr(rs), rps, _ptr(dw), _ptr(db),
-                                         M, N, K, act, _ptr(ws_w), dt, side), "ogv_gemm_wgrad")
+                with _probe("wgrad", dict(M=M, N=N, K=K, elem=x2d.element_size(), bias=has_bias),
+                            when=x2d.dtype == torch.bfloat16):
+                    check(lib.ogv_gemm_wgrad(_ptr(dout), N, _ptr(x2d), x2d.stride(0), _ptr(rs), rps, _ptr(dw), _ptr(db),
+                                             M, N, K, act, _ptr(ws_w), dt, side), "ogv_gemm_wgrad")
             if want_dx:
                 stream_k = _PROBE["armed"] and lib.ogv_gemm_stream_route(1, M, N, K, act) == 1
-                with _probe("sgemm", dict(kind="dgrad", M=M, N=N, K=K, elem=x2d.element_size(), z=bool(act)),
-                            when=stream_k):
+                du = dict(kind="dgrad", M=M, N=N, K=K, elem=x2d.element_size(), z=bool(act))
+                with _probe("sgemm", du, when=stream_k), \
+                        _probe("gemm_tiled", du, when=x2d.dtype == torch.bfloat16 and not stream_k):
                     check(lib.ogv_gemm_dgrad(_ptr(dout), N, _ptr(w2d), _ptr(x2d) if act else None, x2d.stride(0),
                                              _ptr(rs), rps, _ptr(dx), K, M, N, K, act, _ptr(ws_d), dt, _stream()),
                           "ogv_gemm_dgrad")
@@ -400,8 +412,9 @@ def _outlook_bwd(dy, v2d, ldv, logits2d, ldl, dv, lddv, dlogits, lddl, dl_cols, 
     dt = _dt(dy)
     nws = lib.ogv_outlook_bwd_ws_bytes(B, H, W, C, heads, k, dt)
     probs = torch.empty(max(nws // 4, 1), dtype=torch.float32, device=dy.device) if nws else None
-    check(lib.ogv_outlook_agg_bwd(_ptr(dy), _vp(v2d), _vp(logits2d), _vp(dv), _vp(dlogits), _ptr(probs), B, H, W, C,
-                                  heads, k, ldl, ldv, lddv, lddl, dl_cols, dt, _stream()), "ogv_outlook_agg_bwd")
+    with _probe("outlook_bwd", dict(M=M, C=C, heads=heads, k=k, elem=dy.element_size())):
+        check(lib.ogv_outlook_agg_bwd(_ptr(dy), _vp(v2d), _vp(logits2d), _vp(dv), _vp(dlogits), _ptr(probs), B, H, W,
+                                      C, heads, k, ldl, ldv, lddv, lddl, dl_cols, dt, _stream()), "ogv_outlook_agg_bwd")
 
 
 class _OutlookAgg(torch.autograd.Function):

@@ -18,11 +18,14 @@ python3 tools/probe_vs_trace.py "$OUT/prof/bench_kernel_trace.csv" "$OUT/prof.lo
 cat "$OUT/probe_vs_trace.txt"
 gzip -f "$OUT/prof/bench_kernel_trace.csv"
 if [ "${PMC:-1}" = 1 ]; then
-  ARGS="--eager --steps 2 --warmup 1 --no-cpu-baseline --no-parity"
-  timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- python3 bench.py $ARGS > "$OUT/fetch.log" 2>&1 || { echo "pmc fetch rc=$?"; exit 1; }
-  timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- python3 bench.py $ARGS > "$OUT/write.log" 2>&1 || { echo "pmc write rc=$?"; exit 1; }
-  python3 tools/pmc_traffic.py "$OUT/fetch" "$OUT/write" --out "$OUT/pmc_traffic.json"
-  find "$OUT/fetch" "$OUT/write" -name "*counter_collection.csv" -exec gzip -f {} \;
-  find "$OUT/fetch" "$OUT/write" -type f ! -name "*.gz" -delete
+  cp profiles/pmc_traffic.json "$OUT/pmc_traffic.json" 2>/dev/null || true
+  for PR in ${PMC_PROBES:-gemm_tiled outlook_bwd sgemm}; do
+    ARGS="--eager --steps 2 --warmup 1 --no-cpu-baseline --no-parity --probe $PR"
+    timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch_$PR" -o run -- python3 bench.py $ARGS > "$OUT/fetch_$PR.log" 2>&1 || { echo "pmc fetch rc=$?"; exit 1; }
+    timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write_$PR" -o run -- python3 bench.py $ARGS > "$OUT/write_$PR.log" 2>&1 || { echo "pmc write rc=$?"; exit 1; }
+    python3 tools/pmc_traffic.py "$OUT/fetch_$PR" "$OUT/write_$PR" --probe "$PR" --out "$OUT/pmc_traffic.json"
+    find "$OUT/fetch_$PR" "$OUT/write_$PR" -name "*counter_collection.csv" -exec gzip -f {} \;
+    find "$OUT/fetch_$PR" "$OUT/write_$PR" -type f ! -name "*.gz" -delete
+  done
 fi
 du -sh "$OUT"

@@ -17,6 +17,8 @@ import os
 import re
 
 PROBES = {
+    "gemm_tiled": r"gemm_bf16_kernel",
+    "outlook_bwd": r"outlook_bwd",
     "sgemm": r"sgemm_bf16_kernel",
     # bench.py's "gemm_fwd" probe: every Linear / 1x1-conv forward GEMM launch (the only users of the
     # plain bf16 GEMM instantiation: no BN statistics, no conv gather, no transposed weights)
@@ -51,15 +53,21 @@ def main():
     ap.add_argument("fetch_dir")
     ap.add_argument("write_dir")
     ap.add_argument("--out", default="profiles/pmc_traffic.json")
+    ap.add_argument("--probe", default=None, help="the bench.py --probe of this run: only its entry is (re)written, "
+                    "from the launches queued behind the probe's spin; other entries of --out are kept")
     ap.add_argument("--skip-steps", type=int, default=1, help="leading launches per probe treated as warmup: "
                     "steps to drop (the probe keeps the last step's launches)")
     a = ap.parse_args()
     fetch = read_counter(a.fetch_dir, "FETCH_SIZE")
     write = read_counter(a.write_dir, "WRITE_SIZE")
     out = {}
+    if a.probe and os.path.exists(a.out):
+        out = json.load(open(a.out))
     fsel, wsel = behind_sleep(fetch), behind_sleep(write)
     for probe, rx in PROBES.items():
-        if probe == "sgemm" and fsel:   # the probed launches only (same subset as the live probe)
+        if a.probe and probe != a.probe:
+            continue
+        if (probe == "sgemm" or a.probe) and fsel:   # the probed launches only (same subset as the live probe)
             f = [v for i, (_, n, v) in enumerate(fetch) if i in fsel and re.search(rx, n)]
             w = [v for i, (_, n, v) in enumerate(write) if i in wsel and re.search(rx, n)]
         else:

@@ -19,9 +19,11 @@ def main(trace, log):
     line = [ln for ln in open(log) if ln.startswith("{")][-1]
     rec = json.loads(line)
     roof = rec.get("roofline") or {}
-    fam = "sgemm_bf16_kernel" if "sgemm" in roof.get("kernel", "") else None
+    fams = {"sgemm": "sgemm_bf16_kernel", "gemm_tiled": "gemm_bf16_kernel", "outlook_bwd": "outlook_bwd",
+            "outlook_fwd": "outlook_fwd", "grid_fwd": "grid_fwd"}
+    fam = fams.get(roof.get("probe", "sgemm" if "sgemm" in roof.get("kernel", "") else ""))
     if fam is None:
-        print("probe kernel is not the streaming GEMM; nothing to compare")
+        print("probe family has no single-kernel trace match; nothing to compare")
         return
     probed, allk = [], []
     for i, r in enumerate(rows):

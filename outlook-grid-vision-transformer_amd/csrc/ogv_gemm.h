@@ -166,12 +166,14 @@ void set_sg_per_cu(int v);
 void set_sg_prefetch(int v);
 void set_splitk_max(int v);
 void set_bk64_max_m(int v);
+void set_bm64_max_m(int v);
 void set_grid_mfma(int v);
 void set_dw_blocks(int v);
 void set_mb_side(int v);
 void set_ln_bwd_blocks(int v);
 void set_gemm_bn64(int v);
 void set_grid_lds(int v);
+void set_grid_big(int v);
 void set_split_w(int v);
 void set_outlook_tile(int v);
 int split_w();

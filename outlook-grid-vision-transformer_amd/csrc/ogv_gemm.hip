@@ -1022,6 +1022,8 @@ __global__ __launch_bounds__(256) void transpose_f32_kernel(const float* __restr
 // ------------------------------------------------------------------------------------------------
 // internal launchers
 // ------------------------------------------------------------------------------------------------
+static int g_bm64_max_m = 16384;  // tuning knob "bm64_max_m": largest M using 64-row tiles
+void set_bm64_max_m(int v) { g_bm64_max_m = v; }
 static int g_bk64_max_m = 32768;  // tuning knob "bk64_max_m": largest M using 64-wide k-steps (0 = off)
 void set_bk64_max_m(int v) { g_bk64_max_m = v; }
 // Measured (tools/bench_sgemm.py, stages 2-3): 64-wide k-steps win for long reductions without a
@@ -1056,7 +1058,7 @@ static void launch_mm(const void* A, int lda, const Pro& pro, const float* Wt, i
   if constexpr (!STATS && BM == GEMM_BM) {
     // small M (the last stage, M = 8192): 64-row tiles double the blocks and the K-slabs in flight
     // (measured: a loss already at M = 32768, where W-tile reloads dominate)
-    if (M <= 16384) {
+    if (M <= g_bm64_max_m) {
       launch_mm<T, BN, PRO, STATS, 64>(A, lda, pro, Wt, ldw, out, ldo, M, N, K, Ka, Kb, epi, s);
       return;
     }
@@ -1271,7 +1273,7 @@ template <typename T, int BN, int BM = GEMM_BM>
 static void launch_mm_bt(const void* A, int lda, const float* W, int ldw, void* out, int ldo, int M, int N, int K,
                          const Epi& epi, hipStream_t s) {
   if constexpr (BM == GEMM_BM) {
-    if (M <= 16384) {
+    if (M <= g_bm64_max_m) {
       launch_mm_bt<T, BN, 64>(A, lda, W, ldw, out, ldo, M, N, K, epi, s);
       return;
     }

@@ -663,6 +663,377 @@ __global__ __launch_bounds__(256) void grid_lds_dkv_kernel(const bf16* __restric
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Large groups (N = 784 at 224^2 stage 0): one (group, head) pair per block of 16 waves, its whole
+// K and V (2 x N x PITCH bf16, up to 150 KB for head_dim 32) resident in LDS, staged once with
+// batched 16-B loads.  Each wave walks query blocks of 16 against it 64 keys at a time: four
+// S^T = K Q^T MFMAs, ONE running-max / rescale step for the 64 keys (the per-16-key kernels pay the
+// cross-lane max, the exp of the correction and the O rescale four times as often), then 4 x ND
+// P V MFMAs.  The output leaves straight from the accumulators (2-byte stores; the LDS is full).
+constexpr int GB_NW = 16;
+template <int HDP>
+__global__ __launch_bounds__(GB_NW * 64) void grid_big_fwd_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
+                                                                 float* __restrict__ lse, GridGeomM G, float scale,
+                                                                 int Np) {
+  constexpr int KK = HDP / 32, ND = HDP / 16, PITCH = gm_pitch<HDP>(), PIECES = HDP / 8;
+  extern __shared__ __attribute__((aligned(16))) bf16 gsm[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const long C3 = 3L * G.C;
+  const long pr = blockIdx.x;
+  const int h = (int)(pr % G.heads);
+  const long grp = pr / G.heads;
+  bf16* Ks = gsm;
+  bf16* Vs = gsm + (size_t)Np * PITCH;
+  // stage K and V: 8 independent 16-B loads per thread in flight before any LDS store
+  {
+    const int total = 2 * Np * PIECES;
+    for (int base = threadIdx.x; base < total; base += 8 * GB_NW * 64) {
+      bf16x8 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int idx = base + u * GB_NW * 64;
+        const int t = idx / (Np * PIECES), r = idx - t * Np * PIECES;
+        const int row = r / PIECES, pc = r - row * PIECES;
+        const bool ok = idx < total && row < G.N && pc * 8 < G.hd;
+        v[u] = gm_load8(qkv + (t + 1) * G.C + h * G.hd + (ok ? G.pixel(grp, row) : 0) * C3 + pc * 8, ok);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int idx = base + u * GB_NW * 64;
+        if (idx < total) {
+          const int t = idx / (Np * PIECES), r = idx - t * Np * PIECES;
+          const int row = r / PIECES, pc = r - row * PIECES;
+          *reinterpret_cast<bf16x8*>(gsm + (size_t)t * Np * PITCH + row * PITCH + pc * 8) = v[u];
+        }
+      }
+    }
+  }
+  __syncthreads();
+  const int nrb = Np / 16;
+  for (int qb = wave; qb < nrb; qb += GB_NW) {
+    const int qtok = qb * 16 + fr;
+    const bool qok = qtok < G.N;
+    const long qpix = qok ? G.pixel(grp, qtok) : 0;
+    bf16x8 qf[KK];
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      const int d = kk * 32 + fg * 8;
+      qf[kk] = gm_load8(qkv + h * G.hd + qpix * C3 + d, qok && d < G.hd);
+    }
+    f32x4 o[ND];
+#pragma unroll
+    for (int j = 0; j < ND; ++j) o[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float m = -INFINITY, l = 0.f;
+    for (int k0 = 0; k0 < Np; k0 += 64) {
+      const int nc = (Np - k0) >= 64 ? 4 : (Np - k0) / 16;   // 16-key chunks in this step
+      f32x4 sc[4];
+      float mc = -INFINITY;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        sc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (c < nc) {
+#pragma unroll
+          for (int kk = 0; kk < KK; ++kk) {
+            const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks + (k0 + 16 * c + fr) * PITCH + kk * 32 + fg * 8);
+            sc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[kk], sc[c], 0, 0, 0);
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = k0 + 16 * c + 4 * fg + r;
+          sc[c][r] = (c < nc && key < G.N) ? sc[c][r] * scale : -INFINITY;
+          mc = fmaxf(mc, sc[c][r]);
+        }
+      }
+      mc = fmaxf(mc, __shfl_xor(mc, 16, 64));
+      mc = fmaxf(mc, __shfl_xor(mc, 32, 64));
+      const float mn = fmaxf(m, mc);
+      const float corr = __expf(m - mn);   // 0 on the first step (m = -inf)
+      float ps = 0.f;
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          sc[c][r] = __expf(sc[c][r] - mn);
+          ps += sc[c][r];
+        }
+      ps += __shfl_xor(ps, 16, 64);
+      ps += __shfl_xor(ps, 32, 64);
+      l = l * corr + ps;
+      m = mn;
+      float cr[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) cr[r] = __shfl(corr, 4 * fg + r, 64);
+#pragma unroll
+      for (int j = 0; j < ND; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[j][r] *= cr[r];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        if (c >= nc) break;
+        float pw[4] = {sc[c][0], sc[c][1], sc[c][2], sc[c][3]};
+        const gm_s16x4 pa = pack4(pw);
+#pragma unroll
+        for (int j = 0; j < ND; ++j) {
+          const gm_s16x4 vb = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (gm_lds_s16x4*)(Vs + (k0 + 16 * c + 4 * fg + (fr >> 2)) * PITCH + j * 16 + (fr & 3) * 4));
+          o[j] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(pa, vb, o[j], 0, 0, 0);
+        }
+      }
+    }
+    // rows 4fg + r of the C layout are queries qb*16 + 4fg + r
+    float inv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) inv[r] = 1.f / __shfl(l, 4 * fg + r, 64);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int tok = qb * 16 + 4 * fg + r;
+      if (tok >= G.N) continue;
+      bf16* dst = out + G.pixel(grp, tok) * G.C + h * G.hd;
+#pragma unroll
+      for (int j = 0; j < ND; ++j)
+        if (j * 16 + fr < G.hd) dst[j * 16 + fr] = (bf16)(o[j][r] * inv[r]);
+    }
+    if (fg == 0 && qok) lse[qpix * G.heads + h] = m + __logf(l);
+  }
+}
+
+// Stage tokens [0, Np) x head dims of tensors (base_t, row stride ld_t) t = 0, 1 of one pair into
+// [2][Np][PITCH] LDS (zeros past N / hd), 8 independent 16-B loads per thread in flight.
+template <int HDP>
+__device__ __forceinline__ void gb_stage2(bf16* lds, const bf16* __restrict__ b0, long ld0, const bf16* __restrict__ b1,
+                                          long ld1, const GridGeomM& G, long grp, int Np) {
+  constexpr int PITCH = gm_pitch<HDP>(), PIECES = HDP / 8;
+  const int total = 2 * Np * PIECES;
+  for (int base = threadIdx.x; base < total; base += 8 * GB_NW * 64) {
+    bf16x8 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int idx = base + u * GB_NW * 64;
+      const int t = idx / (Np * PIECES), r = idx - t * Np * PIECES;
+      const int row = r / PIECES, pc = r - row * PIECES;
+      const bool ok = idx < total && row < G.N && pc * 8 < G.hd;
+      const long pix = ok ? G.pixel(grp, row) : 0;
+      v[u] = gm_load8((t ? b1 + pix * ld1 : b0 + pix * ld0) + pc * 8, ok);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int idx = base + u * GB_NW * 64;
+      if (idx < total) {
+        const int t = idx / (Np * PIECES), r = idx - t * Np * PIECES;
+        const int row = r / PIECES, pc = r - row * PIECES;
+        *reinterpret_cast<bf16x8*>(lds + (size_t)t * Np * PITCH + row * PITCH + pc * 8) = v[u];
+      }
+    }
+  }
+}
+
+// rows 4fg + r of a C-layout accumulator (times mul[r]) -> base + pixel(tok0 + 4fg + r) * ld, dims j*16 + fr
+template <int HDP>
+__device__ __forceinline__ void gb_store(const f32x4 (&acc)[HDP / 16], const float (&mul)[4], bf16* __restrict__ base,
+                                         long ld, const GridGeomM& G, long grp, int tok0, int lane) {
+  const int fr = lane & 15, fg = lane >> 4;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int tok = tok0 + 4 * fg + r;
+    if (tok >= G.N) continue;
+    bf16* dst = base + G.pixel(grp, tok) * ld;
+#pragma unroll
+    for (int j = 0; j < HDP / 16; ++j)
+      if (j * 16 + fr < G.hd) dst[j * 16 + fr] = (bf16)(acc[j][r] * mul[r]);
+  }
+}
+
+// dQ of large groups: K and V of the pair resident in LDS; a wave per 16-query block walks all keys.
+template <int HDP>
+__global__ __launch_bounds__(GB_NW * 64) void grid_big_dq_kernel(const bf16* __restrict__ dout,
+                                                                const bf16* __restrict__ qkv,
+                                                                const float* __restrict__ lse,
+                                                                const float* __restrict__ delta,
+                                                                bf16* __restrict__ dqkv, GridGeomM G, float scale,
+                                                                int Np) {
+  constexpr int KK = HDP / 32, ND = HDP / 16, PITCH = gm_pitch<HDP>();
+  extern __shared__ __attribute__((aligned(16))) bf16 gsm[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const long C3 = 3L * G.C;
+  const long pr = blockIdx.x;
+  const int h = (int)(pr % G.heads);
+  const long grp = pr / G.heads;
+  const bf16* Ks = gsm;
+  const bf16* Vs = gsm + (size_t)Np * PITCH;
+  gb_stage2<HDP>(gsm, qkv + G.C + h * G.hd, C3, qkv + 2 * G.C + h * G.hd, C3, G, grp, Np);
+  __syncthreads();
+  for (int qb = wave; qb < Np / 16; qb += GB_NW) {
+    const int qtok = qb * 16 + fr;
+    const bool qok = qtok < G.N;
+    const long qpix = qok ? G.pixel(grp, qtok) : 0;
+    bf16x8 qf[KK], gf[KK];  // Q^T and dO^T as B operands (query fr)
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      const int d = kk * 32 + fg * 8;
+      qf[kk] = gm_load8(qkv + h * G.hd + qpix * C3 + d, qok && d < G.hd);
+      gf[kk] = gm_load8(dout + qpix * G.C + h * G.hd + d, qok && d < G.hd);
+    }
+    const float lq = qok ? lse[qpix * G.heads + h] : INFINITY;
+    const float dl = qok ? delta[qpix * G.heads + h] : 0.f;
+    f32x4 dq[ND];
+#pragma unroll
+    for (int j = 0; j < ND; ++j) dq[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int k0 = 0; k0 < Np; k0 += 16) {
+      f32x4 sv = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) {
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks + (k0 + fr) * PITCH + kk * 32 + fg * 8);
+        const bf16x8 vf = *reinterpret_cast<const bf16x8*>(Vs + (k0 + fr) * PITCH + kk * 32 + fg * 8);
+        sv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[kk], sv, 0, 0, 0);    // S^T
+        dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, gf[kk], dp, 0, 0, 0);    // dP^T
+      }
+      float ds[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const bool ok = k0 + 4 * fg + r < G.N;
+        const float pw = ok ? __expf(sv[r] * scale - lq) : 0.f;
+        ds[r] = pw * (dp[r] - dl);
+      }
+      const gm_s16x4 da = pack4(ds);  // A operand: dS[query fr][keys 4fg..]
+#pragma unroll
+      for (int j = 0; j < ND; ++j) {
+        const gm_s16x4 kb = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (gm_lds_s16x4*)(Ks + (k0 + 4 * fg + (fr >> 2)) * PITCH + j * 16 + (fr & 3) * 4));
+        dq[j] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(da, kb, dq[j], 0, 0, 0);
+      }
+    }
+    const float sc4[4] = {scale, scale, scale, scale};
+    gb_store<HDP>(dq, sc4, dqkv + h * G.hd, C3, G, grp, qb * 16, lane);
+  }
+}
+
+// dK, dV of large groups: Q, dO (+ lse, delta) of the pair resident in LDS; a wave per 16-key block.
+template <int HDP>
+__global__ __launch_bounds__(GB_NW * 64) void grid_big_dkv_kernel(const bf16* __restrict__ dout,
+                                                                 const bf16* __restrict__ qkv,
+                                                                 const float* __restrict__ lse,
+                                                                 const float* __restrict__ delta,
+                                                                 bf16* __restrict__ dqkv, GridGeomM G, float scale,
+                                                                 int Np) {
+  constexpr int KK = HDP / 32, ND = HDP / 16, PITCH = gm_pitch<HDP>();
+  extern __shared__ __attribute__((aligned(16))) bf16 gsm[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const long C3 = 3L * G.C;
+  const long pr = blockIdx.x;
+  const int h = (int)(pr % G.heads);
+  const long grp = pr / G.heads;
+  const bf16* Qs = gsm;
+  const bf16* Gs = gsm + (size_t)Np * PITCH;
+  float* lq_s = reinterpret_cast<float*>(gsm + 2 * (size_t)Np * PITCH);
+  float* dl_s = lq_s + Np;
+  gb_stage2<HDP>(gsm, qkv + h * G.hd, C3, dout + h * G.hd, G.C, G, grp, Np);
+  for (int t = threadIdx.x; t < Np; t += GB_NW * 64) {   // padded rows: lse = inf -> P = 0
+    const bool ok = t < G.N;
+    const long pq = ok ? G.pixel(grp, t) : 0;
+    lq_s[t] = ok ? lse[pq * G.heads + h] : INFINITY;
+    dl_s[t] = ok ? delta[pq * G.heads + h] : 0.f;
+  }
+  __syncthreads();
+  for (int kb = wave; kb < Np / 16; kb += GB_NW) {
+    const int ktok = kb * 16 + fr;
+    const bool kok = ktok < G.N;
+    const long kpix = kok ? G.pixel(grp, ktok) : 0;
+    bf16x8 kf[KK], vf[KK];  // K^T, V^T as B operands (key fr)
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      const int d = kk * 32 + fg * 8;
+      kf[kk] = gm_load8(qkv + G.C + h * G.hd + kpix * C3 + d, kok && d < G.hd);
+      vf[kk] = gm_load8(qkv + 2 * G.C + h * G.hd + kpix * C3 + d, kok && d < G.hd);
+    }
+    f32x4 dk[ND], dv[ND];
+#pragma unroll
+    for (int j = 0; j < ND; ++j) {
+      dk[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      dv[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    for (int q0 = 0; q0 < Np; q0 += 16) {
+      // S[query 4fg+r][key fr] = Q K^T ; dP = dO V^T
+      f32x4 sv = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) {
+        const bf16x8 qa = *reinterpret_cast<const bf16x8*>(Qs + (q0 + fr) * PITCH + kk * 32 + fg * 8);
+        const bf16x8 ga = *reinterpret_cast<const bf16x8*>(Gs + (q0 + fr) * PITCH + kk * 32 + fg * 8);
+        sv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kf[kk], sv, 0, 0, 0);
+        dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ga, vf[kk], dp, 0, 0, 0);
+      }
+      float pw[4], ds[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int tok = q0 + 4 * fg + r;   // < Np: padded rows hold lse = inf -> pw = 0
+        pw[r] = kok ? __expf(sv[r] * scale - lq_s[tok]) : 0.f;
+        ds[r] = pw[r] * (dp[r] - dl_s[tok]);
+      }
+      const gm_s16x4 pa = pack4(pw), da = pack4(ds);
+#pragma unroll
+      for (int j = 0; j < ND; ++j) {
+        const int off = (q0 + 4 * fg + (fr >> 2)) * PITCH + j * 16 + (fr & 3) * 4;
+        const gm_s16x4 gb = __builtin_amdgcn_ds_read_tr16_b64_v4i16((gm_lds_s16x4*)(Gs + off));
+        const gm_s16x4 qb2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((gm_lds_s16x4*)(Qs + off));
+        dv[j] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(pa, gb, dv[j], 0, 0, 0);
+        dk[j] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(da, qb2, dk[j], 0, 0, 0);
+      }
+    }
+    const float sc4[4] = {scale, scale, scale, scale}, one4[4] = {1.f, 1.f, 1.f, 1.f};
+    gb_store<HDP>(dk, sc4, dqkv + G.C + h * G.hd, C3, G, grp, kb * 16, lane);
+    gb_store<HDP>(dv, one4, dqkv + 2 * G.C + h * G.hd, C3, G, grp, kb * 16, lane);
+  }
+}
+
+template <int HDP>
+static bool grid_big_bwd_try(const GridGeomM& G, const void* dout, const void* qkv, const float* lse,
+                             const float* delta, void* dqkv, float scale, hipStream_t s);
+
+static int g_grid_big = 1;   // tuning knob "grid_big": one-pair-per-block LDS kernel for large groups
+void set_grid_big(int v) { g_grid_big = v ? 1 : 0; }
+constexpr size_t GB_LDS_MAX = 160 * 1024;
+
+template <int HDP>
+static bool grid_big_fwd_try(const GridGeomM& G, const void* qkv, void* out, float* lse, float scale, hipStream_t s) {
+  const int Np = (G.N + 15) / 16 * 16;
+  const size_t lds = 2 * (size_t)Np * gm_pitch<HDP>() * sizeof(bf16);
+  if (!g_grid_big || lds > GB_LDS_MAX) return false;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(grid_big_fwd_kernel<HDP>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)GB_LDS_MAX);
+    attr = true;
+  }
+  const long pairs = (long)G.B * G.g * G.g * G.heads;
+  grid_big_fwd_kernel<HDP><<<(unsigned)pairs, GB_NW * 64, lds, s>>>((const bf16*)qkv, (bf16*)out, lse, G, scale, Np);
+  return true;
+}
+
+template <int HDP>
+static bool grid_big_bwd_try(const GridGeomM& G, const void* dout, const void* qkv, const float* lse,
+                             const float* delta, void* dqkv, float scale, hipStream_t s) {
+  const int Np = (G.N + 15) / 16 * 16;
+  const size_t l1 = 2 * (size_t)Np * gm_pitch<HDP>() * sizeof(bf16), l2 = l1 + 2 * (size_t)Np * sizeof(float);
+  if (!g_grid_big || l2 > GB_LDS_MAX) return false;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(grid_big_dq_kernel<HDP>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)GB_LDS_MAX);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(grid_big_dkv_kernel<HDP>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)GB_LDS_MAX);
+    attr = true;
+  }
+  const long pairs = (long)G.B * G.g * G.g * G.heads;
+  grid_big_dq_kernel<HDP><<<(unsigned)pairs, GB_NW * 64, l1, s>>>((const bf16*)dout, (const bf16*)qkv, lse, delta,
+                                                                  (bf16*)dqkv, G, scale, Np);
+  grid_big_dkv_kernel<HDP><<<(unsigned)pairs, GB_NW * 64, l2, s>>>((const bf16*)dout, (const bf16*)qkv, lse, delta,
+                                                                   (bf16*)dqkv, G, scale, Np);
+  return true;
+}
+
 static int g_grid_lds = 1;  // tuning knob "grid_lds": LDS-resident pairs when they fit
 void set_grid_lds(int v) { g_grid_lds = v; }
 constexpr size_t GM_LDS_MAX = 64 * 1024;
@@ -691,6 +1062,9 @@ bool grid_mfma_fwd(const void* qkv, void* out, float* lse, int B, int H, int W, 
       }
     }
   }
+  if (G.N > 16 && (G.hd <= 32 ? grid_big_fwd_try<32>(G, qkv, out, lse, scale, s)
+                                : grid_big_fwd_try<64>(G, qkv, out, lse, scale, s)))
+    return true;
   const long units = (long)B * g * g * heads * ((G.N + 15) / 16);
   const unsigned grid = cdiv(units, 4);
   if (G.hd <= 32)
@@ -721,6 +1095,9 @@ bool grid_mfma_bwd(const void* dout, const void* qkv, const float* lse, const fl
     if (G.hd <= 32) OGV_GRID_LDS_BWD(32) else OGV_GRID_LDS_BWD(64)
 #undef OGV_GRID_LDS_BWD
   }
+  if (G.N > 16 && (G.hd <= 32 ? grid_big_bwd_try<32>(G, dout, qkv, lse, delta, dqkv, scale, s)
+                              : grid_big_bwd_try<64>(G, dout, qkv, lse, delta, dqkv, scale, s)))
+    return true;
   const long units = (long)B * g * g * heads * ((G.N + 15) / 16);
   const unsigned grid = cdiv(units, 4);
   if (G.hd <= 32) {

@@ -98,6 +98,10 @@ extern "C" int ogv_set_option(const char* name, int value) {
     set_sgemm_mode(value ? 1 : 0);
     return OGV_OK;
   }
+  if (!strcmp(name, "grid_big")) {
+    set_grid_big(value);
+    return OGV_OK;
+  }
   if (!strcmp(name, "grid_lds")) {
     set_grid_lds(value ? 1 : 0);
     return OGV_OK;
@@ -120,6 +124,10 @@ extern "C" int ogv_set_option(const char* name, int value) {
   }
   if (!strcmp(name, "grid_mfma")) {
     set_grid_mfma(value ? 1 : 0);
+    return OGV_OK;
+  }
+  if (!strcmp(name, "bm64_max_m")) {
+    set_bm64_max_m(value);
     return OGV_OK;
   }
   if (!strcmp(name, "bk64_max_m")) {

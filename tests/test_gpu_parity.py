@@ -368,6 +368,9 @@ GRID_MFMA_CASES = [  # B, H, W, C, heads, g: N >= 16 with head_dim <= 64 runs on
     (3, 10, 10, 48, 2, 2),    # N = 25: two (group, head) pairs per LDS-resident block
     (3, 5, 5, 32, 1, 1),      # N = 25, 3 pairs: ragged last block
     (2, 12, 12, 48, 2, 2),    # N = 36: 3 row blocks on 4 waves
+    # one pair per 16-wave block, K/V resident in up to 150 KB of LDS (groups too large for the
+    # 64 KB multi-pair kernels): N = 784 / 400 / 196 (hd 64), ragged last 64-key step
+    (2, 28, 28, 64, 2, 1), (1, 20, 20, 64, 2, 1), (1, 14, 14, 128, 2, 1), (1, 18, 18, 32, 1, 1),
 ]
 
 

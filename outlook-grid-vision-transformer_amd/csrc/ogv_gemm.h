@@ -153,6 +153,14 @@ int sgemm_fwd_try(const void* A, int lda, const Pro& pro, const float* W, int ld
                   int N, int K, const Epi& epi, hipStream_t s);
 bool sgemm_dgrad_try(const void* dout, int ldd, const float* W, void* dA, int lda, int M, int Nf, int Kf,
                      const Epi& epi, hipStream_t s);
+// Pipelined panel GEMM (ogv_pgemm.hip) for small-M bf16 shapes; 0 / false = not handled.
+int pgemm_fwd_try(const void* A, int lda, const Pro& pro, const float* W, int ldw, void* out, int ldo, int M,
+                  int N, int K, const Epi& epi, hipStream_t s);
+bool pgemm_dgrad_try(const void* dout, int ldd, const float* W, void* dA, int lda, int M, int Nf, int Kf,
+                     const Epi& epi, hipStream_t s);
+void set_pgemm(int v);
+void set_pg_rs(int v);
+void set_pg_tn(int v);
 // Streaming weight gradient (ogv_swgrad.hip) for large-M bf16 shapes: writes [S][N*K + N] fp32
 // partials into part and returns S (0 = not handled); swgrad_ws_floats sizes part + colreduce tmp.
 int swgrad_try(const void* G, int ldg, const void* X, int ldx, const Pro& pro, const float* rs, int rps, float* part,

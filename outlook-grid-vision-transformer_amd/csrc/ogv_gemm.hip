@@ -1127,6 +1127,8 @@ int gemm_fwd_launch(ogv_dtype dt, const void* A, int lda, const Pro& pro, const 
   if (dt == OGV_BF16 && Ka == K && Kb == K) {
     const int r = sgemm_fwd_try(A, lda, pro, W, ldw, out, ldo, M, N, K, epi, s);
     if (r > 0) return r;
+    const int r2 = pgemm_fwd_try(A, lda, pro, W, ldw, out, ldo, M, N, K, epi, s);
+    if (r2 > 0) return r2;
   }
   if (tiny(M, N, dt, epi)) {
     const int K0 = Ka < Kb ? Ka : Kb;
@@ -1309,6 +1311,7 @@ void gemm_dgrad_launch(ogv_dtype dt, const void* dout, int ldd, const float* W, 
   e.res = res;
   // dA[M,K] = dout[M,N] . W[N,K]: W read as [reduction N][output K] (no transposed copy)
   if (dt == OGV_BF16 && sgemm_dgrad_try(dout, ldd, W, dA, lda, M, N, K, e, s)) return;
+  if (dt == OGV_BF16 && pgemm_dgrad_try(dout, ldd, W, dA, lda, M, N, K, e, s)) return;
   if (dt == OGV_BF16) {
     if (wide_cols(K)) launch_mm_bt<bf16, 128>(dout, ldd, W, K, dA, lda, M, K, N, e, s);
     else launch_mm_bt<bf16, 64>(dout, ldd, W, K, dA, lda, M, K, N, e, s);

@@ -1,0 +1,488 @@
+// Pipelined panel GEMM for the small-M projections (stages 2-3 of Model-A-7M, M <= 32768).
+//
+// At M = 8192 - 32768 rows the whole GEMM is a few hundred 128-row panels: every workgroup does
+// a handful of k-steps and leaves, so what bounds the classic LDS-tiled kernel (ogv_gemm.hip) is
+// the serial chain of "load slab -> barrier -> MFMA -> barrier" round trips, not bandwidth or the
+// matrix cores.  This kernel keeps more bytes in flight per CU and shortens that chain:
+//   * A (activations) never goes through LDS: each wave owns 16*RS rows and loads its MFMA
+//     fragments straight from HBM into registers (16 B per lane, a whole 128-B line per row per
+//     64-wide k-step), TWO k-steps ahead of the MFMAs;
+//   * only the weight slab [BN x 64] is shared: staged through registers (fp32 -> bf16 hi / lo) into
+//     a double-buffered LDS tile one k-step ahead, ONE workgroup barrier per k-step;
+//   * the product is computed transposed (D[n][m] = W-slab . A^T, the weight fragment as the MFMA
+//     A operand), so a lane's accumulator holds 4 consecutive output columns of one row and the
+//     epilogue (bias, DropPath row scale, residual, activation derivative, BatchNorm column
+//     statistics) runs from registers with 8-B loads / stores, as in the streaming kernel
+//     (ogv_sgemm.hip), which covers M >= 65536;
+//   * the A prologue (GELU of fc2, or MBConv's BatchNorm-apply + SiLU + SE gate) is applied to the
+//     fragments in registers, once per element and N-tile.
+// Forward: B[n][k] = W[n*ldw + k].  Data gradient (BT): the forward weight [Nf][Kf] read as
+// [reduction][output]; the slab is staged [k][n] as loaded and the fragments come from
+// ds_read_b64_tr_b16 transposed reads, with the slab's rows permuted so the reads are
+// bank-conflict free and each lane still receives 8 CONSECUTIVE k (so the A fragment stays one
+// 16-B load).
+#include "ogv_gemm.h"
+
+namespace ogv {
+
+constexpr int PG_NW = 4;           // waves per workgroup
+constexpr int PG_KB = 64;          // reduction columns per k-step (two 32-wide MFMA sub-steps)
+constexpr int PG_KP = PG_KB + 8;   // [n][k] slab pitch (elements): 144-B rows
+
+template <int TN, bool BT>
+__host__ __device__ constexpr int pg_slab_elems() {
+  return BT ? PG_KB * (TN * 16 + 16) : TN * 16 * PG_KP;
+}
+
+// logical k (0..31 inside a 32-wide sub-step) -> physical slab row for the BT layout: bits 2 and 3
+// swapped, so the rows one tr-read instruction touches (k = 8g + 4h + q over g = 0,1) are 8
+// consecutive rows (conflict-free with a pitch of 8 mod 64 dwords)
+__device__ __forceinline__ int pg_perm(int k) { return (k & ~12) | ((k & 4) << 1) | ((k & 8) >> 1); }
+
+// RS: 16-row fragments per wave (rows per workgroup = 64 * RS); TN: 16-column fragments per
+// workgroup (BN = 16 * TN).  PA: -1 = no prologue, else its activation (sc / sh optional, staged in
+// LDS); GT: the prologue has an SE gate.  ZA: activation derivative at Z in the epilogue.
+template <int RS, int TN, int PA, bool GT, int ZA, bool STATS, bool BT, bool SW>
+__global__ __launch_bounds__(PG_NW * 64, 2) void pgemm_bf16_kernel(const bf16* __restrict__ A, int lda, Pro pro,
+                                                                const float* __restrict__ W, int ldw, Epi epi,
+                                                                bf16* __restrict__ out, int ldo, int M, int N, int K,
+                                                                int nMt, int nNt) {
+  constexpr int BN = TN * 16;
+  constexpr int SLAB = pg_slab_elems<TN, BT>();
+  constexpr int NSLAB = SW ? 2 : 1;          // hi (+ lo) weight halves
+  constexpr int WF4 = BN * PG_KB / 4 / 256;  // float4 weight loads per thread and k-step (= TN)
+  constexpr int BP = BN + 16;                // BT slab pitch
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* slab = reinterpret_cast<bf16*>(smem);  // [2 buffers][NSLAB][SLAB]
+  float* cvec = reinterpret_cast<float*>(smem + (size_t)2 * NSLAB * SLAB * 2);  // [bias | shift] (BN each)
+  float* pvec = cvec + 2 * BN;                                                   // [sc | sh] (K each), PA >= 0
+
+  // XCD-aware map: blocks b and b + 8 share an XCD; all N-tiles of an M-panel run on one XCD so
+  // the panel's A rows come from HBM once and from that XCD's L2 after.
+  const int bid = blockIdx.x, xcd = bid & 7, local = bid >> 3;
+  const int mt = (local / nNt) * 8 + xcd, nt = local % nNt;
+  if (mt >= nMt) return;
+  const int m0 = mt * (PG_NW * 16 * RS), n0 = nt * BN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int mw = m0 + wave * 16 * RS;  // this wave's first row
+
+  for (int c = tid; c < BN; c += PG_NW * 64) {
+    const int n = n0 + c;
+    cvec[c] = (epi.bias && n < N) ? epi.bias[n] : 0.f;
+    cvec[BN + c] = (STATS && epi.stat_shift && n < N) ? bn_shift(epi.stat_shift[n]) : 0.f;
+  }
+  if constexpr (PA >= 0) {
+    for (int k = tid; k < K; k += PG_NW * 64) {
+      pvec[k] = pro.sc ? pro.sc[k] : 1.f;
+      pvec[K + k] = pro.sh ? pro.sh[k] : 0.f;
+    }
+  }
+
+  const int nsteps = (K + PG_KB - 1) / PG_KB;
+
+  // ---- weight slab loads (registers) and staging (bf16 hi / lo -> LDS)
+  float4 wr[WF4];
+  auto load_w = [&](int s) {
+    const int k0 = s * PG_KB;
+#pragma unroll
+    for (int i = 0; i < WF4; ++i) {
+      const int idx = tid + i * 256;
+      wr[i] = float4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (!BT) {
+        const int r = idx / (PG_KB / 4), k = k0 + (idx % (PG_KB / 4)) * 4;
+        if (n0 + r < N && k < K) wr[i] = *reinterpret_cast<const float4*>(W + (long)(n0 + r) * ldw + k);
+      } else {
+        const int kr = idx / (BN / 4), c = (idx % (BN / 4)) * 4;
+        if (k0 + kr < K && n0 + c < N) wr[i] = *reinterpret_cast<const float4*>(W + (long)(k0 + kr) * ldw + n0 + c);
+      }
+    }
+  };
+  auto store_w = [&](int buf) {
+    bf16* hi = slab + (size_t)buf * NSLAB * SLAB;
+#pragma unroll
+    for (int i = 0; i < WF4; ++i) {
+      const int idx = tid + i * 256;
+      int off;
+      if constexpr (!BT) {
+        off = (idx / (PG_KB / 4)) * PG_KP + (idx % (PG_KB / 4)) * 4;
+      } else {
+        const int kr = idx / (BN / 4);
+        off = ((kr & ~31) | pg_perm(kr & 31)) * BP + (idx % (BN / 4)) * 4;
+      }
+      const bf16x4 h = {(bf16)wr[i].x, (bf16)wr[i].y, (bf16)wr[i].z, (bf16)wr[i].w};
+      *reinterpret_cast<bf16x4*>(hi + off) = h;
+      if constexpr (SW) {
+        const bf16x4 l = {(bf16)(wr[i].x - (float)h[0]), (bf16)(wr[i].y - (float)h[1]),
+                          (bf16)(wr[i].z - (float)h[2]), (bf16)(wr[i].w - (float)h[3])};
+        *reinterpret_cast<bf16x4*>(hi + SLAB + off) = l;
+      }
+    }
+  };
+
+  // ---- A fragments: lane (fr, fg) holds row mw + 16 i + fr, k = k0 + 32 kt + 8 fg .. + 8
+  auto load_a = [&](int s, bf16x8 (&a)[RS][2]) {
+    const int k0 = s * PG_KB;
+#pragma unroll
+    for (int i = 0; i < RS; ++i) {
+      const int m = mw + i * 16 + fr;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        const int k = k0 + kt * 32 + fg * 8;
+        bf16x8 v = {};
+        if (m < M && k < K) v = *reinterpret_cast<const bf16x8*>(A + (long)m * lda + k);
+        a[i][kt] = v;
+      }
+    }
+  };
+  // SE gate of step s (prologue with a gate): loaded one k-step ahead, with the weight slab
+  float4 gr[GT ? RS : 1][GT ? 2 : 1][2];
+  auto load_g = [&](int s) {
+    if constexpr (GT) {
+      const int k0 = s * PG_KB;
+#pragma unroll
+      for (int i = 0; i < RS; ++i) {
+        const int m = mw + i * 16 + fr;
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) {
+          const int k = k0 + kt * 32 + fg * 8;
+          gr[i][kt][0] = gr[i][kt][1] = float4{1.f, 1.f, 1.f, 1.f};
+          if (m < M && k < K) {
+            const float* g = pro.gate + (long)(m / pro.rps) * pro.gld + k;
+            gr[i][kt][0] = *reinterpret_cast<const float4*>(g);
+            gr[i][kt][1] = *reinterpret_cast<const float4*>(g + 4);
+          }
+        }
+      }
+    }
+  };
+
+  f32x4 acc[RS][TN];
+#pragma unroll
+  for (int i = 0; i < RS; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  typedef __attribute__((ext_vector_type(8))) short s16x8;
+  const int q = fr >> 2, p4 = (fr & 3) * 4;
+
+  auto compute = [&](int s, bf16x8 (&a)[RS][2], int buf) {
+    if constexpr (PA >= 0) {
+      const int k0 = s * PG_KB;
+#pragma unroll
+      for (int i = 0; i < RS; ++i) {
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) {
+          const int k = k0 + kt * 32 + fg * 8;
+          if (k < K) {
+            float g8[8];
+            if constexpr (GT) {
+              g8[0] = gr[i][kt][0].x; g8[1] = gr[i][kt][0].y; g8[2] = gr[i][kt][0].z; g8[3] = gr[i][kt][0].w;
+              g8[4] = gr[i][kt][1].x; g8[5] = gr[i][kt][1].y; g8[6] = gr[i][kt][1].z; g8[7] = gr[i][kt][1].w;
+            }
+            const float4 sc0 = *reinterpret_cast<const float4*>(pvec + k);
+            const float4 sc1 = *reinterpret_cast<const float4*>(pvec + k + 4);
+            const float4 sh0 = *reinterpret_cast<const float4*>(pvec + K + k);
+            const float4 sh1 = *reinterpret_cast<const float4*>(pvec + K + k + 4);
+            const float sc[8] = {sc0.x, sc0.y, sc0.z, sc0.w, sc1.x, sc1.y, sc1.z, sc1.w};
+            const float sh[8] = {sh0.x, sh0.y, sh0.z, sh0.w, sh1.x, sh1.y, sh1.z, sh1.w};
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              float f = act_fwd(PA, fmaf((float)a[i][kt][e], sc[e], sh[e]));
+              if constexpr (GT) f *= g8[e];
+              a[i][kt][e] = (bf16)f;
+            }
+          }
+        }
+      }
+    }
+    const bf16* hi = slab + (size_t)buf * NSLAB * SLAB;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+#pragma unroll
+        for (int h = 0; h < NSLAB; ++h) {
+          const bf16* t = hi + h * SLAB;
+          bf16x8 wf;
+          if constexpr (!BT) {
+            wf = *reinterpret_cast<const bf16x8*>(t + (j * 16 + fr) * PG_KP + kt * 32 + fg * 8);
+          } else {
+            const int r = kt * 32 + 16 * (fg >> 1) + 4 * (fg & 1) + q;  // pg_perm(8 fg + q)
+            const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(t + r * BP + j * 16 + p4));
+            const s16x4 up = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(t + (r + 8) * BP + j * 16 + p4));
+            const s16x8 w8 = {lo[0], lo[1], lo[2], lo[3], up[0], up[1], up[2], up[3]};
+            wf = __builtin_bit_cast(bf16x8, w8);
+          }
+#pragma unroll
+          for (int i = 0; i < RS; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, a[i][kt], acc[i][j], 0, 0, 0);
+        }
+      }
+    }
+  };
+
+  bf16x8 a0[RS][2], a1[RS][2];
+  load_w(0);
+  load_g(0);
+  load_a(0, a0);
+  if (nsteps > 1) load_a(1, a1);
+  __syncthreads();  // cvec / pvec
+  // one barrier per k-step: step s writes buffer s & 1, whose last readers (step s - 2's MFMAs)
+  // all passed step s - 1's barrier
+  auto step = [&](int s, bf16x8 (&a)[RS][2]) {
+    store_w(s & 1);
+    if (s + 1 < nsteps) load_w(s + 1);
+    __syncthreads();
+    compute(s, a, s & 1);
+    if constexpr (GT) {
+      if (s + 1 < nsteps) load_g(s + 1);
+    }
+    if (s + 2 < nsteps) load_a(s + 2, a);
+  };
+  for (int s = 0; s < nsteps; s += 2) {
+    step(s, a0);
+    if (s + 1 < nsteps) step(s + 1, a1);
+  }
+
+  // ---- epilogue: lane holds out[m = mw + 16 i + fr][n = n0 + 16 j + 4 fg + r], r = 0..3
+  const bf16* res = static_cast<const bf16*>(epi.res);
+  const bf16* Z = static_cast<const bf16*>(epi.Z);
+  float s1[TN][4], s2[TN][4];
+  if constexpr (STATS) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { s1[j][r] = 0.f; s2[j][r] = 0.f; }
+  }
+#pragma unroll
+  for (int i = 0; i < RS; ++i) {
+    const int m = mw + i * 16 + fr;
+    const bool mok = m < M;
+    const float rsc = (epi.rs && mok) ? epi.rs[m / epi.rps] : 1.f;
+    uint2 rv[TN], zv[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {  // residual / Z first: one round trip for the whole row fragment
+      const int n = n0 + j * 16 + 4 * fg;
+      rv[j] = uint2{0u, 0u};
+      zv[j] = uint2{0u, 0u};
+      if (mok && n < N) {
+        if (res) rv[j] = *reinterpret_cast<const uint2*>(res + (long)m * ldo + n);
+        if constexpr (ZA != 0) zv[j] = *reinterpret_cast<const uint2*>(Z + (long)m * epi.ldz + n);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int c = j * 16 + 4 * fg, n = n0 + c;
+      if (!(mok && n < N)) continue;
+      const float4 bs = *reinterpret_cast<const float4*>(cvec + c);
+      const float bias[4] = {bs.x, bs.y, bs.z, bs.w};
+      const bf16* rb = reinterpret_cast<const bf16*>(&rv[j]);
+      const bf16* zb = reinterpret_cast<const bf16*>(&zv[j]);
+      uint2 ov;
+      bf16* ob = reinterpret_cast<bf16*>(&ov);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float x = (acc[i][j][r] + bias[r]) * rsc + (float)rb[r];
+        if constexpr (ZA != 0) x *= act_grad(ZA, (float)zb[r]);
+        ob[r] = (bf16)x;
+        if constexpr (STATS) {
+          const float d = (float)ob[r] - cvec[BN + c + r];
+          s1[j][r] += d;
+          s2[j][r] = fmaf(d, d, s2[j][r]);
+        }
+      }
+      *reinterpret_cast<uint2*>(out + (long)m * ldo + n) = ov;
+    }
+  }
+  if constexpr (STATS) {
+    // over the 16 rows of a lane group (fp32, <= 32 rows per wave), then the 4 waves in fp64
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          s1[j][r] += __shfl_xor(s1[j][r], o, 64);
+          s2[j][r] += __shfl_xor(s2[j][r], o, 64);
+        }
+    __syncthreads();  // slabs are dead
+    double* red = reinterpret_cast<double*>(smem);  // [wave][2][BN]
+    if (fr == 0) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = j * 16 + 4 * fg + r;
+          red[(wave * 2 + 0) * BN + c] = (double)s1[j][r];
+          red[(wave * 2 + 1) * BN + c] = (double)s2[j][r];
+        }
+    }
+    __syncthreads();
+    for (int c = tid; c < BN; c += PG_NW * 64) {
+      if (n0 + c >= N) continue;
+      double t1 = 0.0, t2 = 0.0;
+#pragma unroll
+      for (int w = 0; w < PG_NW; ++w) {
+        t1 += red[(w * 2 + 0) * BN + c];
+        t2 += red[(w * 2 + 1) * BN + c];
+      }
+      epi.stat[((long)mt * 2 + 0) * N + n0 + c] = t1;
+      epi.stat[((long)mt * 2 + 1) * N + n0 + c] = t2;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// plan + dispatch
+// ------------------------------------------------------------------------------------------------
+static int g_pgemm = 1;   // knob "pgemm": route small-M bf16 fwd / dgrad here (0 = tiled kernel)
+static int g_pg_rs = 0;   // knobs "pg_rs" / "pg_tn": force the tile (0 = planner)
+static int g_pg_tn = 0;
+void set_pgemm(int v) { g_pgemm = v; }
+void set_pg_rs(int v) { g_pg_rs = v; }
+void set_pg_tn(int v) { g_pg_tn = v; }
+
+struct PgPlan {
+  int ok = 0, RS = 2, TN = 8, nMt = 0, nNt = 0;
+  size_t lds = 0;
+};
+
+static size_t pg_lds(int TN, bool bt, bool sw, int K, bool pa) {
+  const size_t slab = bt ? (size_t)PG_KB * (TN * 16 + 16) : (size_t)TN * 16 * PG_KP;
+  size_t b = 2 * (sw ? 2 : 1) * slab * 2 + 2 * TN * 16 * 4 + (pa ? 2 * (size_t)K * 4 : 0);
+  const size_t red = (size_t)PG_NW * 2 * TN * 16 * 8;  // STATS reduction reuses the slabs
+  return std::max(b, red);
+}
+
+static bool al16p(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+// N = output columns, K = reduction.  Picks (RS, TN): 128-column tiles unless they pad N by more
+// than 1/16 (then 192, then 64),
+// then enough workgroups (>= 2 per CU) by halving the rows; BatchNorm statistics need the 128-row
+// panel (one partial row per gemm_stat_rows panel).
+static PgPlan pg_plan(int M, int N, int K, bool stats, bool sw, bool bt, bool pa, bool gate) {
+  PgPlan p;
+  if (!g_pgemm || M <= 0 || (N & 7) || (K & 7)) return p;
+  const int tns[3] = {8, 12, 4};
+  int best_tn = 0;
+  for (int t : tns) {
+    if (g_pg_tn && t != g_pg_tn) continue;
+    // 192-column tiles only as 64-row panels (the 128-row one spills at two waves per SIMD), so
+    // never with BatchNorm statistics (128-row partials) or an SE gate (registers)
+    if (t == 12 && (gate || stats || N <= 128)) continue;
+    const int bn = 16 * t, nnt = (N + bn - 1) / bn;
+    if ((long)nnt * bn - N > N / 16 && t != 4 && !g_pg_tn) continue;
+    if (pg_lds(t, bt, sw, K, pa) > 80 * 1024) continue;  // two workgroups per CU
+    best_tn = t;
+    break;
+  }
+  if (!best_tn) return p;
+  p.TN = best_tn;
+  p.nNt = (N + 16 * p.TN - 1) / (16 * p.TN);
+  p.RS = 2;
+  if (p.TN == 12) p.RS = 1;
+  else if (!stats && !g_pg_rs) {
+    const long wg2 = (long)((M + 127) / 128) * p.nNt;
+    if (wg2 < 512) p.RS = 1;
+  }
+  if (g_pg_rs && !stats && p.TN != 12) p.RS = g_pg_rs;
+  p.nMt = (M + 64 * p.RS - 1) / (64 * p.RS);
+  p.lds = pg_lds(p.TN, bt, sw, K, pa);
+  p.ok = 1;
+  return p;
+}
+
+template <int RS, int TN, int PA, bool GT, int ZA, bool STATS, bool BT, bool SW>
+static void pg_launch(const PgPlan& p, const bf16* A, int lda, const Pro& pro, const float* W, int ldw,
+                      const Epi& epi, bf16* out, int ldo, int M, int N, int K, hipStream_t s) {
+  auto kern = pgemm_bf16_kernel<RS, TN, PA, GT, ZA, STATS, BT, SW>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    attr = true;
+  }
+  const unsigned grid = (unsigned)(((p.nMt + 7) / 8) * 8 * p.nNt);
+  kern<<<grid, PG_NW * 64, p.lds, s>>>(A, lda, pro, W, ldw, epi, out, ldo, M, N, K, p.nMt, p.nNt);
+}
+
+template <int PA, bool GT, int ZA, bool STATS, bool BT, bool SW>
+static void pg_tiles(const PgPlan& p, const bf16* A, int lda, const Pro& pro, const float* W, int ldw,
+                     const Epi& epi, bf16* out, int ldo, int M, int N, int K, hipStream_t s) {
+#define OGV_PG(RS_, TN_) pg_launch<RS_, TN_, PA, GT, ZA, STATS, BT, SW>(p, A, lda, pro, W, ldw, epi, out, ldo, M, N, K, s)
+  if (p.RS == 2) {
+    if (p.TN == 8) OGV_PG(2, 8);
+    else OGV_PG(2, 4);
+  } else {
+    if constexpr (!STATS) {
+      if (p.TN == 12) {
+        if constexpr (!GT) OGV_PG(1, 12);
+      } else if (p.TN == 8) OGV_PG(1, 8);
+      else OGV_PG(1, 4);
+    }
+  }
+#undef OGV_PG
+}
+
+// Returns the BatchNorm partial rows written (>= 1) when handled, 0 otherwise (caller falls back).
+int pgemm_fwd_try(const void* A, int lda, const Pro& pro, const float* W, int ldw, void* out, int ldo, int M, int N,
+                  int K, const Epi& epi, hipStream_t s) {
+  if (!g_pgemm || epi.zact || !al16p(A) || (lda & 7) || !al16p(out) || (ldo & 7) || (ldw & 3) || !al16p(W)) return 0;
+  if (epi.res && !al16p(epi.res)) return 0;
+  const bool pa = pro.any();
+  if (pa && pro.act != OGV_ACT_GELU && pro.act != OGV_ACT_SILU) return 0;
+  if (pro.gate && ((pro.gld & 3) || !al16p(pro.gate))) return 0;
+  const bool st = epi.stat != nullptr;
+  const bool sw = (split_w() & 1) != 0;
+  const PgPlan p = pg_plan(M, N, K, st, sw, false, pa, pro.gate != nullptr);
+  if (!p.ok) return 0;
+  const bf16* a = static_cast<const bf16*>(A);
+  bf16* o = static_cast<bf16*>(out);
+#define OGV_PGF(PA_, GT_, ST_)                                                                           \
+  do {                                                                                                   \
+    if (sw) pg_tiles<PA_, GT_, 0, ST_, false, true>(p, a, lda, pro, W, ldw, epi, o, ldo, M, N, K, s);   \
+    else pg_tiles<PA_, GT_, 0, ST_, false, false>(p, a, lda, pro, W, ldw, epi, o, ldo, M, N, K, s);     \
+  } while (0)
+  if (!pa) {
+    if (st) OGV_PGF(-1, false, true);
+    else OGV_PGF(-1, false, false);
+  } else if (pro.act == OGV_ACT_GELU && !pro.gate) {
+    if (st) OGV_PGF(OGV_ACT_GELU, false, true);
+    else OGV_PGF(OGV_ACT_GELU, false, false);
+  } else if (pro.act == OGV_ACT_SILU && pro.gate) {
+    if (st) OGV_PGF(OGV_ACT_SILU, true, true);
+    else OGV_PGF(OGV_ACT_SILU, true, false);
+  } else {
+    return 0;
+  }
+#undef OGV_PGF
+  return st ? p.nMt : 1;
+}
+
+// dA[M, Kf] = epi(dOut[M, Nf] . W[Nf, Kf]): reduction Nf, output columns Kf.
+bool pgemm_dgrad_try(const void* dout, int ldd, const float* W, void* dA, int lda, int M, int Nf, int Kf,
+                     const Epi& epi, hipStream_t s) {
+  if (!g_pgemm || epi.stat || !al16p(dout) || (ldd & 7) || !al16p(dA) || (lda & 7) || (Kf & 3) || !al16p(W))
+    return false;
+  if (epi.res && !al16p(epi.res)) return false;
+  if (epi.zact && (!epi.Z || !al16p(epi.Z) || (epi.ldz & 7))) return false;
+  if (epi.zact != OGV_ACT_NONE && epi.zact != OGV_ACT_GELU && epi.zact != OGV_ACT_SILU) return false;
+  const bool sw = (split_w() & 2) != 0;
+  const PgPlan p = pg_plan(M, Kf, Nf, false, sw, true, false, false);
+  if (!p.ok) return false;
+  const bf16* a = static_cast<const bf16*>(dout);
+  bf16* o = static_cast<bf16*>(dA);
+#define OGV_PGD(ZA_)                                                                                      \
+  do {                                                                                                    \
+    if (sw) pg_tiles<-1, false, ZA_, false, true, true>(p, a, ldd, Pro(), W, Kf, epi, o, lda, M, Kf, Nf, s); \
+    else pg_tiles<-1, false, ZA_, false, true, false>(p, a, ldd, Pro(), W, Kf, epi, o, lda, M, Kf, Nf, s);  \
+  } while (0)
+  if (epi.zact == OGV_ACT_GELU) OGV_PGD(OGV_ACT_GELU);
+  else if (epi.zact == OGV_ACT_SILU) OGV_PGD(OGV_ACT_SILU);
+  else OGV_PGD(0);
+#undef OGV_PGD
+  return true;
+}
+
+}  // namespace ogv

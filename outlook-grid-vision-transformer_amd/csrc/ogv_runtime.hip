@@ -154,6 +154,18 @@ extern "C" int ogv_set_option(const char* name, int value) {
     set_split_w(value);
     return OGV_OK;
   }
+  if (!strcmp(name, "pgemm")) {
+    set_pgemm(value ? 1 : 0);
+    return OGV_OK;
+  }
+  if (!strcmp(name, "pg_rs")) {
+    set_pg_rs(value == 1 || value == 2 ? value : 0);
+    return OGV_OK;
+  }
+  if (!strcmp(name, "pg_tn")) {
+    set_pg_tn(value == 4 || value == 8 || value == 12 ? value : 0);
+    return OGV_OK;
+  }
   if (!strcmp(name, "sgemm_min_m")) {
     set_sgemm_min_m(value);
     return OGV_OK;

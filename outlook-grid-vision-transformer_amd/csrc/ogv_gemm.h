@@ -161,6 +161,7 @@ bool pgemm_dgrad_try(const void* dout, int ldd, const float* W, void* dA, int ld
 void set_pgemm(int v);
 void set_pg_rs(int v);
 void set_pg_tn(int v);
+void set_pg_per_cu(int v);
 // Streaming weight gradient (ogv_swgrad.hip) for large-M bf16 shapes: writes [S][N*K + N] fp32
 // partials into part and returns S (0 = not handled); swgrad_ws_floats sizes part + colreduce tmp.
 int swgrad_try(const void* G, int ldg, const void* X, int ldx, const Pro& pro, const float* rs, int rps, float* part,
@@ -172,6 +173,7 @@ int sgemm_min_m();
 void set_sgemm_min_m(int v);
 void set_sg_per_cu(int v);
 void set_sg_prefetch(int v);
+void set_sg_wgs(int v);
 void set_splitk_max(int v);
 void set_bk64_max_m(int v);
 void set_bm64_max_m(int v);

@@ -1122,14 +1122,23 @@ int gemm_fwd_launch(ogv_dtype dt, const void* A, int lda, const Pro& pro, const 
                     int M, int N, int K, int Ka, int Kb, const Epi& epi, hipStream_t s) {
   if (M <= 0) return 0;
   if (log_gemm())
-    fprintf(stderr, "OGVGEMM fwd dt=%d M=%d N=%d K=%d Ka=%d Kb=%d pro=%d stats=%d res=%d\n", (int)dt, M, N, K, Ka, Kb,
-            (int)pro.any(), epi.stat != nullptr, epi.res != nullptr);
+    fprintf(stderr, "OGVGEMM fwd dt=%d M=%d N=%d K=%d Ka=%d Kb=%d pro=%d stats=%d res=%d lda=%d ldo=%d al=%d%d%d\n",
+            (int)dt, M, N, K, Ka, Kb, (int)pro.any(), epi.stat != nullptr, epi.res != nullptr, lda, ldo,
+            (int)(reinterpret_cast<uintptr_t>(A) & 15), (int)(reinterpret_cast<uintptr_t>(out) & 15),
+            (int)(reinterpret_cast<uintptr_t>(epi.res) & 15));
   if (dt == OGV_BF16 && Ka == K && Kb == K) {
     const int r = sgemm_fwd_try(A, lda, pro, W, ldw, out, ldo, M, N, K, epi, s);
-    if (r > 0) return r;
+    if (r > 0) {
+      if (log_gemm()) fprintf(stderr, "OGVROUTE fwd stream\n");
+      return r;
+    }
     const int r2 = pgemm_fwd_try(A, lda, pro, W, ldw, out, ldo, M, N, K, epi, s);
-    if (r2 > 0) return r2;
+    if (r2 > 0) {
+      if (log_gemm()) fprintf(stderr, "OGVROUTE fwd panel\n");
+      return r2;
+    }
   }
+  if (log_gemm()) fprintf(stderr, "OGVROUTE fwd tiled\n");
   if (tiny(M, N, dt, epi)) {
     const int K0 = Ka < Kb ? Ka : Kb;
     const long outs = (long)M * N;

@@ -27,7 +27,8 @@ namespace ogv {
 
 constexpr int PG_NW = 4;           // waves per workgroup
 constexpr int PG_KB = 64;          // reduction columns per k-step (two 32-wide MFMA sub-steps)
-constexpr int PG_KP = PG_KB + 8;   // [n][k] slab pitch (elements): 144-B rows
+constexpr int PG_KP = PG_KB;       // [n][k] slab pitch (elements): 128-B rows, 16-B chunks rotated by the row
+// (chunk c of row r stored at (c + r) & 7): conflict-free 16-B fragment reads and 8-B staging writes
 
 template <int TN, bool BT>
 __host__ __device__ constexpr int pg_slab_elems() {
@@ -39,39 +40,43 @@ __host__ __device__ constexpr int pg_slab_elems() {
 // consecutive rows (conflict-free with a pitch of 8 mod 64 dwords)
 __device__ __forceinline__ int pg_perm(int k) { return (k & ~12) | ((k & 4) << 1) | ((k & 8) >> 1); }
 
-// RS: 16-row fragments per wave (rows per workgroup = 64 * RS); TN: 16-column fragments per
-// workgroup (BN = 16 * TN).  PA: -1 = no prologue, else its activation (sc / sh optional, staged in
-// LDS); GT: the prologue has an SE gate.  ZA: activation derivative at Z in the epilogue.
+// RS: 16-row fragments per wave (rows per tile = 64 * RS); TN: 16-column fragments per tile
+// (BN = 16 * TN).  PA: -1 = no prologue, else its activation (sc / sh optional, staged in LDS);
+// GT: the prologue has an SE gate.  ZA: activation derivative at Z in the epilogue.
+//
+// Persistent: workgroup b walks the virtual tiles vb = b, b + G, b + 2G, ... (G = gridDim.x, a
+// multiple of 8, so vb keeps b's XCD) and the (tile, k-step) pairs form ONE pipeline: the loads of
+// the next tile's first k-steps are in flight while the current tile's epilogue runs.
 template <int RS, int TN, int PA, bool GT, int ZA, bool STATS, bool BT, bool SW>
 __global__ __launch_bounds__(PG_NW * 64, 2) void pgemm_bf16_kernel(const bf16* __restrict__ A, int lda, Pro pro,
                                                                 const float* __restrict__ W, int ldw, Epi epi,
                                                                 bf16* __restrict__ out, int ldo, int M, int N, int K,
                                                                 int nMt, int nNt) {
   constexpr int BN = TN * 16;
+  constexpr int BM = PG_NW * 16 * RS;
   constexpr int SLAB = pg_slab_elems<TN, BT>();
   constexpr int NSLAB = SW ? 2 : 1;          // hi (+ lo) weight halves
   constexpr int WF4 = BN * PG_KB / 4 / 256;  // float4 weight loads per thread and k-step (= TN)
   constexpr int BP = BN + 16;                // BT slab pitch
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  bf16* slab = reinterpret_cast<bf16*>(smem);  // [2 buffers][NSLAB][SLAB]
-  float* cvec = reinterpret_cast<float*>(smem + (size_t)2 * NSLAB * SLAB * 2);  // [bias | shift] (BN each)
-  float* pvec = cvec + 2 * BN;                                                   // [sc | sh] (K each), PA >= 0
+  bf16* slab = reinterpret_cast<bf16*>(smem);                                    // [2][NSLAB][SLAB]
+  float* cvec = reinterpret_cast<float*>(smem + (size_t)2 * NSLAB * SLAB * 2);  // [2 tiles][bias | shift]
+  double* red = reinterpret_cast<double*>(cvec + 4 * BN);                        // STATS: [wave][2][BN]
+  bf16* stg = reinterpret_cast<bf16*>(red + (STATS ? PG_NW * 2 * BN : 0));        // STATS: [wave][16][16]
+  float* pvec = reinterpret_cast<float*>(stg + (STATS ? PG_NW * 256 : 0));       // [sc | sh], PA >= 0
 
-  // XCD-aware map: blocks b and b + 8 share an XCD; all N-tiles of an M-panel run on one XCD so
-  // the panel's A rows come from HBM once and from that XCD's L2 after.
-  const int bid = blockIdx.x, xcd = bid & 7, local = bid >> 3;
-  const int mt = (local / nNt) * 8 + xcd, nt = local % nNt;
-  if (mt >= nMt) return;
-  const int m0 = mt * (PG_NW * 16 * RS), n0 = nt * BN;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fg = lane >> 4;
-  const int mw = m0 + wave * 16 * RS;  // this wave's first row
+  const int G = gridDim.x, xcd = blockIdx.x & 7;
+  // tiles of this workgroup: vb = blockIdx.x + G * j; M-panel index is non-decreasing in j
+  auto tile_mt = [&](int j) { return (((blockIdx.x + G * j) >> 3) / nNt) * 8 + xcd; };
+  auto tile_nt = [&](int j) { return ((blockIdx.x + G * j) >> 3) % nNt; };
+  int ntiles = 0;
+  while (tile_mt(ntiles) < nMt) ++ntiles;
+  if (ntiles == 0) return;
+  const int nsteps = (K + PG_KB - 1) / PG_KB;
+  const int total = ntiles * nsteps;
 
-  for (int c = tid; c < BN; c += PG_NW * 64) {
-    const int n = n0 + c;
-    cvec[c] = (epi.bias && n < N) ? epi.bias[n] : 0.f;
-    cvec[BN + c] = (STATS && epi.stat_shift && n < N) ? bn_shift(epi.stat_shift[n]) : 0.f;
-  }
   if constexpr (PA >= 0) {
     for (int k = tid; k < K; k += PG_NW * 64) {
       pvec[k] = pro.sc ? pro.sc[k] : 1.f;
@@ -79,12 +84,10 @@ __global__ __launch_bounds__(PG_NW * 64, 2) void pgemm_bf16_kernel(const bf16* _
     }
   }
 
-  const int nsteps = (K + PG_KB - 1) / PG_KB;
-
-  // ---- weight slab loads (registers) and staging (bf16 hi / lo -> LDS)
+  // ---- weight slab of global step g (registers), staging (bf16 hi / lo -> LDS)
   float4 wr[WF4];
-  auto load_w = [&](int s) {
-    const int k0 = s * PG_KB;
+  auto load_w = [&](int g) {
+    const int j = g / nsteps, k0 = (g - j * nsteps) * PG_KB, n0 = tile_nt(j) * BN;
 #pragma unroll
     for (int i = 0; i < WF4; ++i) {
       const int idx = tid + i * 256;
@@ -105,7 +108,8 @@ __global__ __launch_bounds__(PG_NW * 64, 2) void pgemm_bf16_kernel(const bf16* _
       const int idx = tid + i * 256;
       int off;
       if constexpr (!BT) {
-        off = (idx / (PG_KB / 4)) * PG_KP + (idx % (PG_KB / 4)) * 4;
+        const int r = idx / (PG_KB / 4), kq = idx % (PG_KB / 4);
+        off = r * PG_KP + (((kq >> 1) + r) & 7) * 8 + (kq & 1) * 4;
       } else {
         const int kr = idx / (BN / 4);
         off = ((kr & ~31) | pg_perm(kr & 31)) * BP + (idx % (BN / 4)) * 4;
@@ -120,9 +124,10 @@ __global__ __launch_bounds__(PG_NW * 64, 2) void pgemm_bf16_kernel(const bf16* _
     }
   };
 
-  // ---- A fragments: lane (fr, fg) holds row mw + 16 i + fr, k = k0 + 32 kt + 8 fg .. + 8
-  auto load_a = [&](int s, bf16x8 (&a)[RS][2]) {
-    const int k0 = s * PG_KB;
+  // ---- A fragments of global step g: lane (fr, fg) holds row mw + 16 i + fr, k = k0 + 32 kt + 8 fg
+  auto load_a = [&](int g, bf16x8 (&a)[RS][2]) {
+    const int j = g / nsteps, k0 = (g - j * nsteps) * PG_KB;
+    const int mw = tile_mt(j) * BM + wave * 16 * RS;
 #pragma unroll
     for (int i = 0; i < RS; ++i) {
       const int m = mw + i * 16 + fr;
@@ -135,11 +140,12 @@ __global__ __launch_bounds__(PG_NW * 64, 2) void pgemm_bf16_kernel(const bf16* _
       }
     }
   };
-  // SE gate of step s (prologue with a gate): loaded one k-step ahead, with the weight slab
+  // SE gate of step g (prologue with a gate): loaded one k-step ahead, with the weight slab
   float4 gr[GT ? RS : 1][GT ? 2 : 1][2];
-  auto load_g = [&](int s) {
+  auto load_g = [&](int g) {
     if constexpr (GT) {
-      const int k0 = s * PG_KB;
+      const int j = g / nsteps, k0 = (g - j * nsteps) * PG_KB;
+      const int mw = tile_mt(j) * BM + wave * 16 * RS;
 #pragma unroll
       for (int i = 0; i < RS; ++i) {
         const int m = mw + i * 16 + fr;
@@ -148,9 +154,9 @@ __global__ __launch_bounds__(PG_NW * 64, 2) void pgemm_bf16_kernel(const bf16* _
           const int k = k0 + kt * 32 + fg * 8;
           gr[i][kt][0] = gr[i][kt][1] = float4{1.f, 1.f, 1.f, 1.f};
           if (m < M && k < K) {
-            const float* g = pro.gate + (long)(m / pro.rps) * pro.gld + k;
-            gr[i][kt][0] = *reinterpret_cast<const float4*>(g);
-            gr[i][kt][1] = *reinterpret_cast<const float4*>(g + 4);
+            const float* gp = pro.gate + (long)(m / pro.rps) * pro.gld + k;
+            gr[i][kt][0] = *reinterpret_cast<const float4*>(gp);
+            gr[i][kt][1] = *reinterpret_cast<const float4*>(gp + 4);
           }
         }
       }
@@ -167,9 +173,8 @@ __global__ __launch_bounds__(PG_NW * 64, 2) void pgemm_bf16_kernel(const bf16* _
   typedef __attribute__((ext_vector_type(8))) short s16x8;
   const int q = fr >> 2, p4 = (fr & 3) * 4;
 
-  auto compute = [&](int s, bf16x8 (&a)[RS][2], int buf) {
+  auto compute = [&](int k0, bf16x8 (&a)[RS][2], int buf) {
     if constexpr (PA >= 0) {
-      const int k0 = s * PG_KB;
 #pragma unroll
       for (int i = 0; i < RS; ++i) {
 #pragma unroll
@@ -207,7 +212,8 @@ __global__ __launch_bounds__(PG_NW * 64, 2) void pgemm_bf16_kernel(const bf16* _
           const bf16* t = hi + h * SLAB;
           bf16x8 wf;
           if constexpr (!BT) {
-            wf = *reinterpret_cast<const bf16x8*>(t + (j * 16 + fr) * PG_KP + kt * 32 + fg * 8);
+            const int r = j * 16 + fr;
+            wf = *reinterpret_cast<const bf16x8*>(t + r * PG_KP + ((kt * 4 + fg + r) & 7) * 8);
           } else {
             const int r = kt * 32 + 16 * (fg >> 1) + 4 * (fg & 1) + q;  // pg_perm(8 fg + q)
             const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(t + r * BP + j * 16 + p4));
@@ -222,114 +228,141 @@ __global__ __launch_bounds__(PG_NW * 64, 2) void pgemm_bf16_kernel(const bf16* _
     }
   };
 
+  // ---- epilogue of tile j: lane holds out[m = mw + 16 i + fr][n = n0 + 16 jj + 4 fg + r], r = 0..3
+  const bf16* res = static_cast<const bf16*>(epi.res);
+  const bf16* Z = static_cast<const bf16*>(epi.Z);
+  constexpr int JC = TN <= 8 ? TN : TN / 2;  // column fragments per residual / Z round trip
+  auto epilogue = [&](int j) {
+    const int mt = tile_mt(j), n0 = tile_nt(j) * BN, mw = mt * BM + wave * 16 * RS;
+    const float* cv = cvec + (j & 1) * 2 * BN;
+#pragma unroll
+    for (int i = 0; i < RS; ++i) {
+      const int m = mw + i * 16 + fr;
+      const bool mok = m < M;
+      const float rsc = (epi.rs && mok) ? epi.rs[m / epi.rps] : 1.f;
+#pragma unroll
+      for (int jc = 0; jc < TN; jc += JC) {
+        uint2 rv[JC], zv[JC];
+#pragma unroll
+        for (int u = 0; u < JC; ++u) {  // residual / Z of the chunk first: one round trip
+          const int n = n0 + (jc + u) * 16 + 4 * fg;
+          rv[u] = uint2{0u, 0u};
+          zv[u] = uint2{0u, 0u};
+          if (mok && n < N) {
+            if (res) rv[u] = *reinterpret_cast<const uint2*>(res + (long)m * ldo + n);
+            if constexpr (ZA != 0) zv[u] = *reinterpret_cast<const uint2*>(Z + (long)m * epi.ldz + n);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < JC; ++u) {
+          const int jj = jc + u, c = jj * 16 + 4 * fg, n = n0 + c;
+          const bool ok = mok && n < N;
+          const float4 bs = *reinterpret_cast<const float4*>(cv + c);
+          const float bias[4] = {bs.x, bs.y, bs.z, bs.w};
+          const bf16* rb = reinterpret_cast<const bf16*>(&rv[u]);
+          const bf16* zb = reinterpret_cast<const bf16*>(&zv[u]);
+          uint2 ov;
+          bf16* ob = reinterpret_cast<bf16*>(&ov);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float x = (acc[i][jj][r] + bias[r]) * rsc + (float)rb[r];
+            if constexpr (ZA != 0) x *= act_grad(ZA, (float)zb[r]);
+            ob[r] = (bf16)x;
+          }
+          if (ok) *reinterpret_cast<uint2*>(out + (long)m * ldo + n) = ov;
+          if constexpr (STATS) {
+            // BatchNorm column sums of the stored values, fp64 from the first add (d = out - shift
+            // is exact in fp64), so they do not depend on the shift's value: the 16 x 16 fragment
+            // goes through a wave-private LDS tile and comes back one column per lane
+            bf16* st = stg + wave * 256;
+            *reinterpret_cast<uint2*>(st + fr * 16 + 4 * fg) = ov;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const int cc = jj * 16 + fr, nc = n0 + cc;  // this lane's column, rows 4 fg .. 4 fg + 3
+            const double sh = (double)cv[BN + cc];
+            double t1 = 0.0, t2 = 0.0;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int row = 4 * fg + e;
+              if (mw + i * 16 + row < M && nc < N) {
+                const double d = (double)(float)st[row * 16 + fr] - sh;
+                t1 += d;
+                t2 = fma(d, d, t2);
+              }
+            }
+            t1 += __shfl_xor(t1, 16, 64);
+            t2 += __shfl_xor(t2, 16, 64);
+            t1 += __shfl_xor(t1, 32, 64);
+            t2 += __shfl_xor(t2, 32, 64);
+            if (fg == 0) {
+              double* r1 = red + (wave * 2 + 0) * BN + cc;
+              double* r2 = red + (wave * 2 + 1) * BN + cc;
+              *r1 = i == 0 ? t1 : *r1 + t1;
+              *r2 = i == 0 ? t2 : *r2 + t2;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < RS; ++i)
+#pragma unroll
+      for (int jj = 0; jj < TN; ++jj) acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (STATS) {
+      __syncthreads();  // (the previous tile's readers of red passed this tile's k-step barriers)
+      for (int c = tid; c < BN; c += PG_NW * 64) {
+        if (n0 + c >= N) continue;
+        double t1 = 0.0, t2 = 0.0;
+#pragma unroll
+        for (int w = 0; w < PG_NW; ++w) {  // across the waves, fixed order
+          t1 += red[(w * 2 + 0) * BN + c];
+          t2 += red[(w * 2 + 1) * BN + c];
+        }
+        epi.stat[((long)mt * 2 + 0) * N + n0 + c] = t1;
+        epi.stat[((long)mt * 2 + 1) * N + n0 + c] = t2;
+      }
+    }
+  };
+
+  // bias / BatchNorm shift of tile j into its parity slot (read by tile j's epilogue only; the slot
+  // is rewritten by tile j + 2, after tile j + 1's k-step barriers)
+  auto tile_consts = [&](int j) {
+    const int n0 = tile_nt(j) * BN;
+    float* cv = cvec + (j & 1) * 2 * BN;
+    for (int c = tid; c < BN; c += PG_NW * 64) {
+      const int n = n0 + c;
+      cv[c] = (epi.bias && n < N) ? epi.bias[n] : 0.f;
+      cv[BN + c] = (STATS && epi.stat_shift && n < N) ? bn_shift(epi.stat_shift[n]) : 0.f;
+    }
+  };
+
   bf16x8 a0[RS][2], a1[RS][2];
   load_w(0);
   load_g(0);
   load_a(0, a0);
-  if (nsteps > 1) load_a(1, a1);
-  __syncthreads();  // cvec / pvec
-  // one barrier per k-step: step s writes buffer s & 1, whose last readers (step s - 2's MFMAs)
-  // all passed step s - 1's barrier
-  auto step = [&](int s, bf16x8 (&a)[RS][2]) {
-    store_w(s & 1);
-    if (s + 1 < nsteps) load_w(s + 1);
+  if (total > 1) load_a(1, a1);
+  // one barrier per k-step: step g writes buffer g & 1, whose last readers (step g - 2's MFMAs)
+  // all passed step g - 1's barrier
+  auto step = [&](int g, bf16x8 (&a)[RS][2]) {
+    const int j = g / nsteps, s = g - j * nsteps;
+    if (s == 0) tile_consts(j);
+    store_w(g & 1);
+    if (g + 1 < total) load_w(g + 1);
     __syncthreads();
-    compute(s, a, s & 1);
+    compute(s * PG_KB, a, g & 1);
     if constexpr (GT) {
-      if (s + 1 < nsteps) load_g(s + 1);
+      if (g + 1 < total) load_g(g + 1);
     }
-    if (s + 2 < nsteps) load_a(s + 2, a);
+    if (g + 2 < total) load_a(g + 2, a);
+    if (s == nsteps - 1) epilogue(j);
   };
-  for (int s = 0; s < nsteps; s += 2) {
-    step(s, a0);
-    if (s + 1 < nsteps) step(s + 1, a1);
-  }
-
-  // ---- epilogue: lane holds out[m = mw + 16 i + fr][n = n0 + 16 j + 4 fg + r], r = 0..3
-  const bf16* res = static_cast<const bf16*>(epi.res);
-  const bf16* Z = static_cast<const bf16*>(epi.Z);
-  float s1[TN][4], s2[TN][4];
-  if constexpr (STATS) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) { s1[j][r] = 0.f; s2[j][r] = 0.f; }
-  }
-#pragma unroll
-  for (int i = 0; i < RS; ++i) {
-    const int m = mw + i * 16 + fr;
-    const bool mok = m < M;
-    const float rsc = (epi.rs && mok) ? epi.rs[m / epi.rps] : 1.f;
-    uint2 rv[TN], zv[TN];
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {  // residual / Z first: one round trip for the whole row fragment
-      const int n = n0 + j * 16 + 4 * fg;
-      rv[j] = uint2{0u, 0u};
-      zv[j] = uint2{0u, 0u};
-      if (mok && n < N) {
-        if (res) rv[j] = *reinterpret_cast<const uint2*>(res + (long)m * ldo + n);
-        if constexpr (ZA != 0) zv[j] = *reinterpret_cast<const uint2*>(Z + (long)m * epi.ldz + n);
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int c = j * 16 + 4 * fg, n = n0 + c;
-      if (!(mok && n < N)) continue;
-      const float4 bs = *reinterpret_cast<const float4*>(cvec + c);
-      const float bias[4] = {bs.x, bs.y, bs.z, bs.w};
-      const bf16* rb = reinterpret_cast<const bf16*>(&rv[j]);
-      const bf16* zb = reinterpret_cast<const bf16*>(&zv[j]);
-      uint2 ov;
-      bf16* ob = reinterpret_cast<bf16*>(&ov);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float x = (acc[i][j][r] + bias[r]) * rsc + (float)rb[r];
-        if constexpr (ZA != 0) x *= act_grad(ZA, (float)zb[r]);
-        ob[r] = (bf16)x;
-        if constexpr (STATS) {
-          const float d = (float)ob[r] - cvec[BN + c + r];
-          s1[j][r] += d;
-          s2[j][r] = fmaf(d, d, s2[j][r]);
-        }
-      }
-      *reinterpret_cast<uint2*>(out + (long)m * ldo + n) = ov;
-    }
-  }
-  if constexpr (STATS) {
-    // over the 16 rows of a lane group (fp32, <= 32 rows per wave), then the 4 waves in fp64
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-          s1[j][r] += __shfl_xor(s1[j][r], o, 64);
-          s2[j][r] += __shfl_xor(s2[j][r], o, 64);
-        }
-    __syncthreads();  // slabs are dead
-    double* red = reinterpret_cast<double*>(smem);  // [wave][2][BN]
-    if (fr == 0) {
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int c = j * 16 + 4 * fg + r;
-          red[(wave * 2 + 0) * BN + c] = (double)s1[j][r];
-          red[(wave * 2 + 1) * BN + c] = (double)s2[j][r];
-        }
-    }
-    __syncthreads();
-    for (int c = tid; c < BN; c += PG_NW * 64) {
-      if (n0 + c >= N) continue;
-      double t1 = 0.0, t2 = 0.0;
-#pragma unroll
-      for (int w = 0; w < PG_NW; ++w) {
-        t1 += red[(w * 2 + 0) * BN + c];
-        t2 += red[(w * 2 + 1) * BN + c];
-      }
-      epi.stat[((long)mt * 2 + 0) * N + n0 + c] = t1;
-      epi.stat[((long)mt * 2 + 1) * N + n0 + c] = t2;
-    }
+  for (int g = 0; g < total; g += 2) {
+    step(g, a0);
+    if (g + 1 < total) step(g + 1, a1);
   }
 }
 
@@ -339,7 +372,22 @@ __global__ __launch_bounds__(PG_NW * 64, 2) void pgemm_bf16_kernel(const bf16* _
 static int g_pgemm = 1;   // knob "pgemm": route small-M bf16 fwd / dgrad here (0 = tiled kernel)
 static int g_pg_rs = 0;   // knobs "pg_rs" / "pg_tn": force the tile (0 = planner)
 static int g_pg_tn = 0;
+// knob "pg_per_cu": workgroups per CU the grid is capped at (measured: 8, i.e. one tile per workgroup
+// on these shapes, beats 1-2 resident persistent workgroups: the hardware's dynamic dispatch
+// balances the tail better than the static tile walk)
+static int g_pg_per_cu = 8;
 void set_pgemm(int v) { g_pgemm = v; }
+void set_pg_per_cu(int v) { g_pg_per_cu = v < 1 ? 1 : (v > 8 ? 8 : v); }
+static int pg_cus() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  return cus;
+}
 void set_pg_rs(int v) { g_pg_rs = v; }
 void set_pg_tn(int v) { g_pg_tn = v; }
 
@@ -348,11 +396,10 @@ struct PgPlan {
   size_t lds = 0;
 };
 
-static size_t pg_lds(int TN, bool bt, bool sw, int K, bool pa) {
+static size_t pg_lds(int TN, bool bt, bool sw, int K, bool pa, bool stats) {
   const size_t slab = bt ? (size_t)PG_KB * (TN * 16 + 16) : (size_t)TN * 16 * PG_KP;
-  size_t b = 2 * (sw ? 2 : 1) * slab * 2 + 2 * TN * 16 * 4 + (pa ? 2 * (size_t)K * 4 : 0);
-  const size_t red = (size_t)PG_NW * 2 * TN * 16 * 8;  // STATS reduction reuses the slabs
-  return std::max(b, red);
+  return 2 * (sw ? 2 : 1) * slab * 2 + 4 * TN * 16 * 4 + (stats ? (size_t)PG_NW * (2 * TN * 16 * 8 + 512) : 0) +
+         (pa ? 2 * (size_t)K * 4 : 0);
 }
 
 static bool al16p(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
@@ -364,7 +411,10 @@ static bool al16p(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) 
 static PgPlan pg_plan(int M, int N, int K, bool stats, bool sw, bool bt, bool pa, bool gate) {
   PgPlan p;
   if (!g_pgemm || M <= 0 || (N & 7) || (K & 7)) return p;
-  const int tns[3] = {8, 12, 4};
+  // measured (tools/gpu_pgemm_sweep.sh, 7M census): at M <= 16384 64-column tiles win unless
+  // the output is >= 1024 wide
+  const bool narrow = M <= 16384 && N < 1024;
+  const int tns[3] = {narrow ? 4 : 8, 12, 4};
   int best_tn = 0;
   for (int t : tns) {
     if (g_pg_tn && t != g_pg_tn) continue;
@@ -373,7 +423,7 @@ static PgPlan pg_plan(int M, int N, int K, bool stats, bool sw, bool bt, bool pa
     if (t == 12 && (gate || stats || N <= 128)) continue;
     const int bn = 16 * t, nnt = (N + bn - 1) / bn;
     if ((long)nnt * bn - N > N / 16 && t != 4 && !g_pg_tn) continue;
-    if (pg_lds(t, bt, sw, K, pa) > 80 * 1024) continue;  // two workgroups per CU
+    if (pg_lds(t, bt, sw, K, pa, stats) > 80 * 1024) continue;  // two workgroups per CU
     best_tn = t;
     break;
   }
@@ -388,7 +438,7 @@ static PgPlan pg_plan(int M, int N, int K, bool stats, bool sw, bool bt, bool pa
   }
   if (g_pg_rs && !stats && p.TN != 12) p.RS = g_pg_rs;
   p.nMt = (M + 64 * p.RS - 1) / (64 * p.RS);
-  p.lds = pg_lds(p.TN, bt, sw, K, pa);
+  p.lds = pg_lds(p.TN, bt, sw, K, pa, stats);
   p.ok = 1;
   return p;
 }
@@ -403,7 +453,9 @@ static void pg_launch(const PgPlan& p, const bf16* A, int lda, const Pro& pro, c
                               160 * 1024);
     attr = true;
   }
-  const unsigned grid = (unsigned)(((p.nMt + 7) / 8) * 8 * p.nNt);
+  // persistent: at most pg_per_cu workgroups per CU, a multiple of 8 (keeps each one's XCD)
+  const long vb = (long)((p.nMt + 7) / 8) * 8 * p.nNt;
+  const unsigned grid = (unsigned)std::min<long>(vb, (long)pg_cus() * g_pg_per_cu / 8 * 8);
   kern<<<grid, PG_NW * 64, p.lds, s>>>(A, lda, pro, W, ldw, epi, out, ldo, M, N, K, p.nMt, p.nNt);
 }
 

@@ -158,6 +158,14 @@ extern "C" int ogv_set_option(const char* name, int value) {
     set_pgemm(value ? 1 : 0);
     return OGV_OK;
   }
+  if (!strcmp(name, "sg_wgs")) {
+    set_sg_wgs(value);
+    return OGV_OK;
+  }
+  if (!strcmp(name, "pg_per_cu")) {
+    set_pg_per_cu(value);
+    return OGV_OK;
+  }
   if (!strcmp(name, "pg_rs")) {
     set_pg_rs(value == 1 || value == 2 ? value : 0);
     return OGV_OK;

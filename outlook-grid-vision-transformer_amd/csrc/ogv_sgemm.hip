@@ -361,6 +361,8 @@ static int g_sg_per_cu = 2;     // workgroups per CU the planner asks for (tunin
 void set_sg_per_cu(int v) { g_sg_per_cu = v < 1 ? 1 : (v > 4 ? 4 : v); }
 static int g_sg_prefetch = 1;   // knob "sg_prefetch": next-panel register prefetch (no-prologue variants)
 void set_sg_prefetch(int v) { g_sg_prefetch = v ? 1 : 0; }
+static int g_sg_wgs = 0;
+void set_sg_wgs(int v) { g_sg_wgs = v < 0 ? 0 : v; }
 static int g_sg_min_m = 65536;  // smallest M routed to the streaming kernels (tuning knob "sgemm_min_m")
 void set_sgemm_min_m(int v) { g_sg_min_m = v; }
 int sgemm_min_m() { return g_sg_min_m; }
@@ -433,6 +435,8 @@ static SgPlan sgemm_plan_w(int M, int N, int K, bool stats, bool prologue, bool 
   const long panels = ((long)M + 16 * p.RS - 1) / (16 * p.RS);
   const long want = (panels + SG_NW - 1) / SG_NW;
   p.grid = (int)std::min<long>(want, (long)device_cus() * per_cu);
+  if (g_sg_wgs > 0)  // knob "sg_wgs": total workgroups over all N-tiles (persistent at small M)
+    p.grid = (int)std::max<long>(8, std::min<long>(want, (long)g_sg_wgs / p.ntiles));
   p.grid = (p.grid + 7) / 8 * 8;  // the N-tiles of one row range share an XCD: x % 8 fixes the XCD
   if (stats) p.grid = std::min(p.grid, std::max(8, ((M + GEMM_BM - 1) / GEMM_BM) / 8 * 8));  // <= gemm_stat_rows
   p.ok = 1;

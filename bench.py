@@ -41,8 +41,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=512, help="per-GPU batch")
     ap.add_argument("--model", default="model_a_7m")
-    ap.add_argument("--probe", default="gemm_tiled",
-                    choices=["gemm_tiled", "sgemm", "wgrad", "gemm_fwd", "outlook_fwd", "outlook_bwd", "grid_fwd"],
+    ap.add_argument("--probe", default="gemm_panel",
+                    choices=["gemm_panel", "gemm_tiled", "sgemm", "wgrad", "gemm_fwd", "outlook_fwd", "outlook_bwd", "grid_fwd"],
                     help="kernel family whose launches feed `roofline`")
     ap.add_argument("--eager", action="store_true", help="launch kernels one by one instead of graph replay")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -61,9 +61,11 @@ METRIC = {  # BASELINE.json configs[1..4]
 }
 
 PROBE_KERNEL = {  # probe name -> kernel symbol(s) it times (rocprofv3 names)
-    "gemm_tiled": "ogv::gemm_bf16_kernel<*> (tiled MFMA GEMM: the Linear / 1x1-conv forward and data-gradient "
-                  "launches NOT routed to the streaming kernel -- stages 2-3 of 7M, M <= 32768; the largest-time "
-                  "kernel family of the step)",
+    "gemm_panel": "ogv::pgemm_bf16_kernel<*> (pipelined panel GEMM: the Linear / 1x1-conv forward and "
+                  "data-gradient launches at M < 65536 -- stages 1-3 of 7M; the largest-time kernel family "
+                  "of the step)",
+    "gemm_tiled": "ogv::gemm_bf16_kernel<*> (LDS-tiled MFMA GEMM: Linear / 1x1-conv launches routed to "
+                  "neither the streaming nor the panel kernel, and the implicit-GEMM convs)",
     "wgrad": "ogv::wgrad_bf16_kernel<*> / ogv::swgrad_bf16_kernel<*> + colreduce (Linear / 1x1-conv weight gradients)",
     "outlook_bwd": "ogv::outlook_bwd_tile_kernel<*> (LDS-tiled outlook backward: the col2im fold as a gather + dlogits)",
     "sgemm": "ogv::sgemm_bf16_kernel<*> (persistent streaming projection GEMM: the Linear / 1x1-conv fwd and dgrad "

@@ -51,8 +51,9 @@ const char* ogv_last_error(void);
  *   "splitk_max" (default 32): K-slab cap of the fp32 split-K GEMM (SE MLP).
  * Returns OGV_ERR_ARG for an unknown name. */
 int ogv_set_option(const char* name, int value);
-/* Diagnostics (no reference counterpart): 1 if ogv_gemm_fwd (kind 0) / ogv_gemm_dgrad (kind 1) of
- * this shape runs on the persistent streaming kernel (contiguous 16-B aligned bf16 operands), else 0;
+/* Diagnostics (no reference counterpart): which kernel ogv_gemm_fwd (kind 0) / ogv_gemm_dgrad
+ * (kind 1) of this bf16 shape runs on (contiguous 16-B aligned operands): 1 = the persistent
+ * streaming kernel (large M), 2 = the pipelined panel kernel (small M), 0 = the LDS-tiled kernel;
  * ogv_gpu_sleep queues a ~microseconds device-side spin on the stream (timing harnesses). */
 int ogv_gemm_stream_route(int kind, int M, int N, int K, ogv_act act_in);
 int ogv_gpu_sleep(int microseconds, void* stream);

@@ -158,6 +158,7 @@ int pgemm_fwd_try(const void* A, int lda, const Pro& pro, const float* W, int ld
                   int N, int K, const Epi& epi, hipStream_t s);
 bool pgemm_dgrad_try(const void* dout, int ldd, const float* W, void* dA, int lda, int M, int Nf, int Kf,
                      const Epi& epi, hipStream_t s);
+bool pgemm_route(int kind, int M, int N, int K, int act);
 void set_pgemm(int v);
 void set_pg_rs(int v);
 void set_pg_tn(int v);

@@ -537,4 +537,12 @@ bool pgemm_dgrad_try(const void* dout, int ldd, const float* W, void* dA, int ld
   return true;
 }
 
+bool pgemm_route(int kind, int M, int N, int K, int act) {
+  if (kind == 0) {
+    if (act != OGV_ACT_NONE && act != OGV_ACT_GELU && act != OGV_ACT_SILU) return false;
+    return pg_plan(M, N, K, false, (split_w() & 1) != 0, false, act != OGV_ACT_NONE, false).ok;
+  }
+  return pg_plan(M, K, N, false, (split_w() & 2) != 0, true, false, false).ok;  // dgrad: output K
+}
+
 }  // namespace ogv

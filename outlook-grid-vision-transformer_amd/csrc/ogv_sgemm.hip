@@ -542,9 +542,11 @@ __global__ void gpu_sleep_kernel(unsigned long long ticks) {
 }
 
 int sgemm_route(int kind, int M, int N, int K, int act) {
-  if (!sgemm_mode()) return 0;
-  if (kind == 0) return sgemm_plan(M, N, K, false, act != OGV_ACT_NONE, false).ok;
-  return sgemm_plan(M, K, N, false, false, true).ok;  // dgrad: output K, reduction N
+  if (sgemm_mode()) {
+    if (kind == 0 && sgemm_plan(M, N, K, false, act != OGV_ACT_NONE, false).ok) return 1;
+    if (kind != 0 && sgemm_plan(M, K, N, false, false, true).ok) return 1;  // dgrad: output K, reduction N
+  }
+  return pgemm_route(kind, M, N, K, act) ? 2 : 0;
 }
 
 }  // namespace ogv

@@ -108,11 +108,11 @@ def probe_bytes(name: str, u: dict) -> int:
         return e * u["M"] * (3 * u["C"] + 2 * u["k"] * u["k"] * u["heads"])
     if name == "wgrad":         # read G [M,N], X [M,K]; write fp32 dW [N,K] (+ dbias)
         return e * u["M"] * (u["N"] + u["K"]) + 4 * u["N"] * u["K"] + (4 * u["N"] if u["bias"] else 0)
-    if name in ("gemm_fwd", "sgemm", "gemm_tiled") and u.get("kind", "fwd") == "fwd":
+    if name in ("gemm_fwd", "sgemm", "gemm_tiled", "gemm_panel") and u.get("kind", "fwd") == "fwd":
         # read A [M,K] (+ residual [M,N]) + fp32 W [N,K] (+ bias), write out [M,N]
         return (e * u["M"] * (u["K"] + u["N"] * (2 if u["res"] else 1)) + 4 * u["N"] * u["K"]
                 + (4 * u["N"] if u["bias"] else 0))
-    if name in ("sgemm", "gemm_tiled"):   # dgrad: read dOut [M,N] (+ Z [M,K]) + fp32 W [N,K], write dA [M,K]
+    if name in ("sgemm", "gemm_tiled", "gemm_panel"):   # dgrad: read dOut [M,N] (+ Z [M,K]) + fp32 W [N,K], write dA [M,K]
         return e * u["M"] * (u["N"] + u["K"] * (2 if u["z"] else 1)) + 4 * u["N"] * u["K"]
     raise KeyError(name)
 
@@ -259,10 +259,10 @@ class _Linear(torch.autograd.Function):
         N = w2d.shape[0]
         out = torch.empty((M, N), dtype=x2d.dtype, device=x2d.device)
         units = dict(M=M, N=N, K=K, elem=x2d.element_size(), res=residual is not None, bias=bias is not None)
-        stream_k = _PROBE["armed"] and lib.ogv_gemm_stream_route(0, M, N, K, ACT[act_in]) == 1
-        tiled = x2d.dtype == torch.bfloat16 and not stream_k
-        with _probe("gemm_fwd", units), _probe("sgemm", units, when=stream_k), \
-                _probe("gemm_tiled", units, when=tiled):
+        route = lib.ogv_gemm_stream_route(0, M, N, K, ACT[act_in]) if _PROBE["armed"] else -1
+        bf = x2d.dtype == torch.bfloat16
+        with _probe("gemm_fwd", units), _probe("sgemm", units, when=bf and route == 1), \
+                _probe("gemm_panel", units, when=bf and route == 2), _probe("gemm_tiled", units, when=bf and route == 0):
             check(lib.ogv_gemm_fwd(_ptr(x2d), x2d.stride(0), _ptr(w2d), _ptr(bias), _ptr(residual), _ptr(row_scale),
                                    int(rps), _ptr(out), N, M, N, K, ACT[act_in], _dt(x2d), _stream()), "ogv_gemm_fwd")
         ctx.save_for_backward(x2d, w2d, row_scale)
@@ -299,10 +299,11 @@ class _Linear(torch.autograd.Function):
                     check(lib.ogv_gemm_wgrad(_ptr(dout), N, _ptr(x2d), x2d.stride(0), _ptr(rs), rps, _ptr(dw), _ptr(db),
                                              M, N, K, act, _ptr(ws_w), dt, side), "ogv_gemm_wgrad")
             if want_dx:
-                stream_k = _PROBE["armed"] and lib.ogv_gemm_stream_route(1, M, N, K, act) == 1
+                route = lib.ogv_gemm_stream_route(1, M, N, K, act) if _PROBE["armed"] else -1
                 du = dict(kind="dgrad", M=M, N=N, K=K, elem=x2d.element_size(), z=bool(act))
-                with _probe("sgemm", du, when=stream_k), \
-                        _probe("gemm_tiled", du, when=x2d.dtype == torch.bfloat16 and not stream_k):
+                bf = x2d.dtype == torch.bfloat16
+                with _probe("sgemm", du, when=bf and route == 1), _probe("gemm_panel", du, when=bf and route == 2), \
+                        _probe("gemm_tiled", du, when=bf and route == 0):
                     check(lib.ogv_gemm_dgrad(_ptr(dout), N, _ptr(w2d), _ptr(x2d) if act else None, x2d.stride(0),
                                              _ptr(rs), rps, _ptr(dx), K, M, N, K, act, _ptr(ws_d), dt, _stream()),
                           "ogv_gemm_dgrad")

@@ -21,7 +21,10 @@ graph A = fwd + bwd + flatten of the fp32 gradients into ONE bucket (7.5 M param
 Model-A-7M, pre-divided by world size); one all_reduce of that bucket (a single large ring
 collective: xGMI links are point-to-point, so one 30 MB message beats many small DDP buckets);
 graph B = unflatten + clip_grad_norm + AdamW.  Parameters and buffers are broadcast from rank 0
-once at start; each rank keeps its own BatchNorm batch statistics.
+once at start; the BatchNorm running buffers then ride in the same all_reduce every step (rank 0's
+values, the others contribute zeros: DDP's broadcast_buffers), and each rank normalises with its
+own batch statistics.  Eager mode all-reduces 8 MB buckets asynchronously as backward
+produces them.
 """
 from __future__ import annotations
 

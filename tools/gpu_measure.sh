@@ -19,7 +19,7 @@ cat "$OUT/probe_vs_trace.txt"
 gzip -f "$OUT/prof/bench_kernel_trace.csv"
 if [ "${PMC:-1}" = 1 ]; then
   cp profiles/pmc_traffic.json "$OUT/pmc_traffic.json" 2>/dev/null || true
-  for PR in ${PMC_PROBES:-gemm_tiled outlook_bwd sgemm}; do
+  for PR in ${PMC_PROBES:-gemm_panel outlook_bwd sgemm}; do
     ARGS="--eager --steps 2 --warmup 1 --no-cpu-baseline --no-parity --probe $PR"
     timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch_$PR" -o run -- python3 bench.py $ARGS > "$OUT/fetch_$PR.log" 2>&1 || { echo "pmc fetch rc=$?"; exit 1; }
     timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write_$PR" -o run -- python3 bench.py $ARGS > "$OUT/write_$PR.log" 2>&1 || { echo "pmc write rc=$?"; exit 1; }

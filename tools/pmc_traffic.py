@@ -17,7 +17,8 @@ import os
 import re
 
 PROBES = {
-    "gemm_tiled": r"gemm_bf16_kernel",
+    "gemm_tiled": r"(?<!s)(?<!p)gemm_bf16_kernel",
+    "gemm_panel": r"pgemm_bf16_kernel",
     "outlook_bwd": r"outlook_bwd",
     "sgemm": r"sgemm_bf16_kernel",
     # bench.py's "gemm_fwd" probe: every Linear / 1x1-conv forward GEMM launch (the only users of the

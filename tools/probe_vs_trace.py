@@ -19,7 +19,7 @@ def main(trace, log):
     line = [ln for ln in open(log) if ln.startswith("{")][-1]
     rec = json.loads(line)
     roof = rec.get("roofline") or {}
-    fams = {"sgemm": "sgemm_bf16_kernel", "gemm_tiled": "gemm_bf16_kernel", "outlook_bwd": "outlook_bwd",
+    fams = {"sgemm": "sgemm_bf16_kernel", "gemm_tiled": "::gemm_bf16_kernel", "gemm_panel": "pgemm_bf16_kernel", "outlook_bwd": "outlook_bwd",
             "outlook_fwd": "outlook_fwd", "grid_fwd": "grid_fwd"}
     fam = fams.get(roof.get("probe", "sgemm" if "sgemm" in roof.get("kernel", "") else ""))
     if fam is None:

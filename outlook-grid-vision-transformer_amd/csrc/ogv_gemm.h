@@ -163,6 +163,9 @@ void set_pgemm(int v);
 void set_pg_rs(int v);
 void set_pg_tn(int v);
 void set_pg_per_cu(int v);
+void set_pg_dbg(int v);
+void set_wg_blocks(int v);
+void set_wg_tile(int v);
 // Streaming weight gradient (ogv_swgrad.hip) for large-M bf16 shapes: writes [S][N*K + N] fp32
 // partials into part and returns S (0 = not handled); swgrad_ws_floats sizes part + colreduce tmp.
 int swgrad_try(const void* G, int ldg, const void* X, int ldx, const Pro& pro, const float* rs, int rps, float* part,

@@ -1336,14 +1336,25 @@ void gemm_dgrad_launch(ogv_dtype dt, const void* dout, int ldd, const float* W, 
 struct WgradPlan {
   int BN, BK, nNt, nKt, S, mchunk;
 };
+static int g_wg_blocks = 1024;  // knob "wg_blocks": workgroups the bf16 split-M plan aims for
+static int g_wg_tile = 0;       // knob "wg_tile": force BN = BK = 64 (64) or 128 (128); 0 = by shape
+void set_wg_blocks(int v) { g_wg_blocks = v < 64 ? 64 : v; }
+void set_wg_tile(int v) { g_wg_tile = (v == 64 || v == 128) ? v : 0; }
 static WgradPlan wgrad_plan(ogv_dtype dt, int M, int N, int K) {
   WgradPlan p;
-  p.BN = (dt == OGV_BF16 && N > 64) ? 128 : 64;
-  p.BK = (dt == OGV_BF16 && K > 64) ? 128 : 64;
+  // bf16: 64 x 64 tiles (more tiles in flight, no half-empty 128-wide tile at K or N = 192),
+  // except the large M = 32768 projections of 147k-weight layers where 128 x 128 measured faster
+  // (tools/gpu_pgemm_sweep.sh KINDS=wgrad: 7M census 4.35 -> 3.79 ms)
+  p.BN = p.BK = 64;
+  if (dt == OGV_BF16 && M >= 32768 && (long)N * K >= 147456 && std::max(N, K) <= 768) {
+    p.BN = N > 64 ? 128 : 64;
+    p.BK = K > 64 ? 128 : 64;
+  }
+  if (dt == OGV_BF16 && g_wg_tile) p.BN = p.BK = g_wg_tile;
   p.nNt = (N + p.BN - 1) / p.BN;
   p.nKt = (K + p.BK - 1) / p.BK;
   const long tiles = (long)p.nNt * p.nKt;
-  long S = (1024 + tiles - 1) / tiles;
+  long S = ((dt == OGV_BF16 ? g_wg_blocks : 1024) + tiles - 1) / tiles;
   S = std::min(S, ((long)M + (M <= 4096 ? 31 : 255)) / (M <= 4096 ? 32 : 256));  // small M (SE): 32-row slabs
   const double data = 2.0 * M * (N + K) * (dt == OGV_BF16 ? 2 : 4);
   const long cap = (long)(std::max(data / 4, 16.0 * (1 << 20)) / (4.0 * ((double)N * K + N)));

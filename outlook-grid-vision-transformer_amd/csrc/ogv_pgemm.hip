@@ -51,7 +51,7 @@ template <int RS, int TN, int PA, bool GT, int ZA, bool STATS, bool BT, bool SW>
 __global__ __launch_bounds__(PG_NW * 64, 2) void pgemm_bf16_kernel(const bf16* __restrict__ A, int lda, Pro pro,
                                                                 const float* __restrict__ W, int ldw, Epi epi,
                                                                 bf16* __restrict__ out, int ldo, int M, int N, int K,
-                                                                int nMt, int nNt) {
+                                                                int nMt, int nNt, int dbg) {
   constexpr int BN = TN * 16;
   constexpr int BM = PG_NW * 16 * RS;
   constexpr int SLAB = pg_slab_elems<TN, BT>();
@@ -269,7 +269,7 @@ __global__ __launch_bounds__(PG_NW * 64, 2) void pgemm_bf16_kernel(const bf16* _
             if constexpr (ZA != 0) x *= act_grad(ZA, (float)zb[r]);
             ob[r] = (bf16)x;
           }
-          if (ok) *reinterpret_cast<uint2*>(out + (long)m * ldo + n) = ov;
+          if (ok && !(dbg & 4)) *reinterpret_cast<uint2*>(out + (long)m * ldo + n) = ov;
           if constexpr (STATS) {
             // BatchNorm column sums of the stored values, fp64 from the first add (d = out - shift
             // is exact in fp64), so they do not depend on the shift's value: the 16 x 16 fragment
@@ -351,13 +351,13 @@ __global__ __launch_bounds__(PG_NW * 64, 2) void pgemm_bf16_kernel(const bf16* _
     const int j = g / nsteps, s = g - j * nsteps;
     if (s == 0) tile_consts(j);
     store_w(g & 1);
-    if (g + 1 < total) load_w(g + 1);
+    if (g + 1 < total && !(dbg & 1)) load_w(g + 1);
     __syncthreads();
     compute(s * PG_KB, a, g & 1);
     if constexpr (GT) {
       if (g + 1 < total) load_g(g + 1);
     }
-    if (g + 2 < total) load_a(g + 2, a);
+    if (g + 2 < total && !(dbg & 2)) load_a(g + 2, a);
     if (s == nsteps - 1) epilogue(j);
   };
   for (int g = 0; g < total; g += 2) {
@@ -377,6 +377,8 @@ static int g_pg_tn = 0;
 // balances the tail better than the static tile walk)
 static int g_pg_per_cu = 8;
 void set_pgemm(int v) { g_pgemm = v; }
+static int g_pg_dbg = 0;  // knob "pg_dbg" (timing experiments only, wrong results): 1 no weight reloads, 2 no A reloads, 4 no stores
+void set_pg_dbg(int v) { g_pg_dbg = v; }
 void set_pg_per_cu(int v) { g_pg_per_cu = v < 1 ? 1 : (v > 8 ? 8 : v); }
 static int pg_cus() {
   static int cus = 0;
@@ -456,7 +458,7 @@ static void pg_launch(const PgPlan& p, const bf16* A, int lda, const Pro& pro, c
   // persistent: at most pg_per_cu workgroups per CU, a multiple of 8 (keeps each one's XCD)
   const long vb = (long)((p.nMt + 7) / 8) * 8 * p.nNt;
   const unsigned grid = (unsigned)std::min<long>(vb, (long)pg_cus() * g_pg_per_cu / 8 * 8);
-  kern<<<grid, PG_NW * 64, p.lds, s>>>(A, lda, pro, W, ldw, epi, out, ldo, M, N, K, p.nMt, p.nNt);
+  kern<<<grid, PG_NW * 64, p.lds, s>>>(A, lda, pro, W, ldw, epi, out, ldo, M, N, K, p.nMt, p.nNt, g_pg_dbg);
 }
 
 template <int PA, bool GT, int ZA, bool STATS, bool BT, bool SW>

@@ -162,6 +162,18 @@ extern "C" int ogv_set_option(const char* name, int value) {
     set_sg_wgs(value);
     return OGV_OK;
   }
+  if (!strcmp(name, "wg_blocks")) {
+    set_wg_blocks(value);
+    return OGV_OK;
+  }
+  if (!strcmp(name, "wg_tile")) {
+    set_wg_tile(value);
+    return OGV_OK;
+  }
+  if (!strcmp(name, "pg_dbg")) {
+    set_pg_dbg(value);
+    return OGV_OK;
+  }
   if (!strcmp(name, "pg_per_cu")) {
     set_pg_per_cu(value);
     return OGV_OK;

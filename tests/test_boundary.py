@@ -152,3 +152,29 @@ def test_build_model_dispatch_matches_reference_aliases():
         build_model(dict(type="model_c", stages=stages))
     with pytest.raises(ValueError, match="at least one stage"):
         build_model(dict(type="model_b", stages=[]))
+
+
+def test_gemm_routing_table():
+    """Host-side planner (no GPU): which kernel a bf16 projection runs on (ogv_gemm_stream_route:
+    1 streaming, 2 panel, 0 LDS-tiled), on the Model-A-7M shapes and the edges of each route."""
+    import ogv._lib as L
+    lib = L.load()
+    route = lib.ogv_gemm_stream_route
+    fwd, dgrad = 0, 1
+    assert route(fwd, 524288, 48, 64, 0) == 1              # stage 0: streaming kernel
+    assert route(fwd, 524288, 48, 192, 1) == 1             # fc2 with the GELU prologue, K <= 384
+    assert route(fwd, 32768, 768, 192, 0) == 2             # stages 1-3: panel kernel
+    assert route(fwd, 8192, 256, 1024, 1) == 2
+    assert route(dgrad, 32768, 768, 192, 1) == 2
+    assert route(dgrad, 524288, 256, 1024, 0) == 2         # long-reduction dgrad at large M
+    assert route(fwd, 32768, 54, 192, 0) == 0              # N % 8 != 0: LDS-tiled kernel
+    assert route(fwd, 32768, 768, 196, 0) == 0             # K % 8 != 0
+    assert route(fwd, 32768, 768, 192, 3) == 0             # ReLU prologue: not compiled in the panel kernel
+    try:
+        assert lib.ogv_set_option(b"pgemm", 0) == 0
+        assert route(fwd, 32768, 768, 192, 0) == 0
+    finally:
+        assert lib.ogv_set_option(b"pgemm", 1) == 0
+    for name in (b"pg_rs", b"pg_tn", b"pg_per_cu", b"wg_blocks", b"wg_tile", b"sg_wgs"):
+        assert lib.ogv_set_option(name, 0) == 0, name
+    assert lib.ogv_set_option(b"pg_per_cu", 8) == 0 and lib.ogv_set_option(b"wg_blocks", 1024) == 0

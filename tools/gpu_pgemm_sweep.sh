@@ -6,6 +6,6 @@ export TMPDIR=/tmp
 O=gpurun_out/pgsweep; mkdir -p $O
 for cfg in "$@"; do
   opts=""; for o in ${cfg//,/ }; do opts="$opts --opt $o"; done
-  timeout -k 10 300 python3 tools/gemm_shapes.py tools/gemm_shapes_7m.txt --max-m 32768 --kinds fwd,dgrad $opts --reps 5 > "$O/$cfg.log" 2>&1 || { echo "$cfg rc=$?"; tail -5 "$O/$cfg.log"; exit 1; }
+  timeout -k 10 300 python3 tools/gemm_shapes.py tools/gemm_shapes_7m.txt --max-m 32768 --kinds ${KINDS:-fwd,dgrad} $opts --reps 5 > "$O/$cfg.log" 2>&1 || { echo "$cfg rc=$?"; tail -5 "$O/$cfg.log"; exit 1; }
   echo "$cfg $(tail -1 $O/$cfg.log)"
 done

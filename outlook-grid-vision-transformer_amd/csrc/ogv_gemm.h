@@ -164,6 +164,7 @@ void set_pg_rs(int v);
 void set_pg_tn(int v);
 void set_pg_per_cu(int v);
 void set_pg_dbg(int v);
+void set_pg_lds_kb(int v);
 void set_wg_blocks(int v);
 void set_wg_tile(int v);
 // Streaming weight gradient (ogv_swgrad.hip) for large-M bf16 shapes: writes [S][N*K + N] fp32

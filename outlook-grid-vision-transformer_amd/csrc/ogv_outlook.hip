@@ -430,6 +430,101 @@ __device__ __forceinline__ void otile_probs(const bf16* __restrict__ lg, int ldl
   }
 }
 
+// The backward's two staged tensors (v, dy) in one batched pass: both sources' loads of a batch
+// are issued before any LDS store (one memory round trip per batch instead of one per tensor).
+__device__ __forceinline__ void otile_stage2(const bf16* __restrict__ s1, int ld1, const bf16* __restrict__ s2, int ld2,
+                                             int col, int CB, bf16* l1, bf16* l2, const OTile& t, long tile0, int H,
+                                             int W) {
+  const int CH = CB / 8;
+  const int HW2 = t.TW + 2, HP = (t.TH + 2) * HW2;
+  const int total = t.G * HP * CH;
+  for (int base = threadIdx.x; base < total; base += OT_WB * blockDim.x) {
+    uint4 a[OT_WB], b[OT_WB];
+#pragma unroll
+    for (int u = 0; u < OT_WB; ++u) {
+      const int idx = base + u * blockDim.x;
+      a[u] = b[u] = uint4{0u, 0u, 0u, 0u};
+      if (idx < total) {
+        const int sidx = fdiv(idx, t.fCB8), c8 = idx - sidx * CH;
+        const int g = t.G > 1 ? fdiv(sidx, t.fHP) : 0, hp = sidx - g * HP;
+        const long tile = tile0 + g;
+        if (tile < t.ntiles) {
+          int bi, y0, x0;
+          otile_origin(t, tile, bi, y0, x0);
+          const int hy = fdiv(hp, t.fHW2);
+          const int yy = y0 - 1 + hy, xx = x0 - 1 + hp - hy * HW2;
+          if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
+            const long px = (long)(bi * H + yy) * W + xx;
+            a[u] = *reinterpret_cast<const uint4*>(s1 + px * ld1 + col + c8 * 8);
+            b[u] = *reinterpret_cast<const uint4*>(s2 + px * ld2 + col + c8 * 8);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < OT_WB; ++u) {
+      const int idx = base + u * blockDim.x;
+      if (idx < total) {
+        *reinterpret_cast<uint4*>(l1 + (long)idx * 8) = a[u];
+        *reinterpret_cast<uint4*>(l2 + (long)idx * 8) = b[u];
+      }
+    }
+  }
+}
+
+// Softmax item idx of otile_probs split in two: the logits loads (into registers, so they can be
+// issued ahead of the staging loads) and the softmax + LDS store.
+__device__ __forceinline__ void otile_logits_load(const bf16* __restrict__ lg, int ldl, int col, const OTile& t,
+                                                  long tile0, int H, int W, bool halo, int idx, float (&a)[9],
+                                                  int& dst, bool& ok) {
+  const int HW2 = t.TW + 2, HP = (t.TH + 2) * HW2, PT = t.TH * t.TW;
+  const int per = halo ? HP : PT;
+  ok = false;
+  dst = -1;
+  if (idx >= t.G * per * t.HB) return;
+  const int q = fdiv(idx, t.fHB), hb = idx - q * t.HB;
+  const int g = t.G > 1 ? fdiv(q, halo ? t.fHP : t.fPT) : 0, r = q - g * per;
+  int hp = r;
+  if (!halo) {
+    const int ry = fdiv(r, t.fTW);
+    hp = (ry + 1) * HW2 + (r - ry * t.TW) + 1;
+  }
+  dst = (g * HP + hp) * t.HB + hb;
+  const long tile = tile0 + g;
+  if (tile < t.ntiles) {
+    int b, y0, x0;
+    otile_origin(t, tile, b, y0, x0);
+    const int hy = fdiv(hp, t.fHW2);
+    const int yy = y0 - 1 + hy, xx = x0 - 1 + hp - hy * HW2;
+    if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
+      ok = true;
+      const bf16* l = lg + ((long)(b * H + yy) * W + xx) * ldl + col + hb * 9;
+#pragma unroll
+      for (int j = 0; j < 9; ++j) a[j] = (float)l[j];
+    }
+  }
+}
+__device__ __forceinline__ void otile_probs_store(float (&a)[9], int dst, bool ok, float* P) {
+  if (dst < 0) return;
+  if (ok) {
+    float mx = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 9; ++j) mx = fmaxf(mx, a[j]);
+    float sm = 0.f;
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      a[j] = __expf(a[j] - mx);
+      sm += a[j];
+    }
+    const float inv = 1.0f / sm;
+#pragma unroll
+    for (int j = 0; j < 9; ++j) a[j] *= inv;
+  }
+  float* d = P + (long)dst * 9;
+#pragma unroll
+  for (int j = 0; j < 9; ++j) d[j] = ok ? a[j] : 0.f;
+}
+
 template <int HD>
 __global__ __launch_bounds__(256) void outlook_fwd_tile_kernel(const bf16* __restrict__ v, int ldv,
                                                                const bf16* __restrict__ lg, int ldl,
@@ -445,8 +540,24 @@ __global__ __launch_bounds__(256) void outlook_fwd_tile_kernel(const bf16* __res
   const int HW2 = t.TW + 2, HP = (t.TH + 2) * HW2, PT = t.TH * t.TW;
   bf16* vs = reinterpret_cast<bf16*>(smem);
   float* P = reinterpret_cast<float*>(smem + (size_t)t.G * HP * CB * 2);
-  otile_stage(v, ldv, hg * CB, CB, vs, t, tile0, H, W);
-  otile_probs(lg, ldl, hg * t.HB * 9, P, t, tile0, H, W, false);
+  {  // logits of this thread's first two softmax items loaded ahead of the v staging loads
+    float la[2][9];
+    int dst[2];
+    bool lok[2];
+    otile_logits_load(lg, ldl, hg * t.HB * 9, t, tile0, H, W, false, threadIdx.x, la[0], dst[0], lok[0]);
+    otile_logits_load(lg, ldl, hg * t.HB * 9, t, tile0, H, W, false, threadIdx.x + blockDim.x, la[1], dst[1], lok[1]);
+    otile_stage(v, ldv, hg * CB, CB, vs, t, tile0, H, W);
+    otile_probs_store(la[0], dst[0], lok[0], P);
+    otile_probs_store(la[1], dst[1], lok[1], P);
+    const int np = t.G * PT * t.HB;
+    for (int idx = threadIdx.x + 2 * blockDim.x; idx < np; idx += blockDim.x) {
+      float a[9];
+      int d;
+      bool ok;
+      otile_logits_load(lg, ldl, hg * t.HB * 9, t, tile0, H, W, false, idx, a, d, ok);
+      otile_probs_store(a, d, ok, P);
+    }
+  }
   __syncthreads();
   // register blocking along x: a thread produces RX = 4 consecutive pixels of one tile row for one
   // 8-channel chunk from a 3 x (RX+2) window of staged vectors (18 LDS reads for 4 outputs
@@ -521,9 +632,26 @@ __global__ __launch_bounds__(256) void outlook_bwd_tile_kernel(const bf16* __res
   bf16* vs = reinterpret_cast<bf16*>(smem);
   bf16* gs = vs + (size_t)t.G * HP * CB;
   float* P = reinterpret_cast<float*>(gs + (size_t)t.G * HP * CB);
-  otile_stage(v, ldv, hg * CB, CB, vs, t, tile0, H, W);
-  otile_stage(dy, lddy, hg * CB, CB, gs, t, tile0, H, W);
-  otile_probs(lg, ldl, hg * t.HB * 9, P, t, tile0, H, W, true);
+  // prologue in one memory round trip (for up to 2 softmax items per thread): the logits of this
+  // thread's first two softmax items, then v and dy, are all loaded before anything is stored
+  {
+    float la[2][9];
+    int dst[2];
+    bool lok[2];
+    otile_logits_load(lg, ldl, hg * t.HB * 9, t, tile0, H, W, true, threadIdx.x, la[0], dst[0], lok[0]);
+    otile_logits_load(lg, ldl, hg * t.HB * 9, t, tile0, H, W, true, threadIdx.x + blockDim.x, la[1], dst[1], lok[1]);
+    otile_stage2(v, ldv, dy, lddy, hg * CB, CB, vs, gs, t, tile0, H, W);
+    otile_probs_store(la[0], dst[0], lok[0], P);
+    otile_probs_store(la[1], dst[1], lok[1], P);
+    const int np = t.G * HP * t.HB;
+    for (int idx = threadIdx.x + 2 * blockDim.x; idx < np; idx += blockDim.x) {
+      float a[9];
+      int d;
+      bool ok;
+      otile_logits_load(lg, ldl, hg * t.HB * 9, t, tile0, H, W, true, idx, a, d, ok);
+      otile_probs_store(a, d, ok, P);
+    }
+  }
   __syncthreads();
   // dlogits: two threads per (pixel, head), each over half of the head's channels
   const int nl = t.G * PT * t.HB * 2;

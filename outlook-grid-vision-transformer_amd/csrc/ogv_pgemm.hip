@@ -377,6 +377,8 @@ static int g_pg_tn = 0;
 // balances the tail better than the static tile walk)
 static int g_pg_per_cu = 8;
 void set_pgemm(int v) { g_pgemm = v; }
+static int g_pg_lds_kb = 80;  // knob "pg_lds_kb": LDS cap per workgroup the planner allows (80: two per CU)
+void set_pg_lds_kb(int v) { g_pg_lds_kb = v < 16 ? 16 : (v > 160 ? 160 : v); }
 static int g_pg_dbg = 0;  // knob "pg_dbg" (timing experiments only, wrong results): 1 no weight reloads, 2 no A reloads, 4 no stores
 void set_pg_dbg(int v) { g_pg_dbg = v; }
 void set_pg_per_cu(int v) { g_pg_per_cu = v < 1 ? 1 : (v > 8 ? 8 : v); }
@@ -425,7 +427,7 @@ static PgPlan pg_plan(int M, int N, int K, bool stats, bool sw, bool bt, bool pa
     if (t == 12 && (gate || stats || N <= 128)) continue;
     const int bn = 16 * t, nnt = (N + bn - 1) / bn;
     if ((long)nnt * bn - N > N / 16 && t != 4 && !g_pg_tn) continue;
-    if (pg_lds(t, bt, sw, K, pa, stats) > 80 * 1024) continue;  // two workgroups per CU
+    if (pg_lds(t, bt, sw, K, pa, stats) > (size_t)g_pg_lds_kb * 1024) continue;  // two workgroups per CU
     best_tn = t;
     break;
   }

@@ -170,6 +170,10 @@ extern "C" int ogv_set_option(const char* name, int value) {
     set_wg_tile(value);
     return OGV_OK;
   }
+  if (!strcmp(name, "pg_lds_kb")) {
+    set_pg_lds_kb(value);
+    return OGV_OK;
+  }
   if (!strcmp(name, "pg_dbg")) {
     set_pg_dbg(value);
     return OGV_OK;

@@ -76,6 +76,22 @@ int ogv_gpu_sleep(int microseconds, void* stream);
 int ogv_outlook_agg_fwd(const void* v, const void* logits, void* y, int B, int H, int W, int C,
                         int heads, int k, int ld_logits, int ld_v, ogv_dtype dt, void* stream);
 size_t ogv_outlook_bwd_ws_bytes(int B, int H, int W, int C, int heads, int k, ogv_dtype dt);
+
+/* Outlooker forward FUSED with its v / attn projections (bf16, k = 3).  Replaces
+ *   v = self.v(x); a = self.attn(x)                  src/model/outlook_attention.py:100,111
+ *   softmax + F.unfold + mul + sum                   src/model/outlook_attention.py:106-120
+ * x: [M, C] rows (row stride ldx, the LayerNorm2d output); w: fp32 [ldc, C] = [W_v; W_attn; 0]
+ * (rows C .. C+heads*9-1 are attn.weight, the rest zero), bias: fp32 [ldc] or NULL.
+ * Writes y [M, C] and, when cat != NULL, cat [M, ldc] = [v | logits | 0] rounded to bf16 (what
+ * ogv_outlook_agg_bwd reads in training).  ldc must be C + heads*9 rounded up to 8.
+ * ogv_outlook_vproj_supported() says whether a shape takes this kernel (16 | C <= 96,
+ * 8 | head_dim) for inference (train = 0) or training (train = 1) under knob "outlook_vproj"
+ * (0 never, 1 inference only -- the default, 2 both); ogv_outlook_vproj_fwd itself runs any shape
+ * the kernel supports and returns OGV_ERR_ARG for the others. */
+int ogv_outlook_vproj_supported(int B, int H, int W, int C, int heads, int k, int ldc, int train,
+                                ogv_dtype dt);
+int ogv_outlook_vproj_fwd(const void* x, int ldx, const float* w, const float* bias, void* cat, int ldc,
+                          void* y, int B, int H, int W, int C, int heads, int k, ogv_dtype dt, void* stream);
 int ogv_outlook_agg_bwd(const void* dy, const void* v, const void* logits, void* dv, void* dlogits,
                         float* probs_ws, int B, int H, int W, int C, int heads, int k, int ld_logits,
                         int ld_v, int ld_dv, int ld_dlogits, int dl_cols, ogv_dtype dt, void* stream);

@@ -191,6 +191,7 @@ void set_grid_lds(int v);
 void set_grid_big(int v);
 void set_split_w(int v);
 void set_outlook_tile(int v);
+void set_outlook_vproj(int v);
 int split_w();
 
 }  // namespace ogv

@@ -892,9 +892,358 @@ static bool use_tile(int bit, ogv_dtype dt, int k, int hd, std::initializer_list
   return true;
 }
 
+// ------------------------------------------------------------------------------------------------
+// Outlooker forward fused with its v / attn projections (north star: "unfold -> per-window softmax
+// -> weighted fold, fused with the v-projection"; reference src/model/outlook_attention.py:100-120).
+// Input: the LayerNorm2d output x [M, C] (bf16 rows) and the concatenated projection weight
+// Wc = [W_v; W_attn; 0] fp32 [ldc, C] + bias [ldc].  A workgroup owns a TH x TW pixel tile of one
+// image and its one-pixel halo:
+//   1. x of the (TH+2)(TW+2) halo pixels -> LDS (16-B coalesced loads, zeros outside the image);
+//   2. [v | logits] = x . Wc^T + b for every halo pixel on MFMA (v_mfma_f32_16x16x32_bf16, the
+//      weight as bf16 hi + lo halves like every forward GEMM of the build, staged in LDS once per
+//      persistent workgroup), rounded to bf16 in place over the x tile -- the same rounding point
+//      as the unfused GEMM's output; out-of-image halo pixels get v = 0 (zero padding);
+//   3. interior rows of [v | logits | 0] -> cat (the tensor the backward reads: written once,
+//      never read back by the forward), softmax over the 9 logits per (pixel, head) into LDS;
+//   4. y = the 3x3 gather of v weighted by the softmax, entirely from LDS.
+// So the forward reads x once and writes cat and y: the v / logits round trip through HBM of the
+// unfused path (GEMM writes cat, aggregation re-reads it with its halo) and one launch are gone.
+// The halo's projections are recomputed by the neighbouring tiles ((TH+2)(TW+2) / (TH TW) = 1.4x
+// MFMA work, which is not the bound).
+// ------------------------------------------------------------------------------------------------
+struct VTile {
+  int TH, TW, ntx, nty;
+  long ntiles;
+  int HP, HPr;         // halo pixels, rounded up to 16
+  int XP, RP, WP;      // LDS pitches (elements): x tile, result tile, weight slab
+  int ncol;            // computed output columns (16 * NJ >= C + heads * 9)
+  FDiv per_img, fntx, fHW2, fTW, fHB, fCH, fQ;
+};
+
+// waves per workgroup: 4 with two workgroups per CU (16 | C <= 64), 8 with one (C > 64: the split
+// weight slab alone is 47-53 KB); 16-B x chunks per thread and tile, prefetched into registers
+constexpr int VP_RX = 2;   // gather: consecutive output pixels per thread
+template <int NW>
+__host__ __device__ constexpr int vp_pf() { return NW == 8 ? 5 : 9; }
+
+// LDS: [x tile | interior softmax P (aliases x once the GEMM is done)] [result tile] [W hi | lo] [bias]
+// (the x tile holds HP rows: the MFMA's reads of rows HP .. HPr-1 land in the result tile and only
+// feed discarded outputs; the result tile holds HP + 2 rows: the gather window's overshoot)
+static size_t vtile_x_bytes(const VTile& t, int heads) {
+  const size_t xb = (size_t)t.HP * t.XP * 2, pb = (size_t)t.TH * t.TW * heads * 9 * 4;
+  return ((xb > pb ? xb : pb) + 15) / 16 * 16;
+}
+static size_t vtile_lds(const VTile& t, int heads, bool sw) {
+  return vtile_x_bytes(t, heads) + (size_t)(t.HP + 2) * t.RP * 2 + (size_t)(sw ? 2 : 1) * t.ncol * t.WP * 2 +
+         (size_t)t.ncol * 4;
+}
+
+template <int NJ, int NK, bool SW, int NW>
+__global__ __launch_bounds__(NW * 64, 8 / NW) void outlook_vproj_fwd_kernel(
+    const bf16* __restrict__ x, int ldx, const float* __restrict__ Wc, int wrows, const float* __restrict__ bias,
+    bf16* __restrict__ cat, int ldc, bf16* __restrict__ y, int H, int W, int C, int heads, VTile t, int xbytes) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int KP = NK * 32, NCOL = NJ * 16, NT = NW * 64, VP_PF = vp_pf<NW>();
+  const int XP = t.XP, RP = t.RP, WP = t.WP, HW2 = t.TW + 2, HP = t.HP;
+  bf16* xs = reinterpret_cast<bf16*>(smem);                          // [HP][XP]
+  float* P = reinterpret_cast<float*>(smem);                         // [TH*TW][heads][9] (after the GEMM)
+  bf16* rs = reinterpret_cast<bf16*>(smem + xbytes);                 // [HP + 2][RP]: [v | logits | 0]
+  bf16* ws = rs + (size_t)(t.HP + 2) * RP;                           // [hi | lo][NCOL][WP]
+  float* bs = reinterpret_cast<float*>(ws + (size_t)(SW ? 2 : 1) * NCOL * WP);   // [NCOL]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int hd = C / heads, CH8 = C / 8;
+
+  // weight slab (once per persistent workgroup): rows n < wrows of Wc, columns k < C, zeros elsewhere
+  for (int idx = tid; idx < NCOL * (KP / 4); idx += NT) {
+    const int n = idx / (KP / 4), k = (idx - n * (KP / 4)) * 4;
+    float4 w4 = float4{0.f, 0.f, 0.f, 0.f};
+    if (n < wrows && k < C) w4 = *reinterpret_cast<const float4*>(Wc + (long)n * C + k);
+    const bf16x4 h = {(bf16)w4.x, (bf16)w4.y, (bf16)w4.z, (bf16)w4.w};
+    *reinterpret_cast<bf16x4*>(ws + n * WP + k) = h;
+    if constexpr (SW) {
+      const bf16x4 l = {(bf16)(w4.x - (float)h[0]), (bf16)(w4.y - (float)h[1]), (bf16)(w4.z - (float)h[2]),
+                        (bf16)(w4.w - (float)h[3])};
+      *reinterpret_cast<bf16x4*>(ws + (NCOL + n) * WP + k) = l;
+    }
+  }
+  for (int n = tid; n < NCOL; n += NT) bs[n] = (bias && n < wrows) ? bias[n] : 0.f;
+
+  const int G = gridDim.x;
+  const int vid = (blockIdx.x & 7) * (G / 8) + (blockIdx.x >> 3);   // XCD-contiguous logical id
+  const int NI = t.HPr / 16, PT = t.TH * t.TW;
+  constexpr int KC = KP / 8;
+  const int total = HP * KC;   // 16-B chunks of the x halo tile (<= VP_PF * NT, checked by the plan)
+  // x halo tile of `tile` -> registers (zeros outside the image and in columns [C, KP)): issued one
+  // tile ahead, so the next tile's loads are in flight during this tile's MFMA / softmax / gather
+  uint4 pf[VP_PF];
+  auto load_x = [&](long tile) {
+    const int b = fdiv((int)tile, t.per_img);
+    const int r0 = (int)tile - b * t.per_img.d;
+    const int ty0 = fdiv(r0, t.fntx);
+    const int y0 = ty0 * t.TH, x0 = (r0 - ty0 * t.ntx) * t.TW;
+#pragma unroll
+    for (int u = 0; u < VP_PF; ++u) {
+      const int idx = tid + u * NT;
+      pf[u] = uint4{0u, 0u, 0u, 0u};
+      if (idx < total) {
+        const int hp = idx / KC, c8 = idx - hp * KC;
+        const int hy = fdiv(hp, t.fHW2);
+        const int yy = y0 - 1 + hy, xx = x0 - 1 + hp - hy * HW2;
+        if (c8 < CH8 && yy >= 0 && yy < H && xx >= 0 && xx < W)
+          pf[u] = *reinterpret_cast<const uint4*>(x + ((long)(b * H + yy) * W + xx) * ldx + c8 * 8);
+      }
+    }
+  };
+  if (vid < t.ntiles) load_x(vid);
+  for (long tile = vid; tile < t.ntiles; tile += G) {
+    const int b = fdiv((int)tile, t.per_img);
+    const int r0 = (int)tile - b * t.per_img.d;
+    const int ty0 = fdiv(r0, t.fntx);
+    const int y0 = ty0 * t.TH, x0 = (r0 - ty0 * t.ntx) * t.TW;
+    __syncthreads();   // the previous tile's readers of P / the result tile are done (weights staged)
+    // 1. x halo tile (registers) -> xs
+#pragma unroll
+    for (int u = 0; u < VP_PF; ++u) {
+      const int idx = tid + u * NT;
+      if (idx < total) {
+        const int hp = idx / KC, c8 = idx - hp * KC;
+        *reinterpret_cast<uint4*>(xs + hp * XP + c8 * 8) = pf[u];
+      }
+    }
+    __syncthreads();
+    if (tile + G < t.ntiles) load_x(tile + G);
+    // 2. D[n][m] = Wc[n] . x[m] (+ bias) on MFMA, fragment by fragment into the result tile;
+    // out-of-image halo pixels -> 0 (the reference's zero padding of v)
+    // each wave owns row blocks i = wave, wave + NW, ...: its x fragments stay in registers while
+    // the NJ column blocks run as independent MFMA chains (j unrolled at compile time)
+    for (int i = wave; i < NI; i += NW) {
+      bf16x8 xf[NK];
+#pragma unroll
+      for (int kt = 0; kt < NK; ++kt) xf[kt] = *reinterpret_cast<const bf16x8*>(xs + (i * 16 + fr) * XP + kt * 32 + fg * 8);
+      f32x4 acc[NJ];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kt = 0; kt < NK; ++kt) {
+          const bf16x8 wh = *reinterpret_cast<const bf16x8*>(ws + (j * 16 + fr) * WP + kt * 32 + fg * 8);
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, xf[kt], acc[j], 0, 0, 0);
+          if constexpr (SW) {
+            const bf16x8 wl = *reinterpret_cast<const bf16x8*>(ws + (NCOL + j * 16 + fr) * WP + kt * 32 + fg * 8);
+            acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl, xf[kt], acc[j], 0, 0, 0);
+          }
+        }
+      }
+      const int m = i * 16 + fr;   // lane: row m, columns 16 j + 4 fg .. + 3
+      if (m < HP) {
+        const int hy = fdiv(m, t.fHW2);
+        const int yy = y0 - 1 + hy, xx = x0 - 1 + m - hy * HW2;
+        const bool inb = yy >= 0 && yy < H && xx >= 0 && xx < W;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int n = j * 16 + 4 * fg;
+          const float4 b4 = *reinterpret_cast<const float4*>(bs + n);
+          bf16x4 o;
+          o[0] = (bf16)(inb ? acc[j][0] + b4.x : 0.f);
+          o[1] = (bf16)(inb ? acc[j][1] + b4.y : 0.f);
+          o[2] = (bf16)(inb ? acc[j][2] + b4.z : 0.f);
+          o[3] = (bf16)(inb ? acc[j][3] + b4.w : 0.f);
+          *reinterpret_cast<bf16x4*>(rs + m * RP + n) = o;
+        }
+      }
+    }
+    __syncthreads();   // the result tile is complete; xs is free (P aliases it)
+    // 3a. interior rows of [v | logits | 0] -> cat (the backward's input)
+    if (cat) {
+      const int LC = ldc / 8;
+      for (int idx = tid; idx < PT * LC; idx += NT) {
+        const int pt = idx / LC, c8 = idx - pt * LC;
+        const int ty = fdiv(pt, t.fTW), tx = pt - ty * t.TW;
+        if (y0 + ty >= H || x0 + tx >= W) continue;
+        const int s = (ty + 1) * HW2 + tx + 1;
+        *reinterpret_cast<uint4*>(cat + ((long)(b * H + y0 + ty) * W + x0 + tx) * ldc + c8 * 8) =
+            *reinterpret_cast<const uint4*>(rs + s * RP + c8 * 8);
+      }
+    }
+    // 3b. softmax of the interior pixels' logits (bf16-rounded, as the unfused path reads them)
+    for (int idx = tid; idx < PT * heads; idx += NT) {
+      const int pt = fdiv(idx, t.fHB), hb = idx - pt * heads;
+      const int ty = fdiv(pt, t.fTW), tx = pt - ty * t.TW;
+      const bf16* l = rs + ((ty + 1) * HW2 + tx + 1) * RP + C + hb * 9;
+      float a[9], mx = -INFINITY;
+#pragma unroll
+      for (int jj = 0; jj < 9; ++jj) {
+        a[jj] = (float)l[jj];
+        mx = fmaxf(mx, a[jj]);
+      }
+      float sm = 0.f;
+#pragma unroll
+      for (int jj = 0; jj < 9; ++jj) {
+        a[jj] = __expf(a[jj] - mx);
+        sm += a[jj];
+      }
+      const float inv = 1.0f / sm;
+      float* d = P + (long)idx * 9;   // idx = pt * heads + hb
+#pragma unroll
+      for (int jj = 0; jj < 9; ++jj) d[jj] = a[jj] * inv;
+    }
+    __syncthreads();
+    // 4. gather: VP_RX consecutive pixels of one tile row per thread and 8-channel chunk, from a
+    // 3 x (VP_RX + 2) window of result-tile vectors
+    const int TWq = (t.TW + VP_RX - 1) / VP_RX;
+    const int items = t.TH * TWq * CH8;
+    for (int idx = tid; idx < items; idx += NT) {
+      const int q = fdiv(idx, t.fCH), cc = idx - q * CH8;
+      const int ty = fdiv(q, t.fQ), xq = q - ty * TWq;
+      if (y0 + ty >= H) continue;
+      const int hb = (cc * 8) / hd;
+      const int tx0 = xq * VP_RX;
+      const int s0 = (ty + 1) * HW2 + tx0 + 1;
+      float accy[VP_RX][8];
+      float pw[VP_RX][9];
+#pragma unroll
+      for (int r = 0; r < VP_RX; ++r) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) accy[r][i] = 0.f;
+        const bool ok = tx0 + r < t.TW;
+        const float* pp = P + ((long)(ty * t.TW + (ok ? tx0 + r : 0)) * heads + hb) * 9;
+#pragma unroll
+        for (int jj = 0; jj < 9; ++jj) pw[r][jj] = ok ? pp[jj] : 0.f;
+      }
+#pragma unroll
+      for (int ki = 0; ki < 3; ++ki)
+#pragma unroll
+        for (int c = 0; c < VP_RX + 2; ++c) {
+          const uint4 raw = *reinterpret_cast<const uint4*>(rs + (s0 + (ki - 1) * HW2 + c - 1) * RP + cc * 8);
+          const bf16* e = reinterpret_cast<const bf16*>(&raw);
+          float fv[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) fv[i] = (float)e[i];
+#pragma unroll
+          for (int r = 0; r < VP_RX; ++r) {
+            const int kj = c - r;
+            if (kj < 0 || kj > 2) continue;
+            const float w = pw[r][ki * 3 + kj];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) accy[r][i] = fmaf(w, fv[i], accy[r][i]);
+          }
+        }
+#pragma unroll
+      for (int r = 0; r < VP_RX; ++r)
+        if (tx0 + r < t.TW && x0 + tx0 + r < W)
+          store_vec<bf16, 8>(y + ((long)(b * H + y0 + ty) * W + x0 + tx0 + r) * C + cc * 8, accy[r]);
+    }
+  }
+}
+
+// knob "outlook_vproj": 0 = never, 1 = for inference (no cat written; default), 2 = also in training.
+// Measured (tools/bench_vproj.py, cold L2, bs = 512 / 256 / 128): inference 7M stage 0 82 vs 91 us
+// unfused, 14M stage 0 195 vs 201 us, 7M stage 1 / 22M stage 0 within 1-3 %; training (the cat
+// write) 4-14 % slower than the unfused GEMM + aggregation, so training keeps the unfused pair.
+static int g_outlook_vproj = 1;
+void set_outlook_vproj(int v) { g_outlook_vproj = v < 0 ? 0 : (v > 2 ? 2 : v); }
+
+// shapes the fused kernel takes: bf16, k = 3, 16 | C <= 96, 8 | head_dim, ldc = C + 9 heads rounded
+// up to 8, 16-B aligned rows, and an LDS footprint within one CU's 160 KB
+static inline int NK_W(int KP) { return KP > 64 ? 8 : 4; }   // waves per workgroup for a padded K
+
+static bool vproj_plan(int B, int H, int W, int C, int heads, int k, int ldc, ogv_dtype dt, VTile& t) {
+  if (!g_outlook_vproj || dt != OGV_BF16 || k != 3 || B <= 0 || H <= 0 || W <= 0 || heads <= 0) return false;
+  if (C % 16 != 0 || C > 96 || C % heads != 0 || (C / heads) % 8 != 0) return false;
+  const int NL = heads * 9;
+  if (ldc != (C + NL + 7) / 8 * 8) return false;
+  const int KP = (C + 31) / 32 * 32;
+  // 8 x 16 tiles when two workgroups fit one CU's LDS, else 8 x 8, else 8 x 16 at one per CU
+  bool ok = false;
+  for (int pass = 0; pass < 3 && !ok; ++pass) {
+    t = VTile{};
+    t.TH = H < 8 ? H : 8;
+    const int tw = pass == 1 ? 8 : 16;
+    t.TW = W < tw ? W : tw;
+    t.ntx = (W + t.TW - 1) / t.TW;
+    t.nty = (H + t.TH - 1) / t.TH;
+    t.ntiles = (long)B * t.nty * t.ntx;
+    t.HP = (t.TH + 2) * (t.TW + 2);
+    t.HPr = (t.HP + 15) / 16 * 16;
+    t.ncol = (C + NL + 15) / 16 * 16;
+    t.XP = KP + 8;
+    t.RP = t.ncol;
+    t.WP = KP + 8;
+    const size_t lds = vtile_lds(t, heads, true);
+    ok = pass == 2 ? lds <= 160 * 1024 : lds <= 80 * 1024;
+  }
+  if (!ok || t.ntiles >= (1L << 22)) return false;
+  if (t.ncol > 128 || t.HP * (KP / 8) > (NK_W(KP) == 8 ? vp_pf<8>() * 512 : vp_pf<4>() * 256)) return false;
+  t.per_img = fdiv_make(t.nty * t.ntx);
+  t.fntx = fdiv_make(t.ntx);
+  t.fHW2 = fdiv_make(t.TW + 2);
+  t.fTW = fdiv_make(t.TW);
+  t.fHB = fdiv_make(heads);
+  t.fCH = fdiv_make(C / 8);
+  t.fQ = fdiv_make((t.TW + VP_RX - 1) / VP_RX);
+  return true;
+}
+
+template <int NJ, int NK>
+static void vproj_run(const bf16* x, int ldx, const float* Wc, int wrows, const float* bias, bf16* cat, int ldc, bf16* y,
+                      int H, int W, int C, int heads, const VTile& t, bool sw, hipStream_t s) {
+  const size_t lds = vtile_lds(t, heads, sw);
+  const long per_cu = NK == 3 ? 1 : std::min<long>(2, std::max<long>(1, (long)(160 * 1024 / lds)));
+  const long nb = std::min<long>(t.ntiles, 256 * per_cu);
+  const unsigned grid = (unsigned)((nb + 7) / 8 * 8);
+  constexpr int NW = NK == 3 ? 8 : 4;
+  auto kern = sw ? outlook_vproj_fwd_kernel<NJ, NK, true, NW> : outlook_vproj_fwd_kernel<NJ, NK, false, NW>;
+  static bool attr[2] = {false, false};
+  if (!attr[sw]) {   // dynamic LDS above the default grant
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    attr[sw] = true;
+  }
+  kern<<<grid, NW * 64, lds, s>>>(x, ldx, Wc, wrows, bias, cat, ldc, y, H, W, C, heads, t,
+                                    (int)vtile_x_bytes(t, heads));
+}
+
 }  // namespace ogv
 
 using namespace ogv;
+
+extern "C" int ogv_outlook_vproj_supported(int B, int H, int W, int C, int heads, int k, int ldc, int train,
+                                           ogv_dtype dt) {
+  VTile t;
+  if (g_outlook_vproj < (train ? 2 : 1)) return 0;
+  return vproj_plan(B, H, W, C, heads, k, ldc, dt, t) ? 1 : 0;
+}
+
+extern "C" int ogv_outlook_vproj_fwd(const void* x, int ldx, const float* w, const float* bias, void* cat, int ldc,
+                                     void* y, int B, int H, int W, int C, int heads, int k, ogv_dtype dt,
+                                     void* stream) {
+  OGV_REQUIRE(x && w && y, "ogv_outlook_vproj_fwd: null pointer");
+  int rc = check_args(B, H, W, C, heads, k, heads * k * k, C, dt, "ogv_outlook_vproj_fwd");
+  if (rc) return rc;
+  VTile t;
+  OGV_REQUIRE(vproj_plan(B, H, W, C, heads, k, ldc, dt, t),
+              "ogv_outlook_vproj_fwd: unsupported shape (needs bf16, k=3, 16 | C <= 96, 8 | head_dim, "
+              "ldc = C + 9*heads rounded up to 8; see ogv_outlook_vproj_supported)");
+  OGV_REQUIRE(ldx >= C && ldx % 8 == 0 && al16p(x) && al16p(y) && (!cat || al16p(cat)) && al16p(w),
+              "ogv_outlook_vproj_fwd: rows must be 16-B aligned (ldx %d)", ldx);
+  const int NJ = t.ncol / 16, NK = (C + 31) / 32;
+  const bool sw = (split_w() & 1) != 0;
+  hipStream_t s = as_stream(stream);
+  const bf16* xb = (const bf16*)x;
+  bf16 *cb = (bf16*)cat, *yb = (bf16*)y;
+#define OGV_VPROJ(nj, nk)                                                                     \
+  if (NJ == nj && NK == nk) {                                                                 \
+    vproj_run<nj, nk>(xb, ldx, w, ldc, bias, cb, ldc, yb, H, W, C, heads, t, sw, s);          \
+    return check_launch("ogv_outlook_vproj_fwd");                                             \
+  }
+  OGV_VPROJ(2, 1) OGV_VPROJ(3, 1) OGV_VPROJ(4, 1) OGV_VPROJ(5, 1) OGV_VPROJ(6, 1) OGV_VPROJ(7, 1) OGV_VPROJ(8, 1)
+  OGV_VPROJ(2, 2) OGV_VPROJ(3, 2) OGV_VPROJ(4, 2) OGV_VPROJ(5, 2) OGV_VPROJ(6, 2) OGV_VPROJ(7, 2) OGV_VPROJ(8, 2)
+  OGV_VPROJ(2, 3) OGV_VPROJ(3, 3) OGV_VPROJ(4, 3) OGV_VPROJ(5, 3) OGV_VPROJ(6, 3) OGV_VPROJ(7, 3) OGV_VPROJ(8, 3)
+#undef OGV_VPROJ
+  OGV_REQUIRE(false, "ogv_outlook_vproj_fwd: no instantiation for %d column / %d k blocks", NJ, NK);
+  return OGV_ERR_ARG;
+}
 
 extern "C" int ogv_outlook_agg_fwd(const void* v, const void* logits, void* y, int B, int H, int W, int C, int heads,
                                    int k, int ldl, int ldv, ogv_dtype dt, void* stream) {

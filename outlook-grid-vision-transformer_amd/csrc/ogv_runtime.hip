@@ -150,6 +150,10 @@ extern "C" int ogv_set_option(const char* name, int value) {
     set_outlook_tile(value);
     return OGV_OK;
   }
+  if (!strcmp(name, "outlook_vproj")) {
+    set_outlook_vproj(value);
+    return OGV_OK;
+  }
   if (!strcmp(name, "split_w")) {
     set_split_w(value);
     return OGV_OK;

@@ -102,6 +102,8 @@ def probe_bytes(name: str, u: dict) -> int:
     e = u["elem"]
     if name == "outlook_fwd":   # read v [M,C] + logits [M,k*k*h], write y [M,C]
         return e * u["M"] * (2 * u["C"] + u["k"] * u["k"] * u["heads"])
+    if name == "outlook_vproj":  # read x [M,C] + fp32 W [ld,C] (+ bias), write y [M,C] (+ cat [M,ld] in training)
+        return e * u["M"] * (2 * u["C"] + (u["ld"] if u["cat"] else 0)) + 4 * u["ld"] * (u["C"] + 1)
     if name == "grid_fwd":      # read qkv [M,3C], write out [M,C] + fp32 lse [M,h]
         return e * u["M"] * 4 * u["C"] + 4 * u["M"] * u["heads"]
     if name == "outlook_bwd":   # read dy, v, logits; write dv, dlogits
@@ -123,6 +125,8 @@ def probe_flops(name: str, u: dict) -> int:
         return 18 * u["M"] * u["C"] + 45 * u["M"] * u["heads"]
     if name == "outlook_bwd":
         return 36 * u["M"] * u["C"]
+    if name == "outlook_vproj":   # the projection GEMM + the aggregation
+        return 2 * u["M"] * u["ld"] * u["C"] + 18 * u["M"] * u["C"] + 45 * u["M"] * u["heads"]
     if name == "grid_fwd":
         return 4 * u["M"] * u["N"] * u["C"]
     return 2 * u["M"] * u["N"] * u["K"]
@@ -271,45 +275,53 @@ class _Linear(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
-        lib = _lib.load()
         x2d, w2d, rs = ctx.saved_tensors
         M, N, K, rps, act, has_bias, has_res = ctx.meta
         dout = dout.to(x2d.dtype).contiguous()
-        dt = _dt(x2d)
-        dx = dw = db = dres = None
         want_dx = ctx.needs_input_grad[0]
         want_dw = ctx.needs_input_grad[1] or (has_bias and ctx.needs_input_grad[2])
-        if want_dx:
-            dx = torch.empty((M, K), dtype=x2d.dtype, device=x2d.device)
-            ws_d = _ws(lib.ogv_gemm_dgrad_ws_bytes(N, K), x2d.device)
-        if want_dw:
-            dw = torch.empty((N, K), dtype=torch.float32, device=x2d.device)
-            db = torch.empty((N,), dtype=torch.float32, device=x2d.device) if has_bias else None
-            ws_w = _ws(lib.ogv_gemm_wgrad_ws_bytes(M, N, K), x2d.device)
-        # dgrad and wgrad are independent: the weight gradient runs on a side stream (forked from and
-        # joined back into the current one, also inside a captured graph) so the two latency-bound
-        # GEMMs overlap.
-        # (below ~_FORK_MIN_WORK the fork/join latency (~10 us per cross-stream edge) outweighs the overlap)
-        # (while a probe is armed everything stays on the current stream, where its events are)
-        fork = want_dx and want_dw and M * (N + K) >= _FORK_MIN_WORK and not _PROBE["armed"]
-        with _fork(fork, dout, x2d, rs, dw, db, ws_w if want_dw else None) as side:
-            if want_dw:
-                with _probe("wgrad", dict(M=M, N=N, K=K, elem=x2d.element_size(), bias=has_bias),
-                            when=x2d.dtype == torch.bfloat16):
-                    check(lib.ogv_gemm_wgrad(_ptr(dout), N, _ptr(x2d), x2d.stride(0), _ptr(rs), rps, _ptr(dw), _ptr(db),
-                                             M, N, K, act, _ptr(ws_w), dt, side), "ogv_gemm_wgrad")
-            if want_dx:
-                route = lib.ogv_gemm_stream_route(1, M, N, K, act) if _PROBE["armed"] else -1
-                du = dict(kind="dgrad", M=M, N=N, K=K, elem=x2d.element_size(), z=bool(act))
-                bf = x2d.dtype == torch.bfloat16
-                with _probe("sgemm", du, when=bf and route == 1), _probe("gemm_panel", du, when=bf and route == 2), \
-                        _probe("gemm_tiled", du, when=bf and route == 0):
-                    check(lib.ogv_gemm_dgrad(_ptr(dout), N, _ptr(w2d), _ptr(x2d) if act else None, x2d.stride(0),
-                                             _ptr(rs), rps, _ptr(dx), K, M, N, K, act, _ptr(ws_d), dt, _stream()),
-                          "ogv_gemm_dgrad")
-        if has_res and ctx.needs_input_grad[3]:
-            dres = dout
+        dx, dw, db = _linear_bwd(dout, x2d, w2d, rs, rps, act, has_bias, want_dx, want_dw)
+        dres = dout if has_res and ctx.needs_input_grad[3] else None
         return dx, dw, db, dres, None, None, None
+
+
+def _linear_bwd(dout, x2d, w2d, rs, rps, act, has_bias, want_dx, want_dw):
+    """(dx, dW, dbias) of out = rs * (act(x) @ W^T + b) from dout; the weight gradient forks onto the
+    side stream when both are wanted."""
+    lib = _lib.load()
+    M, K = x2d.shape
+    N = w2d.shape[0]
+    dt = _dt(x2d)
+    dx = dw = db = None
+    if want_dx:
+        dx = torch.empty((M, K), dtype=x2d.dtype, device=x2d.device)
+        ws_d = _ws(lib.ogv_gemm_dgrad_ws_bytes(N, K), x2d.device)
+    if want_dw:
+        dw = torch.empty((N, K), dtype=torch.float32, device=x2d.device)
+        db = torch.empty((N,), dtype=torch.float32, device=x2d.device) if has_bias else None
+        ws_w = _ws(lib.ogv_gemm_wgrad_ws_bytes(M, N, K), x2d.device)
+    # dgrad and wgrad are independent: the weight gradient runs on a side stream (forked from and
+    # joined back into the current one, also inside a captured graph) so the two latency-bound
+    # GEMMs overlap.
+    # (below ~_FORK_MIN_WORK the fork/join latency (~10 us per cross-stream edge) outweighs the overlap)
+    # (while a probe is armed everything stays on the current stream, where its events are)
+    fork = want_dx and want_dw and M * (N + K) >= _FORK_MIN_WORK and not _PROBE["armed"]
+    with _fork(fork, dout, x2d, rs, dw, db, ws_w if want_dw else None) as side:
+        if want_dw:
+            with _probe("wgrad", dict(M=M, N=N, K=K, elem=x2d.element_size(), bias=has_bias),
+                        when=x2d.dtype == torch.bfloat16):
+                check(lib.ogv_gemm_wgrad(_ptr(dout), N, _ptr(x2d), x2d.stride(0), _ptr(rs), rps, _ptr(dw), _ptr(db),
+                                         M, N, K, act, _ptr(ws_w), dt, side), "ogv_gemm_wgrad")
+        if want_dx:
+            route = lib.ogv_gemm_stream_route(1, M, N, K, act) if _PROBE["armed"] else -1
+            du = dict(kind="dgrad", M=M, N=N, K=K, elem=x2d.element_size(), z=bool(act))
+            bf = x2d.dtype == torch.bfloat16
+            with _probe("sgemm", du, when=bf and route == 1), _probe("gemm_panel", du, when=bf and route == 2), \
+                    _probe("gemm_tiled", du, when=bf and route == 0):
+                check(lib.ogv_gemm_dgrad(_ptr(dout), N, _ptr(w2d), _ptr(x2d) if act else None, x2d.stride(0),
+                                         _ptr(rs), rps, _ptr(dx), K, M, N, K, act, _ptr(ws_d), dt, _stream()),
+                      "ogv_gemm_dgrad")
+    return dx, dw, db
 
 
 def linear_rows(x2d, weight, bias=None, residual=None, row_scale=None, rps=1, act_in=None):
@@ -479,6 +491,60 @@ class _OutlookAggCat(torch.autograd.Function):
         _outlook_bwd(dy, cat.data_ptr(), ld, cat.data_ptr() + C * es, ld, dcat.data_ptr(), ld, dcat.data_ptr() + C * es,
                      ld, ld - C, B, H, W, C, heads, k)
         return dcat, None, None, None, None, None, None
+
+
+class _OutlookVProj(torch.autograd.Function):
+    """Outlooker forward fused with its v / attn 1x1 projections (ogv_outlook_vproj_fwd): x [M, C]
+    -> y [M, C], writing cat = [v | logits | 0] [M, ld] only when a gradient is wanted.  Backward:
+    the LDS-tiled aggregation backward on cat -> dcat, then ONE dgrad + ONE wgrad of the
+    concatenated weight (as _OutlookAggCat + _Linear)."""
+
+    @staticmethod
+    def forward(ctx, x2d, w, b, C, B, H, W, heads, k, train):
+        lib = _lib.load()
+        M = x2d.shape[0]
+        ld = w.shape[0]
+        y = torch.empty((M, C), dtype=x2d.dtype, device=x2d.device)
+        cat = torch.empty((M, ld), dtype=x2d.dtype, device=x2d.device) if train else None
+        with _probe("outlook_vproj", dict(M=M, C=C, ld=ld, heads=heads, k=k, cat=train, elem=x2d.element_size())):
+            check(lib.ogv_outlook_vproj_fwd(_ptr(x2d), x2d.stride(0), _ptr(w), _ptr(b), _ptr(cat), ld, _ptr(y), B, H, W,
+                                            C, heads, k, _dt(x2d), _stream()), "ogv_outlook_vproj_fwd")
+        ctx.save_for_backward(x2d, w, cat)
+        ctx.meta = (B, H, W, C, heads, k, b is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2d, w, cat = ctx.saved_tensors
+        B, H, W, C, heads, k, has_bias = ctx.meta
+        M, ld = cat.shape
+        es = cat.element_size()
+        dy = dy.to(cat.dtype).contiguous()
+        dcat = torch.empty_like(cat)
+        _outlook_bwd(dy, cat.data_ptr(), ld, cat.data_ptr() + C * es, ld, dcat.data_ptr(), ld, dcat.data_ptr() + C * es,
+                     ld, ld - C, B, H, W, C, heads, k)
+        want_dw = ctx.needs_input_grad[1] or (has_bias and ctx.needs_input_grad[2])
+        dx, dw, db = _linear_bwd(dcat, x2d, w, None, 1, 0, has_bias, ctx.needs_input_grad[0], want_dw)
+        return dx, dw, db, None, None, None, None, None, None, None
+
+
+def outlook_vproj_supported(B, H, W, C, heads, k, ld, dtype, train) -> bool:
+    """Whether OutlookAttention2d takes the fused projection + aggregation forward for this shape
+    (knob "outlook_vproj": 0 never, 1 inference only (default), 2 also in training)."""
+    if dtype != torch.bfloat16:
+        return False
+    return bool(_lib.load().ogv_outlook_vproj_supported(B, H, W, C, heads, k, ld, int(bool(train)), OGV_BF16))
+
+
+def outlook_vproj(x2d, w, b, C, B, H, W, heads, k):
+    """y [M, C] = outlook aggregation of (x2d @ [Wv; Wattn; 0]^T + b) without materialising the
+    projection for the forward (x2d bf16 rows, w fp32 [ld, C], b fp32 [ld] or None)."""
+    require_device(x2d, w, b, what="ogv.outlook_vproj")
+    x2d = _rows_contig(x2d)
+    # the [v | logits] tensor is written for the backward only when a gradient will be wanted
+    train = torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in (x2d, w, b))
+    return _OutlookVProj.apply(x2d, w.contiguous(), None if b is None else b.contiguous(), int(C), int(B), int(H),
+                               int(W), int(heads), int(k), train)
 
 
 def outlook_aggregate_rows(v2d, logits2d, B, H, W, heads, k):

@@ -11,7 +11,10 @@ Drop-in for src/model/outlook_attention.py of the reference:
                                         input run as ONE GEMM over [Wv; Wattn; 0] (v and the logits
                                         are column ranges of its output, read in place by the
                                         LDS-tiled gather; the backward is one gradient buffer,
-                                        one dgrad and one wgrad)
+                                        one dgrad and one wgrad).  For inference (no gradient)
+                                        the projections, softmax and gather run as ONE kernel
+                                        (ogv_outlook_vproj_fwd: the v / logits tile lives in LDS;
+                                        knob outlook_vproj=2 uses it in training too)
 Parameters and their names/shapes are unchanged (attn.weight [heads*k*k, C, 1, 1], v.*, proj.*).
 Tensors are NCHW logically and channels_last physically.
 """
@@ -140,8 +143,14 @@ class OutlookAttention2d(nn.Module):
         else:
             dt = OF.compute_dtype(x)
             w, b = self._cat_params()
-            cat = OF.linear_rows(OF.nchw_to_rows(x.to(dt)), w, b)     # [M, v | logits | 0]
-            y = OF.outlook_aggregate_cat(cat, C, B, H, W, self.num_heads, self.kernel_size)
+            xr = OF.nchw_to_rows(x.to(dt))
+            train = torch.is_grad_enabled() and (x.requires_grad or w.requires_grad)
+            if OF.outlook_vproj_supported(B, H, W, C, self.num_heads, self.kernel_size, w.shape[0], dt, train):
+                # projections + softmax + gather in one kernel (the v / logits tile lives in LDS)
+                y = OF.outlook_vproj(xr, w, b, C, B, H, W, self.num_heads, self.kernel_size)
+            else:
+                cat = OF.linear_rows(xr, w, b)     # [M, v | logits | 0]
+                y = OF.outlook_aggregate_cat(cat, C, B, H, W, self.num_heads, self.kernel_size)
         y = OF.rows_to_nchw(y, B, H, W)
         if self.training and self.proj_drop.p > 0:
             y = self.proj_drop(self.proj(y))

@@ -330,6 +330,94 @@ def test_outlook_tile_matches_thread_kernels(case):
         assert fx.maxabs(a, b) <= 1e-2 * max(1.0, b.abs().max().item())
 
 
+VPROJ_CASES = [  # B, C, heads, H, W: 7M stage 0 / 1, 14M / 22M stage 0 (C = 64), partial tiles, 1x1 and
+    # 1-row images, head_dim 8 (NL = 36), K not a multiple of 32 (C = 16 / 48 / 80)
+    (2, 48, 2, 32, 32), (2, 96, 3, 16, 16), (1, 64, 2, 56, 56), (2, 16, 2, 5, 7), (1, 32, 4, 9, 33),
+    (3, 48, 2, 1, 1), (2, 80, 2, 1, 19), (2, 64, 2, 8, 8),
+]
+
+
+@pytest.mark.parametrize("case", VPROJ_CASES)
+def test_outlook_vproj_vs_oracle(case):
+    """Outlooker forward fused with the v / attn projections (ogv_outlook_vproj_fwd, bf16) vs the
+    oracle on the same bf16-valued x and fp32 weights: y, the saved [v | logits | 0] tensor, and the
+    gradients of x, W and b through the fused op's backward, within 1e-2 * max(1, |ref|)."""
+    from ogv import functional as OF
+    B, C, h, H, W = case
+    nl = 9 * h
+    ld = (C + nl + 7) // 8 * 8
+    assert OF.outlook_vproj_supported(B, H, W, C, h, 3, ld, torch.bfloat16, False), case
+    g = torch.Generator().manual_seed(C * 131 + H * 7 + W)
+    x = torch.randn(B * H * W, C, generator=g).to(torch.bfloat16).float()
+    w = torch.zeros(ld, C)
+    w[:C + nl] = torch.randn(C + nl, C, generator=g) / C ** 0.5
+    w[C:C + nl] *= 3.0        # logits of O(2): a non-trivial softmax
+    b = torch.zeros(ld)
+    b[:C + nl] = 0.1 * torch.randn(C + nl, generator=g)
+    dy = torch.randn(B * H * W, C, generator=g).to(torch.bfloat16).float()
+    # reference: fp64 projection -> oracle aggregation (fp64), autograd for every gradient
+    xr, wr, br = (t.double().clone().requires_grad_() for t in (x, w, b))
+    catr = xr @ wr.t() + br
+    to_nchw = lambda t, c: t.reshape(B, H, W, c).permute(0, 3, 1, 2)
+    yr = orc.outlook_aggregate(to_nchw(catr[:, :C], C), to_nchw(catr[:, C:C + nl], nl), h, 3)
+    yr = yr.permute(0, 2, 3, 1).reshape(-1, C)
+    yr.backward(dy.double())
+    xd = x.to(DEV, torch.bfloat16).requires_grad_()
+    wd, bd = w.to(DEV).requires_grad_(), b.to(DEV).requires_grad_()
+    y = OF.outlook_vproj(xd, wd, bd, C, B, H, W, h, 3)
+    y.backward(dy.to(DEV, torch.bfloat16))
+    tol = lambda r: 1e-2 * max(1.0, r.abs().max().item())
+    assert fx.maxabs(y.float(), yr.detach()) <= tol(yr), "y"
+    assert fx.maxabs(xd.grad.float(), xr.grad) <= tol(xr.grad), "dx"
+    assert fx.maxabs(wd.grad, wr.grad) <= tol(wr.grad) * 3, "dW"      # bf16 dcat summed over M rows
+    assert fx.maxabs(bd.grad, br.grad) <= tol(br.grad) * 3, "db"
+    with torch.no_grad():       # inference: no cat written, same y
+        y2 = OF.outlook_vproj(xd.detach(), wd.detach(), bd.detach(), C, B, H, W, h, 3)
+    assert torch.equal(y2, y.detach())
+
+
+@pytest.mark.parametrize("case", [(2, 48, 2, 32, 32), (2, 96, 3, 16, 16), (1, 64, 2, 56, 56)])
+def test_outlook_vproj_matches_unfused(case):
+    """OutlookAttention2d with the fused forward in training (knob outlook_vproj=2) vs the unfused
+    GEMM + aggregation (0): y, dx and every parameter gradient within bf16 rounding; and the
+    default (1: fused for inference only) in eval / no_grad vs the unfused forward."""
+    from ogv._lib import load
+    from src.model.outlook_attention import OutlookAttention2d
+    lib = load()
+    B, C, h, H, W = case
+    torch.manual_seed(3)
+    m = OutlookAttention2d(C, h).to(DEV)
+    x = torch.randn(B, C, H, W, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    dy = torch.randn(B, C, H, W, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    outs = []
+    try:
+        for knob in (2, 0):
+            assert lib.ogv_set_option(b"outlook_vproj", knob) == 0
+            m.zero_grad()
+            xx = x.clone().requires_grad_()
+            y = m(xx)
+            y.backward(dy)
+            outs.append([y.float(), xx.grad.float()] + [p.grad.clone() for p in m.parameters()])
+        inf = []
+        for knob in (1, 0):
+            assert lib.ogv_set_option(b"outlook_vproj", knob) == 0
+            with torch.no_grad():
+                inf.append(m.eval()(x).float())
+    finally:
+        assert lib.ogv_set_option(b"outlook_vproj", 1) == 0
+    for a, b in zip(*outs):
+        assert fx.maxabs(a, b) <= 1e-2 * max(1.0, b.abs().max().item())
+    assert fx.maxabs(inf[0], inf[1]) <= 1e-2 * max(1.0, inf[1].abs().max().item())
+    # the default no_grad forward IS the fused kernel: bit-identical to a direct call
+    from ogv import functional as OF
+    with torch.no_grad():
+        w, b = m._cat_params()
+        yd = OF.outlook_vproj(OF.nchw_to_rows(x), w, b, C, B, H, W, h, 3)
+        yd = m.proj(OF.rows_to_nchw(yd, B, H, W))
+    assert torch.equal(yd.float(), inf[0])
+    assert fx.maxabs(inf[0], outs[0][0]) <= 1e-2 * max(1.0, inf[1].abs().max().item())
+
+
 GRID_CASES = [  # B, H, W, C, heads, g
     (2, 32, 32, 48, 2, 8), (2, 16, 16, 96, 3, 8), (2, 8, 8, 192, 6, 4), (2, 4, 4, 256, 8, 2),
     (1, 8, 12, 16, 4, 2), (2, 6, 6, 24, 2, 3), (1, 4, 4, 32, 2, 1), (1, 4, 4, 32, 2, 4),

@@ -1,0 +1,70 @@
+"""Outlooker forward: the fused projection + aggregation kernel (ogv_outlook_vproj_fwd) vs the
+unfused pair (concatenated [Wv; Wattn; 0] GEMM -> cat, then the aggregation reading cat), per
+Model-A stage shape, cold L2 (512 MB flush before each rep), HIP events, median of --reps.
+Algorithmic bytes: fused 2*M*(2C + ld) (+ the fp32 weight), i.e. read x, write y and cat;
+the unfused pair moves 2*M*(C + ld) + 2*M*(2C + 9h) (+ the cat halo re-reads).
+    python tools/bench_vproj.py [--reps 20]"""
+import argparse
+import pathlib
+import sys
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "outlook-grid-vision-transformer_amd"))
+import torch  # noqa: E402
+
+import ogv  # noqa: E402
+from ogv import functional as OF  # noqa: E402
+from ogv._lib import ACT, OGV_BF16, load  # noqa: E402
+
+SHAPES = [("7m_s0", 512, 48, 2, 32), ("7m_s1", 512, 96, 3, 16), ("14m_s0", 256, 64, 2, 64),
+          ("22m_s0", 128, 64, 2, 224)]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=20)
+    a = ap.parse_args()
+    ogv.load()
+    lib = load()
+    s = lambda: OF._stream()  # noqa: E731
+    flush = torch.empty(512 << 20, dtype=torch.uint8, device="cuda")
+    for name, B, C, h, S in SHAPES:
+        M = B * S * S
+        ld = (C + 9 * h + 7) // 8 * 8
+        x = torch.randn(M, C, device="cuda").to(torch.bfloat16)
+        w = torch.randn(ld, C, device="cuda") / C ** 0.5
+        w[C + 9 * h:] = 0
+        b = torch.zeros(ld, device="cuda")
+        cat = torch.empty(M, ld, device="cuda", dtype=torch.bfloat16)
+        y = torch.empty(M, C, device="cuda", dtype=torch.bfloat16)
+        p = OF._ptr
+        runs = {
+            "unfused": lambda: (OF.check(lib.ogv_gemm_fwd(p(x), C, p(w), p(b), None, None, 1, p(cat), ld, M, ld, C,
+                                                          ACT[None], OGV_BF16, s()), "gemm"),
+                                OF.check(lib.ogv_outlook_agg_fwd(p(cat), OF._vp(cat.data_ptr() + 2 * C), p(y), B, S,
+                                                                 S, C, h, 3, ld, ld, OGV_BF16, s()), "agg")),
+            "fused_train": lambda: OF.check(lib.ogv_outlook_vproj_fwd(p(x), C, p(w), p(b), p(cat), ld, p(y), B, S, S, C,
+                                                                      h, 3, OGV_BF16, s()), "vproj"),
+            "fused_eval": lambda: OF.check(lib.ogv_outlook_vproj_fwd(p(x), C, p(w), p(b), None, ld, p(y), B, S, S, C, h,
+                                                                     3, OGV_BF16, s()), "vproj"),
+        }
+        nbytes = {"unfused": 2 * M * (C + ld) + 2 * M * (2 * C + 9 * h), "fused_train": 2 * M * (2 * C + ld),
+                  "fused_eval": 2 * M * 2 * C}
+        row = [f"{name:7s} M={M:8d}"]
+        for kind, fn in runs.items():
+            ts = []
+            for _ in range(a.reps):
+                flush.zero_()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                fn()
+                e1.record()
+                ts.append((e0, e1))
+            torch.cuda.synchronize()
+            ms = sorted(u.elapsed_time(v) for u, v in ts)[len(ts) // 2]
+            row.append(f"{kind} {ms * 1e3:8.1f}us {nbytes[kind] / ms / 1e6:6.0f}GB/s")
+        print("  ".join(row), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1234,8 +1234,15 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (long)M * N) return;
   const int m = (int)(i / N), n = (int)(i - (long)m * N);
-  float v = 0.f;
-  for (int s = 0; s < S; ++s) v += part[(long)s * M * N + i];
+  const long MN = (long)M * N;
+  float a[4] = {0.f, 0.f, 0.f, 0.f};   // four slices' loads in flight per trip
+  int s = 0;
+  for (; s + 3 < S; s += 4) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) a[u] += part[(long)(s + u) * MN + i];
+  }
+  for (; s < S; ++s) a[0] += part[(long)s * MN + i];
+  float v = (a[0] + a[1]) + (a[2] + a[3]);
   if (epi.bias) v += epi.bias[n];
   if (epi.rs) v *= epi.rs[m / epi.rps];
   if (epi.res) v += static_cast<const float*>(epi.res)[(long)m * ldo + n];

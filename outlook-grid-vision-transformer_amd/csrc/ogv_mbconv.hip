@@ -93,11 +93,23 @@ __global__ __launch_bounds__(256) void bn_reduce_finalize_kernel(const double* _
   const int cl = threadIdx.x & 15, rg = threadIdx.x >> 4;
   const int c = blockIdx.x * 16 + cl;
   double s1 = 0.0, s2 = 0.0;
-  if (c < K)
-    for (long r = rg; r < R; r += 16) {
-      s1 += part[r * ld + c];
-      s2 += part[r * ld + K + c];
+  if (c < K) {   // four row groups' loads in flight per trip (the loop is latency-bound otherwise)
+    double a1[4] = {0.0, 0.0, 0.0, 0.0}, a2[4] = {0.0, 0.0, 0.0, 0.0};
+    long r = rg;
+    for (; r + 48 < R; r += 64) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a1[u] += part[(r + 16 * u) * ld + c];
+        a2[u] += part[(r + 16 * u) * ld + K + c];
+      }
     }
+    for (; r < R; r += 16) {
+      a1[0] += part[r * ld + c];
+      a2[0] += part[r * ld + K + c];
+    }
+    s1 = (a1[0] + a1[1]) + (a1[2] + a1[3]);
+    s2 = (a2[0] + a2[1]) + (a2[2] + a2[3]);
+  }
   red[0][rg][cl] = s1;
   red[1][rg][cl] = s2;
   __syncthreads();
@@ -131,11 +143,23 @@ __global__ __launch_bounds__(256) void bn_reduce_coeffs_kernel(const float* __re
   const int cl = threadIdx.x & 15, rg = threadIdx.x >> 4;
   const int c = blockIdx.x * 16 + cl;
   float s1 = 0.f, s2 = 0.f;
-  if (c < K)
-    for (long r = rg; r < R; r += 16) {
-      s1 += part[r * ld + c];
-      s2 += part[r * ld + K + c];
+  if (c < K) {   // four row groups' loads in flight per trip
+    float a1[4] = {0.f, 0.f, 0.f, 0.f}, a2[4] = {0.f, 0.f, 0.f, 0.f};
+    long r = rg;
+    for (; r + 48 < R; r += 64) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a1[u] += part[(r + 16 * u) * ld + c];
+        a2[u] += part[(r + 16 * u) * ld + K + c];
+      }
     }
+    for (; r < R; r += 16) {
+      a1[0] += part[r * ld + c];
+      a2[0] += part[r * ld + K + c];
+    }
+    s1 = (a1[0] + a1[1]) + (a1[2] + a1[3]);
+    s2 = (a2[0] + a2[1]) + (a2[2] + a2[3]);
+  }
   red[0][rg][cl] = s1;
   red[1][rg][cl] = s2;
   __syncthreads();

@@ -118,16 +118,25 @@ class OutlookAttention2d(nn.Module):
         C, n = self.dim, self.attn.out_channels
         ld = (C + n + 7) // 8 * 8
         wv, wa = self.v.weight.reshape(C, C), self.attn.weight.reshape(n, C)
-        parts = [wv.float(), wa.float()]
-        if ld > C + n:
-            parts.append(wv.new_zeros(ld - C - n, C, dtype=torch.float32))
+        zw, zb = self._zero_pads(wv.device, ld - C - n)
+        parts = [wv.float(), wa.float()] + ([zw] if ld > C + n else [])
         w = torch.cat(parts)
         if self.v.bias is None and self.attn.bias is None:
             return w, None
         bv = self.v.bias if self.v.bias is not None else wv.new_zeros(C)
         ba = self.attn.bias if self.attn.bias is not None else wa.new_zeros(n)
-        bparts = [bv.float(), ba.float()] + ([bv.new_zeros(ld - C - n, dtype=torch.float32)] if ld > C + n else [])
+        bparts = [bv.float(), ba.float()] + ([zb] if ld > C + n else [])
         return w, torch.cat(bparts)
+
+    def _zero_pads(self, device, rows):
+        """Zero rows of the concatenated weight / bias, allocated once per device (not parameters or
+        buffers: the state_dict is unchanged) -- no fill launches per forward."""
+        pads = self.__dict__.setdefault("_pads", {})
+        z = pads.get(device)
+        if z is None or z[0].shape[0] != rows:
+            z = pads[device] = (torch.zeros(max(rows, 0), self.dim, device=device),
+                                torch.zeros(max(rows, 0), device=device))
+        return z
 
     def forward(self, x: torch.Tensor, residual=None, row_scale=None) -> torch.Tensor:
         if self.stride != 1:

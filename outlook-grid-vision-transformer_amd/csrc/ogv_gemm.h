@@ -159,6 +159,8 @@ int pgemm_fwd_try(const void* A, int lda, const Pro& pro, const float* W, int ld
 bool pgemm_dgrad_try(const void* dout, int ldd, const float* W, void* dA, int lda, int M, int Nf, int Kf,
                      const Epi& epi, hipStream_t s);
 bool pgemm_route(int kind, int M, int N, int K, int act);
+int pgemm_conv_try(const void* A, const ConvG& cv, const float* Wt, void* out, int M, int N, const Epi& epi,
+                   hipStream_t s);
 void set_pgemm(int v);
 void set_pg_rs(int v);
 void set_pg_tn(int v);

@@ -47,11 +47,14 @@ __device__ __forceinline__ int pg_perm(int k) { return (k & ~12) | ((k & 4) << 1
 // Persistent: workgroup b walks the virtual tiles vb = b, b + G, b + 2G, ... (G = gridDim.x, a
 // multiple of 8, so vb keeps b's XCD) and the (tile, k-step) pairs form ONE pipeline: the loads of
 // the next tile's first k-steps are in flight while the current tile's epilogue runs.
-template <int RS, int TN, int PA, bool GT, int ZA, bool STATS, bool BT, bool SW>
+// CV: implicit-GEMM 3x3 convolution (stem / downsample convs, their data gradients as transposed
+// convs): row m = output pixel, column k = tap * Cs + channel (tap-major weight), A fragments
+// gathered from the NHWC source (cv, conv_src; zero outside the image); lda unused.
+template <int RS, int TN, int PA, bool GT, int ZA, bool STATS, bool BT, bool SW, bool CV = false>
 __global__ __launch_bounds__(PG_NW * 64, 2) void pgemm_bf16_kernel(const bf16* __restrict__ A, int lda, Pro pro,
                                                                 const float* __restrict__ W, int ldw, Epi epi,
                                                                 bf16* __restrict__ out, int ldo, int M, int N, int K,
-                                                                int nMt, int nNt, int dbg) {
+                                                                int nMt, int nNt, int dbg, ConvG cv) {
   constexpr int BN = TN * 16;
   constexpr int BM = PG_NW * 16 * RS;
   constexpr int SLAB = pg_slab_elems<TN, BT>();
@@ -131,12 +134,27 @@ __global__ __launch_bounds__(PG_NW * 64, 2) void pgemm_bf16_kernel(const bf16* _
 #pragma unroll
     for (int i = 0; i < RS; ++i) {
       const int m = mw + i * 16 + fr;
+      if constexpr (CV) {
+        const ConvRow cr = conv_row(cv, m < M ? m : 0);
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
-        const int k = k0 + kt * 32 + fg * 8;
-        bf16x8 v = {};
-        if (m < M && k < K) v = *reinterpret_cast<const bf16x8*>(A + (long)m * lda + k);
-        a[i][kt] = v;
+        for (int kt = 0; kt < 2; ++kt) {
+          const int k = k0 + kt * 32 + fg * 8;
+          bf16x8 v = {};
+          if (m < M && k < K) {
+            const int tap = k / cv.Cs;            // 8 | Cs: the 8 columns share one tap
+            const long off = conv_src(cv, cr, tap);
+            if (off >= 0) v = *reinterpret_cast<const bf16x8*>(A + off + (k - tap * cv.Cs));
+          }
+          a[i][kt] = v;
+        }
+      } else {
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) {
+          const int k = k0 + kt * 32 + fg * 8;
+          bf16x8 v = {};
+          if (m < M && k < K) v = *reinterpret_cast<const bf16x8*>(A + (long)m * lda + k);
+          a[i][kt] = v;
+        }
       }
     }
   };
@@ -447,10 +465,10 @@ static PgPlan pg_plan(int M, int N, int K, bool stats, bool sw, bool bt, bool pa
   return p;
 }
 
-template <int RS, int TN, int PA, bool GT, int ZA, bool STATS, bool BT, bool SW>
+template <int RS, int TN, int PA, bool GT, int ZA, bool STATS, bool BT, bool SW, bool CV>
 static void pg_launch(const PgPlan& p, const bf16* A, int lda, const Pro& pro, const float* W, int ldw,
-                      const Epi& epi, bf16* out, int ldo, int M, int N, int K, hipStream_t s) {
-  auto kern = pgemm_bf16_kernel<RS, TN, PA, GT, ZA, STATS, BT, SW>;
+                      const Epi& epi, bf16* out, int ldo, int M, int N, int K, const ConvG& cv, hipStream_t s) {
+  auto kern = pgemm_bf16_kernel<RS, TN, PA, GT, ZA, STATS, BT, SW, CV>;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -460,13 +478,14 @@ static void pg_launch(const PgPlan& p, const bf16* A, int lda, const Pro& pro, c
   // persistent: at most pg_per_cu workgroups per CU, a multiple of 8 (keeps each one's XCD)
   const long vb = (long)((p.nMt + 7) / 8) * 8 * p.nNt;
   const unsigned grid = (unsigned)std::min<long>(vb, (long)pg_cus() * g_pg_per_cu / 8 * 8);
-  kern<<<grid, PG_NW * 64, p.lds, s>>>(A, lda, pro, W, ldw, epi, out, ldo, M, N, K, p.nMt, p.nNt, g_pg_dbg);
+  kern<<<grid, PG_NW * 64, p.lds, s>>>(A, lda, pro, W, ldw, epi, out, ldo, M, N, K, p.nMt, p.nNt, g_pg_dbg, cv);
 }
 
-template <int PA, bool GT, int ZA, bool STATS, bool BT, bool SW>
+template <int PA, bool GT, int ZA, bool STATS, bool BT, bool SW, bool CV = false>
 static void pg_tiles(const PgPlan& p, const bf16* A, int lda, const Pro& pro, const float* W, int ldw,
-                     const Epi& epi, bf16* out, int ldo, int M, int N, int K, hipStream_t s) {
-#define OGV_PG(RS_, TN_) pg_launch<RS_, TN_, PA, GT, ZA, STATS, BT, SW>(p, A, lda, pro, W, ldw, epi, out, ldo, M, N, K, s)
+                     const Epi& epi, bf16* out, int ldo, int M, int N, int K, hipStream_t s,
+                     const ConvG& cv = ConvG()) {
+#define OGV_PG(RS_, TN_) pg_launch<RS_, TN_, PA, GT, ZA, STATS, BT, SW, CV>(p, A, lda, pro, W, ldw, epi, out, ldo, M, N, K, cv, s)
   if (p.RS == 2) {
     if (p.TN == 8) OGV_PG(2, 8);
     else OGV_PG(2, 4);
@@ -539,6 +558,31 @@ bool pgemm_dgrad_try(const void* dout, int ldd, const float* W, void* dA, int ld
   else OGV_PGD(0);
 #undef OGV_PGD
   return true;
+}
+
+// Implicit-GEMM 3x3 conv (ogv_convbn forward): out[M, N] = epi(gather(A; cv)[M, 9 Cs] . Wt[N, 9 Cs]^T).
+// Returns the BatchNorm partial rows written (>= 1) when handled, 0 otherwise (caller falls back).
+int pgemm_conv_try(const void* A, const ConvG& cv, const float* Wt, void* out, int M, int N, const Epi& epi,
+                   hipStream_t s) {
+  const int K = 9 * cv.Cs;
+  // forward convs only: measured (7M step, rocprofv3) downsample fwd + BN stats 113 -> 67 us, but the
+  // stride-2 transposed convs of the data gradient (3 of 4 taps empty per output) 144 -> 225 us
+  if (!g_pgemm || cv.transposed || (cv.Cs & 7) || !al16p(A) || !al16p(out) || !al16p(Wt) || epi.zact || epi.res)
+    return 0;
+  const bool st = epi.stat != nullptr;
+  const bool sw = (split_w() & (cv.transposed ? 2 : 1)) != 0;
+  const PgPlan p = pg_plan(M, N, K, st, sw, false, false, false);
+  if (!p.ok) return 0;
+  const bf16* a = static_cast<const bf16*>(A);
+  bf16* o = static_cast<bf16*>(out);
+  if (st) {
+    if (sw) pg_tiles<-1, false, 0, true, false, true, true>(p, a, 0, Pro(), Wt, K, epi, o, N, M, N, K, s, cv);
+    else pg_tiles<-1, false, 0, true, false, false, true>(p, a, 0, Pro(), Wt, K, epi, o, N, M, N, K, s, cv);
+  } else {
+    if (sw) pg_tiles<-1, false, 0, false, false, true, true>(p, a, 0, Pro(), Wt, K, epi, o, N, M, N, K, s, cv);
+    else pg_tiles<-1, false, 0, false, false, false, true>(p, a, 0, Pro(), Wt, K, epi, o, N, M, N, K, s, cv);
+  }
+  return st ? p.nMt : 1;
 }
 
 bool pgemm_route(int kind, int M, int N, int K, int act) {

@@ -194,6 +194,7 @@ void set_grid_big(int v);
 void set_split_w(int v);
 void set_outlook_tile(int v);
 void set_outlook_vproj(int v);
+void set_pg_split(int v);
 int split_w();
 
 }  // namespace ogv

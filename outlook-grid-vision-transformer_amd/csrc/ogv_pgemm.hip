@@ -40,6 +40,16 @@ __host__ __device__ constexpr int pg_slab_elems() {
 // consecutive rows (conflict-free with a pitch of 8 mod 64 dwords)
 __device__ __forceinline__ int pg_perm(int k) { return (k & ~12) | ((k & 4) << 1) | ((k & 8) >> 1); }
 
+// forward slab row of tile column c (see store_w) and its inverse
+__device__ __forceinline__ int pg_col_slot(int c) {
+  const int cc = c & 31;
+  return (c & ~31) | (((cc >> 2) & 1) << 4) | ((cc >> 3) << 2) | (cc & 3);
+}
+__device__ __forceinline__ int pg_slot_col(int r) {
+  const int rr = r & 31;
+  return (r & ~31) | (((rr >> 2) & 3) << 3) | (((rr >> 4) & 1) << 2) | (rr & 3);
+}
+
 // RS: 16-row fragments per wave (rows per tile = 64 * RS); TN: 16-column fragments per tile
 // (BN = 16 * TN).  PA: -1 = no prologue, else its activation (sc / sh optional, staged in LDS);
 // GT: the prologue has an SE gate.  ZA: activation derivative at Z in the epilogue.
@@ -111,7 +121,10 @@ __global__ __launch_bounds__(PG_NW * 64, 2) void pgemm_bf16_kernel(const bf16* _
       const int idx = tid + i * 256;
       int off;
       if constexpr (!BT) {
-        const int r = idx / (PG_KB / 4), kq = idx % (PG_KB / 4);
+        // weight row (tile column) c -> slab row pg_col_slot(c): fragment pair (2q, 2q+1) holds
+        // columns 32q + 8g + 4h + r' at fragment 2q+h, row 4g + r', so a lane's accumulators of the
+        // pair are 8 CONSECUTIVE output columns (16-B epilogue loads / stores)
+        const int r = pg_col_slot(idx / (PG_KB / 4)), kq = idx % (PG_KB / 4);
         off = r * PG_KP + (((kq >> 1) + r) & 7) * 8 + (kq & 1) * 4;
       } else {
         const int kr = idx / (BN / 4);
@@ -253,6 +266,72 @@ __global__ __launch_bounds__(PG_NW * 64, 2) void pgemm_bf16_kernel(const bf16* _
   auto epilogue = [&](int j) {
     const int mt = tile_mt(j), n0 = tile_nt(j) * BN, mw = mt * BM + wave * 16 * RS;
     const float* cv = cvec + (j & 1) * 2 * BN;
+    if constexpr (!BT) {
+      // lane: row m, columns 32 q + 8 fg .. + 7 of every fragment pair q (pg_col_slot)
+#pragma unroll
+      for (int i = 0; i < RS; ++i) {
+        const int m = mw + i * 16 + fr;
+        const bool mok = m < M;
+        const float rsc = (epi.rs && mok) ? epi.rs[m / epi.rps] : 1.f;
+        uint4 rv[TN / 2];
+#pragma unroll
+        for (int q = 0; q < TN / 2; ++q) {   // residual of the row first: one round trip
+          const int n = n0 + 32 * q + 8 * fg;
+          rv[q] = uint4{0u, 0u, 0u, 0u};
+          if (res && mok && n < N) rv[q] = *reinterpret_cast<const uint4*>(res + (long)m * ldo + n);
+        }
+#pragma unroll
+        for (int q = 0; q < TN / 2; ++q) {
+          const int c = 32 * q + 8 * fg, n = n0 + c;
+          const bool ok = mok && n < N;
+          const float4 b0 = *reinterpret_cast<const float4*>(cv + c);
+          const float4 b1 = *reinterpret_cast<const float4*>(cv + c + 4);
+          const float bias[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+          const bf16* rb = reinterpret_cast<const bf16*>(&rv[q]);
+          uint4 ov;
+          bf16* ob = reinterpret_cast<bf16*>(&ov);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) ob[e] = (bf16)((acc[i][2 * q + (e >> 2)][e & 3] + bias[e]) * rsc + (float)rb[e]);
+          if (ok && !(dbg & 4)) *reinterpret_cast<uint4*>(out + (long)m * ldo + n) = ov;
+          if constexpr (STATS) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {   // fragment 2q + h: the same wave-private 16 x 16 pass as below
+              const int jj = 2 * q + h;
+              bf16* st = stg + wave * 256;
+              *reinterpret_cast<uint2*>(st + fr * 16 + 4 * fg) = reinterpret_cast<const uint2*>(&ov)[h];
+              __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+              __builtin_amdgcn_wave_barrier();
+              __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+              const int cc = pg_slot_col(jj * 16 + fr), nc = n0 + cc;   // this lane's column
+              const double sh = (double)cv[BN + cc];
+              double t1 = 0.0, t2 = 0.0;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const int row = 4 * fg + e;
+                if (mw + i * 16 + row < M && nc < N) {
+                  const double d = (double)(float)st[row * 16 + fr] - sh;
+                  t1 += d;
+                  t2 = fma(d, d, t2);
+                }
+              }
+              t1 += __shfl_xor(t1, 16, 64);
+              t2 += __shfl_xor(t2, 16, 64);
+              t1 += __shfl_xor(t1, 32, 64);
+              t2 += __shfl_xor(t2, 32, 64);
+              if (fg == 0) {
+                double* r1 = red + (wave * 2 + 0) * BN + cc;
+                double* r2 = red + (wave * 2 + 1) * BN + cc;
+                *r1 = i == 0 ? t1 : *r1 + t1;
+                *r2 = i == 0 ? t2 : *r2 + t2;
+              }
+              __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+              __builtin_amdgcn_wave_barrier();
+              __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+          }
+        }
+      }
+    } else {
 #pragma unroll
     for (int i = 0; i < RS; ++i) {
       const int m = mw + i * 16 + fr;
@@ -326,6 +405,7 @@ __global__ __launch_bounds__(PG_NW * 64, 2) void pgemm_bf16_kernel(const bf16* _
         }
       }
     }
+    }   // BT
 #pragma unroll
     for (int i = 0; i < RS; ++i)
 #pragma unroll
@@ -388,6 +468,10 @@ __global__ __launch_bounds__(PG_NW * 64, 2) void pgemm_bf16_kernel(const bf16* _
 // plan + dispatch
 // ------------------------------------------------------------------------------------------------
 static int g_pgemm = 1;   // knob "pgemm": route small-M bf16 fwd / dgrad here (0 = tiled kernel)
+// knob "pg_split" (bit mask, default 3 = follow split_w): bit 1 lets the panel kernel's forward
+// launches use the split (hi + lo) weights, bit 2 its implicit-conv launches
+static int g_pg_split = 3;
+void set_pg_split(int v) { g_pg_split = v & 3; }
 static int g_pg_rs = 0;   // knobs "pg_rs" / "pg_tn": force the tile (0 = planner)
 static int g_pg_tn = 0;
 // knob "pg_per_cu": workgroups per CU the grid is capped at (measured: 8, i.e. one tile per workgroup
@@ -509,7 +593,7 @@ int pgemm_fwd_try(const void* A, int lda, const Pro& pro, const float* W, int ld
   if (pa && pro.act != OGV_ACT_GELU && pro.act != OGV_ACT_SILU) return 0;
   if (pro.gate && ((pro.gld & 3) || !al16p(pro.gate))) return 0;
   const bool st = epi.stat != nullptr;
-  const bool sw = (split_w() & 1) != 0;
+  const bool sw = (split_w() & 1) != 0 && (g_pg_split & 1);
   const PgPlan p = pg_plan(M, N, K, st, sw, false, pa, pro.gate != nullptr);
   if (!p.ok) return 0;
   const bf16* a = static_cast<const bf16*>(A);
@@ -570,7 +654,7 @@ int pgemm_conv_try(const void* A, const ConvG& cv, const float* Wt, void* out, i
   if (!g_pgemm || cv.transposed || (cv.Cs & 7) || !al16p(A) || !al16p(out) || !al16p(Wt) || epi.zact || epi.res)
     return 0;
   const bool st = epi.stat != nullptr;
-  const bool sw = (split_w() & (cv.transposed ? 2 : 1)) != 0;
+  const bool sw = (split_w() & (cv.transposed ? 2 : 1)) != 0 && (g_pg_split & 2);
   const PgPlan p = pg_plan(M, N, K, st, sw, false, false, false);
   if (!p.ok) return 0;
   const bf16* a = static_cast<const bf16*>(A);
@@ -588,7 +672,7 @@ int pgemm_conv_try(const void* A, const ConvG& cv, const float* Wt, void* out, i
 bool pgemm_route(int kind, int M, int N, int K, int act) {
   if (kind == 0) {
     if (act != OGV_ACT_NONE && act != OGV_ACT_GELU && act != OGV_ACT_SILU) return false;
-    return pg_plan(M, N, K, false, (split_w() & 1) != 0, false, act != OGV_ACT_NONE, false).ok;
+    return pg_plan(M, N, K, false, (split_w() & 1) != 0 && (g_pg_split & 1), false, act != OGV_ACT_NONE, false).ok;
   }
   return pg_plan(M, K, N, false, (split_w() & 2) != 0, true, false, false).ok;  // dgrad: output K
 }

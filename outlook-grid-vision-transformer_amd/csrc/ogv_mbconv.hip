@@ -1410,10 +1410,13 @@ static void mbconv_bwd_impl(const void* dout, const void* x, const Saved& sv, vo
   OGV_V_DISPATCH(rp.V, O::template se_reduce, w.bufA, sv.d, sv.sc2, sv.sh2, sv.mean2, sv.inv2, s.act, w.R, s.B, HW,
                  s.mid, rp, st, sv.gate, w.dz2);
   // B4) SE MLP backward (fp32, B rows): dgate = R0 -> dz2 -> (W2, b2) -> dz1 (act') -> (W1, b1) -> dpooled
+  // (the two weight gradients go to the side stream, behind the project weight gradient, as soon
+  // as their inputs exist; joined before B6, ahead of the next use of w.gemm in B8)
   {
     Pro p2;
     p2.act = s.act;
-    gemm_wgrad_launch(OGV_F32, w.dz2, s.mid, sv.z1, s.se, p2, nullptr, 1, G.se_w2, G.se_b2, s.B, s.mid, s.se, w.gemm, st);
+    gemm_wgrad_launch(OGV_F32, w.dz2, s.mid, sv.z1, s.se, p2, nullptr, 1, G.se_w2, G.se_b2, s.B, s.mid, s.se, w.gemm,
+                      fork_side(st));
     {  // dz1 = act'(z1) * (dz2 . W2):  W2 [mid, se] read reduction-major (no transpose launch)
       Epi e;
       e.Z = sv.z1;
@@ -1422,7 +1425,7 @@ static void mbconv_bwd_impl(const void* dout, const void* x, const Saved& sv, vo
       gemm_fwd_splitk_f32(w.dz2, s.mid, Pro(), P.se_w2, s.se, w.dz1, s.se, s.B, s.se, s.mid, e, w.split, st, true);
     }
     gemm_wgrad_launch(OGV_F32, w.dz1, s.se, sv.pooled, s.mid, Pro(), nullptr, 1, G.se_w1, G.se_b1, s.B, s.se, s.mid,
-                      w.gemm, st);
+                      w.gemm, fork_side(st));
     {  // dpool = dz1 . W1:  W1 [se, mid] read reduction-major
       gemm_fwd_splitk_f32(w.dz1, s.se, Pro(), P.se_w1, s.mid, w.dpool, s.mid, s.B, s.mid, s.se, Epi(), w.split, st,
                           true);

@@ -178,3 +178,35 @@ def test_gemm_routing_table():
     for name in (b"pg_rs", b"pg_tn", b"pg_per_cu", b"wg_blocks", b"wg_tile", b"sg_wgs"):
         assert lib.ogv_set_option(name, 0) == 0, name
     assert lib.ogv_set_option(b"pg_per_cu", 8) == 0 and lib.ogv_set_option(b"wg_blocks", 1024) == 0
+
+
+def test_outlook_vproj_plan_and_knob():
+    """Which shapes the fused Outlooker forward takes (host-side plan, no GPU): bf16, k = 3,
+    16 | C <= 96, 8 | head_dim, ld = C + 9 heads rounded up to 8; knob outlook_vproj: 0 never,
+    1 inference only (default), 2 also in training; unsupported calls fail before any launch."""
+    import ogv._lib as L
+    lib = L.load()
+    ld = lambda C, h: (C + 9 * h + 7) // 8 * 8  # noqa: E731
+    sup = lambda B, H, W, C, h, train, dt=L.OGV_BF16, k=3, l=None: lib.ogv_outlook_vproj_supported(  # noqa: E731
+        B, H, W, C, h, k, ld(C, h) if l is None else l, int(train), dt)
+    try:
+        assert sup(512, 32, 32, 48, 2, False) == 1          # 7M stage 0
+        assert sup(512, 16, 16, 96, 3, False) == 1          # 7M stage 1
+        assert sup(128, 224, 224, 64, 2, False) == 1        # 22M stage 0
+        assert sup(512, 8, 8, 192, 6, False) == 0           # C > 96: unfused GEMM + aggregation
+        assert sup(2, 8, 8, 48, 2, False, dt=L.OGV_F32) == 0
+        assert sup(2, 8, 8, 48, 2, False, k=5) == 0
+        assert sup(2, 8, 8, 40, 5, False) == 0              # head_dim 8 but 16 does not divide C
+        assert sup(2, 8, 8, 48, 2, False, l=72 + 8) == 0    # wrong row stride of cat
+        assert sup(512, 32, 32, 48, 2, True) == 0           # default: training keeps the unfused pair
+        assert lib.ogv_set_option(b"outlook_vproj", 2) == 0
+        assert sup(512, 32, 32, 48, 2, True) == 1
+        assert lib.ogv_set_option(b"outlook_vproj", 0) == 0
+        assert sup(512, 32, 32, 48, 2, False) == 0
+    finally:
+        assert lib.ogv_set_option(b"outlook_vproj", 1) == 0
+    x = ctypes.c_void_p(16)
+    rc = lib.ogv_outlook_vproj_fwd(x, 192, x, None, None, 200, x, 2, 8, 8, 192, 6, 3, L.OGV_BF16, None)
+    assert rc != 0 and b"unsupported" in lib.ogv_last_error()
+    rc = lib.ogv_outlook_vproj_fwd(None, 48, x, None, None, 72, x, 2, 8, 8, 48, 2, 3, L.OGV_BF16, None)
+    assert rc != 0 and b"null" in lib.ogv_last_error()

@@ -81,6 +81,11 @@ struct ConvG {
   int Hr = 0, Wr = 0;          // row grid
   int Hs = 0, Ws = 0, Cs = 0;  // source grid / channels
   int stride = 1, transposed = 0;
+  // parity class of a stride-2 transposed conv (panel kernel only; -1 = off): rows are the output
+  // pixels (2Y + (par >> 1), 2X + (par & 1)) and the reduction runs over the ntap taps that can hit
+  // them (tap[0..ntap), tap-major columns k = t * Cs + c)
+  int par = -1, ntap = 9;
+  int tap[4] = {0, 0, 0, 0};
 };
 struct ConvRow {
   int b, ry, rx;
@@ -161,6 +166,7 @@ bool pgemm_dgrad_try(const void* dout, int ldd, const float* W, void* dA, int ld
 bool pgemm_route(int kind, int M, int N, int K, int act);
 int pgemm_conv_try(const void* A, const ConvG& cv, const float* Wt, void* out, int M, int N, const Epi& epi,
                    hipStream_t s);
+bool pgemm_tconv_try(const void* A, const ConvG& cv, const float* Wt, void* out, int M, int N, hipStream_t s);
 void set_pgemm(int v);
 void set_pg_rs(int v);
 void set_pg_tn(int v);

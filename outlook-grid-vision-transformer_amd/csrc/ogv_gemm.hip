@@ -1193,6 +1193,9 @@ void conv_gemm_launch(ogv_dtype dt, const void* A, const ConvG& cv, const float*
   // the pipelined panel kernel with implicit-conv A fragments (8 | Cs), BN partial rows per 128-row
   // panel exactly like the tiled kernel's (gemm_stat_rows)
   if (dt == OGV_BF16 && pgemm_conv_try(A, cv, Wt, out, M, N, epi, s)) return;
+  if (dt == OGV_BF16 && !epi.stat && !epi.res && !epi.zact && !epi.bias && !epi.rs &&
+      pgemm_tconv_try(A, cv, Wt, out, M, N, s))
+    return;
   if (dt == OGV_BF16) {
     if (st) launch_conv_mm<bf16, true>(A, cv, Wt, out, M, N, K, epi, s);
     else launch_conv_mm<bf16, false>(A, cv, Wt, out, M, N, K, epi, s);

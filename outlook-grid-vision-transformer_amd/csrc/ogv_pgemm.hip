@@ -107,7 +107,14 @@ __global__ __launch_bounds__(PG_NW * 64, 2) void pgemm_bf16_kernel(const bf16* _
       wr[i] = float4{0.f, 0.f, 0.f, 0.f};
       if constexpr (!BT) {
         const int r = idx / (PG_KB / 4), k = k0 + (idx % (PG_KB / 4)) * 4;
-        if (n0 + r < N && k < K) wr[i] = *reinterpret_cast<const float4*>(W + (long)(n0 + r) * ldw + k);
+        int kc = k;
+        if constexpr (CV) {
+          if (cv.par >= 0) {   // the class's tap t -> the weight's full tap-major column block
+            const int t = k / cv.Cs;
+            kc = cv.tap[t < 4 ? t : 3] * cv.Cs + (k - t * cv.Cs);
+          }
+        }
+        if (n0 + r < N && k < K) wr[i] = *reinterpret_cast<const float4*>(W + (long)(n0 + r) * ldw + kc);
       } else {
         const int kr = idx / (BN / 4), c = (idx % (BN / 4)) * 4;
         if (k0 + kr < K && n0 + c < N) wr[i] = *reinterpret_cast<const float4*>(W + (long)(k0 + kr) * ldw + n0 + c);
@@ -148,6 +155,26 @@ __global__ __launch_bounds__(PG_NW * 64, 2) void pgemm_bf16_kernel(const bf16* _
     for (int i = 0; i < RS; ++i) {
       const int m = mw + i * 16 + fr;
       if constexpr (CV) {
+        if (cv.par >= 0) {   // parity class of a stride-2 transposed conv
+          const int h2 = cv.Hr >> 1, w2 = cv.Wr >> 1, mm = m < M ? m : 0;
+          const int b = mm / (h2 * w2), rem = mm - b * h2 * w2, Y = rem / w2;
+          const int ry = 2 * Y + (cv.par >> 1), rx = 2 * (rem - Y * w2) + (cv.par & 1);
+#pragma unroll
+          for (int kt = 0; kt < 2; ++kt) {
+            const int k = k0 + kt * 32 + fg * 8;
+            bf16x8 v = {};
+            if (m < M && k < K) {
+              const int t = k / cv.Cs, tp = cv.tap[t < 4 ? t : 3];
+              const int ky = tp / 3, kx = tp - 3 * ky;
+              const int sy = (ry + 1 - ky) >> 1, sx = (rx + 1 - kx) >> 1;   // even by the class
+              if (sy >= 0 && sy < cv.Hs && sx >= 0 && sx < cv.Ws)
+                v = *reinterpret_cast<const bf16x8*>(A + ((long)(b * cv.Hs + sy) * cv.Ws + sx) * cv.Cs +
+                                                     (k - t * cv.Cs));
+            }
+            a[i][kt] = v;
+          }
+          continue;
+        }
         const ConvRow cr = conv_row(cv, m < M ? m : 0);
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt) {
@@ -263,6 +290,17 @@ __global__ __launch_bounds__(PG_NW * 64, 2) void pgemm_bf16_kernel(const bf16* _
   const bf16* res = static_cast<const bf16*>(epi.res);
   const bf16* Z = static_cast<const bf16*>(epi.Z);
   constexpr int JC = TN <= 8 ? TN : TN / 2;  // column fragments per residual / Z round trip
+  // output row of GEMM row m: the pixel itself, except for a parity class (its strided pixels)
+  auto orow = [&](int m) -> long {
+    if constexpr (CV) {
+      if (cv.par >= 0) {
+        const int h2 = cv.Hr >> 1, w2 = cv.Wr >> 1;
+        const int b = m / (h2 * w2), rem = m - b * h2 * w2, Y = rem / w2;
+        return ((long)b * cv.Hr + 2 * Y + (cv.par >> 1)) * cv.Wr + 2 * (rem - Y * w2) + (cv.par & 1);
+      }
+    }
+    return m;
+  };
   auto epilogue = [&](int j) {
     const int mt = tile_mt(j), n0 = tile_nt(j) * BN, mw = mt * BM + wave * 16 * RS;
     const float* cv = cvec + (j & 1) * 2 * BN;
@@ -292,7 +330,7 @@ __global__ __launch_bounds__(PG_NW * 64, 2) void pgemm_bf16_kernel(const bf16* _
           bf16* ob = reinterpret_cast<bf16*>(&ov);
 #pragma unroll
           for (int e = 0; e < 8; ++e) ob[e] = (bf16)((acc[i][2 * q + (e >> 2)][e & 3] + bias[e]) * rsc + (float)rb[e]);
-          if (ok && !(dbg & 4)) *reinterpret_cast<uint4*>(out + (long)m * ldo + n) = ov;
+          if (ok && !(dbg & 4)) *reinterpret_cast<uint4*>(out + orow(m) * ldo + n) = ov;
           if constexpr (STATS) {
 #pragma unroll
             for (int h = 0; h < 2; ++h) {   // fragment 2q + h: the same wave-private 16 x 16 pass as below
@@ -470,8 +508,8 @@ __global__ __launch_bounds__(PG_NW * 64, 2) void pgemm_bf16_kernel(const bf16* _
 static int g_pgemm = 1;   // knob "pgemm": route small-M bf16 fwd / dgrad here (0 = tiled kernel)
 // knob "pg_split" (bit mask, default 3 = follow split_w): bit 1 lets the panel kernel's forward
 // launches use the split (hi + lo) weights, bit 2 its implicit-conv launches
-static int g_pg_split = 3;
-void set_pg_split(int v) { g_pg_split = v & 3; }
+static int g_pg_split = 7;   // bit 4: stride-2 transposed convs as parity classes (pgemm_tconv_try)
+void set_pg_split(int v) { g_pg_split = v & 7; }
 static int g_pg_rs = 0;   // knobs "pg_rs" / "pg_tn": force the tile (0 = planner)
 static int g_pg_tn = 0;
 // knob "pg_per_cu": workgroups per CU the grid is capped at (measured: 8, i.e. one tile per workgroup
@@ -641,6 +679,42 @@ bool pgemm_dgrad_try(const void* dout, int ldd, const float* W, void* dA, int ld
   else if (epi.zact == OGV_ACT_SILU) OGV_PGD(OGV_ACT_SILU);
   else OGV_PGD(0);
 #undef OGV_PGD
+  return true;
+}
+
+// Stride-2 transposed conv (a downsample's data gradient) as four parity-class GEMMs: output pixel
+// (y, x) only receives taps with ky = y + 1 (mod 2), kx = x + 1 (mod 2), i.e. 1, 2, 2 or 4 of the 9
+// (K / 2.25 on average, no zero taps staged or multiplied).  Returns false (nothing launched) when
+// a class does not fit the panel kernel.
+bool pgemm_tconv_try(const void* A, const ConvG& cv, const float* Wt, void* out, int M, int N, hipStream_t s) {
+  if (!g_pgemm || !(g_pg_split & 4) || !cv.transposed || cv.stride != 2 || (cv.Hr & 1) || (cv.Wr & 1) || (cv.Cs & 7) ||
+      !al16p(A) || !al16p(out) || !al16p(Wt) || M % (cv.Hr * cv.Wr))
+    return false;
+  const bool sw = (split_w() & 2) != 0;
+  const int Mc = M / 4;
+  ConvG g[4];
+  PgPlan p[4];
+  for (int par = 0; par < 4; ++par) {
+    g[par] = cv;
+    g[par].par = par;
+    const int kys[2][2] = {{1, -1}, {0, 2}};
+    int nt = 0;
+    for (int a = 0; a < 2; ++a)
+      for (int b = 0; b < 2; ++b) {
+        const int ky = kys[par >> 1][a], kx = kys[par & 1][b];
+        if (ky >= 0 && kx >= 0) g[par].tap[nt++] = ky * 3 + kx;
+      }
+    g[par].ntap = nt;
+    p[par] = pg_plan(Mc, N, nt * cv.Cs, false, sw, false, false, false);
+    if (!p[par].ok) return false;
+  }
+  const bf16* a = static_cast<const bf16*>(A);
+  bf16* o = static_cast<bf16*>(out);
+  for (int par = 0; par < 4; ++par) {
+    const int K = g[par].ntap * cv.Cs;
+    if (sw) pg_tiles<-1, false, 0, false, false, true, true>(p[par], a, 0, Pro(), Wt, 9 * cv.Cs, Epi(), o, N, Mc, N, K, s, g[par]);
+    else pg_tiles<-1, false, 0, false, false, false, true>(p[par], a, 0, Pro(), Wt, 9 * cv.Cs, Epi(), o, N, Mc, N, K, s, g[par]);
+  }
   return true;
 }
 

@@ -52,6 +52,7 @@ ACTS = {"silu": nn.SiLU(), "gelu": nn.GELU(), "relu": nn.ReLU(), None: nn.Identi
     (3, 16, 24, 9, 7, 2, True, True, "gelu"),        # odd sizes, ragged row tiles
     (2, 8, 40, 5, 6, 1, False, True, "relu"),        # use_bn=False: conv bias, no BN
     (2, 5, 12, 6, 6, 2, True, True, None),           # Cin % 8 != 0 on the strided path
+    (3, 16, 24, 10, 6, 2, True, True, "gelu"),       # dgrad as 4 parity-class GEMMs, non-square
 ])
 def test_conv_bn_act(case, dtype):
     from ogv import functional as OF

@@ -41,6 +41,9 @@ def _dt(t: torch.Tensor) -> int:
 _SIDE = {}
 # smallest M*(N+K) of a Linear backward whose weight gradient is forked onto the side stream
 _FORK_MIN_WORK = int(os.environ.get("OGV_FORK_MIN_WORK", "0"))
+# fork policy for the Linears whose dgrad applies an activation derivative (the MLP fc2 inputs):
+# "1" = fork like the others, "0" = weight gradient after the data gradient on the current stream
+_FORK_ACT = os.environ.get("OGV_FORK_ACT", "1") != "0"
 
 
 def _side_stream(device):
@@ -305,7 +308,8 @@ def _linear_bwd(dout, x2d, w2d, rs, rps, act, has_bias, want_dx, want_dw):
     # GEMMs overlap.
     # (below ~_FORK_MIN_WORK the fork/join latency (~10 us per cross-stream edge) outweighs the overlap)
     # (while a probe is armed everything stays on the current stream, where its events are)
-    fork = want_dx and want_dw and M * (N + K) >= _FORK_MIN_WORK and not _PROBE["armed"]
+    fork = (want_dx and want_dw and M * (N + K) >= _FORK_MIN_WORK and not _PROBE["armed"]
+            and (_FORK_ACT or not act))
     with _fork(fork, dout, x2d, rs, dw, db, ws_w if want_dw else None) as side:
         if want_dw:
             with _probe("wgrad", dict(M=M, N=N, K=K, elem=x2d.element_size(), bias=has_bias),

@@ -709,3 +709,33 @@ def test_mbconv_fused_image_groups(C, H, B):
         test_mbconv_fused_vs_unfused(C, H, B, True)
     finally:
         assert lib.ogv_set_option(b"dw_blocks", 0) == 0
+
+
+def test_outgrid_block_with_dropouts():
+    """proj_drop / ffn_drop > 0 (no reference config uses them; the modules then take torch Dropout on
+    the HIP kernels' outputs with an explicit residual add): training forward + backward finite and
+    reproducible under a fixed seed, different from the dropout-free block; eval mode identical to
+    the dropout-free block (Dropout is the identity there)."""
+    from src.model.Out_Grid_Block import OutGridBlock
+    from src.stage_config import StageCfg
+    base = dict(dim=48, depth=1, num_heads=2, grid_size=4, outlook_heads=2)
+    torch.manual_seed(11)
+    ref = OutGridBlock(StageCfg(**base)).to(DEV)
+    drop = OutGridBlock(StageCfg(**base, proj_drop=0.2, ffn_drop=0.1)).to(DEV)
+    drop.load_state_dict(ref.state_dict())
+    x = torch.randn(2, 48, 8, 8, device=DEV).contiguous(memory_format=torch.channels_last)
+    outs = []
+    for _ in range(2):
+        torch.manual_seed(5)
+        xx = x.clone().requires_grad_()
+        y = drop.train()(xx)
+        y.float().square().mean().backward()
+        assert torch.isfinite(y).all() and torch.isfinite(xx.grad).all()
+        outs.append((y.detach(), xx.grad.clone()))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    torch.manual_seed(5)
+    y0 = ref.train()(x)
+    assert not torch.equal(y0.detach(), outs[0][0])
+    drop.load_state_dict(ref.state_dict())   # same BatchNorm running statistics for eval
+    with torch.no_grad():
+        assert torch.equal(drop.eval()(x), ref.eval()(x))

@@ -739,3 +739,30 @@ def test_outgrid_block_with_dropouts():
     drop.load_state_dict(ref.state_dict())   # same BatchNorm running statistics for eval
     with torch.no_grad():
         assert torch.equal(drop.eval()(x), ref.eval()(x))
+
+
+@pytest.mark.parametrize("shape", [(512, 48, 2, 32, 32), (4, 64, 2, 224, 224)])
+def test_outlook_vproj_full_size_matches_unfused(shape):
+    """Full-size property (7M stage 0 at bs=512; 22M stage 0 at 224^2): the fused projection +
+    aggregation kernel equals the unfused GEMM -> cat -> aggregation pair on the same inputs within
+    bf16 output rounding, and the cat it writes for training equals the GEMM's [v | logits | 0]."""
+    from ogv import functional as OF
+    B, C, h, H, W = shape
+    ld = (C + 9 * h + 7) // 8 * 8
+    g = torch.Generator(device=DEV).manual_seed(B + H)
+    x = torch.randn(B * H * W, C, device=DEV, generator=g).to(torch.bfloat16)
+    w = torch.randn(ld, C, device=DEV, generator=g) / C ** 0.5
+    w[C:C + 9 * h] *= 3.0
+    w[C + 9 * h:] = 0
+    b = 0.1 * torch.randn(ld, device=DEV, generator=g)
+    b[C + 9 * h:] = 0
+    with torch.no_grad():
+        cat = OF.linear_rows(x, w, b)
+        y_ref = OF.outlook_aggregate_cat(cat, C, B, H, W, h, 3)
+    wq, bq = w.clone().requires_grad_(), b.clone().requires_grad_()
+    y = OF.outlook_vproj(x, wq, bq, C, B, H, W, h, 3)     # training mode: writes cat as well
+    tol = 1e-2 * max(1.0, y_ref.float().abs().max().item())
+    assert fx.maxabs(y.detach().float(), y_ref.float()) <= tol
+    cat_f = y.grad_fn.saved_tensors[2]
+    assert fx.maxabs(cat_f.float(), cat.float()) <= 1e-2 * max(1.0, cat.float().abs().max().item())
+    assert torch.equal(cat_f[:, C + 9 * h:], torch.zeros_like(cat_f[:, C + 9 * h:]))

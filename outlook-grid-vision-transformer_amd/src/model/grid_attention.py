@@ -62,16 +62,33 @@ class MultiHeadSelfAttention(nn.Module):
         self.proj = Linear(cfg.dim, cfg.dim, bias=True)
         self.proj_drop = nn.Dropout(cfg.proj_drop)
 
+    def _attend_dropout(self, qkv, B, H, W, g, capture):
+        """Training with attn_drop > 0 (no reference config uses it): the probability matrix is
+        materialised so Dropout can act on it -- grid_attention.py:70-86 in torch ops on the device
+        (fp32), with the grid partition of grid_partition.py:13-15 as a view."""
+        h, hd, N = self.num_heads, self.head_dim, (H // g) * (W // g)
+        t = qkv.view(B, H // g, g, W // g, g, 3, h, hd).permute(5, 0, 2, 4, 6, 1, 3, 7).reshape(3, B * g * g, h, N, hd)
+        q, k, v = t[0].float(), t[1].float(), t[2].float()
+        attn = ((q @ k.transpose(-2, -1)) * self.scale).softmax(dim=-1)
+        if capture:
+            self.last_attn = attn.detach()
+        attn = self.attn_drop(attn)
+        if capture:
+            self.last_attn_postdrop = attn.detach()
+        out = (attn @ v).to(qkv.dtype)                                   # [B g g, h, N, hd]
+        return out.view(B, g, g, h, H // g, W // g, hd).permute(0, 4, 1, 5, 2, 3, 6).reshape(B * H * W, self.dim)
+
     def attend_rows(self, x2d, B, H, W, g, residual=None, row_scale=None):
         """Rows of a [B, H, W, C] image (or [B, 1, N, C] token set) -> attended rows (+ residual)."""
-        if self.training and self.attn_drop.p > 0:
-            raise NotImplementedError("ogv grid attention: attn_drop > 0 in training is not implemented")
         capture = bool(getattr(self, "capture_attn", False))
         qkv = self.qkv(x2d, rps=H * W)
-        out, probs = OF.grid_attention_rows(qkv, B, H, W, self.num_heads, g, self.scale, want_probs=capture)
-        if capture:
-            self.last_attn = probs.detach()
-            self.last_attn_postdrop = self.last_attn
+        if self.training and self.attn_drop.p > 0:
+            out = self._attend_dropout(qkv, B, H, W, g, capture)
+        else:
+            out, probs = OF.grid_attention_rows(qkv, B, H, W, self.num_heads, g, self.scale, want_probs=capture)
+            if capture:
+                self.last_attn = probs.detach()
+                self.last_attn_postdrop = self.last_attn
         if self.training and self.proj_drop.p > 0:
             y = self.proj_drop(self.proj(out, rps=H * W))
             if residual is None:

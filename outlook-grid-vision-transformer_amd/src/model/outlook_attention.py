@@ -128,6 +128,21 @@ class OutlookAttention2d(nn.Module):
         bparts = [bv.float(), ba.float()] + ([zb] if ld > C + n else [])
         return w, torch.cat(bparts)
 
+    def _forward_dropout(self, x):
+        """Training with attn_drop > 0 (no reference config uses it): Dropout acts on the softmax
+        probabilities, so they are materialised -- outlook_attention.py:100-120 in torch ops on the
+        device (fp32) around the two 1x1 convs on the HIP GEMM."""
+        B, C, H, W = x.shape
+        k, heads, hd = self.kernel_size, self.num_heads, self.head_dim
+        kk = k * k
+        a = self.attn(x).float().reshape(B, heads, kk, H * W).permute(0, 3, 1, 2).softmax(dim=-1)
+        a = self.attn_drop(a)                                                     # [B, HW, heads, kk]
+        v = self.v(x).float()
+        v_unf = F.unfold(v, kernel_size=k, padding=k // 2).view(B, heads, hd, kk, H * W).permute(0, 4, 1, 2, 3)
+        y = (v_unf * a.unsqueeze(3)).sum(dim=-1)                                  # [B, HW, heads, hd]
+        y = y.permute(0, 2, 3, 1).reshape(B, C, H, W).to(OF.compute_dtype(x))
+        return y.contiguous(memory_format=torch.channels_last)
+
     def _zero_pads(self, device, rows):
         """Zero rows of the concatenated weight / bias, allocated once per device (not parameters or
         buffers: the state_dict is unchanged) -- no fill launches per forward."""
@@ -141,10 +156,10 @@ class OutlookAttention2d(nn.Module):
     def forward(self, x: torch.Tensor, residual=None, row_scale=None) -> torch.Tensor:
         if self.stride != 1:
             raise NotImplementedError("ogv OutlookAttention2d implements stride=1 (the OutGridBlock path)")
-        if self.training and self.attn_drop.p > 0:
-            raise NotImplementedError("ogv OutlookAttention2d: attn_drop > 0 in training is not implemented")
         B, C, H, W = x.shape
-        if self._hooked():
+        if self.training and self.attn_drop.p > 0:
+            y = self._forward_dropout(x)
+        elif self._hooked():
             a = self.attn(x)                     # [B, heads*k*k, H, W]  (analysis hooks read this)
             v = self.v(x)                        # [B, C, H, W]
             y = OF.outlook_aggregate_rows(OF.nchw_to_rows(v), OF.nchw_to_rows(a), B, H, W,
@@ -160,7 +175,8 @@ class OutlookAttention2d(nn.Module):
             else:
                 cat = OF.linear_rows(xr, w, b)     # [M, v | logits | 0]
                 y = OF.outlook_aggregate_cat(cat, C, B, H, W, self.num_heads, self.kernel_size)
-        y = OF.rows_to_nchw(y, B, H, W)
+        if y.dim() == 2:
+            y = OF.rows_to_nchw(y, B, H, W)
         if self.training and self.proj_drop.p > 0:
             y = self.proj_drop(self.proj(y))
             if residual is None:

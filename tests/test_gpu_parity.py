@@ -766,3 +766,40 @@ def test_outlook_vproj_full_size_matches_unfused(shape):
     cat_f = y.grad_fn.saved_tensors[2]
     assert fx.maxabs(cat_f.float(), cat.float()) <= 1e-2 * max(1.0, cat.float().abs().max().item())
     assert torch.equal(cat_f[:, C + 9 * h:], torch.zeros_like(cat_f[:, C + 9 * h:]))
+
+
+@pytest.mark.parametrize("which", ["outlook", "grid"])
+def test_attn_drop_materialising_path(which):
+    """attn_drop > 0 in training (no reference config uses it) takes the materialising path
+    (probabilities in torch ops, then Dropout).  With p -> 0 it must equal the fused kernels' result
+    (fp32, within 1e-4: the math is the same), with p = 0.3 it is reproducible under a fixed seed,
+    gradients are finite, and eval mode ignores it."""
+    from src.model.outlook_attention import OutlookAttention2d
+    from src.model.grid_attention import GridAttention2D, GridAttention2DConfig
+    torch.manual_seed(2)
+    if which == "outlook":
+        mk = lambda p: OutlookAttention2d(48, 2, attn_drop=p)  # noqa: E731
+        x = torch.randn(2, 48, 8, 8, device=DEV).contiguous(memory_format=torch.channels_last)
+    else:
+        mk = lambda p: GridAttention2D(GridAttention2DConfig(mode="grid", dim=48, num_heads=2, grid_size=2,  # noqa: E731
+                                                             attn_drop=p))
+        x = torch.randn(2, 8, 8, 48, device=DEV)
+    ref = mk(0.0).to(DEV).train()
+    tiny = mk(1e-12).to(DEV).train()
+    tiny.load_state_dict(ref.state_dict())
+    y_ref = ref(x)
+    y_tiny = tiny(x)
+    assert fx.maxabs(y_tiny.detach(), y_ref.detach().float()) <= 1e-4 * max(1.0, y_ref.abs().max().item())
+    drop = mk(0.3).to(DEV).train()
+    drop.load_state_dict(ref.state_dict())
+    outs = []
+    for _ in range(2):
+        torch.manual_seed(9)
+        xx = x.clone().requires_grad_()
+        y = drop(xx)
+        y.square().mean().backward()
+        assert torch.isfinite(y).all() and torch.isfinite(xx.grad).all()
+        outs.append(y.detach())
+    assert torch.equal(outs[0], outs[1]) and not torch.equal(outs[0], y_ref.detach())
+    with torch.no_grad():
+        assert torch.equal(drop.eval()(x), ref.eval()(x))

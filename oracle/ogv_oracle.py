@@ -200,16 +200,22 @@ def ln2d(x, w, b, eps=1e-6):
     return y.permute(0, 3, 1, 2).contiguous()
 
 
-def outlook_attention(x, p: P, pre: str, heads: int, k: int = 3):
+def outlook_attention(x, p: P, pre: str, heads: int, k: int = 3, stride: int = 1):
+    """outlook_attention.py:91-124 (stride > 1: logits average-pooled by the stride, strided unfold,
+    output at H/s x W/s)."""
     B, C, H, W = x.shape
-    kk, hd, L = k * k, C // heads, H * W
+    kk, hd = k * k, C // heads
     logits = F.conv2d(x, p[pre + "attn.weight"], p.get(pre + "attn.bias"))
-    prob = logits.view(B, heads, kk, L).permute(0, 3, 1, 2).contiguous().softmax(dim=-1)      # [B,L,h,kk]
+    if stride > 1:
+        logits = F.avg_pool2d(logits, kernel_size=stride, stride=stride)
+    Hs, Ws = logits.shape[-2:]
+    L = Hs * Ws
+    prob = logits.reshape(B, heads, kk, L).permute(0, 3, 1, 2).contiguous().softmax(dim=-1)   # [B,L,h,kk]
     v = F.conv2d(x, p[pre + "v.weight"], p.get(pre + "v.bias"))
-    cols = F.unfold(v, kernel_size=k, padding=k // 2)                                        # [B,C*kk,L]
+    cols = F.unfold(v, kernel_size=k, padding=k // 2, stride=stride)                        # [B,C*kk,L]
     cols = cols.view(B, heads, hd, kk, L).permute(0, 4, 1, 2, 3).contiguous()                # [B,L,h,hd,kk]
     y = (cols * prob.unsqueeze(3)).sum(dim=-1)                                               # [B,L,h,hd]
-    y = y.permute(0, 2, 3, 1).contiguous().view(B, C, H, W)
+    y = y.permute(0, 2, 3, 1).contiguous().view(B, C, Hs, Ws)
     return F.conv2d(y, p[pre + "proj.weight"], p[pre + "proj.bias"])
 
 

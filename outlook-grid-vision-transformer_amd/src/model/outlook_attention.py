@@ -128,19 +128,25 @@ class OutlookAttention2d(nn.Module):
         bparts = [bv.float(), ba.float()] + ([zb] if ld > C + n else [])
         return w, torch.cat(bparts)
 
-    def _forward_dropout(self, x):
-        """Training with attn_drop > 0 (no reference config uses it): Dropout acts on the softmax
-        probabilities, so they are materialised -- outlook_attention.py:100-120 in torch ops on the
-        device (fp32) around the two 1x1 convs on the HIP GEMM."""
+    def _forward_materialised(self, x):
+        """stride > 1, or training with attn_drop > 0 (no reference config uses either): the softmax
+        probabilities are materialised -- outlook_attention.py:100-120 in torch ops on the device
+        (fp32) around the two 1x1 convs on the HIP GEMM: logits average-pooled by the stride, the
+        unfold strided, Dropout on the probabilities.  Output [B, C, H/s, W/s]."""
         B, C, H, W = x.shape
-        k, heads, hd = self.kernel_size, self.num_heads, self.head_dim
+        k, s, heads, hd = self.kernel_size, self.stride, self.num_heads, self.head_dim
         kk = k * k
-        a = self.attn(x).float().reshape(B, heads, kk, H * W).permute(0, 3, 1, 2).softmax(dim=-1)
-        a = self.attn_drop(a)                                                     # [B, HW, heads, kk]
+        a = self.attn(x).float()
+        if s > 1:
+            a = F.avg_pool2d(a, kernel_size=s, stride=s)
+        Hs, Ws = a.shape[-2:]
+        a = a.reshape(B, heads, kk, Hs * Ws).permute(0, 3, 1, 2).softmax(dim=-1)
+        a = self.attn_drop(a)                                                     # [B, L, heads, kk]
         v = self.v(x).float()
-        v_unf = F.unfold(v, kernel_size=k, padding=k // 2).view(B, heads, hd, kk, H * W).permute(0, 4, 1, 2, 3)
-        y = (v_unf * a.unsqueeze(3)).sum(dim=-1)                                  # [B, HW, heads, hd]
-        y = y.permute(0, 2, 3, 1).reshape(B, C, H, W).to(OF.compute_dtype(x))
+        v_unf = F.unfold(v, kernel_size=k, padding=k // 2, stride=s)
+        v_unf = v_unf.view(B, heads, hd, kk, Hs * Ws).permute(0, 4, 1, 2, 3)
+        y = (v_unf * a.unsqueeze(3)).sum(dim=-1)                                  # [B, L, heads, hd]
+        y = y.permute(0, 2, 3, 1).reshape(B, C, Hs, Ws).to(OF.compute_dtype(x))
         return y.contiguous(memory_format=torch.channels_last)
 
     def _zero_pads(self, device, rows):
@@ -154,11 +160,9 @@ class OutlookAttention2d(nn.Module):
         return z
 
     def forward(self, x: torch.Tensor, residual=None, row_scale=None) -> torch.Tensor:
-        if self.stride != 1:
-            raise NotImplementedError("ogv OutlookAttention2d implements stride=1 (the OutGridBlock path)")
         B, C, H, W = x.shape
-        if self.training and self.attn_drop.p > 0:
-            y = self._forward_dropout(x)
+        if self.stride != 1 or (self.training and self.attn_drop.p > 0):
+            y = self._forward_materialised(x)
         elif self._hooked():
             a = self.attn(x)                     # [B, heads*k*k, H, W]  (analysis hooks read this)
             v = self.v(x)                        # [B, C, H, W]

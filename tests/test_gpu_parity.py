@@ -44,7 +44,7 @@ def _module(meta):
 
     k = meta["kind"]
     if k == "outlook_attn":
-        return OutlookAttention2d(meta["dim"], meta["heads"], meta["k"])
+        return OutlookAttention2d(meta["dim"], meta["heads"], meta["k"], stride=meta.get("stride", 1))
     if k == "layernorm2d":
         return LayerNorm2d(meta["dim"], eps=meta["eps"])
     if k == "outlooker_block":
@@ -114,7 +114,7 @@ def test_golden_fp32(name):
 def _oracle_fn(meta):
     p = {k: v.to(DEV) for k, v in fx.oracle_params(meta, requires_grad=False).items()}
     kind = meta["kind"]
-    return {"outlook_attn": lambda xt: orc.outlook_attention(xt, p, "", meta["heads"], meta["k"]),
+    return {"outlook_attn": lambda xt: orc.outlook_attention(xt, p, "", meta["heads"], meta["k"], meta.get("stride", 1)),
             "grid_attn": lambda xt: orc.grid_attention(xt, p, "", meta["heads"], meta["g"]),
             "layernorm2d": lambda xt: orc.ln2d(xt, p["ln.weight"], p["ln.bias"], meta["eps"]),
             "outlooker_block": lambda xt: orc.outlooker_block(xt, p, "", meta["heads"]),

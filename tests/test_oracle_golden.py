@@ -37,7 +37,7 @@ def _check(name, fwd):
 
 @pytest.mark.parametrize("name", fx.fixture_names("outlook_attn_"))
 def test_outlook_attention(name):
-    _check(name, lambda x, p, m: orc.outlook_attention(x, p, "", m["heads"], m["k"]))
+    _check(name, lambda x, p, m: orc.outlook_attention(x, p, "", m["heads"], m["k"], m.get("stride", 1)))
 
 
 @pytest.mark.parametrize("name", [n for n in fx.fixture_names("grid_attn_") if "capture" not in n])

@@ -508,8 +508,13 @@ __global__ __launch_bounds__(PG_NW * 64, 2) void pgemm_bf16_kernel(const bf16* _
 static int g_pgemm = 1;   // knob "pgemm": route small-M bf16 fwd / dgrad here (0 = tiled kernel)
 // knob "pg_split" (bit mask, default 3 = follow split_w): bit 1 lets the panel kernel's forward
 // launches use the split (hi + lo) weights, bit 2 its implicit-conv launches
-static int g_pg_split = 7;   // bit 4: stride-2 transposed convs as parity classes (pgemm_tconv_try)
-void set_pg_split(int v) { g_pg_split = v & 7; }
+// Bit 8 off (pg_split=7: the launches with an A prologue -- GELU fc2, MBConv project -- multiply by the
+// single bf16 weight) measured 18.75-18.77 -> 18.62-18.67 ms/step with the Model-A-7M logits error
+// 0.48% -> 0.57% of |ref|, but the 224^2 stage-0 OutGridBlock eval fixture then misses the 1e-2
+// bound, so the default keeps every forward split.
+static int g_pg_split = 15;  // bit 4: stride-2 transposed convs as parity classes (pgemm_tconv_try);
+                             // bit 8: split weights also on the launches with an A prologue
+void set_pg_split(int v) { g_pg_split = v & 15; }
 static int g_pg_rs = 0;   // knobs "pg_rs" / "pg_tn": force the tile (0 = planner)
 static int g_pg_tn = 0;
 // knob "pg_per_cu": workgroups per CU the grid is capped at (measured: 8, i.e. one tile per workgroup
@@ -631,7 +636,7 @@ int pgemm_fwd_try(const void* A, int lda, const Pro& pro, const float* W, int ld
   if (pa && pro.act != OGV_ACT_GELU && pro.act != OGV_ACT_SILU) return 0;
   if (pro.gate && ((pro.gld & 3) || !al16p(pro.gate))) return 0;
   const bool st = epi.stat != nullptr;
-  const bool sw = (split_w() & 1) != 0 && (g_pg_split & 1);
+  const bool sw = (split_w() & 1) != 0 && (g_pg_split & 1) && (!pa || (g_pg_split & 8));
   const PgPlan p = pg_plan(M, N, K, st, sw, false, pa, pro.gate != nullptr);
   if (!p.ok) return 0;
   const bf16* a = static_cast<const bf16*>(A);
@@ -746,7 +751,8 @@ int pgemm_conv_try(const void* A, const ConvG& cv, const float* Wt, void* out, i
 bool pgemm_route(int kind, int M, int N, int K, int act) {
   if (kind == 0) {
     if (act != OGV_ACT_NONE && act != OGV_ACT_GELU && act != OGV_ACT_SILU) return false;
-    return pg_plan(M, N, K, false, (split_w() & 1) != 0 && (g_pg_split & 1), false, act != OGV_ACT_NONE, false).ok;
+    return pg_plan(M, N, K, false, (split_w() & 1) != 0 && (g_pg_split & 1) && (act == OGV_ACT_NONE || (g_pg_split & 8)),
+                   false, act != OGV_ACT_NONE, false).ok;
   }
   return pg_plan(M, K, N, false, (split_w() & 2) != 0, true, false, false).ok;  // dgrad: output K
 }

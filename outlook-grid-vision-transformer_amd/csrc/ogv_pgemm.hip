@@ -506,8 +506,10 @@ __global__ __launch_bounds__(PG_NW * 64, 2) void pgemm_bf16_kernel(const bf16* _
 // plan + dispatch
 // ------------------------------------------------------------------------------------------------
 static int g_pgemm = 1;   // knob "pgemm": route small-M bf16 fwd / dgrad here (0 = tiled kernel)
-// knob "pg_split" (bit mask, default 3 = follow split_w): bit 1 lets the panel kernel's forward
-// launches use the split (hi + lo) weights, bit 2 its implicit-conv launches
+// knob "pg_split" (bit mask, default 15 = all four bits): bit 1 lets the panel kernel's forward
+// launches use the split (hi + lo) weights (when split_w is on), bit 2 its implicit-conv launches,
+// bit 4 runs the stride-2 transposed convs as parity classes (pgemm_tconv_try), bit 8 keeps the split
+// weights on the launches with an A prologue.
 // Bit 8 off (pg_split=7: the launches with an A prologue -- GELU fc2, MBConv project -- multiply by the
 // single bf16 weight) measured 18.75-18.77 -> 18.62-18.67 ms/step with the Model-A-7M logits error
 // 0.48% -> 0.57% of |ref|, but the 224^2 stage-0 OutGridBlock eval fixture then misses the 1e-2

@@ -208,6 +208,136 @@ def probe_reset():
     _PROBE["recs"] = []
 
 
+# ------------------------------------------------------------------------------------------------
+# step census (bench.py roofline.step): HIP events around EVERY C-ABI op of one eager step, each
+# with the algorithmic bytes / flops of the kernels it launches (each kernel reads its operands once
+# and writes its results once: DESIGN.md §3), so Σ roofline time / Σ measured time
+# can be reported over the whole step.  Forks are off while armed (every op on one stream, where
+# its events are).
+# ------------------------------------------------------------------------------------------------
+_CENSUS = {"armed": False, "recs": []}
+
+
+def _serial() -> bool:
+    return _PROBE["armed"] or _CENSUS["armed"]
+
+
+def op_cost(name: str, u: dict):
+    """(algorithmic HBM bytes, flops) of one C-ABI op.  s = activation element size; M rows of C
+    channels; weights are fp32 [N, K]."""
+    s = u["elem"]
+    M = u.get("M", 0)
+    if name == "gemm_fwd":
+        return probe_bytes("gemm_fwd", u), 2 * M * u["N"] * u["K"]
+    if name == "gemm_dgrad":
+        return probe_bytes("sgemm", dict(u, kind="dgrad")), 2 * M * u["N"] * u["K"]
+    if name == "gemm_wgrad":
+        return probe_bytes("wgrad", u), 2 * M * u["N"] * u["K"]
+    C = u.get("C", 0)
+    if name == "layernorm_fwd":      # read x, write y (+ fp32 mean / rstd)
+        return s * 2 * M * C + 8 * M, 8 * M * C
+    if name == "layernorm_bwd":      # read dy, x (+ dres), write dx (+ fp32 mean / rstd, gamma / beta partials)
+        return s * M * C * (4 if u.get("dres") else 3) + 8 * M + 8 * C, 10 * M * C
+    if name in ("outlook_fwd", "outlook_bwd", "outlook_vproj", "grid_fwd"):
+        return probe_bytes(name, u), probe_flops(name, u)
+    if name == "grid_bwd":           # read dO, qkv, O (+ lse), write dqkv (+ delta)
+        return s * M * 8 * C + 8 * M * u["heads"], 8 * M * u["N"] * C
+    if name == "dwconv_fwd":         # read x, write y
+        return s * (M + u["Mo"]) * C + 36 * C, 18 * u["Mo"] * C
+    if name == "dwconv_bwd":         # dgrad: read dy, write dx; wgrad: read dy, x
+        return s * 2 * (M + u["Mo"]) * C + 36 * C, 36 * u["Mo"] * C
+    if name in ("mbconv_fwd", "mbconv_bwd"):
+        m, se, B = u["mid"], u["se"], u["B"]
+        w = 4 * (2 * m * C + 9 * m + 2 * m * se)                   # fp32 weights
+        if name == "mbconv_fwd":     # expand (x -> e), dw (e -> d), SE pool (d), project (d -> p), BN3 + residual (p, x -> out)
+            return s * M * (5 * C + 5 * m) + w, 2 * M * m * C * 2 + 18 * M * m
+        # BN3 reduce + apply, project dgrad + wgrad, SE reduce, BN2 apply, dw wgrad + dgrad, BN1 apply,
+        # expand wgrad + dgrad (+ the residual)
+        return s * M * (11 * C + 17 * m) + 2 * w, 2 * M * m * C * 4 + 36 * M * m
+    if name in ("convbn_fwd", "convbn_bwd"):
+        Mi, Mo, Ci, Co = M, u["Mo"], u["Cin"], u["Cout"]
+        f = 2 * Mo * Co * 9 * Ci
+        if name == "convbn_fwd":     # conv (x -> y), BN apply + act (y -> out)
+            return s * (Mi * Ci + 3 * Mo * Co) + 4 * 9 * Ci * Co, f
+        # BN reduce (dout, y), BN apply (dout, y -> dy), wgrad (dy, x), dgrad (dy -> dx)
+        return s * (7 * Mo * Co + 2 * Mi * Ci) + 8 * 9 * Ci * Co, 2 * f
+    if name == "bn_act_fwd":         # (statistics pass over x when training) + apply
+        return s * M * C * (3 if u.get("train") else 2), 4 * M * C
+    if name == "bn_act_bwd":         # reduce (dout, x) + apply (dout, x -> dx)
+        return s * M * C * 5, 8 * M * C
+    raise KeyError(name)
+
+
+def census_arm():
+    if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+        raise RuntimeError("ogv census: timing events cannot be recorded into a ROCm graph")
+    _CENSUS["armed"] = True
+
+
+def census_disarm():
+    _CENSUS["armed"] = False
+
+
+def census_reset():
+    _CENSUS["recs"] = []
+
+
+class _census:
+    """One C-ABI op of the census: events around it on the current stream (same device spin in front
+    as the probes), recorded with its name, algorithmic bytes and flops."""
+
+    def __init__(self, name, units):
+        self.on = _CENSUS["armed"]
+        if self.on:
+            self.name = name
+            self.nbytes, self.nflops = op_cost(name, units)
+            self.e0 = torch.cuda.Event(enable_timing=True)
+            self.e1 = torch.cuda.Event(enable_timing=True)
+
+    def __enter__(self):
+        if self.on:
+            check(_lib.load().ogv_gpu_sleep(40, _stream()), "ogv_gpu_sleep")
+            self.e0.record()
+        return self
+
+    def __exit__(self, *a):
+        if self.on:
+            self.e1.record()
+            _CENSUS["recs"].append((self.name, self.e0, self.e1, self.nbytes, self.nflops))
+        return False
+
+
+def census_results(hbm_gbs: float, mfma_tflops: float):
+    """Per-op-family table and totals of the recorded ops: algorithmic bytes / flops, roofline time
+    max(bytes / HBM peak, flops / MFMA peak), measured time (each interval minus the empty
+    event-pair overhead)."""
+    recs = _CENSUS["recs"]
+    if not recs:
+        return None
+    torch.cuda.synchronize()
+    ovh = _empty_pair_ms()
+    fam = {}
+    for name, a, b, nb, nf in recs:
+        ms = max(a.elapsed_time(b) - ovh, 1e-6)
+        bound = max(nb / (hbm_gbs * 1e9), nf / (mfma_tflops * 1e12)) * 1e3
+        d = fam.setdefault(name, {"launches": 0, "bytes": 0, "flops": 0, "bound_ms": 0.0, "measured_ms": 0.0})
+        d["launches"] += 1
+        d["bytes"] += nb
+        d["flops"] += nf
+        d["bound_ms"] += bound
+        d["measured_ms"] += ms
+    for d in fam.values():
+        d["frac"] = round(d["bound_ms"] / d["measured_ms"], 4)
+        d["bound_ms"] = round(d["bound_ms"], 4)
+        d["measured_ms"] = round(d["measured_ms"], 4)
+    tb = sum(d["bound_ms"] for d in fam.values())
+    tm = sum(d["measured_ms"] for d in fam.values())
+    return {"ops": len(recs), "bytes": sum(d["bytes"] for d in fam.values()),
+            "flops": sum(d["flops"] for d in fam.values()), "bound_ms": round(tb, 4), "measured_ms": round(tm, 4),
+            "frac": round(tb / tm, 4), "event_overhead_ms": round(ovh, 5),
+            "families": dict(sorted(fam.items(), key=lambda kv: -kv[1]["measured_ms"]))}
+
+
 def compute_dtype(x: torch.Tensor) -> torch.dtype:
     """Activation dtype for the kernels: the autocast dtype inside an autocast region (fp16 is
     computed as bf16 on MI355X), else the input dtype (fp32 or bf16)."""
@@ -269,7 +399,8 @@ class _Linear(torch.autograd.Function):
         route = lib.ogv_gemm_stream_route(0, M, N, K, ACT[act_in]) if _PROBE["armed"] else -1
         bf = x2d.dtype == torch.bfloat16
         with _probe("gemm_fwd", units), _probe("sgemm", units, when=bf and route == 1), \
-                _probe("gemm_panel", units, when=bf and route == 2), _probe("gemm_tiled", units, when=bf and route == 0):
+                _probe("gemm_panel", units, when=bf and route == 2), _probe("gemm_tiled", units, when=bf and route == 0), \
+                _census("gemm_fwd", units):
             check(lib.ogv_gemm_fwd(_ptr(x2d), x2d.stride(0), _ptr(w2d), _ptr(bias), _ptr(residual), _ptr(row_scale),
                                    int(rps), _ptr(out), N, M, N, K, ACT[act_in], _dt(x2d), _stream()), "ogv_gemm_fwd")
         ctx.save_for_backward(x2d, w2d, row_scale)
@@ -308,12 +439,12 @@ def _linear_bwd(dout, x2d, w2d, rs, rps, act, has_bias, want_dx, want_dw):
     # GEMMs overlap.
     # (below ~_FORK_MIN_WORK the fork/join latency (~10 us per cross-stream edge) outweighs the overlap)
     # (while a probe is armed everything stays on the current stream, where its events are)
-    fork = (want_dx and want_dw and M * (N + K) >= _FORK_MIN_WORK and not _PROBE["armed"]
+    fork = (want_dx and want_dw and M * (N + K) >= _FORK_MIN_WORK and not _serial()
             and (_FORK_ACT or not act))
     with _fork(fork, dout, x2d, rs, dw, db, ws_w if want_dw else None) as side:
         if want_dw:
-            with _probe("wgrad", dict(M=M, N=N, K=K, elem=x2d.element_size(), bias=has_bias),
-                        when=x2d.dtype == torch.bfloat16):
+            wu = dict(M=M, N=N, K=K, elem=x2d.element_size(), bias=has_bias)
+            with _probe("wgrad", wu, when=x2d.dtype == torch.bfloat16), _census("gemm_wgrad", wu):
                 check(lib.ogv_gemm_wgrad(_ptr(dout), N, _ptr(x2d), x2d.stride(0), _ptr(rs), rps, _ptr(dw), _ptr(db),
                                          M, N, K, act, _ptr(ws_w), dt, side), "ogv_gemm_wgrad")
         if want_dx:
@@ -321,7 +452,7 @@ def _linear_bwd(dout, x2d, w2d, rs, rps, act, has_bias, want_dx, want_dw):
             du = dict(kind="dgrad", M=M, N=N, K=K, elem=x2d.element_size(), z=bool(act))
             bf = x2d.dtype == torch.bfloat16
             with _probe("sgemm", du, when=bf and route == 1), _probe("gemm_panel", du, when=bf and route == 2), \
-                    _probe("gemm_tiled", du, when=bf and route == 0):
+                    _probe("gemm_tiled", du, when=bf and route == 0), _census("gemm_dgrad", du):
                 check(lib.ogv_gemm_dgrad(_ptr(dout), N, _ptr(w2d), _ptr(x2d) if act else None, x2d.stride(0),
                                          _ptr(rs), rps, _ptr(dx), K, M, N, K, act, _ptr(ws_d), dt, _stream()),
                       "ogv_gemm_dgrad")
@@ -355,8 +486,9 @@ class _LayerNorm(torch.autograd.Function):
         y = torch.empty_like(x2d)
         mean = torch.empty((M,), dtype=torch.float32, device=x2d.device)
         rstd = torch.empty((M,), dtype=torch.float32, device=x2d.device)
-        check(lib.ogv_layernorm_fwd(_ptr(x2d), _ptr(gamma), _ptr(beta), _ptr(y), _ptr(mean), _ptr(rstd), M, C,
-                                    float(eps), _dt(x2d), _stream()), "ogv_layernorm_fwd")
+        with _census("layernorm_fwd", dict(M=M, C=C, elem=x2d.element_size())):
+            check(lib.ogv_layernorm_fwd(_ptr(x2d), _ptr(gamma), _ptr(beta), _ptr(y), _ptr(mean), _ptr(rstd), M, C,
+                                        float(eps), _dt(x2d), _stream()), "ogv_layernorm_fwd")
         ctx.save_for_backward(x2d, gamma, mean, rstd)
         ctx.affine = (gamma is not None, beta is not None)
         return y
@@ -371,9 +503,10 @@ class _LayerNorm(torch.autograd.Function):
         dgamma = torch.empty((C,), dtype=torch.float32, device=x2d.device) if ctx.affine[0] else None
         dbeta = torch.empty((C,), dtype=torch.float32, device=x2d.device) if ctx.affine[1] else None
         ws = _ws(lib.ogv_layernorm_bwd_ws_bytes(M, C), x2d.device)
-        check(lib.ogv_layernorm_bwd(_ptr(dy), _ptr(x2d), _ptr(gamma), _ptr(mean), _ptr(rstd), None, _ptr(dx),
-                                    _ptr(dgamma), _ptr(dbeta), _ptr(ws), M, C, _dt(x2d), _stream()),
-              "ogv_layernorm_bwd")
+        with _census("layernorm_bwd", dict(M=M, C=C, elem=x2d.element_size(), dres=False)):
+            check(lib.ogv_layernorm_bwd(_ptr(dy), _ptr(x2d), _ptr(gamma), _ptr(mean), _ptr(rstd), None, _ptr(dx),
+                                        _ptr(dgamma), _ptr(dbeta), _ptr(ws), M, C, _dt(x2d), _stream()),
+                  "ogv_layernorm_bwd")
         return dx, dgamma, dbeta, None
 
 
@@ -401,9 +534,10 @@ class _LayerNormPair(torch.autograd.Function):
         dgamma = torch.empty((C,), dtype=torch.float32, device=x2d.device) if ctx.affine[0] else None
         dbeta = torch.empty((C,), dtype=torch.float32, device=x2d.device) if ctx.affine[1] else None
         ws = _ws(lib.ogv_layernorm_bwd_ws_bytes(M, C), x2d.device)
-        check(lib.ogv_layernorm_bwd(_ptr(dy), _ptr(x2d), _ptr(gamma), _ptr(mean), _ptr(rstd), _ptr(dres), _ptr(dx),
-                                    _ptr(dgamma), _ptr(dbeta), _ptr(ws), M, C, _dt(x2d), _stream()),
-              "ogv_layernorm_bwd")
+        with _census("layernorm_bwd", dict(M=M, C=C, elem=x2d.element_size(), dres=dres is not None)):
+            check(lib.ogv_layernorm_bwd(_ptr(dy), _ptr(x2d), _ptr(gamma), _ptr(mean), _ptr(rstd), _ptr(dres), _ptr(dx),
+                                        _ptr(dgamma), _ptr(dbeta), _ptr(ws), M, C, _dt(x2d), _stream()),
+                  "ogv_layernorm_bwd")
         return dx, dgamma, dbeta, None
 
 
@@ -429,7 +563,8 @@ def _outlook_bwd(dy, v2d, ldv, logits2d, ldl, dv, lddv, dlogits, lddl, dl_cols, 
     dt = _dt(dy)
     nws = lib.ogv_outlook_bwd_ws_bytes(B, H, W, C, heads, k, dt)
     probs = torch.empty(max(nws // 4, 1), dtype=torch.float32, device=dy.device) if nws else None
-    with _probe("outlook_bwd", dict(M=M, C=C, heads=heads, k=k, elem=dy.element_size())):
+    ou = dict(M=M, C=C, heads=heads, k=k, elem=dy.element_size())
+    with _probe("outlook_bwd", ou), _census("outlook_bwd", ou):
         check(lib.ogv_outlook_agg_bwd(_ptr(dy), _vp(v2d), _vp(logits2d), _vp(dv), _vp(dlogits), _ptr(probs), B, H, W,
                                       C, heads, k, ldl, ldv, lddv, lddl, dl_cols, dt, _stream()), "ogv_outlook_agg_bwd")
 
@@ -442,7 +577,8 @@ class _OutlookAgg(torch.autograd.Function):
         lib = _lib.load()
         M, C = v2d.shape
         y = torch.empty((M, C), dtype=v2d.dtype, device=v2d.device)
-        with _probe("outlook_fwd", dict(M=M, C=C, heads=heads, k=k, elem=v2d.element_size())):
+        ou = dict(M=M, C=C, heads=heads, k=k, elem=v2d.element_size())
+        with _probe("outlook_fwd", ou), _census("outlook_fwd", ou):
             check(lib.ogv_outlook_agg_fwd(_ptr(v2d), _ptr(logits2d), _ptr(y), B, H, W, C, heads, k,
                                           logits2d.stride(0), v2d.stride(0), _dt(v2d), _stream()),
                   "ogv_outlook_agg_fwd")
@@ -477,7 +613,8 @@ class _OutlookAggCat(torch.autograd.Function):
         M, ld = cat.shape
         y = torch.empty((M, C), dtype=cat.dtype, device=cat.device)
         es = cat.element_size()
-        with _probe("outlook_fwd", dict(M=M, C=C, heads=heads, k=k, elem=es)):
+        ou = dict(M=M, C=C, heads=heads, k=k, elem=es)
+        with _probe("outlook_fwd", ou), _census("outlook_fwd", ou):
             check(lib.ogv_outlook_agg_fwd(_ptr(cat), _vp(cat.data_ptr() + C * es), _ptr(y), B, H, W, C, heads, k, ld, ld,
                                           _dt(cat), _stream()), "ogv_outlook_agg_fwd")
         ctx.save_for_backward(cat)
@@ -510,7 +647,8 @@ class _OutlookVProj(torch.autograd.Function):
         ld = w.shape[0]
         y = torch.empty((M, C), dtype=x2d.dtype, device=x2d.device)
         cat = torch.empty((M, ld), dtype=x2d.dtype, device=x2d.device) if train else None
-        with _probe("outlook_vproj", dict(M=M, C=C, ld=ld, heads=heads, k=k, cat=train, elem=x2d.element_size())):
+        ou = dict(M=M, C=C, ld=ld, heads=heads, k=k, cat=train, elem=x2d.element_size())
+        with _probe("outlook_vproj", ou), _census("outlook_vproj", ou):
             check(lib.ogv_outlook_vproj_fwd(_ptr(x2d), x2d.stride(0), _ptr(w), _ptr(b), _ptr(cat), ld, _ptr(y), B, H, W,
                                             C, heads, k, _dt(x2d), _stream()), "ogv_outlook_vproj_fwd")
         ctx.save_for_backward(x2d, w, cat)
@@ -583,7 +721,8 @@ class _GridAttn(torch.autograd.Function):
         N = (H // g) * (W // g)
         probs = (torch.empty((B * g * g, heads, N, N), dtype=torch.float32, device=qkv2d.device)
                  if want_probs else None)
-        with _probe("grid_fwd", dict(M=M, C=C, heads=heads, N=N, elem=qkv2d.element_size())):
+        gu = dict(M=M, C=C, heads=heads, N=N, elem=qkv2d.element_size())
+        with _probe("grid_fwd", gu), _census("grid_fwd", gu):
             check(lib.ogv_grid_attn_fwd(_ptr(qkv2d), _ptr(out), _ptr(lse), _ptr(probs), B, H, W, C, heads, g,
                                         float(scale), _dt(qkv2d), _stream()), "ogv_grid_attn_fwd")
         ctx.save_for_backward(qkv2d, out, lse)
@@ -601,8 +740,10 @@ class _GridAttn(torch.autograd.Function):
         dout = dout.to(qkv2d.dtype).contiguous()
         dqkv = torch.empty_like(qkv2d)
         delta = torch.empty((qkv2d.shape[0], heads), dtype=torch.float32, device=qkv2d.device)
-        check(lib.ogv_grid_attn_bwd(_ptr(dout), _ptr(qkv2d), _ptr(out), _ptr(lse), _ptr(dqkv), _ptr(delta), B, H, W, C,
-                                    heads, g, scale, _dt(qkv2d), _stream()), "ogv_grid_attn_bwd")
+        gu = dict(M=qkv2d.shape[0], C=C, heads=heads, N=(H // g) * (W // g), elem=qkv2d.element_size())
+        with _census("grid_bwd", gu):
+            check(lib.ogv_grid_attn_bwd(_ptr(dout), _ptr(qkv2d), _ptr(out), _ptr(lse), _ptr(dqkv), _ptr(delta), B, H, W,
+                                        C, heads, g, scale, _dt(qkv2d), _stream()), "ogv_grid_attn_bwd")
         return dqkv, None, None, None, None, None, None, None
 
 
@@ -624,8 +765,9 @@ class _DwConv3x3(torch.autograd.Function):
         Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
         y = torch.empty((B * Ho * Wo, C), dtype=x2d.dtype, device=x2d.device)
         ws = _ws(lib.ogv_dwconv_fwd_ws_bytes(C), x2d.device)
-        check(lib.ogv_dwconv3x3_fwd(_ptr(x2d), _ptr(w), _ptr(bias), _ptr(y), B, H, W, C, stride, _ptr(ws), _dt(x2d),
-                                    _stream()), "ogv_dwconv3x3_fwd")
+        with _census("dwconv_fwd", dict(M=x2d.shape[0], Mo=y.shape[0], C=C, elem=x2d.element_size())):
+            check(lib.ogv_dwconv3x3_fwd(_ptr(x2d), _ptr(w), _ptr(bias), _ptr(y), B, H, W, C, stride, _ptr(ws), _dt(x2d),
+                                        _stream()), "ogv_dwconv3x3_fwd")
         ctx.save_for_backward(x2d, w)
         ctx.meta = (B, H, W, C, stride, bias is not None)
         return y
@@ -640,8 +782,9 @@ class _DwConv3x3(torch.autograd.Function):
         dw = torch.empty_like(w) if ctx.needs_input_grad[1] else None
         db = torch.empty((C,), dtype=torch.float32, device=x2d.device) if (has_bias and ctx.needs_input_grad[2]) else None
         ws = _ws(lib.ogv_dwconv_bwd_ws_bytes(B, H, W, C, stride), x2d.device)
-        check(lib.ogv_dwconv3x3_bwd(_ptr(dy), _ptr(x2d), _ptr(w), _ptr(dx), _ptr(dw), _ptr(db), B, H, W, C, stride,
-                                    _ptr(ws), _dt(x2d), _stream()), "ogv_dwconv3x3_bwd")
+        with _census("dwconv_bwd", dict(M=x2d.shape[0], Mo=dy.shape[0], C=C, elem=x2d.element_size())):
+            check(lib.ogv_dwconv3x3_bwd(_ptr(dy), _ptr(x2d), _ptr(w), _ptr(dx), _ptr(dw), _ptr(db), B, H, W, C, stride,
+                                        _ptr(ws), _dt(x2d), _stream()), "ogv_dwconv3x3_bwd")
         return dx, dw, db, None, None, None, None
 
 
@@ -657,6 +800,11 @@ def dwconv3x3_nchw(x, weight, bias=None, stride=1):
 # ------------------------------------------------------------------------------------------------
 # Fused MBConv (expand+BN1+act -> dw3x3+BN2+act -> SE -> project+BN3 -> +x)
 # ------------------------------------------------------------------------------------------------
+def _mb_units(geom, x2d):
+    B, H, W, C, mid, se = geom[:6]
+    return dict(M=B * H * W, B=B, C=C, mid=mid, se=se, elem=x2d.element_size())
+
+
 class _MBConv(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x2d, geom, buffers, *params):
@@ -669,8 +817,9 @@ class _MBConv(torch.autograd.Function):
         saved = torch.empty(lib.ogv_mbconv_saved_bytes(ctypes.byref(desc), dt), dtype=torch.uint8, device=x2d.device)
         ws = _ws(lib.ogv_mbconv_ws_bytes(ctypes.byref(desc), dt), x2d.device)
         out = torch.empty_like(x2d)
-        check(lib.ogv_mbconv_fwd(_ptr(x2d), _ptr(out), _ptr(saved), _ptr(ws), ctypes.byref(desc), ctypes.byref(P), dt,
-                                 _stream()), "ogv_mbconv_fwd")
+        with _census("mbconv_fwd", _mb_units(geom, x2d)):
+            check(lib.ogv_mbconv_fwd(_ptr(x2d), _ptr(out), _ptr(saved), _ptr(ws), ctypes.byref(desc), ctypes.byref(P),
+                                     dt, _stream()), "ogv_mbconv_fwd")
         ctx.save_for_backward(x2d, saved, *params)
         ctx.geom, ctx.buffers = geom, buffers
         return out
@@ -689,8 +838,9 @@ class _MBConv(torch.autograd.Function):
         dout = dout.to(x2d.dtype).contiguous()
         dx = torch.empty_like(x2d)
         ws = _ws(lib.ogv_mbconv_ws_bytes(ctypes.byref(desc), dt), x2d.device)
-        check(lib.ogv_mbconv_bwd(_ptr(dout), _ptr(x2d), _ptr(saved), _ptr(dx), ctypes.byref(G), _ptr(ws),
-                                 ctypes.byref(desc), ctypes.byref(P), dt, _stream()), "ogv_mbconv_bwd")
+        with _census("mbconv_bwd", _mb_units(ctx.geom, x2d)):
+            check(lib.ogv_mbconv_bwd(_ptr(dout), _ptr(x2d), _ptr(saved), _ptr(dx), ctypes.byref(G), _ptr(ws),
+                                     ctypes.byref(desc), ctypes.byref(P), dt, _stream()), "ogv_mbconv_bwd")
         return (dx, None, None, *grads)
 
 
@@ -732,8 +882,10 @@ class _ConvBN(torch.autograd.Function):
         out = torch.empty((B * Ho * Wo, Cout), dtype=x2d.dtype, device=x2d.device)
         saved = torch.empty(lib.ogv_convbn_saved_bytes(ctypes.byref(desc), dt), dtype=torch.uint8, device=x2d.device)
         ws = _ws(lib.ogv_convbn_ws_bytes(ctypes.byref(desc), dt), x2d.device)
-        check(lib.ogv_convbn_fwd(_ptr(x2d), _ptr(out), _ptr(saved), _ptr(ws), ctypes.byref(desc), ctypes.byref(P), dt,
-                                 _stream()), "ogv_convbn_fwd")
+        cu = dict(M=x2d.shape[0], Mo=out.shape[0], Cin=Cin, Cout=Cout, elem=x2d.element_size())
+        with _census("convbn_fwd", cu):
+            check(lib.ogv_convbn_fwd(_ptr(x2d), _ptr(out), _ptr(saved), _ptr(ws), ctypes.byref(desc), ctypes.byref(P),
+                                     dt, _stream()), "ogv_convbn_fwd")
         ctx.save_for_backward(x2d, saved, w, bias, bn_w, bn_b)
         ctx.geom = geom
         return out
@@ -752,8 +904,12 @@ class _ConvBN(torch.autograd.Function):
         dg = torch.empty_like(bn_w) if bn_w is not None else None
         dbb = torch.empty_like(bn_b) if bn_b is not None else None
         ws = _ws(lib.ogv_convbn_ws_bytes(ctypes.byref(desc), dt), x2d.device)
-        check(lib.ogv_convbn_bwd(_ptr(dout), _ptr(x2d), _ptr(saved), _ptr(dx), _ptr(dw), _ptr(db), _ptr(dg), _ptr(dbb),
-                                 _ptr(ws), ctypes.byref(desc), ctypes.byref(P), dt, _stream()), "ogv_convbn_bwd")
+        B, H, W, Cin, Cout = ctx.geom[:5]
+        cu = dict(M=x2d.shape[0], Mo=dout.shape[0], Cin=Cin, Cout=Cout, elem=x2d.element_size())
+        with _census("convbn_bwd", cu):
+            check(lib.ogv_convbn_bwd(_ptr(dout), _ptr(x2d), _ptr(saved), _ptr(dx), _ptr(dw), _ptr(db), _ptr(dg),
+                                     _ptr(dbb), _ptr(ws), ctypes.byref(desc), ctypes.byref(P), dt, _stream()),
+                  "ogv_convbn_bwd")
         return dx, None, None, None, dw, db, dg, dbb
 
 
@@ -786,8 +942,9 @@ class _BNAct(torch.autograd.Function):
         out = torch.empty_like(x2d)
         saved = torch.empty(lib.ogv_bn_act_saved_bytes(C) // 4, dtype=torch.float32, device=x2d.device)
         ws = _ws(lib.ogv_bn_act_ws_bytes(M, C), x2d.device)
-        check(lib.ogv_bn_act_fwd(_ptr(x2d), _ptr(out), _ptr(saved), _ptr(ws), _ptr(bn_w), _ptr(bn_b), _ptr(rm), _ptr(rv),
-                                 M, C, train, eps, mom, act, dt, _stream()), "ogv_bn_act_fwd")
+        with _census("bn_act_fwd", dict(M=M, C=C, train=train, elem=x2d.element_size())):
+            check(lib.ogv_bn_act_fwd(_ptr(x2d), _ptr(out), _ptr(saved), _ptr(ws), _ptr(bn_w), _ptr(bn_b), _ptr(rm),
+                                     _ptr(rv), M, C, train, eps, mom, act, dt, _stream()), "ogv_bn_act_fwd")
         ctx.save_for_backward(x2d, saved, bn_w, bn_b)
         ctx.meta = meta
         return out
@@ -804,8 +961,9 @@ class _BNAct(torch.autograd.Function):
         dg = torch.empty_like(bn_w) if bn_w is not None else None
         dbb = torch.empty_like(bn_b) if bn_b is not None else None
         ws = _ws(lib.ogv_bn_act_ws_bytes(M, C), x2d.device)
-        check(lib.ogv_bn_act_bwd(_ptr(dout), _ptr(x2d), _ptr(saved), _ptr(dx), _ptr(dg), _ptr(dbb), _ptr(ws), _ptr(bn_w),
-                                 M, C, train, act, dt, _stream()), "ogv_bn_act_bwd")
+        with _census("bn_act_bwd", dict(M=M, C=C, elem=x2d.element_size())):
+            check(lib.ogv_bn_act_bwd(_ptr(dout), _ptr(x2d), _ptr(saved), _ptr(dx), _ptr(dg), _ptr(dbb), _ptr(ws),
+                                     _ptr(bn_w), M, C, train, act, dt, _stream()), "ogv_bn_act_bwd")
         return dx, None, None, None, dg, dbb
 
 

@@ -64,6 +64,11 @@ def one_hot(targets: torch.Tensor, num_classes: int) -> torch.Tensor:
 
 
 def _soft_targets(targets, perm, K, lam_a, lam_b):
+    """Soft targets on the device.  Divergence from the reference, on purpose (no host sync): a label
+    outside [0, K) -- e.g. an ignore_index of -100 -- does not raise like F.one_hot
+    (cutmix_mixup_aug.py:6-7); its row becomes NaN, so that batch's loss is non-finite and the
+    Trainer's device guard skips the update and counts it in ``Trainer.nonfinite_steps`` (read it
+    per epoch).  The non-mix CE path (F.cross_entropy) instead ignores -100 labels."""
     _need_hip(targets, "ogv mix targets")
     t = targets.to(torch.int64).contiguous()
     out = torch.empty(t.shape[0], K, device=t.device, dtype=torch.float32)

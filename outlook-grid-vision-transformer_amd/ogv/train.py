@@ -192,6 +192,17 @@ def load_optimizer_state(optimizer: torch.optim.Optimizer, state_dict: dict):
         if isinstance(og["lr"], torch.Tensor):
             og["lr"].fill_(float(g["lr"]))
             g["lr"] = og["lr"]
+    for g in optimizer.param_groups:
+        if not (g.get("fused") or g.get("capturable")):
+            continue
+        # torch placed each state['step'] from the SAVED groups' flags: a plain (non-fused,
+        # non-capturable) AdamW checkpoint -- the reference's (src/training/train_full_model.py:56-57)
+        # -- leaves them as CPU scalars, which a fused / capturable step cannot use (and a captured
+        # graph would not record the CPU increment).  Move them next to their parameters.
+        for p in g["params"]:
+            st = optimizer.state.get(p)
+            if st and isinstance(st.get("step"), torch.Tensor) and st["step"].device != p.device:
+                st["step"] = st["step"].to(p.device, torch.float32)
     for p, st in optimizer.state.items():
         old = old_state.get(p, {})
         for k, v in list(st.items()):
@@ -202,12 +213,14 @@ def load_optimizer_state(optimizer: torch.optim.Optimizer, state_dict: dict):
 
 
 # ------------------------------------------------------------------------------- distributed
-def setup_distributed():
-    """One process per GPU (torchrun env).  Returns (rank, world, local_rank, device)."""
+def setup_distributed(cpu: bool = False):
+    """One process per GPU (torchrun env).  Returns (rank, world, local_rank, device).  The process
+    group uses "nccl" (= RCCL over xGMI on ROCm) on HIP devices, "gloo" on the CPU (``cpu=True``
+    forces the CPU: bench.py's launcher rehearsal and the world-2 tests)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if torch.cuda.is_available():
+    if not cpu and torch.cuda.is_available():
         torch.cuda.set_device(local)
         device = torch.device("cuda", local)
     else:
@@ -314,6 +327,7 @@ class Trainer:
             self._ng, self._nb = sum(self._sizes), sum(self._bsizes)
             self.flat = torch.zeros(self._ng + self._nb + 1, device=dev, dtype=torch.float32)
             self.meta = torch.zeros(self._nb + 1, device=dev, dtype=torch.float32)
+            self._zbuf = torch.zeros(self._nb, device=dev, dtype=torch.float32)   # a non-zero rank's buffer share
             self._buckets = []
             self._overlap = False
             if bucket_mb and bucket_mb > 0 and not self.graphs:
@@ -371,11 +385,14 @@ class Trainer:
         return loss.detach()
 
     def _meta_values(self, loss):
-        bscale = 1.0 if self.rank == 0 else 0.0
+        """[BatchNorm running buffers | non-finite flag]: rank 0 contributes its buffers, every other
+        rank contributes ZEROS (not b * 0: a non-finite running statistic on another rank -- a skipped
+        NaN batch still updates them in train mode -- would turn the sum into NaN on every rank)."""
         flag = self._found.view(1) if self.device_side else \
             torch.tensor([0.0 if bool(torch.isfinite(loss)) else 1.0], device=self.flat.device)
-        parts = [b.detach().reshape(-1).float() * bscale for b in self._bufs] + [flag]
-        return parts
+        if self.rank == 0:
+            return [b.detach().reshape(-1).float() for b in self._bufs] + [flag]
+        return [self._zbuf, flag]
 
     def _launch_meta(self, loss):
         torch.cat(self._meta_values(loss), out=self.meta)

@@ -153,6 +153,43 @@ def test_dp_nonfinite_loss_on_one_rank_skips_everywhere(tmp_path):
         assert d["nonfinite"] == 1 and d["sched"] == 1, d
 
 
+def _nan_train_worker(rank, world, port, out_dir, bucket_mb):
+    """Train-mode BatchNorm with a NaN batch on rank 1: rank 1's running statistics go NaN in its
+    forward, the step is skipped everywhere, and the buffer exchange (rank 0 contributes its values,
+    the others zeros -- not b * 0) leaves every rank holding rank 0's finite statistics."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        model = _model(seed=0)
+        tr = Trainer(model, amp_dtype=None, total_steps=10, warmup_ratio=0.0, bucket_mb=bucket_mb)
+        X, Y = _data()
+        model.train()
+        tr.step(X[0, rank * 4:(rank + 1) * 4], Y[0, rank * 4:(rank + 1) * 4])
+        before = [p.detach().clone() for p in model.parameters()]
+        x = X[1, rank * 4:(rank + 1) * 4].clone()
+        if rank == 1:
+            x[0, 0] = float("nan")
+        tr.step(x, Y[1, rank * 4:(rank + 1) * 4])
+        bufs = [b.clone() for b in model.buffers() if b.is_floating_point()]
+        torch.save({"same": all(torch.equal(a, b) for a, b in zip(before, model.parameters())), "bufs": bufs,
+                    "nonfinite": tr.nonfinite_steps}, os.path.join(out_dir, f"nant{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("bucket_mb", [8.0, 0.0])
+def test_dp_nonfinite_train_mode_keeps_bn_buffers_finite(tmp_path, bucket_mb):
+    mp.spawn(_nan_train_worker, args=(2, _free_port(), str(tmp_path), bucket_mb), nprocs=2, join=True)
+    d0 = torch.load(tmp_path / "nant0.pt", weights_only=True)
+    d1 = torch.load(tmp_path / "nant1.pt", weights_only=True)
+    for d in (d0, d1):
+        assert d["same"] and d["nonfinite"] == 1
+        assert all(torch.isfinite(b).all() for b in d["bufs"]), "a NaN rank poisoned the running statistics"
+    for a, b in zip(d0["bufs"], d1["bufs"]):
+        assert torch.equal(a, b)
+
+
 def test_nonfinite_loss_skips_step_host():
     """one_epoch_train.py:98-108: a non-finite loss skips the update and the schedule step."""
     model = _model(seed=0).eval()

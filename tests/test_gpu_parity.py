@@ -164,6 +164,9 @@ def test_golden_bf16(name):
     assert e <= bound, f"{name} bf16 fwd max|d| {e:.3e} > {bound:.3e} (torch {e_torch:.3e})"
     e = fx.maxabs(dx.float(), arr["dx"])
     assert e <= _tol(arr["dx"], 3e-2), f"{name} bf16 dx max|d| {e:.3e}"
+    # the trained quantity: bf16-path weight gradients (full or sketched) at 3e-2 of |ref|
+    grads = {k: p.grad for k, p in mod.named_parameters()}
+    assert fx.compare_grads(grads, arr, BF16_GRAD, 1e-4, name + " bf16") > 0
 
 
 def test_capture_attn_hook():
@@ -190,43 +193,54 @@ def test_outlook_attn_forward_hook_sees_logits():
     assert seen == [torch.Size([2, 36, 8, 8])]
 
 
-@pytest.mark.parametrize("fixture", ["model_a_7m", "model_a_14m", "model_b"])
-@pytest.mark.parametrize("mode", ["eval", "train"])
+MODEL_FIXTURES = [n for n in fx.fixture_names("model_a_") + fx.fixture_names("model_b_") if not n.endswith("_autocast")]
+# bf16 tolerances of the whole-model checks (north star: forward 1e-2 * max(1, |ref|); the trained
+# quantity -- every parameter's gradient norm and the sketched first / last block weight gradients --
+# at 3e-2, bf16 storage of activations and gradients with fp32 accumulation)
+BF16_FWD, BF16_GRAD = 1e-2, 3e-2
+
+
+@pytest.mark.parametrize("name", MODEL_FIXTURES)
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_model_logits(fixture, mode, dtype):
-    """Model A (MaxOutNet) and Model B (OutlookerFrontGridNet) logits / loss / grad norms vs the
-    reference's recorded values."""
-    meta, arr = fx.load(f"{fixture}_{mode}_b2")
-    ref_fn = (lambda x, p: orc.model_a(x, p, meta["stages"], train=(mode == "train"))) if meta["kind"] == "model_a" \
-        else (lambda x, p: orc.model_b(x, p, meta["stages"], meta["outlooker_front_depth"], train=(mode == "train")))
+def test_model_logits(name, dtype):
+    """Model A (MaxOutNet: 7M, 14M, 22M@224) and Model B (OutlookerFrontGridNet) logits, loss, grad
+    norms and weight-gradient sketches vs the reference's recorded values.  fp32: 1e-3 logits, 5e-3
+    gradients.  bf16: the plain 1e-2 * max(1, |ref|) forward bound with no allowance, and 3e-2 on the
+    gradients.  The train-mode B=2 fixtures (batch-statistics BatchNorm over two images, too
+    ill-conditioned for any bf16 storage) are fp32-only; their bf16 counterparts are the B=16 / B=8
+    train fixtures."""
+    meta, arr = fx.load(name)
+    mode = meta["mode"]
+    bf = dtype == torch.bfloat16
+    if bf and mode == "train" and name.endswith("_b2"):
+        pytest.skip("B=2 train-mode fixture: fp32 only (bf16 is held on the B=16 / B=8 train fixtures)")
     mod = _module(meta)
     gp.fill_module(mod, meta["seed"])
     mod = mod.to(DEV).train(mode == "train")
     x = torch.from_numpy(gp.input_from_spec(meta["x"])).to(DEV).contiguous(memory_format=torch.channels_last)
-    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=dtype == torch.bfloat16):
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=bf):
         logits = mod(x)
     loss = torch.nn.functional.cross_entropy(logits.float(), torch.from_numpy(arr["targets"]).to(DEV),
                                              label_smoothing=0.1)
     e = fx.maxabs(logits.detach().float(), arr["logits"])
-    if dtype == torch.float32:
-        assert e <= 1e-3, f"{fixture} {mode} fp32 logits max|d| {e:.3e}"
-    else:
-        # stock PyTorch bf16 autocast of the same model (oracle functions on the GPU)
-        p = {k: v.to(DEV) for k, v in fx.oracle_params(meta, requires_grad=False).items()}
-        with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
-            lt = ref_fn(x, p)
-        e_t = fx.maxabs(lt.float(), arr["logits"])
-        bound, e_emul = _bf16_bound(meta, arr, arr["logits"], lambda xx: ref_fn(xx, p), x)
-        print(f"{fixture} {mode}: bf16 logits max|d| ours {e:.3e} (bound {bound:.3e}, storage emulation {e_emul}) "
-              f"torch-autocast {e_t:.3e}")
-        assert e <= bound, f"{fixture} {mode} bf16 logits max|d| {e:.3e} > {bound:.3e} (torch autocast {e_t:.3e})"
+    ref_max = float(np.abs(arr["logits"]).max())
+    bound = (BF16_FWD if bf else 1e-3) * max(1.0, ref_max)
+    print(f"{name} {'bf16' if bf else 'fp32'}: logits max|d| {e:.3e} (bound {bound:.3e}, |ref| {ref_max:.3f}), "
+          f"loss {loss.item():.6f} vs {arr['loss'][0]:.6f}")
+    assert e <= bound, f"{name} logits max|d| {e:.3e} > {bound:.3e}"
+    lref = float(arr["loss"][0])
+    assert abs(loss.item() - lref) <= (BF16_FWD if bf else 1e-4) * max(1.0, lref)
     loss.backward()
     names = meta["param_names"]
     params = dict(mod.named_parameters())
     assert list(params) == names
     gn = np.array([params[k].grad.norm().item() if params[k].grad is not None else 0.0 for k in names])
-    if dtype == torch.float32:
-        np.testing.assert_allclose(gn, arr["grad_norms"], rtol=5e-3, atol=1e-5)
+    rtol, atol = (BF16_GRAD, 1e-4) if bf else (5e-3, 1e-5)
+    worst = np.max(np.abs(gn - arr["grad_norms"]) / (atol + rtol * np.abs(arr["grad_norms"])))
+    print(f"{name}: grad norms worst |d| / tol = {worst:.3f}")
+    np.testing.assert_allclose(gn, arr["grad_norms"], rtol=rtol, atol=atol)
+    n = fx.compare_grads({k: p.grad for k, p in params.items()}, arr, rtol, atol, name)
+    assert n > 0 or not any(k.startswith(("grad.", "gsketch.")) for k in arr)
 
 
 # ------------------------------------------------------------------ kernel level vs oracle

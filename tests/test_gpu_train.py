@@ -271,3 +271,85 @@ def test_model_b_step_with_cutmix_soft_targets():
     assert torch.isfinite(torch.tensor(l_eager)) and abs(l_replay - l_eager) <= 1e-3 * max(1.0, abs(l_eager))
     moved = sum(int(not torch.equal(a, b)) for a, b in zip(before, m.parameters()))
     assert moved > 0.9 * len(before)
+
+
+def test_resume_from_plain_adamw_checkpoint(tmp_path):
+    """A checkpoint written with the reference's optimizer -- a plain torch.optim.AdamW (not fused,
+    not capturable: src/training/train_full_model.py:56-57) -- resumes into a fresh graphs=True
+    Trainer: every state['step'] lands on the device as fp32 (torch leaves them as CPU scalars for
+    such a checkpoint), and the captured / replayed steps keep advancing them."""
+    import torch.nn.functional as F
+    from ogv.train import Trainer, param_groups_no_wd
+    from src.training.chekpoints import load_checkpoint, save_checkpoint
+    m0 = _model(12)
+    plain = torch.optim.AdamW(param_groups_no_wd(m0, 0.05), lr=5e-4)
+    for i in range(2):
+        x, y = _batch(8, 60 + i)
+        plain.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            loss = F.cross_entropy(m0(x).float(), y, label_smoothing=0.1)
+        loss.backward()
+        plain.step()
+    save_checkpoint(str(tmp_path / "plain.pt"), m0, plain, None, None, epoch=0, best_top1=0.0)
+    m1 = _model(13)
+    t = Trainer(m1, total_steps=20, warmup_ratio=0.1, graphs=True, capture_warmup=0)
+    load_checkpoint(str(tmp_path / "plain.pt"), m1, t.opt, None, None)
+    steps = [t.opt.state[p]["step"] for p in t.params]
+    assert all(s.device.type == "cuda" and s.dtype == torch.float32 and float(s) == 2.0 for s in steps)
+    for i in range(3):                               # capture (eager on a side stream), replay, replay
+        loss = t.step(*_batch(8, 70 + i))
+        assert torch.isfinite(loss).item()
+    torch.cuda.synchronize()
+    assert all(float(t.opt.state[p]["step"]) == 5.0 for p in t.params)
+
+
+def _dp_eval_worker(rank, world, port, out):
+    import os
+    import torch.distributed as dist
+    from ogv.train import Trainer
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import ogv
+    ogv.load()
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.backends.cudnn.benchmark = False
+        m = _model(21 + rank).eval()          # BN on running statistics: the shards then see the same model
+        t = Trainer(m, total_steps=50, warmup_ratio=0.1, graphs=True, capture_warmup=1)
+        for i in range(3):                    # eager, capture, replay
+            x, y = _batch(16, 80 + i)
+            t.step(x[rank * 8:(rank + 1) * 8].contiguous(memory_format=torch.channels_last), y[rank * 8:(rank + 1) * 8])
+        torch.save([p.detach().cpu() for p in m.parameters()], f"{out}/e{rank}.pt")
+    finally:
+        dist.destroy_process_group()
+
+
+def test_graph_dp_world2_matches_single_process(tmp_path):
+    """Graph-mode DP (graph A, all_reduce of the flat bucket, graph B) on two 8-image shards equals a
+    single-process graph-mode Trainer on the concatenated 16-image batch (BatchNorm in eval mode so
+    per-rank batch statistics do not enter): parameters within one AdamW step of lr per step (Adam
+    turns last-bit differences of near-zero gradients -- the row sums are split differently -- into
+    sign flips)."""
+    import socket
+    import torch.multiprocessing as mp
+    from ogv.train import Trainer
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    mp.spawn(_dp_eval_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    r0 = torch.load(tmp_path / "e0.pt", weights_only=True)
+    r1 = torch.load(tmp_path / "e1.pt", weights_only=True)
+    m = _model(21).eval()
+    t = Trainer(m, total_steps=50, warmup_ratio=0.1, graphs=True, capture_warmup=1)
+    for i in range(3):
+        t.step(*_batch(16, 80 + i))
+    init = [p.detach().cpu() for p in _model(21).parameters()]
+    lr_sum = 3 * 2 * 5e-4
+    d_dp = d_move = 0.0
+    for a, b, p, p0 in zip(r0, r1, m.parameters(), init):
+        assert torch.equal(a, b), "ranks diverged"
+        err = float((a - p.detach().cpu()).abs().max())
+        assert err <= lr_sum + 1e-6, err
+        d_dp += float((a - p.detach().cpu()).double().norm() ** 2)
+        d_move += float((p.detach().cpu() - p0).double().norm() ** 2)
+    # the DP trajectory differs from the single-process one by far less than the training moved
+    assert d_dp ** 0.5 <= 0.25 * d_move ** 0.5, (d_dp ** 0.5, d_move ** 0.5)

@@ -90,7 +90,7 @@ def main():
         y = torch.empty_like(v)
         st = torch.cuda.current_stream().cuda_stream
         us = timeit(lambda: lib.ogv_outlook_agg_fwd(v.data_ptr(), lg.data_ptr(), y.data_ptr(), a.batch, H, H, C, h, 3,
-                                                     9 * h, 1, st), a.reps)
+                                                     9 * h, C, 1, st), a.reps)   # ld_logits, ld_v, dtype
         rec("outlook", f"s{C}.fwd", M, C, 9 * h, us, 2 * M * (2 * C + 9 * h), 18 * M * C)
         # grid attention
         qkv = torch.randn(M, 3 * C, device=dev, dtype=bf)

@@ -200,6 +200,7 @@ void set_grid_big(int v);
 void set_split_w(int v);
 void set_outlook_tile(int v);
 void set_outlook_vproj(int v);
+void set_vp_dbg(int v);
 void set_pg_split(int v);
 int split_w();
 

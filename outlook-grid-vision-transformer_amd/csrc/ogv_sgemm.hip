@@ -53,6 +53,11 @@ __global__ __launch_bounds__(SG_NW * 64) void sgemm_bf16_kernel(const bf16* __re
   bf16* Wl = Ws + (size_t)nbp * KP;  // SW: lo tile
   double* sacc = reinterpret_cast<double*>(smem + (size_t)nbp * KP * 2 * (SW ? 2 : 1));
   float* cvec = reinterpret_cast<float*>(sacc + (STATS ? SG_NW * 2 * nbp : 0));  // [bias | stat shift]
+  // prologue variants: [sc | sh] (K each) and one gate row per wave (the SE gate of the image the
+  // wave's current panel belongs to), so the prologue reads no global memory of its own
+  constexpr int KK = KT * 32;
+  float* pvec = cvec + 2 * nbp;                 // PA >= 0: [sc | sh]
+  float* gsl = pvec + 2 * KK + wave * KK;       // PA >= 0: this wave's gate row
 
   // ---- weight tile -> LDS (bf16), zero outside [0,nb) x [0,K).  Batches of SG_WB independent
   // 16-B loads per thread are issued before any is consumed, so staging costs a few L2 round trips
@@ -136,6 +141,12 @@ __global__ __launch_bounds__(SG_NW * 64) void sgemm_bf16_kernel(const bf16* __re
   if constexpr (STATS) {
     for (int i = lane; i < 2 * nbp; i += 64) sacc[wave * 2 * nbp + i] = 0.0;
   }
+  if constexpr (PA >= 0) {
+    for (int k = tid; k < KK; k += SG_NW * 64) {
+      pvec[k] = (pro.sc && k < K) ? pro.sc[k] : 1.f;
+      pvec[KK + k] = (pro.sh && k < K) ? pro.sh[k] : 0.f;
+    }
+  }
   for (int c = tid; c < nbp; c += SG_NW * 64) {
     cvec[c] = (epi.bias && c < nb) ? epi.bias[n0 + c] : 0.f;
     if (STATS) cvec[nbp + c] = (epi.stat_shift && c < nb) ? bn_shift(epi.stat_shift[n0 + c]) : 0.f;
@@ -148,6 +159,17 @@ __global__ __launch_bounds__(SG_NW * 64) void sgemm_bf16_kernel(const bf16* __re
   const bf16* res = static_cast<const bf16*>(epi.res);
   const bf16* Z = static_cast<const bf16*>(epi.Z);
 
+  // gate row of panel pp (pipelined prologue: every row of a panel belongs to one image), raw:
+  // lane holds gate[img][lane + 64 u]
+  constexpr int GPL = (KK + 63) / 64;
+  auto fetch_gate = [&](long pp, float (&g)[GPL]) {
+    if constexpr (PA >= 0) {
+      const long mi = pp * 16 * RS;
+      const float* gp = pro.gate + (mi < M ? mi / pro.rps : 0) * pro.gld;
+#pragma unroll
+      for (int u = 0; u < GPL; ++u) g[u] = (lane + 64 * u < K) ? gp[lane + 64 * u] : 1.f;
+    }
+  };
   // A fragments (+ row scales) of panel pp, raw
   auto fetch = [&](long pp, bf16x8 (&dst)[RS][KT], float (&rs)[RS]) {
 #pragma unroll
@@ -167,10 +189,18 @@ __global__ __launch_bounds__(SG_NW * 64) void sgemm_bf16_kernel(const bf16* __re
   // taken, so a wave keeps two panels of loads in flight across its MFMAs and stores (knob
   // "sg_prefetch").  With a prologue its sc / sh / gate loads would wait on that prefetch
   // (in-order vmcnt), so those variants fetch each panel when they reach it.
-  const bool pipe = PA < 0 && pf;
+  // With a prologue the pipeline stays on when its operands come from LDS: sc / sh (staged above)
+  // and a gate that is constant over a panel (16 RS | rows per image): the gate row is prefetched
+  // with the panel and parked in a wave-private LDS row.
+  const bool gate_rows = PA >= 0 && pro.gate != nullptr;
+  const bool pipe = pf && (PA < 0 || !gate_rows || pro.rps % (16 * RS) == 0);
   bf16x8 an[RS][KT];
   float rsn[RS];
-  if (pipe && (long)blockIdx.x * SG_NW + wave < P) fetch((long)blockIdx.x * SG_NW + wave, an, rsn);
+  float gn[GPL];
+  if (pipe && (long)blockIdx.x * SG_NW + wave < P) {
+    fetch((long)blockIdx.x * SG_NW + wave, an, rsn);
+    if (gate_rows) fetch_gate((long)blockIdx.x * SG_NW + wave, gn);
+  }
 
   for (long p = (long)blockIdx.x * SG_NW + wave; p < P; p += GW) {
     const long mp = p * 16 * RS;
@@ -186,11 +216,47 @@ __global__ __launch_bounds__(SG_NW * 64) void sgemm_bf16_kernel(const bf16* __re
 #pragma unroll
         for (int kt = 0; kt < KT; ++kt) a[i][kt] = an[i][kt];
       }
-      if (p + GW < P) fetch(p + GW, an, rsn);
+      if (gate_rows) {   // park this panel's gate row before its registers are reused
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int u = 0; u < GPL; ++u)
+          if (lane + 64 * u < KK) gsl[lane + 64 * u] = gn[u];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
+      if (p + GW < P) {
+        fetch(p + GW, an, rsn);
+        if (gate_rows) fetch_gate(p + GW, gn);
+      }
     } else {
       fetch(p, a, rsc);
     }
     if constexpr (PA >= 0) {
+      if (pipe) {   // sc / sh / gate from LDS (broadcast reads: the 16 lanes of a column group agree)
+#pragma unroll
+        for (int i = 0; i < RS; ++i) {
+#pragma unroll
+          for (int kt = 0; kt < KT; ++kt) {
+            const int k = kt * 32 + fg * 8;
+            if (m[i] < M && k < K) {
+              float f[8], sc[8], sh[8], g8[8];
+              load_vec<float, 8>(pvec + k, sc);
+              load_vec<float, 8>(pvec + KK + k, sh);
+              if (gate_rows) load_vec<float, 8>(gsl + k, g8);
+#pragma unroll
+              for (int q = 0; q < 8; ++q) {
+                f[q] = act_fwd(PA, fmaf((float)a[i][kt][q], sc[q], sh[q]));
+                if (gate_rows) f[q] *= g8[q];
+                a[i][kt][q] = (bf16)f[q];
+              }
+            }
+          }
+        }
+      }
+    }
+    if constexpr (PA >= 0) if (!pipe) {
 #pragma unroll
       for (int i = 0; i < RS; ++i) {
 #pragma unroll
@@ -417,8 +483,9 @@ static SgPlan sgemm_plan_w(int M, int N, int K, bool stats, bool prologue, bool 
   const int KP = KT * 32 + 8;
   p.KT = KT;
   p.RS = KT <= 2 ? 2 : 1;
-  auto lds_of = [&](int nb) {  // nb padded to the chunk
-    return (size_t)nb * KP * 2 * wtiles + (stats ? (size_t)SG_NW * 2 * nb * 8 : 0) + (size_t)nb * 8;
+  auto lds_of = [&](int nb) {  // nb padded to the chunk (+ the prologue's [sc | sh] and per-wave gate rows)
+    return (size_t)nb * KP * 2 * wtiles + (stats ? (size_t)SG_NW * 2 * nb * 8 : 0) + (size_t)nb * 8 +
+           (prologue ? (size_t)(2 + SG_NW) * KT * 32 * 4 : 0);
   };
   // widest tile (multiple of the 64-column chunk) whose bf16 copy fits next to the staging slabs
   int NB = (N + SG_CW - 1) / SG_CW * SG_CW;

@@ -23,12 +23,20 @@ SHAPES = [("7m_s0", 512, 48, 2, 32), ("7m_s1", 512, 96, 3, 16), ("14m_s0", 256, 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE")
+    ap.add_argument("--shapes", default="", help="comma list of shape names (default all)")
+    ap.add_argument("--kinds", default="unfused,fused_train,fused_eval")
     a = ap.parse_args()
     ogv.load()
     lib = load()
+    for o in a.opt:
+        k, v = o.split("=")
+        assert lib.ogv_set_option(k.encode(), int(v)) == 0, o
     s = lambda: OF._stream()  # noqa: E731
     flush = torch.empty(512 << 20, dtype=torch.uint8, device="cuda")
     for name, B, C, h, S in SHAPES:
+        if a.shapes and name not in a.shapes.split(","):
+            continue
         M = B * S * S
         ld = (C + 9 * h + 7) // 8 * 8
         x = torch.randn(M, C, device="cuda").to(torch.bfloat16)
@@ -52,6 +60,8 @@ def main():
                   "fused_eval": 2 * M * 2 * C}
         row = [f"{name:7s} M={M:8d}"]
         for kind, fn in runs.items():
+            if kind not in a.kinds.split(","):
+                continue
             ts = []
             for _ in range(a.reps):
                 flush.zero_()
@@ -63,7 +73,7 @@ def main():
             torch.cuda.synchronize()
             ms = sorted(u.elapsed_time(v) for u, v in ts)[len(ts) // 2]
             row.append(f"{kind} {ms * 1e3:8.1f}us {nbytes[kind] / ms / 1e6:6.0f}GB/s")
-        print("  ".join(row), flush=True)
+        print("  ".join(row) + (f"  {a.opt}" if a.opt else ""), flush=True)
 
 
 if __name__ == "__main__":

@@ -46,9 +46,13 @@ const char* ogv_last_error(void);
  *   "bk64_max_m": largest M using 64-wide k-steps in the tiled GEMM; "grid_mfma" 1/0: MFMA grid
  *   attention for bf16; "dw_blocks" (default 0 = ~32 rows per block): target block count of the
  *   depthwise kernels; "mb_side" 1/0: weight gradients of the fused MBConv backward on a side stream;
- *   "ln_bwd_blocks" (default 1024): grid cap of the LayerNorm backward; "sg_prefetch" 1/0: next-panel
- *   register prefetch in the streaming GEMM; "sg_per_cu" (default 2): streaming-GEMM workgroups per CU;
- *   "splitk_max" (default 32): K-slab cap of the fp32 split-K GEMM (SE MLP).
+ *   "ln_bwd_blocks" (default 1024): grid cap of the LayerNorm backward; "sg_prefetch" (bit mask, default 3):
+ *   bit 1 next-panel register prefetch in the streaming GEMM, bit 2 also for its prologue variants;
+ *   "sg_per_cu" (default 2): streaming-GEMM workgroups per CU; "splitk_max" (default 32): K-slab
+ *   cap of the fp32 split-K GEMM; "se_gemv" 1 (default) / 0: the Squeeze-Excite MLP on the GEMV
+ *   kernels of ogv_se.hip instead of split-K GEMM + reduce; "outlook_vproj" 0/1/2: fused Outlooker
+ *   projection + aggregation never / inference (default) / also training; "vp_dbg", "pg_dbg":
+ *   phase-skipping timing experiments (wrong results).
  * Returns OGV_ERR_ARG for an unknown name. */
 int ogv_set_option(const char* name, int value);
 /* Diagnostics (no reference counterpart): which kernel ogv_gemm_fwd (kind 0) / ogv_gemm_dgrad

@@ -201,6 +201,12 @@ void set_split_w(int v);
 void set_outlook_tile(int v);
 void set_outlook_vproj(int v);
 void set_vp_dbg(int v);
+// Squeeze-Excite GEMVs (ogv_se.hip); knob "se_gemv" (1 default, 0 = the split-K tiled GEMM + reduce)
+void se_gemv_launch(const float* in, int ldi, int pro_act, const float* W, int ldw, const float* bias,
+                    const float* Z, int ldz, int zact, float* out, int ldo, float* sig_out, int B, int N, int K,
+                    bool rm, hipStream_t s);
+bool se_gemv_on();
+void set_se_gemv(int v);
 void set_pg_split(int v);
 int split_w();
 

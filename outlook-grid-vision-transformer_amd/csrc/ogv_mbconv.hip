@@ -1345,13 +1345,21 @@ static void mbconv_fwd_impl(const void* x, void* out, const Saved& sv, const Fwd
     OGV_V_DISPATCH(rp.V, O::template pool, sv.d, sv.sc2, sv.sh2, s.act, sv.pooled, s.B, HW, s.mid, rp, st);
     Epi e1;
     e1.bias = P.se_b1;
-    gemm_fwd_splitk_f32(sv.pooled, s.mid, Pro(), P.se_w1, s.mid, sv.z1, s.se, s.B, s.se, s.mid, e1, w.split, st);
+    if (se_gemv_on())
+      se_gemv_launch(sv.pooled, s.mid, OGV_ACT_NONE, P.se_w1, s.mid, P.se_b1, nullptr, 0, 0, sv.z1, s.se, nullptr, s.B,
+                     s.se, s.mid, false, st);
+    else
+      gemm_fwd_splitk_f32(sv.pooled, s.mid, Pro(), P.se_w1, s.mid, sv.z1, s.se, s.B, s.se, s.mid, e1, w.split, st);
     Pro p2;
     p2.act = s.act;
     Epi e2;
     e2.bias = P.se_b2;
-    gemm_fwd_splitk_f32(sv.z1, s.se, p2, P.se_w2, s.se, sv.z2, s.mid, s.B, s.mid, s.se, e2, w.split, st, false,
-                        sv.gate);  // gate = sigmoid(z2) written by the split-K reduce
+    if (se_gemv_on())   // gate = sigmoid(z2) written by the same launch
+      se_gemv_launch(sv.z1, s.se, s.act, P.se_w2, s.se, P.se_b2, nullptr, 0, 0, sv.z2, s.mid, sv.gate, s.B, s.mid,
+                     s.se, false, st);
+    else
+      gemm_fwd_splitk_f32(sv.z1, s.se, p2, P.se_w2, s.se, sv.z2, s.mid, s.B, s.mid, s.se, e2, w.split, st, false,
+                          sv.gate);  // gate = sigmoid(z2) written by the split-K reduce
   }
   // 4) project GEMM on act(BN2(d)) * gate (+ BN3 stats), then out = x + BN3(p)
   {
@@ -1422,13 +1430,21 @@ static void mbconv_bwd_impl(const void* dout, const void* x, const Saved& sv, vo
       e.Z = sv.z1;
       e.ldz = s.se;
       e.zact = s.act;
-      gemm_fwd_splitk_f32(w.dz2, s.mid, Pro(), P.se_w2, s.se, w.dz1, s.se, s.B, s.se, s.mid, e, w.split, st, true);
+      if (se_gemv_on())
+        se_gemv_launch(w.dz2, s.mid, OGV_ACT_NONE, P.se_w2, s.se, nullptr, sv.z1, s.se, s.act, w.dz1, s.se, nullptr,
+                       s.B, s.se, s.mid, true, st);
+      else
+        gemm_fwd_splitk_f32(w.dz2, s.mid, Pro(), P.se_w2, s.se, w.dz1, s.se, s.B, s.se, s.mid, e, w.split, st, true);
     }
     gemm_wgrad_launch(OGV_F32, w.dz1, s.se, sv.pooled, s.mid, Pro(), nullptr, 1, G.se_w1, G.se_b1, s.B, s.se, s.mid,
                       w.gemm, fork_side(st));
     {  // dpool = dz1 . W1:  W1 [se, mid] read reduction-major
-      gemm_fwd_splitk_f32(w.dz1, s.se, Pro(), P.se_w1, s.mid, w.dpool, s.mid, s.B, s.mid, s.se, Epi(), w.split, st,
-                          true);
+      if (se_gemv_on())
+        se_gemv_launch(w.dz1, s.se, OGV_ACT_NONE, P.se_w1, s.mid, nullptr, nullptr, 0, 0, w.dpool, s.mid, nullptr, s.B,
+                       s.mid, s.se, true, st);
+      else
+        gemm_fwd_splitk_f32(w.dz1, s.se, Pro(), P.se_w1, s.mid, w.dpool, s.mid, s.B, s.mid, s.se, Epi(), w.split, st,
+                            true);
     }
   }
   // B5) BN2 backward: dd = ca*(dy2 - cb - dhat*cc)  -> bufB

@@ -1224,6 +1224,25 @@ static long vtile_rs_cycles(const VTile& t, int C, int heads, int ldc, int RP) {
   return tot;
 }
 
+// the least-conflicted result-tile pitch (the model above), memoised per tile geometry: the search
+// costs ~1 ms of host time, so it must not run on every launch
+static int vtile_best_rp(const VTile& t, int C, int heads, int ldc) {
+  struct Entry { int C, heads, ldc, TH, TW, rp; };
+  static Entry cache[64];
+  static int n = 0;
+  for (int i = 0; i < n; ++i)
+    if (cache[i].C == C && cache[i].heads == heads && cache[i].ldc == ldc && cache[i].TH == t.TH && cache[i].TW == t.TW)
+      return cache[i].rp;
+  int rp_best = t.ncol;
+  long best = -1;
+  for (int rp = t.ncol; rp <= t.ncol + 72; rp += 8) {
+    const long c = vtile_rs_cycles(t, C, heads, ldc, rp);
+    if (best < 0 || c < best) { best = c; rp_best = rp; }
+  }
+  if (n < 64) cache[n++] = Entry{C, heads, ldc, t.TH, t.TW, rp_best};
+  return rp_best;
+}
+
 // knob "outlook_vproj": 0 = never, 1 = for inference (no cat written; default), 2 = also in training.
 // Measured (tools/bench_vproj.py, cold L2, bs = 512 / 256 / 128): inference 7M stage 0 82 vs 91 us
 // unfused, 14M stage 0 195 vs 201 us, 7M stage 1 / 22M stage 0 within 1-3 %; training (the cat
@@ -1262,12 +1281,7 @@ static bool vproj_plan(int B, int H, int W, int C, int heads, int k, int ldc, og
     // group on 16 distinct bank quads (KP = 32, 64, 96: conflict-free by the bank model)
     t.XP = KP + 16;
     t.WP = KP + 16;
-    t.RP = t.ncol;
-    long best = -1;
-    for (int rp = t.ncol; rp <= t.ncol + 72; rp += 8) {   // the least-conflicted result-tile pitch
-      const long c = vtile_rs_cycles(t, C, heads, ldc, rp);
-      if (best < 0 || c < best) { best = c; t.RP = rp; }
-    }
+    t.RP = vtile_best_rp(t, C, heads, ldc);
     const size_t lds = vtile_lds(t, heads, true);
     ok = pass == 2 ? lds <= 160 * 1024 : lds <= 80 * 1024;
   }

@@ -154,6 +154,10 @@ extern "C" int ogv_set_option(const char* name, int value) {
     set_outlook_vproj(value);
     return OGV_OK;
   }
+  if (!strcmp(name, "se_gemv")) {
+    set_se_gemv(value);
+    return OGV_OK;
+  }
   if (!strcmp(name, "vp_dbg")) {
     set_vp_dbg(value);
     return OGV_OK;

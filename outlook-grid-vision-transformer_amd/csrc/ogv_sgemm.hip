@@ -193,7 +193,7 @@ __global__ __launch_bounds__(SG_NW * 64) void sgemm_bf16_kernel(const bf16* __re
   // and a gate that is constant over a panel (16 RS | rows per image): the gate row is prefetched
   // with the panel and parked in a wave-private LDS row.
   const bool gate_rows = PA >= 0 && pro.gate != nullptr;
-  const bool pipe = pf && (PA < 0 || !gate_rows || pro.rps % (16 * RS) == 0);
+  const bool pipe = (pf & 1) && (PA < 0 || ((pf & 2) && (!gate_rows || pro.rps % (16 * RS) == 0)));
   bf16x8 an[RS][KT];
   float rsn[RS];
   float gn[GPL];
@@ -425,8 +425,10 @@ void set_sgemm_mode(int v) { g_sgemm_mode = v; }
 static int g_sg_per_cu = 2;     // workgroups per CU the planner asks for (tuning knob "sg_per_cu"),
                                 // clamped at launch to the kernel's real occupancy
 void set_sg_per_cu(int v) { g_sg_per_cu = v < 1 ? 1 : (v > 4 ? 4 : v); }
-static int g_sg_prefetch = 1;   // knob "sg_prefetch": next-panel register prefetch (no-prologue variants)
-void set_sg_prefetch(int v) { g_sg_prefetch = v ? 1 : 0; }
+// knob "sg_prefetch": bit 1 next-panel register prefetch, bit 2 also for the prologue variants
+// (sc / sh / gate then come from LDS); default 3
+static int g_sg_prefetch = 3;
+void set_sg_prefetch(int v) { g_sg_prefetch = v & 3; }
 static int g_sg_wgs = 0;
 void set_sg_wgs(int v) { g_sg_wgs = v < 0 ? 0 : v; }
 static int g_sg_min_m = 65536;  // smallest M routed to the streaming kernels (tuning knob "sgemm_min_m")

@@ -16,6 +16,7 @@ typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((ext_vector_type(4))) short s16x4;
 
 namespace ogv {
+int skip_mask();   // knob "skip" (ogv_gemm.hip): what-if timing experiments only
 
 // BatchNorm batch statistics are accumulated as sums shifted by the running mean (fp64).  A
 // non-finite running mean (a NaN batch poisons it, exactly as in torch's BatchNorm2d) must not

@@ -207,7 +207,10 @@ void se_gemv_launch(const float* in, int ldi, int pro_act, const float* W, int l
                     bool rm, hipStream_t s);
 bool se_gemv_on();
 void set_se_gemv(int v);
+void set_dw_fuse(int v);
 void set_pg_split(int v);
 int split_w();
+int skip_mask();
+void set_skip(int v);
 
 }  // namespace ogv

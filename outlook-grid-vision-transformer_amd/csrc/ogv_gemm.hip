@@ -1039,6 +1039,12 @@ static bool use_bk64(int M, int K, int ncols, bool pro, bool zact) {
 static int g_split_w = 1;
 void set_split_w(int v) { g_split_w = v & 3; }
 int split_w() { return g_split_w; }
+// knob "skip" (timing what-if experiments only -- outputs are left unwritten): bit 1 panel GEMMs,
+// 2 streaming GEMMs, 4 weight gradients (wgrad / swgrad launches), 8 MBConv depthwise kernels,
+// 16 LayerNorm, 32 grid attention, 64 Outlooker aggregation
+static int g_skip = 0;
+int skip_mask() { return g_skip; }
+void set_skip(int v) { g_skip = v; }
 #define OGV_SW_LAUNCH(COND, KERN, grid, s, ...)  \
   do {                                           \
     if (COND) {                                  \
@@ -1411,6 +1417,7 @@ static void launch_wgrad_bf16(const WgradPlan& p, const void* G, int ldg, const 
 void gemm_wgrad_launch(ogv_dtype dt, const void* G, int ldg, const void* X, int ldx, const Pro& pro, const float* rs,
                        int rps, float* dW, float* dbias, int M, int N, int K, void* ws, hipStream_t s,
                        const ConvG* xc) {
+  if (skip_mask() & 4) return;
   if (M <= 0) {
     (void)hipMemsetAsync(dW, 0, (size_t)N * K * sizeof(float), s);
     if (dbias) (void)hipMemsetAsync(dbias, 0, (size_t)N * sizeof(float), s);

@@ -420,6 +420,7 @@ using namespace ogv;
 
 extern "C" int ogv_grid_attn_fwd(const void* qkv, void* out, float* lse, float* probs, int B, int H, int W, int C,
                                  int heads, int g, float scale, ogv_dtype dt, void* stream) {
+  if (skip_mask() & 32) return OGV_OK;
   OGV_REQUIRE(qkv && out && lse, "ogv_grid_attn_fwd: null pointer");
   GridGeom G;
   int rc = make_geom(G, B, H, W, C, heads, g, dt, "ogv_grid_attn_fwd");
@@ -435,6 +436,7 @@ extern "C" int ogv_grid_attn_fwd(const void* qkv, void* out, float* lse, float* 
 extern "C" int ogv_grid_attn_bwd(const void* dout, const void* qkv, const void* out, const float* lse, void* dqkv,
                                  float* delta_ws, int B, int H, int W, int C, int heads, int g, float scale,
                                  ogv_dtype dt, void* stream) {
+  if (skip_mask() & 32) return OGV_OK;
   OGV_REQUIRE(dout && qkv && out && lse && dqkv && delta_ws, "ogv_grid_attn_bwd: null pointer");
   GridGeom G;
   int rc = make_geom(G, B, H, W, C, heads, g, dt, "ogv_grid_attn_bwd");

@@ -491,14 +491,19 @@ __global__ __launch_bounds__(256) void dw_fwd_tile_kernel(const T* __restrict__ 
   if (stat) dw_reduce_store<2, V, double>(q, ring, t.chunks, stat + ti.rid * 2 * t.C, t.C, t.C, ti.ct * t.CT);
 }
 
-// dy1 = (dw3x3^T dd) * act'(e*sc1 + sh1) -> out; stats: sum dy1, sum dy1*(e - mean1)*invstd1
-template <typename T, int V, int LDQ, int ACT>
+// dy1 = (dw3x3^T dd) * act'(e*sc1 + sh1) -> out; stats: sum dy1, sum dy1*(e - mean1)*invstd1.
+// WG: the weight gradient in the same pass -- dW[tap] = sum_p dd[p] a[p + tap] = sum_q a[q] dd[q - tap]
+// with a = act(e*sc1 + sh1): the transposed conv already reads dd[q - tap] for every tap of output
+// pixel q and loads e[q], so the 9 partial sums cost 9 FMAs per element and no second pass over dd
+// and e (part[rid][tap][c], as dw_wgrad_tile_kernel writes them)
+template <typename T, int V, int LDQ, int ACT, bool WG = false>
 __global__ __launch_bounds__(256) void dw_dgrad_tile_kernel(const T* __restrict__ dd, const float* __restrict__ wdw,
                                                             const T* __restrict__ e, const float* __restrict__ sc,
                                                             const float* __restrict__ sh,
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ invstd, int act,
-                                                            T* __restrict__ out, float* __restrict__ stat, DwTile t) {
+                                                            T* __restrict__ out, float* __restrict__ stat, DwTile t,
+                                                            float* __restrict__ part = nullptr) {
   extern __shared__ __attribute__((aligned(16))) float ring[];
   TileIdx ti;
   if (!tile_idx(t, ti)) return;
@@ -518,6 +523,11 @@ __global__ __launch_bounds__(256) void dw_dgrad_tile_kernel(const T* __restrict_
   float q[2][V];
 #pragma unroll
   for (int i = 0; i < V; ++i) { q[0][i] = 0.f; q[1][i] = 0.f; }
+  float q9[WG ? 9 : 1][V];
+#pragma unroll
+  for (int k = 0; k < (WG ? 9 : 1); ++k)
+#pragma unroll
+    for (int i = 0; i < V; ++i) q9[k][i] = 0.f;
   const int cc = cok ? c : 0;
   RawVec<T, V> ce[DW_R];  // e at this thread's output pixel of the current rows
   auto pre = [&](VRow q, int px) {
@@ -528,9 +538,12 @@ __global__ __launch_bounds__(256) void dw_dgrad_tile_kernel(const T* __restrict_
     const long off = ((b * t.H + y) * t.W + ti.x0 + px) * t.C + c;
     float ev[V];
     ce[r].unpack(ev);
-    float acc[V];
+    float acc[V], av[V];
 #pragma unroll
-    for (int i = 0; i < V; ++i) acc[i] = 0.f;
+    for (int i = 0; i < V; ++i) {
+      acc[i] = 0.f;
+      if constexpr (WG) av[i] = act_fwd(ACT, fmaf(ev[i], s[i], h[i]));
+    }
 #pragma unroll
     for (int ki = 0; ki < 3; ++ki)
 #pragma unroll
@@ -544,6 +557,12 @@ __global__ __launch_bounds__(256) void dw_dgrad_tile_kernel(const T* __restrict_
           acc[i + 1] = fmaf(w[ki * 3 + kj][i + 1], a.y, acc[i + 1]);
           acc[i + 2] = fmaf(w[ki * 3 + kj][i + 2], a.z, acc[i + 2]);
           acc[i + 3] = fmaf(w[ki * 3 + kj][i + 3], a.w, acc[i + 3]);
+          if constexpr (WG) {
+            q9[ki * 3 + kj][i] = fmaf(av[i], a.x, q9[ki * 3 + kj][i]);
+            q9[ki * 3 + kj][i + 1] = fmaf(av[i + 1], a.y, q9[ki * 3 + kj][i + 1]);
+            q9[ki * 3 + kj][i + 2] = fmaf(av[i + 2], a.z, q9[ki * 3 + kj][i + 2]);
+            q9[ki * 3 + kj][i + 3] = fmaf(av[i + 3], a.w, q9[ki * 3 + kj][i + 3]);
+          }
         }
       }
     float o2[V];
@@ -556,6 +575,7 @@ __global__ __launch_bounds__(256) void dw_dgrad_tile_kernel(const T* __restrict_
     store_vec<T, V>(out + off, o2);
   });
   dw_reduce_store<2, V, float>(q, ring, t.chunks, stat + ti.rid * 2 * t.C, t.C, t.C, ti.ct * t.CT);
+  if constexpr (WG) dw_reduce_store<9, V, float>(q9, ring, t.chunks, part + ti.rid * 9 * t.C, t.C, t.C, ti.ct * t.CT);
 }
 
 // dWdw partials: part[rid][tap][c] = sum over the block's pixels dd[p,c] * act(e*sc1+sh1)[p+tap, c]
@@ -1138,6 +1158,9 @@ static BwdWs bwd_ws_layout(void* base, const ogv_mbconv_desc& s, size_t esz, siz
 // captured hipGraph (the side stream joins the capture).  Knob "mb_side" (default 1).
 static int g_mb_side = 1;
 void set_mb_side(int v) { g_mb_side = v; }
+// knob "dw_fuse": 1 (default) = the depthwise data and weight gradients in one pass over (dd, e)
+static int g_dw_fuse = 1;
+void set_dw_fuse(int v) { g_dw_fuse = v; }
 struct SideStream {
   hipStream_t s = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
@@ -1193,6 +1216,7 @@ struct Ops {
   }
   static void dw_fwd(const void* e, const float* w, const float* sc, const float* sh, int act, void* out, double* stat,
                      const float* shift, const DwTile& t, hipStream_t st) {
+    if (skip_mask() & 8) return;
     constexpr int V = 4;
     const size_t lds = t.lds_bytes(2, V, sizeof(double));
     OGV_DW_ACT(act, if (t.ldq <= 1) dw_fwd_tile_kernel<T, V, 1, A><<<dw_grid(t), 256, lds, st>>>(
@@ -1202,20 +1226,27 @@ struct Ops {
                else dw_fwd_tile_kernel<T, V, 3, A><<<dw_grid(t), 256, lds, st>>>(
                         (const T*)e, w, sc, sh, act, (T*)out, stat, shift, t))
   }
+  // part != nullptr: the weight-gradient partials in the same pass (dw_dgrad_tile_kernel<.., WG>)
   static void dw_dgrad(const void* dd, const float* w, const void* e, const float* sc, const float* sh,
                        const float* mean, const float* inv, int act, void* out, float* stat, const DwTile& t,
-                       hipStream_t st) {
+                       hipStream_t st, float* part = nullptr) {
+    if (skip_mask() & 8) return;
     constexpr int V = 4;
-    const size_t lds = t.lds_bytes(2, V, sizeof(float));
-    OGV_DW_ACT(act, if (t.ldq <= 1) dw_dgrad_tile_kernel<T, V, 1, A><<<dw_grid(t), 256, lds, st>>>(
-                        (const T*)dd, w, (const T*)e, sc, sh, mean, inv, act, (T*)out, stat, t);
-               else if (t.ldq <= 2) dw_dgrad_tile_kernel<T, V, 2, A><<<dw_grid(t), 256, lds, st>>>(
-                        (const T*)dd, w, (const T*)e, sc, sh, mean, inv, act, (T*)out, stat, t);
-               else dw_dgrad_tile_kernel<T, V, 3, A><<<dw_grid(t), 256, lds, st>>>(
-                        (const T*)dd, w, (const T*)e, sc, sh, mean, inv, act, (T*)out, stat, t))
+    const size_t lds = t.lds_bytes(part ? 9 : 2, V, sizeof(float));
+#define OGV_DWD(WG_)                                                                                                 \
+    OGV_DW_ACT(act, if (t.ldq <= 1) dw_dgrad_tile_kernel<T, V, 1, A, WG_><<<dw_grid(t), 256, lds, st>>>(             \
+                        (const T*)dd, w, (const T*)e, sc, sh, mean, inv, act, (T*)out, stat, t, part);               \
+               else if (t.ldq <= 2) dw_dgrad_tile_kernel<T, V, 2, A, WG_><<<dw_grid(t), 256, lds, st>>>(             \
+                        (const T*)dd, w, (const T*)e, sc, sh, mean, inv, act, (T*)out, stat, t, part);               \
+               else dw_dgrad_tile_kernel<T, V, 3, A, WG_><<<dw_grid(t), 256, lds, st>>>(                              \
+                        (const T*)dd, w, (const T*)e, sc, sh, mean, inv, act, (T*)out, stat, t, part))
+    if (part) { OGV_DWD(true) }
+    else { OGV_DWD(false) }
+#undef OGV_DWD
   }
   static void dw_wgrad(const void* dd, const void* e, const float* sc, const float* sh, int act, float* part,
                        const DwTile& t, hipStream_t st) {
+    if (skip_mask() & 8) return;
     constexpr int V = 4;
     const size_t lds = t.lds_bytes(9, V, sizeof(float));
     OGV_DW_ACT(act, if (t.ldq <= 1) dw_wgrad_tile_kernel<T, V, 1, A><<<dw_grid(t), 256, lds, st>>>(
@@ -1459,12 +1490,19 @@ static void mbconv_bwd_impl(const void* dout, const void* x, const Saved& sv, vo
   {
     const DwTile t = dw_tile_plan(s.B, s.H, s.W, s.mid, 4);
     join_side(st, sd);
-    sd = fork_side(st);  // bufB (dd) complete: dWdw on the side stream overlaps the data gradient
-    O::dw_wgrad(w.bufB, sv.e, sv.sc1, sv.sh1, s.act, w.part9, t, sd);
-    colreduce(w.part9, w.sums9, t.rows(), 9L * s.mid, 9L * s.mid, w.tmp2, sd);
-    tapmajor_to_chan_kernel<<<cdiv(9 * s.mid, 256), 256, 0, sd>>>(w.sums9, G.w_dw, s.mid);
-    O::dw_dgrad(w.bufB, P.w_dw, sv.e, sv.sc1, sv.sh1, sv.mean1, sv.inv1, s.act,
-                     w.bufA, w.stat, t, st);
+    if (g_dw_fuse) {   // one pass over (dd, e): data gradient + BN1 sums + dWdw partials
+      O::dw_dgrad(w.bufB, P.w_dw, sv.e, sv.sc1, sv.sh1, sv.mean1, sv.inv1, s.act, w.bufA, w.stat, t, st, w.part9);
+      sd = fork_side(st);  // the partials' reduction overlaps the BN1 backward
+      colreduce(w.part9, w.sums9, t.rows(), 9L * s.mid, 9L * s.mid, w.tmp2, sd);
+      tapmajor_to_chan_kernel<<<cdiv(9 * s.mid, 256), 256, 0, sd>>>(w.sums9, G.w_dw, s.mid);
+    } else {
+      sd = fork_side(st);  // bufB (dd) complete: dWdw on the side stream overlaps the data gradient
+      O::dw_wgrad(w.bufB, sv.e, sv.sc1, sv.sh1, s.act, w.part9, t, sd);
+      colreduce(w.part9, w.sums9, t.rows(), 9L * s.mid, 9L * s.mid, w.tmp2, sd);
+      tapmajor_to_chan_kernel<<<cdiv(9 * s.mid, 256), 256, 0, sd>>>(w.sums9, G.w_dw, s.mid);
+      O::dw_dgrad(w.bufB, P.w_dw, sv.e, sv.sc1, sv.sh1, sv.mean1, sv.inv1, s.act,
+                       w.bufA, w.stat, t, st);
+    }
   }
   join_side(st, sd);  // B7 overwrites bufB
   // B7) BN1 backward: de = ca*(dy1 - cb - ehat*cc) -> bufB

@@ -1279,11 +1279,15 @@ static bool vproj_plan(int B, int H, int W, int C, int heads, int k, int ldc, og
     t.ncol = (C + NL + 15) / 16 * 16;
     // 16 B per row over 16 rows: a pitch of KP + 16 elements puts the 16 fragment rows of one lane
     // group on 16 distinct bank quads (KP = 32, 64, 96: conflict-free by the bank model)
-    t.XP = KP + 16;
-    t.WP = KP + 16;
-    t.RP = vtile_best_rp(t, C, heads, ldc);
-    const size_t lds = vtile_lds(t, heads, true);
-    ok = pass == 2 ? lds <= 160 * 1024 : lds <= 80 * 1024;
+    // (the conflict-free pitches first; if they push the tile over the LDS budget, the previous
+    // pad-8 pitches -- 2-way conflicts on the fragment reads -- rather than a smaller tile)
+    for (int pad = 16; pad >= 8 && !ok; pad -= 8) {
+      t.XP = KP + pad;
+      t.WP = KP + pad;
+      t.RP = pad == 16 ? vtile_best_rp(t, C, heads, ldc) : t.ncol;
+      const size_t lds = vtile_lds(t, heads, true);
+      ok = pass == 2 ? lds <= 160 * 1024 : lds <= 80 * 1024;
+    }
   }
   if (!ok || t.ntiles >= (1L << 22)) return false;
   if (t.ncol > 128 || t.HP * (KP / 8) > (NK_W(KP) == 8 ? vp_pf<8>() * 512 : vp_pf<4>() * 256)) return false;
@@ -1359,6 +1363,7 @@ extern "C" int ogv_outlook_vproj_fwd(const void* x, int ldx, const float* w, con
 
 extern "C" int ogv_outlook_agg_fwd(const void* v, const void* logits, void* y, int B, int H, int W, int C, int heads,
                                    int k, int ldl, int ldv, ogv_dtype dt, void* stream) {
+  if (skip_mask() & 64) return OGV_OK;
   OGV_REQUIRE(v && logits && y, "ogv_outlook_agg_fwd: null pointer");
   int rc = check_args(B, H, W, C, heads, k, ldl, ldv, dt, "ogv_outlook_agg_fwd");
   if (rc) return rc;
@@ -1385,6 +1390,7 @@ extern "C" size_t ogv_outlook_bwd_ws_bytes(int B, int H, int W, int C, int heads
 extern "C" int ogv_outlook_agg_bwd(const void* dy, const void* v, const void* logits, void* dv, void* dlogits,
                                    float* probs_ws, int B, int H, int W, int C, int heads, int k, int ldl, int ldv,
                                    int lddv, int lddl, int dl_cols, ogv_dtype dt, void* stream) {
+  if (skip_mask() & 64) return OGV_OK;
   OGV_REQUIRE(dy && v && logits && dv && dlogits, "ogv_outlook_agg_bwd: null pointer");
   int rc = check_args(B, H, W, C, heads, k, ldl, ldv, dt, "ogv_outlook_agg_bwd");
   if (rc) return rc;

@@ -597,6 +597,7 @@ static PgPlan pg_plan(int M, int N, int K, bool stats, bool sw, bool bt, bool pa
 template <int RS, int TN, int PA, bool GT, int ZA, bool STATS, bool BT, bool SW, bool CV>
 static void pg_launch(const PgPlan& p, const bf16* A, int lda, const Pro& pro, const float* W, int ldw,
                       const Epi& epi, bf16* out, int ldo, int M, int N, int K, const ConvG& cv, hipStream_t s) {
+  if (skip_mask() & 1) return;
   auto kern = pgemm_bf16_kernel<RS, TN, PA, GT, ZA, STATS, BT, SW, CV>;
   static bool attr = false;
   if (!attr) {

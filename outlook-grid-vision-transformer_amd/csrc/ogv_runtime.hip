@@ -154,6 +154,14 @@ extern "C" int ogv_set_option(const char* name, int value) {
     set_outlook_vproj(value);
     return OGV_OK;
   }
+  if (!strcmp(name, "skip")) {
+    set_skip(value);
+    return OGV_OK;
+  }
+  if (!strcmp(name, "dw_fuse")) {
+    set_dw_fuse(value);
+    return OGV_OK;
+  }
   if (!strcmp(name, "se_gemv")) {
     set_se_gemv(value);
     return OGV_OK;

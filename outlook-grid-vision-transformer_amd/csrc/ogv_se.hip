@@ -33,12 +33,40 @@ __global__ __launch_bounds__(SE_NT) void se_gemv_kernel(const float* __restrict_
   extern __shared__ __attribute__((aligned(16))) float xs[];   // [SE_RB][Kp] (+ RM: [4][SE_RB][64])
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int b0 = blockIdx.x * SE_RB;
-  const int Kp = (K + 3) / 4 * 4;
-  for (int i = tid; i < SE_RB * Kp; i += SE_NT) {
-    const int r = i / Kp, k = i - r * Kp;
-    float v = 0.f;
-    if (b0 + r < B && k < K) v = act_fwd(pro_act, in[(long)(b0 + r) * ldi + k]);
-    xs[i] = v;
+  const int Kp = (K + 3) / 4 * 4, K4 = Kp / 4, tot4 = SE_RB * K4;
+  // staging: up to SU independent 16-B loads per thread in flight before any is stored (one L2
+  // round trip per batch, not per element)
+  constexpr int SU = 8;
+  const bool av = (ldi & 3) == 0 && (reinterpret_cast<uintptr_t>(in) & 15) == 0;
+  for (int base = tid; base < tot4; base += SE_NT * SU) {
+    float4 v[SU];
+#pragma unroll
+    for (int u = 0; u < SU; ++u) {
+      const int idx = base + u * SE_NT, r = idx / K4, k = (idx - r * K4) * 4;
+      v[u] = float4{0.f, 0.f, 0.f, 0.f};
+      if (idx < tot4 && b0 + r < B) {
+        const float* src = in + (long)(b0 + r) * ldi + k;
+        if (av && k + 4 <= K) v[u] = *reinterpret_cast<const float4*>(src);
+        else {
+          v[u].x = k < K ? src[0] : 0.f;
+          v[u].y = k + 1 < K ? src[1] : 0.f;
+          v[u].z = k + 2 < K ? src[2] : 0.f;
+          v[u].w = k + 3 < K ? src[3] : 0.f;
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < SU; ++u) {
+      const int idx = base + u * SE_NT, r = idx / K4, k = (idx - r * K4) * 4;
+      if (idx >= tot4) continue;
+      const bool live = b0 + r < B;
+      float4 a;
+      a.x = live && k < K ? act_fwd(pro_act, v[u].x) : 0.f;
+      a.y = live && k + 1 < K ? act_fwd(pro_act, v[u].y) : 0.f;
+      a.z = live && k + 2 < K ? act_fwd(pro_act, v[u].z) : 0.f;
+      a.w = live && k + 3 < K ? act_fwd(pro_act, v[u].w) : 0.f;
+      *reinterpret_cast<float4*>(xs + r * Kp + k) = a;
+    }
   }
   __syncthreads();
   auto finish = [&](int r, int n, float v) {
@@ -59,6 +87,7 @@ __global__ __launch_bounds__(SE_NT) void se_gemv_kernel(const float* __restrict_
       for (int r = 0; r < SE_RB; ++r) acc[r] = 0.f;
       if (n < N) {
         const float* wr = W + (long)n * ldw;
+#pragma unroll 4
         for (int k = 4 * kl; k < K; k += 64) {
           float w4[4];
           if (wv) {
@@ -87,17 +116,27 @@ __global__ __launch_bounds__(SE_NT) void se_gemv_kernel(const float* __restrict_
       }
     }
   } else {
-    // column n = blockIdx.y * 64 + lane; wave w reduces k = w, w + 4, ...  (fixed-order combine)
+    // column n = blockIdx.y * 64 + lane; wave w reduces the contiguous k range [k0, k1) in steps of 4
+    // (four coalesced weight rows, one 16-B broadcast read of each staged input row), then the four
+    // waves combine in a fixed order
     float* red = xs + SE_RB * Kp;   // [4][SE_RB][64]
     const int n = blockIdx.y * 64 + lane;
+    const int kq = (Kp / 4 + 3) / 4 * 4;   // k per wave, a multiple of 4
+    const int k0 = wave * kq, k1 = min(Kp, k0 + kq);
     float acc[SE_RB];
 #pragma unroll
     for (int r = 0; r < SE_RB; ++r) acc[r] = 0.f;
     if (n < N) {
-      for (int k = wave; k < K; k += 4) {
-        const float w = W[(long)k * ldw + n];
+#pragma unroll 2
+      for (int k = k0; k < k1; k += 4) {
+        float w4[4];
 #pragma unroll
-        for (int r = 0; r < SE_RB; ++r) acc[r] = fmaf(xs[r * Kp + k], w, acc[r]);
+        for (int e = 0; e < 4; ++e) w4[e] = k + e < K ? W[(long)(k + e) * ldw + n] : 0.f;
+#pragma unroll
+        for (int r = 0; r < SE_RB; ++r) {
+          const float4 x = *reinterpret_cast<const float4*>(xs + r * Kp + k);
+          acc[r] = fmaf(x.x, w4[0], fmaf(x.y, w4[1], fmaf(x.z, w4[2], fmaf(x.w, w4[3], acc[r]))));
+        }
       }
     }
 #pragma unroll

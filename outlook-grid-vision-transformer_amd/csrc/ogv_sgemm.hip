@@ -519,6 +519,7 @@ static SgPlan sgemm_plan_w(int M, int N, int K, bool stats, bool prologue, bool 
 template <int KT, int RS, int PA, int ZA, bool STATS, bool BT>
 static int sg_launch(const SgPlan& p, const bf16* A, int lda, const Pro& pro, const float* W, int ldw,
                      const Epi& epi, bf16* out, int ldo, int M, int N, int K, hipStream_t s) {
+  if (skip_mask() & 2) return p.grid;
   const int sw = p.sw;
   auto kern = sw ? sgemm_bf16_kernel<KT, RS, PA, ZA, STATS, BT, true> : sgemm_bf16_kernel<KT, RS, PA, ZA, STATS, BT, false>;
   static bool attr[2] = {false, false};

@@ -253,7 +253,9 @@ def test_model_logits(name, dtype):
         # that cancel, so bf16 storage of dlogits costs several % there in any implementation)
         tol = np.maximum(tol, atol + np.abs(arr["grad_norms_cpu_bf16_autocast"] - ref_gn))
     ratio = np.abs(gn - ref_gn) / tol
-    print(f"{name}: grad norms worst |d| / tol = {ratio.max():.3f} ({names[int(np.argmax(ratio))]})")
+    w = int(np.argmax(ratio))
+    print(f"{name}: grad norms worst |d| / tol = {ratio.max():.3f} ({names[w]}: ours {gn[w]:.6g} ref {ref_gn[w]:.6g}"
+          + (f" ref-bf16 {arr['grad_norms_cpu_bf16_autocast'][w]:.6g})" if "grad_norms_cpu_bf16_autocast" in arr else ")"))
     assert e <= bound, f"{name} logits max|d| {e:.3e} > {bound:.3e}"
     assert abs(loss.item() - lref) <= (BF16_FWD if bf else 1e-4) * max(1.0, lref)
     assert ratio.max() <= 1.0, f"{name} grad norm {names[int(np.argmax(ratio))]}: |d| / tol = {ratio.max():.3f}"

@@ -1,0 +1,17 @@
+set -u
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out/r7
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread -s -k "not model_logits" > gpurun_out/r7/pytest.log 2>&1
+rc=$?; echo "pytest rc=$rc"; grep -E "passed|failed|Error" gpurun_out/r7/pytest.log | tail -8
+[ $rc -le 1 ] || exit $rc
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread -s -k "model_logits" > gpurun_out/r7/pytest_models.log 2>&1
+rc=$?; echo "pytest models rc=$rc"; grep -E "grad norms worst|passed|failed|Error" gpurun_out/r7/pytest_models.log | tail -30
+[ $rc -le 1 ] || exit $rc
+timeout -k 10 120 python3 tools/bench_vproj.py --reps 10 2>&1 | grep -v amdgpu || exit 1
+B="timeout -k 10 300 python3 bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-parity --step-roofline 0"
+for o in "" "--opt se_gemv=0" "" "--opt outlook_vproj=2" ""; do
+  $B $o > gpurun_out/r7/b.log 2>&1 || exit 1
+  python3 -c "import json; d=json.loads([l for l in open('gpurun_out/r7/b.log') if l.startswith('{')][-1]); print('$o', d['ms_per_step'])"
+done
+OUT=gpurun_out/r7/prof BENCH_ARGS="--step-roofline 0" bash tools/gpu_prof.sh > /dev/null 2>&1; echo "prof rc=$?"

@@ -1,0 +1,73 @@
+"""Where the bf16 path's Outlooker logit-bias gradient error comes from (diagnostic, GPU):
+model fixture in bf16 three ways -- (a) the fused kernels (default), (b) the materialising
+Outlooker (softmax / unfold / sum in fp32 torch ops, dlogits still rounded to bf16 before the
+1x1 conv's weight-gradient GEMM), (c) as (b) but the bias gradient summed from the fp32 dlogits --
+and the relative error of every attn.attn.bias gradient norm against the fixture.
+    python tools/diag_attn_bias.py [model_b_train_b16]"""
+import pathlib
+import sys
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+for p in (ROOT / "outlook-grid-vision-transformer_amd", ROOT / "tests", ROOT / "tests" / "golden", ROOT / "oracle"):
+    sys.path.insert(0, str(p))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import _fixtures as fx  # noqa: E402
+import gen_params as gp  # noqa: E402
+import ogv  # noqa: E402
+from ogv import functional as OF  # noqa: E402
+from src.model.outlook_attention import OutlookAttention2d  # noqa: E402
+
+
+def run(name, mode):
+    from test_gpu_parity import _module
+    meta, arr = fx.load(name)
+    mod = _module(meta)
+    gp.fill_module(mod, meta["seed"])
+    mod = mod.cuda().train(meta["mode"] == "train")
+    orig_fwd, orig_bwd = OutlookAttention2d.forward, OF._Linear.backward
+    if mode != "fused":
+        def fwd(self, x, residual=None, row_scale=None):
+            y = self._forward_materialised(x)
+            return self.proj(y, residual=residual, row_scale=row_scale)
+        OutlookAttention2d.forward = fwd
+    if mode == "fp32_bias_sum":
+        def bwd(ctx, dout):
+            r = list(orig_bwd(ctx, dout))
+            if r[2] is not None and dout.dtype == torch.float32:
+                r[2] = dout.sum(0)
+            return tuple(r)
+        OF._Linear.backward = staticmethod(bwd)
+    try:
+        x = torch.from_numpy(gp.input_from_spec(meta["x"])).cuda().contiguous(memory_format=torch.channels_last)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            logits = mod(x)
+        torch.nn.functional.cross_entropy(logits.float(), torch.from_numpy(arr["targets"]).cuda(),
+                                          label_smoothing=0.1).backward()
+    finally:
+        OutlookAttention2d.forward, OF._Linear.backward = orig_fwd, orig_bwd
+    names = meta["param_names"]
+    params = dict(mod.named_parameters())
+    out = {}
+    for i, k in enumerate(names):
+        if k.endswith("attn.attn.bias"):
+            g = params[k].grad.norm().item()
+            out[k] = (g / arr["grad_norms"][i] - 1.0,
+                      arr["grad_norms_cpu_bf16_autocast"][i] / arr["grad_norms"][i] - 1.0
+                      if "grad_norms_cpu_bf16_autocast" in arr else float("nan"))
+    return out
+
+
+def main():
+    ogv.load()
+    names = sys.argv[1:] or ["model_b_train_b16", "model_a_7m_train_b16", "model_a_14m_train_b8"]
+    for name in names:
+        res = {m: run(name, m) for m in ("fused", "materialised", "fp32_bias_sum")}
+        for k in res["fused"]:
+            print(f"{name} {k:36s} rel err: fused {res['fused'][k][0]:+.4f}  materialised {res['materialised'][k][0]:+.4f}"
+                  f"  fp32-bias-sum {res['fp32_bias_sum'][k][0]:+.4f}  reference-bf16 {res['fused'][k][1]:+.4f}")
+
+
+if __name__ == "__main__":
+    main()

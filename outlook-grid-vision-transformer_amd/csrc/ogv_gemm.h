@@ -208,6 +208,7 @@ void se_gemv_launch(const float* in, int ldi, int pro_act, const float* W, int l
 bool se_gemv_on();
 void set_se_gemv(int v);
 void set_dw_fuse(int v);
+void set_swg_min_m(int v);
 void set_pg_split(int v);
 int split_w();
 int skip_mask();

@@ -154,6 +154,10 @@ extern "C" int ogv_set_option(const char* name, int value) {
     set_outlook_vproj(value);
     return OGV_OK;
   }
+  if (!strcmp(name, "swg_min_m")) {
+    set_swg_min_m(value);
+    return OGV_OK;
+  }
   if (!strcmp(name, "skip")) {
     set_skip(value);
     return OGV_OK;

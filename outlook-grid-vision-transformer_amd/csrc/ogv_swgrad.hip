@@ -238,9 +238,13 @@ static int sw_tile(int D) {  // tile edge for an output dim: multiple of 16 in {
   return 64;
 }
 
+// knob "swg_min_m": smallest M routed to the streaming weight gradient (0 = sgemm_min_m)
+static int g_swg_min_m = 0;
+void set_swg_min_m(int v) { g_swg_min_m = v < 0 ? 0 : v; }
+
 static SwPlan swgrad_plan(int M, int N, int K) {
   SwPlan p;
-  if (M < sgemm_min_m() || (N & 7) || (K & 7)) return p;
+  if (M < (g_swg_min_m ? g_swg_min_m : sgemm_min_m()) || (N & 7) || (K & 7)) return p;
   p.BN = sw_tile(N);
   p.BK = sw_tile(K);
   p.nNt = (N + p.BN - 1) / p.BN;

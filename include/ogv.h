@@ -53,6 +53,9 @@ const char* ogv_last_error(void);
  *   kernels of ogv_se.hip instead of split-K GEMM + reduce; "outlook_vproj" 0/1/2: fused Outlooker
  *   projection + aggregation never / inference (default) / also training; "vp_dbg", "pg_dbg":
  *   phase-skipping timing experiments (wrong results).
+ * Options pick kernel plans, and every *_ws_bytes query sizes the workspace for the plans in force
+ * when it is called: set options first, then size workspaces (a workspace sized under other option
+ * values can be too small -- e.g. wg_blocks / wg_tile / swg_min_m change the split-M partial count).
  * Returns OGV_ERR_ARG for an unknown name. */
 int ogv_set_option(const char* name, int value);
 /* Diagnostics (no reference counterpart): which kernel ogv_gemm_fwd (kind 0) / ogv_gemm_dgrad

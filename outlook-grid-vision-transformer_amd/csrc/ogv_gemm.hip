@@ -1393,6 +1393,7 @@ size_t wgrad_ws_bytes(int M, int N, int K) {
     const long ld = (long)N * K + N;
     best = std::max(best, ((size_t)p.S * ld + colreduce_tmp_floats(p.S, ld)) * sizeof(float));
   }
+  best = std::max(best, wgrad2_ws_floats(M > 0 ? M : 1, N, K) * sizeof(float));
   return std::max(best, swgrad_ws_floats(M > 0 ? M : 1, N, K) * sizeof(float));
 }
 
@@ -1429,7 +1430,10 @@ void gemm_wgrad_launch(ogv_dtype dt, const void* G, int ldg, const void* X, int 
   const long ldp = (long)N * K + N;
   float* part = (float*)ws;
   if (dt == OGV_BF16 && !xc) {
-    const int S = swgrad_try(G, ldg, X, ldx, pro, rs, rps, part, dbias != nullptr, M, N, K, s);
+    const bool b = dbias != nullptr;
+    int S = wg2_mode() == 2 ? wgrad2_try(G, ldg, X, ldx, pro, rs, rps, part, b, M, N, K, s) : 0;
+    if (S == 0) S = swgrad_try(G, ldg, X, ldx, pro, rs, rps, part, b, M, N, K, s);
+    if (S == 0 && wg2_mode() == 1) S = wgrad2_try(G, ldg, X, ldx, pro, rs, rps, part, b, M, N, K, s);
     if (S > 0) {
       colreduce(part, dW, S, dbias ? ldp : (long)N * K, ldp, part + (size_t)S * ldp, s, dbias, (long)N * K);
       return;

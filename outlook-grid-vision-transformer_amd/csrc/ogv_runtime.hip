@@ -158,6 +158,18 @@ extern "C" int ogv_set_option(const char* name, int value) {
     set_swg_min_m(value);
     return OGV_OK;
   }
+  if (!strcmp(name, "wg2")) {
+    set_wg2(value);
+    return OGV_OK;
+  }
+  if (!strcmp(name, "wg2_blocks")) {
+    set_wg2_blocks(value);
+    return OGV_OK;
+  }
+  if (!strcmp(name, "wg2_tile")) {
+    set_wg2_tile(value);
+    return OGV_OK;
+  }
   if (!strcmp(name, "skip")) {
     set_skip(value);
     return OGV_OK;

@@ -1,0 +1,346 @@
+// Pipelined bf16 weight gradient (gfx950) for the mid-M projections (M = 8k-131k rows).
+//
+//   dW[n, k] = sum_m rs(m) G[m, n] * pro(X)[m, k],   dbias[n] = sum_m rs(m) G[m, n]
+//
+// The split-M tiled kernel of ogv_gemm.hip stages 32 rows per step behind two barriers with the
+// next step's loads one short MFMA phase ahead: at these shapes a workgroup's step is a few dozen
+// MFMAs, so every step waits out an L2/HBM round trip, and its X prologue (GELU of MLP fc2, BN +
+// SiLU + SE gate of MBConv project) runs in that serial staging phase, once per N tile (measured
+// isolated, M=32768 N=192 K=768: 156 us with the GELU prologue vs 50 us without it).  Here:
+//   * 64 rows per step (two 32-deep MFMA k-blocks), two LDS buffers, ONE barrier per step;
+//   * two register sets: step t+1 is staged from registers while step t+2's loads are in flight,
+//     so each load has two compute phases to land;
+//   * the prologue form is a template parameter (no runtime switch per element), and the tile
+//     edge may cover all of N (BN = 192), so the prologue runs once per X element;
+//   * loads use clamped, always-valid addresses and select zero afterwards (no branch per load).
+// Output: fp32 partials [S][N*K + N] (the tiled kernel's layout, reduced by the caller's colreduce).
+// Fragment reads: ds_read_b64_tr_b16 with the same m-permutation as the tiled kernel (rows 4g+q and
+// 16+4g+q of each 32-row block; an odd multiple of 16 as pitch keeps them conflict-free).
+#include "ogv_gemm.h"
+
+namespace ogv {
+
+constexpr int W2_MS = 64;   // rows per pipeline step
+constexpr int W2_NT = 256;  // 4 waves, 2 x 2 over the output tile
+
+// prologue forms: -1 none; OGV_ACT_GELU: gelu(x); OGV_ACT_SILU: silu(x * sc + sh) * gate; 99: any (runtime)
+constexpr int W2_GENERIC = 99;
+
+template <int BN, int BK, int PA>
+__global__ __launch_bounds__(W2_NT) void wgrad2_bf16_kernel(const bf16* __restrict__ G, int ldg,
+                                                            const bf16* __restrict__ X, int ldx, Pro pro,
+                                                            const float* __restrict__ rs, int rps,
+                                                            float* __restrict__ part, long ldp, int want_bias, int M,
+                                                            int N, int K, int mchunk, int nNt, int tiles, int S) {
+  constexpr int MS = W2_MS;
+  constexpr int GP = BN + 16, XP = BK + 16;      // odd multiples of 16 for BN in {64, 96, 128, 192}, BK in {64, 128}
+  constexpr int GC = BN / 8, XC = BK / 8;        // 16-B chunks per staged row
+  constexpr int GV = MS * GC / W2_NT, XV = MS * XC / W2_NT;
+  static_assert(GV * W2_NT == MS * GC && XV * W2_NT == MS * XC, "tile edge must make whole chunk passes");
+  constexpr int TN = BN / 32, TK = BK / 32;      // 16-wide fragments per wave (wave tile BN/2 x BK/2)
+  constexpr int BUF = MS * (GP + XP);            // bf16 elements per LDS buffer
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * BUF];
+
+  const int b = blockIdx.x, xcd = b & 7, local = b >> 3;
+  const int tile = local % tiles, s = (local / tiles) * 8 + xcd;
+  if (s >= S) return;
+  const int nt = tile % nNt, kt = tile / nNt;
+  const int n0 = nt * BN, k0 = kt * BK;
+  const int mbeg = s * mchunk, mend = min(M, mbeg + mchunk);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave >> 1, wk = wave & 1;
+
+  f32x4 acc[TN][TK];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TK; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // per-chunk coordinates (chunk id = tid + v * 256 -> row id / GC, column chunk id % GC).  XC
+  // divides 256, so a thread's X chunks all sit in one column chunk (its BN scale / shift and column
+  // guard are loop-invariant scalars); G chunks may not (BN = 96 / 192).
+  int grow[GV], gcol[GV];
+  bool gok[GV];
+#pragma unroll
+  for (int v = 0; v < GV; ++v) {
+    const int id = tid + v * W2_NT;
+    grow[v] = id / GC;
+    gcol[v] = (id % GC) * 8;
+    gok[v] = n0 + gcol[v] < N;
+  }
+  static_assert(W2_NT % XC == 0, "X chunk columns must be thread-invariant");
+  const int xrow0 = tid / XC, xcol = (tid % XC) * 8;
+  constexpr int XRP = W2_NT / XC;  // X rows per chunk pass
+  const bool xok = k0 + xcol < K;
+  const int xk = xok ? k0 + xcol : 0;
+  // dbias[n] = sum_m G[m, n] rides on the MFMA: the waves of the first K tile with wk == 0 multiply
+  // their G fragments by a ones fragment as well (+1/TK MFMAs, no per-thread bias registers)
+  const bool bias_wave = want_bias && kt == 0 && wk == 0;
+  f32x4 bacc[TN];
+#pragma unroll
+  for (int i = 0; i < TN; ++i) bacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // loop-invariant BN scale / shift of the X columns (SiLU form)
+  constexpr bool SG = PA == OGV_ACT_SILU;
+  float psc[8], psh[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) { psc[t] = 1.f; psh[t] = 0.f; }
+  if constexpr (SG) {
+    load_vec<float, 8>(pro.sc + xk, psc);
+    load_vec<float, 8>(pro.sh + xk, psh);
+  }
+
+  struct Regs {
+    uint4 g[GV], x[XV];
+    float r[GV];
+    float gt[SG ? XV : 1][8];
+  };
+  auto load = [&](Regs& R, int m0) {
+#pragma unroll
+    for (int v = 0; v < GV; ++v) {
+      const int m = min(m0 + grow[v], mend - 1);
+      R.g[v] = *reinterpret_cast<const uint4*>(G + (long)m * ldg + (gok[v] ? n0 + gcol[v] : 0));
+      R.r[v] = rs ? rs[m / rps] : 1.f;
+    }
+#pragma unroll
+    for (int v = 0; v < XV; ++v) {
+      const int m = min(m0 + xrow0 + v * XRP, mend - 1);
+      R.x[v] = *reinterpret_cast<const uint4*>(X + (long)m * ldx + xk);
+      if constexpr (SG) load_vec<float, 8>(pro.gate + (long)(m / pro.rps) * pro.gld + xk, R.gt[v]);
+    }
+  };
+  auto stage = [&](Regs& R, int m0, bf16* buf) {
+    bf16* Gs = buf;
+    bf16* Xs = buf + MS * GP;
+#pragma unroll
+    for (int v = 0; v < GV; ++v) {
+      const bool ok = gok[v] && m0 + grow[v] < mend;
+      uint4 u = ok ? R.g[v] : uint4{0u, 0u, 0u, 0u};
+      bf16* e = reinterpret_cast<bf16*>(&u);
+      if (rs) {
+#pragma unroll
+        for (int t = 0; t < 8; ++t) e[t] = (bf16)((float)e[t] * R.r[v]);
+      }
+      *reinterpret_cast<uint4*>(Gs + grow[v] * GP + gcol[v]) = u;
+    }
+#pragma unroll
+    for (int v = 0; v < XV; ++v) {
+      const int m = m0 + xrow0 + v * XRP;
+      const bool ok = xok && m < mend;
+      uint4 u = ok ? R.x[v] : uint4{0u, 0u, 0u, 0u};
+      if constexpr (PA >= 0) {
+        bf16* e = reinterpret_cast<bf16*>(&u);
+        float f[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) f[t] = (float)e[t];
+        if constexpr (PA == W2_GENERIC) {
+          if (ok) pro_apply_run<8>(pro, f, m, k0 + xcol, K);
+        } else if constexpr (SG) {
+#pragma unroll
+          for (int t = 0; t < 8; ++t) f[t] = act_fwd(OGV_ACT_SILU, fmaf(f[t], psc[t], psh[t])) * R.gt[v][t];
+        } else {
+#pragma unroll
+          for (int t = 0; t < 8; ++t) f[t] = act_fwd(PA, f[t]);
+        }
+#pragma unroll
+        for (int t = 0; t < 8; ++t) e[t] = ok ? (bf16)f[t] : (bf16)0.f;
+      }
+      *reinterpret_cast<uint4*>(Xs + (xrow0 + v * XRP) * XP + xcol) = u;
+    }
+  };
+  const int g = lane >> 4, c16 = lane & 15, q = c16 >> 2, p4 = (c16 & 3) * 4;
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  typedef __attribute__((ext_vector_type(8))) short s16x8;
+  auto compute = [&](const bf16* buf) {
+    const bf16* Gs = buf;
+    const bf16* Xs = buf + MS * GP;
+#pragma unroll
+    for (int kb = 0; kb < MS / 32; ++kb) {
+      const int r0 = kb * 32 + 4 * g + q;
+      bf16x8 af[TN], xf[TK];
+#pragma unroll
+      for (int i = 0; i < TN; ++i) {
+        const int col = wn * (BN / 2) + i * 16 + p4;
+        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Gs + r0 * GP + col));
+        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Gs + (r0 + 16) * GP + col));
+        s16x8 a8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        af[i] = __builtin_bit_cast(bf16x8, a8);
+      }
+#pragma unroll
+      for (int j = 0; j < TK; ++j) {
+        const int col = wk * (BK / 2) + j * 16 + p4;
+        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Xs + r0 * XP + col));
+        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Xs + (r0 + 16) * XP + col));
+        s16x8 x8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        xf[j] = __builtin_bit_cast(bf16x8, x8);
+      }
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TK; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], xf[j], acc[i][j], 0, 0, 0);
+      if (bias_wave) {
+        const s16x8 one8 = {0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80};  // bf16 1.0
+        const bf16x8 ones = __builtin_bit_cast(bf16x8, one8);
+#pragma unroll
+        for (int i = 0; i < TN; ++i) bacc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], ones, bacc[i], 0, 0, 0);
+      }
+    }
+  };
+
+  // ---- pipeline: LDS buffers 0/1 alternate; register sets A/B hold steps t+1 / t+2
+  const int nsteps = (mend - mbeg + MS - 1) / MS;
+  bf16* buf0 = smem;
+  bf16* buf1 = smem + BUF;
+  Regs RA, RB;
+  load(RA, mbeg);
+  if (nsteps > 1) load(RB, mbeg + MS);
+  stage(RA, mbeg, buf0);
+  if (nsteps > 2) load(RA, mbeg + 2 * MS);
+  __syncthreads();
+  for (int t = 0; t < nsteps; t += 2) {
+    compute(buf0);
+    if (t + 1 < nsteps) {
+      stage(RB, mbeg + (t + 1) * MS, buf1);
+      if (t + 3 < nsteps) load(RB, mbeg + (t + 3) * MS);
+    }
+    __syncthreads();
+    if (t + 1 >= nsteps) break;
+    compute(buf1);
+    if (t + 2 < nsteps) {
+      stage(RA, mbeg + (t + 2) * MS, buf0);
+      if (t + 4 < nsteps) load(RA, mbeg + (t + 4) * MS);
+    }
+    __syncthreads();
+  }
+
+  float* dst = part + (long)s * ldp;
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TK; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + wn * (BN / 2) + i * 16 + 4 * g + r;
+        const int k = k0 + wk * (BK / 2) + j * 16 + c16;
+        if (n < N && k < K) dst[(long)n * K + k] = acc[i][j][r];
+      }
+  if (bias_wave && c16 == 0) {  // every column of the ones product holds the row sum
+#pragma unroll
+    for (int i = 0; i < TN; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + wn * (BN / 2) + i * 16 + 4 * g + r;
+        if (n < N) dst[(long)N * K + n] = bacc[i][r];
+      }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+static int g_wg2 = 0;          // knob "wg2": 0 off, 1 = this kernel below the streaming-wgrad M, 2 = at every M
+static int g_wg2_blocks = 1024;  // knob "wg2_blocks": workgroups the split-M plan aims for
+static int g_wg2_tile = 0;     // knob "wg2_tile": force the N edge (64 / 96 / 128 / 192; K edge 64 / 128)
+int wg2_mode() { return g_wg2; }
+void set_wg2(int v) { g_wg2 = v < 0 ? 0 : (v > 2 ? 2 : v); }
+void set_wg2_blocks(int v) { g_wg2_blocks = v < 64 ? 64 : v; }
+void set_wg2_tile(int v) { g_wg2_tile = (v == 64 || v == 96 || v == 128 || v == 192) ? v : 0; }
+
+struct W2Plan {
+  int ok = 0, BN = 0, BK = 0, nNt = 0, nKt = 0, S = 0, mchunk = 0;
+};
+
+// N edge (G columns): {64, 96, 128, 192}; K edge (X columns, whose chunk columns must be
+// thread-invariant): {64, 128}
+static int w2_tile_n(int N, bool pro) {
+  if (N <= 64) return 64;
+  if (N <= 96) return 96;
+  if (N <= 128) return 128;
+  if (pro && N <= 192) return 192;  // the X prologue then runs once per element
+  if (N % 128 == 0) return 128;
+  if (N % 96 == 0) return 96;
+  if (N % 64 == 0) return 64;
+  return 128;
+}
+static int w2_tile_k(int K) {
+  if (K <= 64) return 64;
+  if (K % 128 == 0 || K % 64 != 0) return 128;
+  return 64;
+}
+
+static W2Plan wgrad2_plan(int M, int N, int K, bool pro) {
+  W2Plan p;
+  if ((N & 7) || (K & 7) || M <= 0) return p;
+  p.BN = g_wg2_tile ? g_wg2_tile : w2_tile_n(N, pro);
+  p.BK = (g_wg2_tile == 64 || g_wg2_tile == 128) ? g_wg2_tile : w2_tile_k(K);
+  if (p.BN == 192) p.BK = 64;  // 192 x 128 runs out of registers
+  p.nNt = (N + p.BN - 1) / p.BN;
+  p.nKt = (K + p.BK - 1) / p.BK;
+  const long tiles = (long)p.nNt * p.nKt;
+  long S = (g_wg2_blocks + tiles - 1) / tiles;
+  S = std::min<long>(S, ((long)M + 4 * W2_MS - 1) / (4 * W2_MS));  // >= 4 steps per workgroup
+  S = std::max<long>(1, S);
+  int mchunk = (int)((M + S - 1) / S);
+  mchunk = (mchunk + W2_MS - 1) / W2_MS * W2_MS;
+  p.S = (M + mchunk - 1) / mchunk;
+  p.mchunk = mchunk;
+  p.ok = 1;
+  return p;
+}
+
+size_t wgrad2_ws_floats(int M, int N, int K) {
+  // sized for the larger of the two tile plans (with / without a prologue), knob-independent of "wg2"
+  size_t best = 0;
+  for (bool pro : {false, true}) {
+    const W2Plan p = wgrad2_plan(M, N, K, pro);
+    if (!p.ok) continue;
+    const long ld = (long)N * K + N;
+    best = std::max(best, (size_t)p.S * ld + colreduce_tmp_floats(p.S, ld));
+  }
+  return best;
+}
+
+template <int BN, int BK, int PA>
+static void w2_launch(const W2Plan& p, const bf16* G, int ldg, const bf16* X, int ldx, const Pro& pro, const float* rs,
+                      int rps, float* part, long ldp, bool bias, int M, int N, int K, hipStream_t s) {
+  const int tiles = p.nNt * p.nKt;
+  const unsigned grid = (unsigned)(((p.S + 7) / 8) * 8 * tiles);
+  wgrad2_bf16_kernel<BN, BK, PA><<<grid, W2_NT, 0, s>>>(G, ldg, X, ldx, pro, rs, rps, part, ldp, bias ? 1 : 0, M, N, K,
+                                                        p.mchunk, p.nNt, tiles, p.S);
+}
+
+template <int PA>
+static void w2_dispatch(const W2Plan& p, const bf16* G, int ldg, const bf16* X, int ldx, const Pro& pro,
+                        const float* rs, int rps, float* part, long ldp, bool bias, int M, int N, int K,
+                        hipStream_t s) {
+#define OGV_W2_K(BN_)                                                                                        \
+  do {                                                                                                       \
+    if (p.BK == 64) w2_launch<BN_, 64, PA>(p, G, ldg, X, ldx, pro, rs, rps, part, ldp, bias, M, N, K, s);    \
+    else w2_launch<BN_, 128, PA>(p, G, ldg, X, ldx, pro, rs, rps, part, ldp, bias, M, N, K, s);             \
+  } while (0)
+  if (p.BN == 64) OGV_W2_K(64);
+  else if (p.BN == 96) OGV_W2_K(96);
+  else if (p.BN == 128) OGV_W2_K(128);
+  else OGV_W2_K(192);
+#undef OGV_W2_K
+}
+
+// Returns the number of partial rows written into part (layout [S][N*K + N]), 0 if not handled.
+int wgrad2_try(const void* G, int ldg, const void* X, int ldx, const Pro& pro, const float* rs, int rps, float* part,
+               bool bias, int M, int N, int K, hipStream_t s) {
+  if (!g_wg2) return 0;
+  if ((ldg & 7) || (ldx & 7) || (reinterpret_cast<uintptr_t>(G) & 15) || (reinterpret_cast<uintptr_t>(X) & 15))
+    return 0;
+  W2Plan p = wgrad2_plan(M, N, K, pro.any());
+  if (!p.ok) return 0;
+  const long ldp = (long)N * K + N;
+  const bf16* g = static_cast<const bf16*>(G);
+  const bf16* x = static_cast<const bf16*>(X);
+  const bool gelu_only = pro.act == OGV_ACT_GELU && !pro.sc && !pro.sh && !pro.gate;
+  const bool bn_silu_gate = pro.act == OGV_ACT_SILU && pro.sc && pro.sh && pro.gate && !(pro.gld & 3);
+  if (!pro.any()) w2_dispatch<-1>(p, g, ldg, x, ldx, pro, rs, rps, part, ldp, bias, M, N, K, s);
+  else if (gelu_only) w2_dispatch<OGV_ACT_GELU>(p, g, ldg, x, ldx, pro, rs, rps, part, ldp, bias, M, N, K, s);
+  else if (bn_silu_gate) w2_dispatch<OGV_ACT_SILU>(p, g, ldg, x, ldx, pro, rs, rps, part, ldp, bias, M, N, K, s);
+  else w2_dispatch<W2_GENERIC>(p, g, ldg, x, ldx, pro, rs, rps, part, ldp, bias, M, N, K, s);
+  return p.S;
+}
+
+}  // namespace ogv

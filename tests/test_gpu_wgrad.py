@@ -1,0 +1,151 @@
+"""bf16 weight gradient through the C ABI (ogv_gemm_wgrad): the split-M tiled kernel (ogv_gemm.hip),
+the streaming kernel (ogv_swgrad.hip) and the pipelined kernel (ogv_wgrad2.hip, knob wg2) against
+fp64 torch on the same seeded inputs.
+
+    dW[n, k] = sum_m rs(m) dOut[m, n] * act(A[m, k]),   dbias[n] = sum_m rs(m) dOut[m, n]
+
+Cases: the Model-A-7M step's own shapes (M = 32768 / 8192 / 131072 rows, the GELU prologue of fc2),
+ragged rows (M not a multiple of the 64-row pipeline step, fewer rows than one step), output
+widths that pad the 64 / 96 / 128 / 192 tile edges, the per-sample DropPath row scale, no bias;
+every tile edge forced through wg2_tile; and whole bf16 module fixtures (the MBConv project's BN +
+SiLU + SE-gate prologue form, which only the fused MBConv op issues) with wg2 = 2 against the
+reference's goldens.  Tolerance: bf16 operands (the prologue output rounded to bf16, as the kernel
+does -- the fp64 reference rounds it the same way), fp32 accumulation -> 1e-2 * max|ref|.
+"""
+import ctypes
+
+import pytest
+import torch
+
+import _fixtures as fx
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+BF16, ACT = 1, {None: 0, "gelu": 1, "silu": 2}
+
+
+@pytest.fixture(autouse=True, scope="module")
+def _lib():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import ogv
+    ogv.load()
+
+
+def _L():
+    from ogv._lib import load
+    return load()
+
+
+def _opt(name, v):
+    assert _L().ogv_set_option(name.encode(), int(v)) == 0
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _wgrad(d, x, s, rps, act, bias, M, N, K):
+    dW = torch.full((N, K), float("nan"), device=DEV)
+    db = torch.full((N,), float("nan"), device=DEV) if bias else None
+    # sized after the knobs are set (the plan, hence the partial count, depends on them)
+    ws = torch.empty(_L().ogv_gemm_wgrad_ws_bytes(M, N, K), device=DEV, dtype=torch.uint8)
+    st = torch.cuda.current_stream().cuda_stream
+    rc = _L().ogv_gemm_wgrad(_p(d), N, _p(x), K, _p(s), rps, _p(dW), _p(db), M, N, K, ACT[act], _p(ws), BF16,
+                             ctypes.c_void_p(st))
+    assert rc == 0
+    torch.cuda.synchronize()
+    return dW, db
+
+
+def _ref(d, x, s, rps, act, M):
+    f = {None: lambda t: t, "gelu": torch.nn.functional.gelu, "silu": torch.nn.functional.silu}[act]
+    a = f(x.double())
+    if act:
+        a = a.to(torch.bfloat16).double()  # the kernel rounds the prologue's output to bf16
+    g = d.double()
+    if s is not None:
+        # the kernel scales dOut by rs in fp32 and stages it as bf16
+        g = (g.float() * s.float().repeat_interleave(rps)[:M, None]).to(torch.bfloat16).double()
+    return g.t() @ a, g.sum(0)
+
+
+CASES = [  # M, N, K, prologue act, bias, rowscale
+    (32768, 192, 768, "gelu", True, True), (32768, 768, 192, None, True, False),
+    (32768, 192, 192, None, True, False), (32768, 576, 192, None, False, True),
+    (32768, 192, 384, "gelu", False, False), (8192, 256, 1024, "gelu", True, False),
+    (8192, 1024, 256, None, True, True), (8192, 72, 256, None, True, False),
+    (131072, 96, 384, "gelu", True, False), (1000, 200, 136, "gelu", True, True),
+    (777, 96, 64, None, True, False), (40, 48, 24, None, True, False), (130, 328, 248, "silu", True, True),
+]
+MODES = [("default", {}), ("wg2=1", {"wg2": 1}), ("wg2=2", {"wg2": 2})]
+
+
+def _inputs(M, N, K, rs, seed):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(M, K, generator=g).to(torch.bfloat16)
+    d = torch.randn(M, N, generator=g).to(torch.bfloat16)
+    rps = 64
+    s = (torch.rand((M + rps - 1) // rps, generator=g) * 2).float() if rs else None
+    return x, d, s, rps
+
+
+def _check(case, knobs, seed=0):
+    M, N, K, act, bias, rs = case
+    x, d, s, rps = _inputs(M, N, K, rs, seed + M + N + K)
+    ref_w, ref_b = _ref(d, x, s, rps, act, M)
+    xd, dd = x.to(DEV), d.to(DEV)
+    sd = s.to(DEV) if s is not None else None
+    for k, v in knobs.items():
+        _opt(k, v)
+    try:
+        dW, db = _wgrad(dd, xd, sd, rps, act, bias, M, N, K)
+    finally:
+        for k in knobs:
+            _opt(k, {"wg2_blocks": 1024}.get(k, 0))
+    assert torch.isfinite(dW).all(), "unwritten / non-finite dW"
+    assert fx.maxrel(dW, ref_w) <= 1e-2, (case, knobs, fx.maxrel(dW, ref_w))
+    if bias:
+        assert torch.isfinite(db).all()
+        assert fx.maxrel(db, ref_b) <= 1e-2, (case, knobs, fx.maxrel(db, ref_b))
+    return dW, db
+
+
+@pytest.mark.parametrize("mode", MODES, ids=[m[0] for m in MODES])
+@pytest.mark.parametrize("case", CASES, ids=lambda c: "x".join(str(v) for v in c[:3]) + f"-{c[3]}")
+def test_wgrad_vs_fp64(case, mode):
+    _check(case, mode[1])
+
+
+@pytest.mark.parametrize("tile", [64, 96, 128, 192])
+@pytest.mark.parametrize("case", [(32768, 192, 768, "gelu", True, True), (1000, 200, 136, None, True, False),
+                                  (130, 328, 248, "silu", False, True)],
+                         ids=lambda c: "x".join(str(v) for v in c[:3]))
+def test_wgrad2_forced_tiles(case, tile):
+    _check(case, {"wg2": 2, "wg2_tile": tile})
+
+
+@pytest.mark.parametrize("blocks", [64, 4096])
+def test_wgrad2_slab_counts(blocks):
+    """Few long slabs (many pipeline steps per workgroup) and many short ones (one or two steps)."""
+    _check((32768, 192, 768, "gelu", True, True), {"wg2": 2, "wg2_blocks": blocks})
+    _check((8192, 256, 1024, "gelu", True, False), {"wg2": 2, "wg2_blocks": blocks})
+
+
+def test_wgrad2_deterministic():
+    case = (32768, 192, 768, "gelu", True, True)
+    a = _check(case, {"wg2": 2})
+    b = _check(case, {"wg2": 2})
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+
+
+@pytest.mark.parametrize("name", fx.fixture_names("mbconv_") + fx.fixture_names("outgrid_block_")[:2])
+def test_modules_bf16_with_wgrad2(name):
+    """Whole bf16 modules (fused MBConv: BN + SiLU + SE-gate prologue) with every weight gradient on
+    the pipelined kernel, against the reference's goldens (test_gpu_parity.test_golden_bf16)."""
+    import test_gpu_parity as tp
+    _opt("wg2", 2)
+    try:
+        tp.test_golden_bf16(name)
+    finally:
+        _opt("wg2", 0)

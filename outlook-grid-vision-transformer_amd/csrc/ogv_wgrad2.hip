@@ -236,7 +236,7 @@ __global__ __launch_bounds__(W2_NT) void wgrad2_bf16_kernel(const bf16* __restri
 }
 
 // ------------------------------------------------------------------------------------------------
-static int g_wg2 = 0;          // knob "wg2": 0 off, 1 = this kernel below the streaming-wgrad M, 2 = at every M
+static int g_wg2 = 2;          // knob "wg2": 0 off, 1 = this kernel below the streaming-wgrad M, 2 = at every M (default: measured faster than both other kernels at every 7M shape but one, which ties)
 static int g_wg2_blocks = 1024;  // knob "wg2_blocks": workgroups the split-M plan aims for
 static int g_wg2_tile = 0;     // knob "wg2_tile": force the N edge (64 / 96 / 128 / 192; K edge 64 / 128)
 int wg2_mode() { return g_wg2; }
@@ -248,30 +248,23 @@ struct W2Plan {
   int ok = 0, BN = 0, BK = 0, nNt = 0, nKt = 0, S = 0, mchunk = 0;
 };
 
-// N edge (G columns): {64, 96, 128, 192}; K edge (X columns, whose chunk columns must be
-// thread-invariant): {64, 128}
-static int w2_tile_n(int N, bool pro) {
-  if (N <= 64) return 64;
-  if (N <= 96) return 96;
-  if (N <= 128) return 128;
-  if (pro && N <= 192) return 192;  // the X prologue then runs once per element
-  if (N % 128 == 0) return 128;
-  if (N % 96 == 0) return 96;
-  if (N % 64 == 0) return 64;
-  return 128;
-}
-static int w2_tile_k(int K) {
-  if (K <= 64) return 64;
-  if (K % 128 == 0 || K % 64 != 0) return 128;
-  return 64;
+// Tile edges (measured, tools/bench_wgrad.py over the 7M step's shapes, profiles/r03_wgrad_isolated.txt):
+// 64 x 64 everywhere (3 workgroups per CU, the most tiles in flight), except a prologue operand
+// with N <= 192, where one N tile covers all of G's columns so the X prologue runs once per element
+// (N edge 96 / 128 / 192; X edge 64).
+static void w2_tiles(int N, bool pro, int& BN, int& BK) {
+  BN = BK = 64;
+  if (pro && N > 64 && N <= 192) BN = N <= 96 ? 96 : (N <= 128 ? 128 : 192);
 }
 
 static W2Plan wgrad2_plan(int M, int N, int K, bool pro) {
   W2Plan p;
   if ((N & 7) || (K & 7) || M <= 0) return p;
-  p.BN = g_wg2_tile ? g_wg2_tile : w2_tile_n(N, pro);
-  p.BK = (g_wg2_tile == 64 || g_wg2_tile == 128) ? g_wg2_tile : w2_tile_k(K);
-  if (p.BN == 192) p.BK = 64;  // 192 x 128 runs out of registers
+  w2_tiles(N, pro, p.BN, p.BK);
+  if (g_wg2_tile) {
+    p.BN = g_wg2_tile;
+    p.BK = g_wg2_tile == 128 ? 128 : 64;  // (N edges 96 / 192 pair with a 64-wide X edge)
+  }
   p.nNt = (N + p.BN - 1) / p.BN;
   p.nKt = (K + p.BK - 1) / p.BK;
   const long tiles = (long)p.nNt * p.nKt;
@@ -311,16 +304,12 @@ template <int PA>
 static void w2_dispatch(const W2Plan& p, const bf16* G, int ldg, const bf16* X, int ldx, const Pro& pro,
                         const float* rs, int rps, float* part, long ldp, bool bias, int M, int N, int K,
                         hipStream_t s) {
-#define OGV_W2_K(BN_)                                                                                        \
-  do {                                                                                                       \
-    if (p.BK == 64) w2_launch<BN_, 64, PA>(p, G, ldg, X, ldx, pro, rs, rps, part, ldp, bias, M, N, K, s);    \
-    else w2_launch<BN_, 128, PA>(p, G, ldg, X, ldx, pro, rs, rps, part, ldp, bias, M, N, K, s);             \
-  } while (0)
-  if (p.BN == 64) OGV_W2_K(64);
-  else if (p.BN == 96) OGV_W2_K(96);
-  else if (p.BN == 128) OGV_W2_K(128);
-  else OGV_W2_K(192);
-#undef OGV_W2_K
+  // instantiated: 64 x 64, 96 x 64, 128 x 64, 192 x 64 and 128 x 128 (forced by wg2_tile=128 only)
+  if (p.BN == 128 && p.BK == 128) w2_launch<128, 128, PA>(p, G, ldg, X, ldx, pro, rs, rps, part, ldp, bias, M, N, K, s);
+  else if (p.BN == 64) w2_launch<64, 64, PA>(p, G, ldg, X, ldx, pro, rs, rps, part, ldp, bias, M, N, K, s);
+  else if (p.BN == 96) w2_launch<96, 64, PA>(p, G, ldg, X, ldx, pro, rs, rps, part, ldp, bias, M, N, K, s);
+  else if (p.BN == 128) w2_launch<128, 64, PA>(p, G, ldg, X, ldx, pro, rs, rps, part, ldp, bias, M, N, K, s);
+  else w2_launch<192, 64, PA>(p, G, ldg, X, ldx, pro, rs, rps, part, ldp, bias, M, N, K, s);
 }
 
 // Returns the number of partial rows written into part (layout [S][N*K + N]), 0 if not handled.

@@ -151,6 +151,11 @@ int ogv_layernorm_bwd(const void* dy, const void* x, const float* gamma, const f
 int ogv_gemm_fwd(const void* A, int lda, const float* W, const float* bias, const void* res,
                  const float* rs, int rps, void* out, int ldo, int M, int N, int K, ogv_act act_in,
                  ogv_dtype dt, void* stream);
+/* Forward with a second output (no reference counterpart; fuses the activation module between two
+ * Linear layers, src/model/Out_Grid_Block.py MLP fc1 -> act -> fc2): out = A . W^T + bias and
+ * aout = act_out(out) of the stored bf16 values, both [M, N] bf16.  bf16 only. */
+int ogv_gemm_fwd_act(const void* A, int lda, const float* W, const float* bias, void* out, int ldo,
+                     void* aout, int ldao, int M, int N, int K, ogv_act act_out, ogv_dtype dt, void* stream);
 size_t ogv_gemm_dgrad_ws_bytes(int N, int K);
 int ogv_gemm_dgrad(const void* dout, int ldd, const float* W, const void* Z, int ldz, const float* rs,
                    int rps, void* dA, int lda, int M, int N, int K, ogv_act act_in, void* ws,

@@ -69,6 +69,10 @@ struct Epi {
   int ldz = 0, zact = 0;
   double* stat = nullptr;
   const float* stat_shift = nullptr;
+  // second output (bf16 forward kernels): aout[m, n] = aact(out[m, n]) of the stored (rounded) value,
+  // e.g. GELU(fc1) materialised for the next GEMM and its weight gradient (ogv_gemm_fwd_act)
+  void* aout = nullptr;
+  int ldao = 0, aact = 0;
 };
 
 // Implicit-GEMM gather for 3x3 / pad-1 convolutions.  The A operand (or the wgrad X operand) is

@@ -128,6 +128,12 @@ __device__ __forceinline__ void gemm_epilogue_bf16(f32x4 (&acc)[TM][TN], float* 
             v[q] = (float)ob[q];
           }
           store_vec<bf16, 8>(out + o, v);
+          if (epi.aout) {
+            float a[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) a[q] = act_fwd(epi.aact, v[q]);
+            store_vec<bf16, 8>(static_cast<bf16*>(epi.aout) + (long)m * epi.ldao + n, a);
+          }
         } else {
 #pragma unroll
           for (int q = 0; q < 8; ++q) {
@@ -136,6 +142,8 @@ __device__ __forceinline__ void gemm_epilogue_bf16(f32x4 (&acc)[TM][TN], float* 
             if (epi.zact) v[q] *= act_grad(epi.zact, (float)Z[(long)m * epi.ldz + n + q]);
             ob[q] = (bf16)v[q];
             out[o + q] = ob[q];
+            if (epi.aout)
+              static_cast<bf16*>(epi.aout)[(long)m * epi.ldao + n + q] = (bf16)act_fwd(epi.aact, (float)ob[q]);
           }
         }
         if constexpr (STATS) {
@@ -1493,6 +1501,28 @@ extern "C" int ogv_gemm_fwd(const void* A, int lda, const float* W, const float*
   epi.rps = rps > 0 ? rps : 1;
   gemm_fwd_launch(dt, A, lda, pro, W, K, out, ldo, M, N, K, K, K, epi, as_stream(stream));
   return check_launch("ogv_gemm_fwd");
+}
+
+// out = A . W^T + bias (bf16, stored rounded) and aout = act(out) of the stored values, one launch:
+// the pre-activation for the next layer's data gradient (act'(Z)) and the activation for its
+// forward and weight gradient, so neither recomputes the activation per element.
+extern "C" int ogv_gemm_fwd_act(const void* A, int lda, const float* W, const float* bias, void* out, int ldo,
+                                void* aout, int ldao, int M, int N, int K, ogv_act act_out, ogv_dtype dt,
+                                void* stream) {
+  int rc = check_common(M, N, K, act_out, dt, "ogv_gemm_fwd_act");
+  if (rc) return rc;
+  OGV_REQUIRE(dt == OGV_BF16, "ogv_gemm_fwd_act: bf16 only");
+  OGV_REQUIRE(A && W && out && aout, "ogv_gemm_fwd_act: null pointer");
+  OGV_REQUIRE(act_out != OGV_ACT_NONE, "ogv_gemm_fwd_act: needs an activation");
+  OGV_REQUIRE(lda >= K, "ogv_gemm_fwd_act: lda %d < K %d", lda, K);
+  OGV_REQUIRE(ldo >= N && ldao >= N, "ogv_gemm_fwd_act: ldo %d / ldao %d < N %d", ldo, ldao, N);
+  Epi epi;
+  epi.bias = bias;
+  epi.aout = aout;
+  epi.ldao = ldao;
+  epi.aact = (int)act_out;
+  gemm_fwd_launch(dt, A, lda, Pro(), W, K, out, ldo, M, N, K, K, K, epi, as_stream(stream));
+  return check_launch("ogv_gemm_fwd_act");
 }
 
 extern "C" size_t ogv_gemm_dgrad_ws_bytes(int N, int K) { return dgrad_ws_bytes(N, K); }

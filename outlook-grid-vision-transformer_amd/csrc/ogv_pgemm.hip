@@ -331,6 +331,13 @@ __global__ __launch_bounds__(PG_NW * 64, 2) void pgemm_bf16_kernel(const bf16* _
 #pragma unroll
           for (int e = 0; e < 8; ++e) ob[e] = (bf16)((acc[i][2 * q + (e >> 2)][e & 3] + bias[e]) * rsc + (float)rb[e]);
           if (ok && !(dbg & 4)) *reinterpret_cast<uint4*>(out + orow(m) * ldo + n) = ov;
+          if (epi.aout && ok) {
+            uint4 av;
+            bf16* ab = reinterpret_cast<bf16*>(&av);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) ab[e] = (bf16)act_fwd(epi.aact, (float)ob[e]);
+            *reinterpret_cast<uint4*>(static_cast<bf16*>(epi.aout) + orow(m) * epi.ldao + n) = av;
+          }
           if constexpr (STATS) {
 #pragma unroll
             for (int h = 0; h < 2; ++h) {   // fragment 2q + h: the same wave-private 16 x 16 pass as below

@@ -365,6 +365,13 @@ __global__ __launch_bounds__(SG_NW * 64) void sgemm_bf16_kernel(const bf16* __re
             }
           }
           *reinterpret_cast<uint2*>(out + m[i] * ldo + n0 + cc) = ov;
+          if (epi.aout) {
+            uint2 av;
+            bf16* ab = reinterpret_cast<bf16*>(&av);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) ab[r] = (bf16)act_fwd(epi.aact, (float)ob[r]);
+            *reinterpret_cast<uint2*>(static_cast<bf16*>(epi.aout) + (long)m[i] * epi.ldao + n0 + cc) = av;
+          }
         }
       }
       if constexpr (STATS) {

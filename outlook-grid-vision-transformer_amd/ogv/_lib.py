@@ -72,6 +72,7 @@ SIGNATURES = {
     "ogv_layernorm_bwd_ws_bytes": (_sz, [_i, _i]),
     "ogv_layernorm_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _p]),
     "ogv_gemm_fwd": (_i, [_p, _i, _p, _p, _p, _p, _i, _p, _i, _i, _i, _i, _i, _i, _p]),
+    "ogv_gemm_fwd_act": (_i, [_p, _i, _p, _p, _p, _i, _p, _i, _i, _i, _i, _i, _i, _p]),
     "ogv_gemm_dgrad_ws_bytes": (_sz, [_i, _i]),
     "ogv_gemm_dgrad": (_i, [_p, _i, _p, _p, _i, _p, _i, _p, _i, _i, _i, _i, _i, _p, _i, _p]),
     "ogv_gemm_wgrad_ws_bytes": (_sz, [_i, _i, _i]),

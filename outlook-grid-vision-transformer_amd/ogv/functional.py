@@ -114,9 +114,9 @@ def probe_bytes(name: str, u: dict) -> int:
     if name == "wgrad":         # read G [M,N], X [M,K]; write fp32 dW [N,K] (+ dbias)
         return e * u["M"] * (u["N"] + u["K"]) + 4 * u["N"] * u["K"] + (4 * u["N"] if u["bias"] else 0)
     if name in ("gemm_fwd", "sgemm", "gemm_tiled", "gemm_panel") and u.get("kind", "fwd") == "fwd":
-        # read A [M,K] (+ residual [M,N]) + fp32 W [N,K] (+ bias), write out [M,N]
-        return (e * u["M"] * (u["K"] + u["N"] * (2 if u["res"] else 1)) + 4 * u["N"] * u["K"]
-                + (4 * u["N"] if u["bias"] else 0))
+        # read A [M,K] (+ residual [M,N]) + fp32 W [N,K] (+ bias), write out [M,N] (+ act(out) [M,N])
+        return (e * u["M"] * (u["K"] + u["N"] * (2 if u["res"] else 1) + (u["N"] if u.get("aout") else 0))
+                + 4 * u["N"] * u["K"] + (4 * u["N"] if u["bias"] else 0))
     if name in ("sgemm", "gemm_tiled", "gemm_panel"):   # dgrad: read dOut [M,N] (+ Z [M,K]) + fp32 W [N,K], write dA [M,K]
         return e * u["M"] * (u["N"] + u["K"] * (2 if u["z"] else 1)) + 4 * u["N"] * u["K"]
     raise KeyError(name)
@@ -390,43 +390,82 @@ def _rows_contig(t: torch.Tensor) -> torch.Tensor:
 # ------------------------------------------------------------------------------------------------
 class _Linear(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x2d, w2d, bias, residual, row_scale, rps, act_in):
+    def forward(ctx, x2d, w2d, bias, residual, row_scale, rps, act_in, x_act):
+        # x_act (optional): act_in(x2d) already materialised by the producing GEMM (ogv_gemm_fwd_act):
+        # the product and the weight gradient read it with no prologue; x2d (the pre-activation)
+        # only feeds the data gradient's act'(x2d) epilogue
         lib = _lib.load()
         M, K = x2d.shape
         N = w2d.shape[0]
         out = torch.empty((M, N), dtype=x2d.dtype, device=x2d.device)
+        a_in = x_act if x_act is not None else x2d
+        act_fwd = None if x_act is not None else act_in
         units = dict(M=M, N=N, K=K, elem=x2d.element_size(), res=residual is not None, bias=bias is not None)
-        route = lib.ogv_gemm_stream_route(0, M, N, K, ACT[act_in]) if _PROBE["armed"] else -1
+        route = lib.ogv_gemm_stream_route(0, M, N, K, ACT[act_fwd]) if _PROBE["armed"] else -1
         bf = x2d.dtype == torch.bfloat16
         with _probe("gemm_fwd", units), _probe("sgemm", units, when=bf and route == 1), \
                 _probe("gemm_panel", units, when=bf and route == 2), _probe("gemm_tiled", units, when=bf and route == 0), \
                 _census("gemm_fwd", units):
-            check(lib.ogv_gemm_fwd(_ptr(x2d), x2d.stride(0), _ptr(w2d), _ptr(bias), _ptr(residual), _ptr(row_scale),
-                                   int(rps), _ptr(out), N, M, N, K, ACT[act_in], _dt(x2d), _stream()), "ogv_gemm_fwd")
-        ctx.save_for_backward(x2d, w2d, row_scale)
+            check(lib.ogv_gemm_fwd(_ptr(a_in), a_in.stride(0), _ptr(w2d), _ptr(bias), _ptr(residual), _ptr(row_scale),
+                                   int(rps), _ptr(out), N, M, N, K, ACT[act_fwd], _dt(x2d), _stream()), "ogv_gemm_fwd")
+        ctx.save_for_backward(x2d, w2d, row_scale, x_act)
         ctx.meta = (M, N, K, int(rps), ACT[act_in], bias is not None, residual is not None)
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        x2d, w2d, rs = ctx.saved_tensors
+        x2d, w2d, rs, x_act = ctx.saved_tensors
         M, N, K, rps, act, has_bias, has_res = ctx.meta
         dout = dout.to(x2d.dtype).contiguous()
         want_dx = ctx.needs_input_grad[0]
         want_dw = ctx.needs_input_grad[1] or (has_bias and ctx.needs_input_grad[2])
-        dx, dw, db = _linear_bwd(dout, x2d, w2d, rs, rps, act, has_bias, want_dx, want_dw)
+        dx, dw, db = _linear_bwd(dout, x2d, w2d, rs, rps, act, has_bias, want_dx, want_dw, x_act)
         dres = dout if has_res and ctx.needs_input_grad[3] else None
-        return dx, dw, db, dres, None, None, None
+        return dx, dw, db, dres, None, None, None, None
 
 
-def _linear_bwd(dout, x2d, w2d, rs, rps, act, has_bias, want_dx, want_dw):
+class _LinearAct(torch.autograd.Function):
+    """First Linear of a Linear -> act -> Linear pair: (Z, act(Z)) from one GEMM launch
+    (ogv_gemm_fwd_act).  act(Z) is a non-differentiable by-product: the second layer, given it as
+    x_act, returns its input gradient with respect to Z (act'(Z) in its data-gradient epilogue)."""
+
+    @staticmethod
+    def forward(ctx, x2d, w2d, bias, act):
+        lib = _lib.load()
+        M, K = x2d.shape
+        N = w2d.shape[0]
+        out = torch.empty((M, N), dtype=x2d.dtype, device=x2d.device)
+        aout = torch.empty((M, N), dtype=x2d.dtype, device=x2d.device)
+        units = dict(M=M, N=N, K=K, elem=x2d.element_size(), res=False, bias=bias is not None, aout=True)
+        with _probe("gemm_fwd", units), _census("gemm_fwd", units):
+            check(lib.ogv_gemm_fwd_act(_ptr(x2d), x2d.stride(0), _ptr(w2d), _ptr(bias), _ptr(out), N, _ptr(aout), N,
+                                       M, N, K, ACT[act], _dt(x2d), _stream()), "ogv_gemm_fwd_act")
+        ctx.mark_non_differentiable(aout)
+        ctx.save_for_backward(x2d, w2d)
+        ctx.meta = bias is not None
+        return out, aout
+
+    @staticmethod
+    def backward(ctx, dout, _daout):
+        x2d, w2d = ctx.saved_tensors
+        has_bias = ctx.meta
+        dout = dout.to(x2d.dtype).contiguous()
+        want_dx = ctx.needs_input_grad[0]
+        want_dw = ctx.needs_input_grad[1] or (has_bias and ctx.needs_input_grad[2])
+        dx, dw, db = _linear_bwd(dout, x2d, w2d, None, 1, 0, has_bias, want_dx, want_dw)
+        return dx, dw, db, None
+
+
+def _linear_bwd(dout, x2d, w2d, rs, rps, act, has_bias, want_dx, want_dw, x_act=None):
     """(dx, dW, dbias) of out = rs * (act(x) @ W^T + b) from dout; the weight gradient forks onto the
-    side stream when both are wanted."""
+    side stream when both are wanted.  With x_act (= act(x) materialised) the weight gradient reads it
+    with no prologue."""
     lib = _lib.load()
     M, K = x2d.shape
     N = w2d.shape[0]
     dt = _dt(x2d)
     dx = dw = db = None
+    xw, wact = (x_act, 0) if x_act is not None else (x2d, act)
     if want_dx:
         dx = torch.empty((M, K), dtype=x2d.dtype, device=x2d.device)
         ws_d = _ws(lib.ogv_gemm_dgrad_ws_bytes(N, K), x2d.device)
@@ -441,12 +480,12 @@ def _linear_bwd(dout, x2d, w2d, rs, rps, act, has_bias, want_dx, want_dw):
     # (while a probe is armed everything stays on the current stream, where its events are)
     fork = (want_dx and want_dw and M * (N + K) >= _FORK_MIN_WORK and not _serial()
             and (_FORK_ACT or not act))
-    with _fork(fork, dout, x2d, rs, dw, db, ws_w if want_dw else None) as side:
+    with _fork(fork, dout, xw, rs, dw, db, ws_w if want_dw else None) as side:
         if want_dw:
             wu = dict(M=M, N=N, K=K, elem=x2d.element_size(), bias=has_bias)
             with _probe("wgrad", wu, when=x2d.dtype == torch.bfloat16), _census("gemm_wgrad", wu):
-                check(lib.ogv_gemm_wgrad(_ptr(dout), N, _ptr(x2d), x2d.stride(0), _ptr(rs), rps, _ptr(dw), _ptr(db),
-                                         M, N, K, act, _ptr(ws_w), dt, side), "ogv_gemm_wgrad")
+                check(lib.ogv_gemm_wgrad(_ptr(dout), N, _ptr(xw), xw.stride(0), _ptr(rs), rps, _ptr(dw), _ptr(db),
+                                         M, N, K, wact, _ptr(ws_w), dt, side), "ogv_gemm_wgrad")
         if want_dx:
             route = lib.ogv_gemm_stream_route(1, M, N, K, act) if _PROBE["armed"] else -1
             du = dict(kind="dgrad", M=M, N=N, K=K, elem=x2d.element_size(), z=bool(act))
@@ -459,9 +498,24 @@ def _linear_bwd(dout, x2d, w2d, rs, rps, act, has_bias, want_dx, want_dw):
     return dx, dw, db
 
 
-def linear_rows(x2d, weight, bias=None, residual=None, row_scale=None, rps=1, act_in=None):
-    """x2d [M,K] (row stride >= K), weight [N,K] (or [N,K,1,1]), residual [M,N]."""
-    require_device(x2d, weight, bias, residual, row_scale, what="ogv.linear")
+# knob: OGV_MAT_ACT=0 keeps the activation between two Linears as the second GEMM's prologue
+_MAT_ACT = os.environ.get("OGV_MAT_ACT", "1") != "0"
+
+
+def materialise_act(x: torch.Tensor, *mods) -> bool:
+    """Whether a Linear -> act -> Linear pair should run as ogv_gemm_fwd_act + a prologue-free second
+    GEMM: bf16 compute, autograd recording (the materialised activation is kept for the weight
+    gradient; inference keeps the prologue form and its smaller footprint), no hooks on either
+    Linear (their outputs must stay the reference's single tensors)."""
+    if not _MAT_ACT or not torch.is_grad_enabled() or compute_dtype(x) != torch.bfloat16:
+        return False
+    return not any(m._forward_hooks or m._forward_pre_hooks for m in mods)
+
+
+def linear_rows(x2d, weight, bias=None, residual=None, row_scale=None, rps=1, act_in=None, x_act=None):
+    """x2d [M,K] (row stride >= K), weight [N,K] (or [N,K,1,1]), residual [M,N].  x_act: act_in(x2d)
+    as materialised by linear_rows_act (same shape)."""
+    require_device(x2d, weight, bias, residual, row_scale, x_act, what="ogv.linear")
     x2d = _rows_contig(x2d)
     w2d = f32(weight).reshape(weight.shape[0], -1)
     if w2d.shape[1] != x2d.shape[1]:
@@ -472,7 +526,24 @@ def linear_rows(x2d, weight, bias=None, residual=None, row_scale=None, rps=1, ac
             raise ValueError("ogv.linear: residual shape mismatch")
     if row_scale is not None:
         row_scale = row_scale.float().contiguous()
-    return _Linear.apply(x2d, w2d, f32(bias), residual, row_scale, int(rps), act_in)
+    if x_act is not None:
+        if act_in is None or x_act.shape != x2d.shape or x_act.dtype != x2d.dtype:
+            raise ValueError("ogv.linear: x_act must be act_in(x2d) with x2d's shape and dtype")
+        x_act = _rows_contig(x_act)
+    return _Linear.apply(x2d, w2d, f32(bias), residual, row_scale, int(rps), act_in, x_act)
+
+
+def linear_rows_act(x2d, weight, bias, act):
+    """(Z, act(Z)) = (x2d @ W^T + b, its activation), both [M, N] bf16, one launch.  act(Z) carries no
+    gradient of its own: pass it to the next linear_rows as x_act with act_in=act and Z as x2d."""
+    require_device(x2d, weight, bias, what="ogv.linear_act")
+    x2d = _rows_contig(x2d)
+    if x2d.dtype != torch.bfloat16:
+        raise ValueError("ogv.linear_act: bf16 only")
+    w2d = f32(weight).reshape(weight.shape[0], -1)
+    if w2d.shape[1] != x2d.shape[1]:
+        raise ValueError(f"ogv.linear_act: weight in_features {w2d.shape[1]} != input features {x2d.shape[1]}")
+    return _LinearAct.apply(x2d, w2d, f32(bias), act)
 
 
 # ------------------------------------------------------------------------------------------------

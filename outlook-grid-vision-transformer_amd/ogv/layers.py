@@ -33,12 +33,18 @@ class Conv1x1(nn.Conv2d):
     def __init__(self, in_channels: int, out_channels: int, bias: bool = True):
         super().__init__(in_channels, out_channels, kernel_size=1, bias=bias)
 
-    def forward(self, x, residual=None, row_scale=None, act_in=None):
+    def forward(self, x, residual=None, row_scale=None, act_in=None, x_act=None, emit_act=None):
+        """emit_act: return (y, emit_act(y)) from one launch (bf16); x_act: act_in(x) as emitted by
+        the previous layer (the product and the weight gradient read it, x feeds act'(x))."""
         B, C, H, W = x.shape
         dt = OF.compute_dtype(x)
         x2d = OF.nchw_to_rows(x.to(dt))
+        if emit_act is not None:
+            y, a = OF.linear_rows_act(x2d, self.weight, self.bias, emit_act)
+            return OF.rows_to_nchw(y, B, H, W), OF.rows_to_nchw(a, B, H, W)
         r2d = OF.nchw_to_rows(residual.to(dt)) if residual is not None else None
-        y = OF.linear_rows(x2d, self.weight, self.bias, r2d, row_scale, H * W, act_in)
+        xa2d = OF.nchw_to_rows(x_act) if x_act is not None else None
+        y = OF.linear_rows(x2d, self.weight, self.bias, r2d, row_scale, H * W, act_in, xa2d)
         return OF.rows_to_nchw(y, B, H, W)
 
 
@@ -56,14 +62,19 @@ class Linear(nn.Linear):
     """nn.Linear over the last dim of a contiguous [..., in] tensor (BHWC or [B, N, C]).
     ``rps`` = rows per sample for the DropPath row scale."""
 
-    def forward(self, x, residual=None, row_scale=None, rps=None, act_in=None):
+    def forward(self, x, residual=None, row_scale=None, rps=None, act_in=None, x_act=None, emit_act=None):
+        """emit_act / x_act: as Conv1x1.forward."""
         lead = x.shape[:-1]
         dt = OF.compute_dtype(x)
         x2d = x.to(dt).reshape(-1, x.shape[-1])
+        if emit_act is not None:
+            y, a = OF.linear_rows_act(x2d, self.weight, self.bias, emit_act)
+            return y.view(*lead, self.out_features), a.view(*lead, self.out_features)
         r2d = residual.to(dt).reshape(-1, self.out_features) if residual is not None else None
         if rps is None:
             rps = max(1, x2d.shape[0] // max(1, lead[0] if len(lead) else 1))
-        y = OF.linear_rows(x2d, self.weight, self.bias, r2d, row_scale, rps, act_in)
+        xa2d = x_act.reshape(-1, x.shape[-1]) if x_act is not None else None
+        y = OF.linear_rows(x2d, self.weight, self.bias, r2d, row_scale, rps, act_in, xa2d)
         return y.view(*lead, self.out_features)
 
 

@@ -44,6 +44,9 @@ class MLP(nn.Module):
             if row_scale is not None:
                 y = y * row_scale.view(-1, *([1] * (y.ndim - 1))).to(y.dtype)
             return residual + y
+        if OF.materialise_act(x, self.fc1, self.fc2):   # fc1 also writes act(fc1(x)): fc2 and its wgrad skip the prologue
+            z, az = self.fc1(x, rps=rps, emit_act=a)
+            return self.fc2(z, residual=residual, row_scale=row_scale, rps=rps, act_in=a, x_act=az)
         return self.fc2(self.fc1(x, rps=rps), residual=residual, row_scale=row_scale, rps=rps, act_in=a)
 
 

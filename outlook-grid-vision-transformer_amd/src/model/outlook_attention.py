@@ -82,6 +82,9 @@ class MLP2d(nn.Module):
             if row_scale is not None:
                 y = y * row_scale.view(-1, 1, 1, 1).to(y.dtype)
             return residual + y
+        if OF.materialise_act(x, self.fc1, self.fc2):   # fc1 also writes act(fc1(x)): fc2 and its wgrad skip the prologue
+            z, az = self.fc1(x, emit_act=a)
+            return self.fc2(z, residual=residual, row_scale=row_scale, act_in=a, x_act=az)
         return self.fc2(self.fc1(x), residual=residual, row_scale=row_scale, act_in=a)
 
 

@@ -151,3 +151,82 @@ def test_modules_bf16_legacy_wgrad(name):
         tp.test_golden_bf16(name)
     finally:
         _opt("wg2", 2)
+
+
+# ------------------------------------------------------------------------------------------------
+# ogv_gemm_fwd_act: fc1 of a Linear -> act -> Linear pair writes Z and act(Z) in one launch; the MLPs
+# then run fc2 and its weight gradient on act(Z) with no prologue (functional.materialise_act).
+FWD_ACT_CASES = [  # M, N, K, act: streaming (large M), panel (M = 32768 / 8192), tiled (ragged / N % 8)
+    (524288, 192, 48, "gelu"), (131072, 384, 96, "gelu"), (32768, 768, 192, "gelu"), (8192, 1024, 256, "silu"),
+    (1000, 200, 136, "gelu"), (130, 54, 24, "gelu"),
+]
+
+
+@pytest.mark.parametrize("case", FWD_ACT_CASES, ids=lambda c: "x".join(str(v) for v in c[:3]) + f"-{c[3]}")
+def test_gemm_fwd_act(case):
+    """out is bit-identical to ogv_gemm_fwd's; aout = act(out) of the stored bf16 values within one
+    bf16 rounding (the kernels' erf is the A&S 7.1.26 form, |err| <= 1.5e-7)."""
+    M, N, K, act = case
+    g = torch.Generator().manual_seed(M + N + K)
+    x = torch.randn(M, K, generator=g).to(torch.bfloat16).to(DEV)
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(DEV)
+    b = (0.1 * torch.randn(N, generator=g)).to(DEV)
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    ref = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    assert _L().ogv_gemm_fwd(_p(x), K, _p(w), _p(b), None, None, 1, _p(ref), N, M, N, K, 0, BF16, st) == 0
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    aout = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    assert _L().ogv_gemm_fwd_act(_p(x), K, _p(w), _p(b), _p(out), N, _p(aout), N, M, N, K, ACT[act], BF16, st) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    f = {"gelu": torch.nn.functional.gelu, "silu": torch.nn.functional.silu}[act]
+    want = f(out.float())
+    assert ((aout.float() - want).abs() <= 2 ** -7 * want.abs() + 1e-6).all()
+
+
+def test_gemm_fwd_act_rejects():
+    x = torch.zeros(64, 32, device=DEV)
+    w = torch.zeros(16, 32, device=DEV)
+    o = torch.zeros(64, 16, device=DEV)
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    assert _L().ogv_gemm_fwd_act(_p(x), 32, _p(w), None, _p(o), 16, _p(o), 16, 64, 16, 32, 1, 0, st) != 0  # fp32
+    xb, ob = x.bfloat16(), o.bfloat16()
+    assert _L().ogv_gemm_fwd_act(_p(xb), 32, _p(w), None, _p(ob), 16, _p(ob), 16, 64, 16, 32, 0, BF16, st) != 0
+
+
+@pytest.mark.parametrize("which,C,H,B", [("mlp", 192, 8, 16), ("mlp", 48, 32, 4), ("mlp2d", 96, 16, 6),
+                                         ("mlp2d", 256, 4, 8)])
+def test_mlp_materialised_act_matches_prologue(which, C, H, B):
+    """A bf16 MLP with the activation materialised by fc1 (default) against the same module with the
+    activation as fc2's prologue (OGV_MAT_ACT=0 form): same bf16 operands everywhere, so outputs and
+    the input gradient agree to bf16 rounding and the weight gradients to the fp32 summation order."""
+    from ogv import functional as OF
+    from src.model.Out_Grid_Block import MLP
+    from src.model.outlook_attention import MLP2d
+    torch.manual_seed(C + H)
+    mod = (MLP(C, 4.0) if which == "mlp" else MLP2d(C, 2.0)).to(DEV)
+    if which == "mlp":
+        x = torch.randn(B, H, H, C, device=DEV)
+        res = torch.randn(B, H, H, C, device=DEV).bfloat16()
+    else:
+        x = torch.randn(B, C, H, H, device=DEV).contiguous(memory_format=torch.channels_last)
+        res = torch.randn(B, C, H, H, device=DEV).contiguous(memory_format=torch.channels_last).bfloat16()
+    rs = (torch.rand(B, device=DEV) * 2)
+    runs = []
+    for mat in (True, False):
+        OF._MAT_ACT = mat
+        try:
+            xi = x.clone().bfloat16().requires_grad_()
+            for p in mod.parameters():
+                p.grad = None
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                y = mod(xi, residual=res, row_scale=rs)
+            y.float().square().sum().backward()
+            runs.append((y.detach().float(), xi.grad.float(), [p.grad.clone() for p in mod.parameters()]))
+        finally:
+            OF._MAT_ACT = True
+    (y0, dx0, g0), (y1, dx1, g1) = runs
+    assert fx.maxrel(y0, y1) <= 1e-2
+    assert fx.maxrel(dx0, dx1) <= 1e-2
+    for a, b in zip(g0, g1):
+        assert fx.maxrel(a, b) <= 1e-3

@@ -160,22 +160,39 @@ __device__ __forceinline__ float act_grad(int act, float x) {
 }
 
 // ---------------------------------------------------------------- wave reductions (wave64)
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+// Exchanges inside a row of 16 lanes go through DPP (an operand modifier of a VALU instruction);
+// __shfl_xor lowers to ds_bpermute, an LDS round trip per call.  Butterfly partners: xor 1 and
+// xor 2 (quad_perm), then the mirrored lane of the other quad (row_half_mirror) and of the other
+// half-row (row_mirror): after those four steps every lane of a row holds the row total, the same
+// value in all 16 lanes (a + b == b + a).  The steps across rows (16, 32) stay shuffles.
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
 }
+constexpr int DPP_XOR1 = 0xB1, DPP_XOR2 = 0x4E, DPP_HALF_MIRROR = 0x141, DPP_MIRROR = 0x140;
+
 template <int G>
 __device__ __forceinline__ float group_sum(float v) {  // sum within aligned groups of G lanes
-#pragma unroll
-  for (int o = G / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  static_assert(G == 1 || G == 2 || G == 4 || G == 8 || G == 16 || G == 32 || G == 64, "power of two <= 64");
+  if constexpr (G >= 2) v += dpp_mov<DPP_XOR1>(v);
+  if constexpr (G >= 4) v += dpp_mov<DPP_XOR2>(v);
+  if constexpr (G >= 8) v += dpp_mov<DPP_HALF_MIRROR>(v);
+  if constexpr (G >= 16) v += dpp_mov<DPP_MIRROR>(v);
+  if constexpr (G >= 32) v += __shfl_xor(v, 16, 64);
+  if constexpr (G >= 64) v += __shfl_xor(v, 32, 64);
   return v;
 }
 template <int G>
 __device__ __forceinline__ float group_max(float v) {
-#pragma unroll
-  for (int o = G / 2; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  static_assert(G == 1 || G == 2 || G == 4 || G == 8 || G == 16 || G == 32 || G == 64, "power of two <= 64");
+  if constexpr (G >= 2) v = fmaxf(v, dpp_mov<DPP_XOR1>(v));
+  if constexpr (G >= 4) v = fmaxf(v, dpp_mov<DPP_XOR2>(v));
+  if constexpr (G >= 8) v = fmaxf(v, dpp_mov<DPP_HALF_MIRROR>(v));
+  if constexpr (G >= 16) v = fmaxf(v, dpp_mov<DPP_MIRROR>(v));
+  if constexpr (G >= 32) v = fmaxf(v, __shfl_xor(v, 16, 64));
+  if constexpr (G >= 64) v = fmaxf(v, __shfl_xor(v, 32, 64));
   return v;
 }
+__device__ __forceinline__ float wave_sum(float v) { return group_sum<64>(v); }
 
 }  // namespace ogv

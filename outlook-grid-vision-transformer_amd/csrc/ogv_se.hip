@@ -105,9 +105,7 @@ __global__ __launch_bounds__(SE_NT) void se_gemv_kernel(const float* __restrict_
         }
       }
 #pragma unroll
-      for (int r = 0; r < SE_RB; ++r)
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) acc[r] += __shfl_xor(acc[r], o, 64);
+      for (int r = 0; r < SE_RB; ++r) acc[r] = group_sum<16>(acc[r]);
       if (n < N && kl < SE_RB && b0 + kl < B) {
         float v = acc[0];
 #pragma unroll

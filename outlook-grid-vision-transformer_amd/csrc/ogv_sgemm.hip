@@ -375,17 +375,15 @@ __global__ __launch_bounds__(SG_NW * 64) void sgemm_bf16_kernel(const bf16* __re
         }
       }
       if constexpr (STATS) {
-        // rows are spread over the 16 lanes fr of a group: reduce (xor 1..8), fp32 over <= 32 rows,
+        // rows are spread over the 16 lanes fr of a group: reduce (DPP butterfly), fp32 over <= 32 rows,
         // then fp64 across panels in the wave's LDS accumulator
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-#pragma unroll
-            for (int o = 1; o < 16; o <<= 1) {
-              s1[j][r] += __shfl_xor(s1[j][r], o, 64);
-              s2[j][r] += __shfl_xor(s2[j][r], o, 64);
-            }
+          for (int r = 0; r < 4; ++r) {
+            s1[j][r] = group_sum<16>(s1[j][r]);
+            s2[j][r] = group_sum<16>(s2[j][r]);
+          }
         if (fr == 0) {
           double* sa = sacc + wave * 2 * nbp;
 #pragma unroll

@@ -441,6 +441,7 @@ class _LinearAct(torch.autograd.Function):
             check(lib.ogv_gemm_fwd_act(_ptr(x2d), x2d.stride(0), _ptr(w2d), _ptr(bias), _ptr(out), N, _ptr(aout), N,
                                        M, N, K, ACT[act], _dt(x2d), _stream()), "ogv_gemm_fwd_act")
         ctx.mark_non_differentiable(aout)
+        ctx.set_materialize_grads(False)   # no zero-filled gradient for aout (an [M, N] fill per call)
         ctx.save_for_backward(x2d, w2d)
         ctx.meta = bias is not None
         return out, aout
@@ -449,6 +450,8 @@ class _LinearAct(torch.autograd.Function):
     def backward(ctx, dout, _daout):
         x2d, w2d = ctx.saved_tensors
         has_bias = ctx.meta
+        if dout is None:   # Z unused downstream (possible once grads are not materialised)
+            return None, None, None, None
         dout = dout.to(x2d.dtype).contiguous()
         want_dx = ctx.needs_input_grad[0]
         want_dw = ctx.needs_input_grad[1] or (has_bias and ctx.needs_input_grad[2])

@@ -92,13 +92,22 @@ size_t ogv_outlook_bwd_ws_bytes(int B, int H, int W, int C, int heads, int k, og
  * Writes y [M, C] and, when cat != NULL, cat [M, ldc] = [v | logits | 0] rounded to bf16 (what
  * ogv_outlook_agg_bwd reads in training).  ldc must be C + heads*9 rounded up to 8.
  * ogv_outlook_vproj_supported() says whether a shape takes this kernel (16 | C <= 96,
- * 8 | head_dim) for inference (train = 0) or training (train = 1) under knob "outlook_vproj"
- * (0 never, 1 inference only -- the default, 2 both); ogv_outlook_vproj_fwd itself runs any shape
- * the kernel supports and returns OGV_ERR_ARG for the others. */
+ * 8 | head_dim) for inference (train = 0) or training (train = 1: the forward with cat = NULL plus
+ * ogv_outlook_vproj_bwd) under knob "outlook_vproj" (0 never, 1 inference only, 2 both);
+ * ogv_outlook_vproj_fwd itself runs any shape the kernel supports and returns OGV_ERR_ARG for the
+ * others.
+ * ogv_outlook_vproj_bwd: the backward of the same fused op with the projections RECOMPUTED from x
+ * (the forward's weights and rounding, so v / logits are those the forward used): reads x, dy
+ * ([M, C] contiguous) and writes dcat [M, ldc] = [dv | dlogits | 0], the gradient of the
+ * concatenated projection output, for one dgrad + one wgrad of w.  Replaces the autograd of
+ * src/model/outlook_attention.py:100-120 (unfold / softmax / fold). */
 int ogv_outlook_vproj_supported(int B, int H, int W, int C, int heads, int k, int ldc, int train,
                                 ogv_dtype dt);
 int ogv_outlook_vproj_fwd(const void* x, int ldx, const float* w, const float* bias, void* cat, int ldc,
                           void* y, int B, int H, int W, int C, int heads, int k, ogv_dtype dt, void* stream);
+int ogv_outlook_vproj_bwd(const void* x, int ldx, const float* w, const float* bias, const void* dy,
+                          void* dcat, int ldc, int B, int H, int W, int C, int heads, int k, ogv_dtype dt,
+                          void* stream);
 int ogv_outlook_agg_bwd(const void* dy, const void* v, const void* logits, void* dv, void* dlogits,
                         float* probs_ws, int B, int H, int W, int C, int heads, int k, int ld_logits,
                         int ld_v, int ld_dv, int ld_dlogits, int dl_cols, ogv_dtype dt, void* stream);

@@ -1155,6 +1155,285 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void outlook_vproj_fwd_kernel(
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Outlooker backward fused with the RECOMPUTE of its v / attn projections -- the training half of
+// the fused Outlooker (the forward above then writes only y: [v | logits] never reaches HBM).
+// Per TH x TW tile, as the forward: x of the halo pixels -> LDS, [v | logits] = x . Wc^T + b on
+// MFMA with the forward's fragments, weights and rounding point (bit-identical v / logits to what
+// the forward aggregated), then the softmax of EVERY in-image halo pixel into LDS and, from LDS,
+//   dP[p,h,j]      = dy[p, h, :] . v[p + off_j, h, :]
+//   dlogits[p,h,j] = P[p,h,j] (dP[p,h,j] - sum_j' P[p,h,j'] dP[p,h,j'])
+//   dv[q, h, :]    = sum_j P[q - off_j, h, j] dy[q - off_j, h, :]   (the col2im fold as a gather)
+// (the autograd of src/model/outlook_attention.py:100-120), written as ONE gradient
+// dcat = [dv | dlogits | 0] [M, ld] that the concatenated projection's dgrad and wgrad consume.
+// dlogits go into the result tile's (then dead) logit columns and leave with 16-B stores.
+// HBM: x and dy read (with the halo), dcat written -- the unfused pair's cat write (forward GEMM),
+// cat re-read (aggregation) and cat re-read (backward) are gone.
+// LDS: [x tile | P over the halo (aliases x after the MFMA)] [result tile] [dy halo tile, pitch C]
+//      [W hi | lo] [bias]
+// ------------------------------------------------------------------------------------------------
+static size_t vtile_bwd_x_bytes(const VTile& t, int heads) {
+  const size_t xb = (size_t)t.HP * t.XP * 2, pb = (size_t)t.HP * heads * 9 * 4;
+  return ((xb > pb ? xb : pb) + 15) / 16 * 16;
+}
+static size_t vtile_bwd_lds(const VTile& t, int C, int heads, bool sw) {
+  return vtile_bwd_x_bytes(t, heads) + (size_t)(t.HP + 2) * t.RP * 2 + (size_t)t.HP * C * 2 +
+         (size_t)(sw ? 2 : 1) * t.ncol * t.WP * 2 + (size_t)t.ncol * 4;
+}
+
+// 16-B chunks per thread and tile of each prefetched halo tile (x, dy): 6 at 4 waves covers 8 x 16
+// tiles at K <= 64 and 8 x 8 tiles at K <= 80; 5 at 8 waves covers 8 x 16 tiles at K <= 96
+template <int NW>
+__host__ __device__ constexpr int vp_bwd_pf() { return NW == 8 ? 5 : 6; }
+
+template <int NJ, int NK, bool SW, int NW>
+__global__ __launch_bounds__(NW * 64, 8 / NW) void outlook_vproj_bwd_kernel(
+    const bf16* __restrict__ x, int ldx, const float* __restrict__ Wc, int wrows, const float* __restrict__ bias,
+    const bf16* __restrict__ dy, int lddy, bf16* __restrict__ dcat, int ldc, int H, int W, int C, int heads, VTile t,
+    int xbytes, int dbg) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int KP = NK * 32, NCOL = NJ * 16, NT = NW * 64, VP_PF = vp_bwd_pf<NW>();
+  const int XP = t.XP, RP = t.RP, WP = t.WP, HW2 = t.TW + 2, HP = t.HP;
+  bf16* xs = reinterpret_cast<bf16*>(smem);                          // [HP][XP]
+  float* P = reinterpret_cast<float*>(smem);                         // [HP][heads][9] (after the GEMM)
+  bf16* rs = reinterpret_cast<bf16*>(smem + xbytes);                 // [HP + 2][RP]: [v | logits | 0]
+  bf16* gs = rs + (size_t)(HP + 2) * RP;                             // [HP][C]: dy with the halo
+  bf16* ws = gs + (size_t)HP * C;                                    // [hi | lo][NCOL][WP]
+  float* bs = reinterpret_cast<float*>(ws + (size_t)(SW ? 2 : 1) * NCOL * WP);   // [NCOL]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int hd = C / heads, CH8 = C / 8, HC8 = hd / 8;
+
+  for (int idx = tid; idx < NCOL * (KP / 4); idx += NT) {
+    const int n = idx / (KP / 4), k = (idx - n * (KP / 4)) * 4;
+    float4 w4 = float4{0.f, 0.f, 0.f, 0.f};
+    if (n < wrows && k < C) w4 = *reinterpret_cast<const float4*>(Wc + (long)n * C + k);
+    const bf16x4 h = {(bf16)w4.x, (bf16)w4.y, (bf16)w4.z, (bf16)w4.w};
+    *reinterpret_cast<bf16x4*>(ws + n * WP + k) = h;
+    if constexpr (SW) {
+      const bf16x4 l = {(bf16)(w4.x - (float)h[0]), (bf16)(w4.y - (float)h[1]), (bf16)(w4.z - (float)h[2]),
+                        (bf16)(w4.w - (float)h[3])};
+      *reinterpret_cast<bf16x4*>(ws + (NCOL + n) * WP + k) = l;
+    }
+  }
+  for (int n = tid; n < NCOL; n += NT) bs[n] = (bias && n < wrows) ? bias[n] : 0.f;
+
+  const int G = gridDim.x;
+  const int vid = (blockIdx.x & 7) * (G / 8) + (blockIdx.x >> 3);   // XCD-contiguous logical id
+  const int NI = t.HPr / 16, PT = t.TH * t.TW;
+  constexpr int KC = KP / 8;
+  const int total = HP * KC;      // 16-B chunks of the x halo tile (<= VP_PF * NT, checked by the plan)
+  const int gtotal = HP * CH8;    // ... of the dy halo tile (<= total)
+  // x and dy halo tiles of `tile` -> registers, issued one tile ahead
+  uint4 pf[VP_PF], pg[VP_PF];
+  auto load_tile = [&](long tile) {
+    if (dbg & 16) return;
+    const int b = fdiv((int)tile, t.per_img);
+    const int r0 = (int)tile - b * t.per_img.d;
+    const int ty0 = fdiv(r0, t.fntx);
+    const int y0 = ty0 * t.TH, x0 = (r0 - ty0 * t.ntx) * t.TW;
+#pragma unroll
+    for (int u = 0; u < VP_PF; ++u) {
+      const int idx = tid + u * NT;
+      pf[u] = pg[u] = uint4{0u, 0u, 0u, 0u};
+      if (idx < total) {
+        const int hp = idx / KC, c8 = idx - hp * KC;
+        const int hy = fdiv(hp, t.fHW2);
+        const int yy = y0 - 1 + hy, xx = x0 - 1 + hp - hy * HW2;
+        if (c8 < CH8 && yy >= 0 && yy < H && xx >= 0 && xx < W)
+          pf[u] = *reinterpret_cast<const uint4*>(x + ((long)(b * H + yy) * W + xx) * ldx + c8 * 8);
+      }
+      if (idx < gtotal) {
+        const int hp = fdiv(idx, t.fCH), c8 = idx - hp * CH8;
+        const int hy = fdiv(hp, t.fHW2);
+        const int yy = y0 - 1 + hy, xx = x0 - 1 + hp - hy * HW2;
+        if (yy >= 0 && yy < H && xx >= 0 && xx < W)
+          pg[u] = *reinterpret_cast<const uint4*>(dy + ((long)(b * H + yy) * W + xx) * lddy + c8 * 8);
+      }
+    }
+  };
+  if (vid < t.ntiles) load_tile(vid);
+  for (long tile = vid; tile < t.ntiles; tile += G) {
+    const int b = fdiv((int)tile, t.per_img);
+    const int r0 = (int)tile - b * t.per_img.d;
+    const int ty0 = fdiv(r0, t.fntx);
+    const int y0 = ty0 * t.TH, x0 = (r0 - ty0 * t.ntx) * t.TW;
+    __syncthreads();   // the previous tile's readers of P / gs / the result tile are done (weights staged)
+    // 1. x and dy halo tiles (registers) -> LDS
+#pragma unroll
+    for (int u = 0; u < VP_PF; ++u) {
+      const int idx = tid + u * NT;
+      if (idx < total) {
+        const int hp = idx / KC, c8 = idx - hp * KC;
+        *reinterpret_cast<uint4*>(xs + hp * XP + c8 * 8) = pf[u];
+      }
+      if (idx < gtotal) *reinterpret_cast<uint4*>(gs + (long)idx * 8) = pg[u];   // [hp][C]: idx = hp * CH8 + c8
+    }
+    __syncthreads();
+    if (tile + G < t.ntiles) load_tile(tile + G);
+    // 2. [v | logits] of every halo pixel on MFMA (the forward kernel's phase 2, same order; two row
+    // blocks per weight-fragment read: the x / dy prefetch registers are live across this phase)
+    constexpr int RB = 2;
+    for (int i0 = wave; i0 < ((dbg & 1) ? 0 : NI); i0 += NW * RB) {
+      bf16x8 xf[RB][NK];
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        const int i = i0 + r * NW;
+#pragma unroll
+        for (int kt = 0; kt < NK; ++kt)
+          xf[r][kt] = i < NI ? *reinterpret_cast<const bf16x8*>(xs + (i * 16 + fr) * XP + kt * 32 + fg * 8) : bf16x8{};
+      }
+      f32x4 acc[RB][NJ];
+#pragma unroll
+      for (int r = 0; r < RB; ++r)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[r][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+#pragma unroll
+        for (int kt = 0; kt < NK; ++kt) {
+          const bf16x8 wh = *reinterpret_cast<const bf16x8*>(ws + (j * 16 + fr) * WP + kt * 32 + fg * 8);
+#pragma unroll
+          for (int r = 0; r < RB; ++r) acc[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, xf[r][kt], acc[r][j], 0, 0, 0);
+          if constexpr (SW) {
+            const bf16x8 wl = *reinterpret_cast<const bf16x8*>(ws + (NCOL + j * 16 + fr) * WP + kt * 32 + fg * 8);
+#pragma unroll
+            for (int r = 0; r < RB; ++r)
+              acc[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl, xf[r][kt], acc[r][j], 0, 0, 0);
+          }
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        const int m = (i0 + r * NW) * 16 + fr;
+        if (i0 + r * NW >= NI || m >= HP) continue;
+        const int hy = fdiv(m, t.fHW2);
+        const int yy = y0 - 1 + hy, xx = x0 - 1 + m - hy * HW2;
+        const bool inb = yy >= 0 && yy < H && xx >= 0 && xx < W;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int n = j * 16 + 4 * fg;
+          const float4 b4 = *reinterpret_cast<const float4*>(bs + n);
+          bf16x4 o;
+          o[0] = (bf16)(inb ? acc[r][j][0] + b4.x : 0.f);
+          o[1] = (bf16)(inb ? acc[r][j][1] + b4.y : 0.f);
+          o[2] = (bf16)(inb ? acc[r][j][2] + b4.z : 0.f);
+          o[3] = (bf16)(inb ? acc[r][j][3] + b4.w : 0.f);
+          *reinterpret_cast<bf16x4*>(rs + m * RP + n) = o;
+        }
+      }
+    }
+    __syncthreads();   // the result tile is complete; xs is free (P aliases it)
+    // 3. softmax of every halo pixel's logits (0 outside the image: those pixels take no part)
+    for (int idx = tid; idx < ((dbg & 4) ? 0 : HP * heads); idx += NT) {
+      const int hp = fdiv(idx, t.fHB), hb = idx - hp * heads;
+      const int hy = fdiv(hp, t.fHW2);
+      const int yy = y0 - 1 + hy, xx = x0 - 1 + hp - hy * HW2;
+      float* d = P + (long)idx * 9;   // idx = hp * heads + hb
+      if (yy < 0 || yy >= H || xx < 0 || xx >= W) {
+#pragma unroll
+        for (int jj = 0; jj < 9; ++jj) d[jj] = 0.f;
+        continue;
+      }
+      const bf16* l = rs + hp * RP + C + hb * 9;
+      float a[9], mx = -INFINITY;
+#pragma unroll
+      for (int jj = 0; jj < 9; ++jj) {
+        a[jj] = (float)l[jj];
+        mx = fmaxf(mx, a[jj]);
+      }
+      float sm = 0.f;
+#pragma unroll
+      for (int jj = 0; jj < 9; ++jj) {
+        a[jj] = __expf(a[jj] - mx);
+        sm += a[jj];
+      }
+      const float inv = 1.0f / sm;
+#pragma unroll
+      for (int jj = 0; jj < 9; ++jj) d[jj] = a[jj] * inv;
+    }
+    __syncthreads();
+    // 4a. dlogits of the interior pixels: two threads per (pixel, head), each over half of the
+    // head's 8-channel chunks; the result replaces the pixel's logits in the result tile (the
+    // logit columns are dead after step 3; step 4 reads only the v columns of rs)
+    for (int idx = tid; idx < ((dbg & 2) ? 0 : PT * heads * 2); idx += NT) {
+      const int half = idx & 1, r = idx >> 1;
+      const int pt = fdiv(r, t.fHB), hb = r - pt * heads;
+      const int ty = fdiv(pt, t.fTW), tx = pt - ty * t.TW;
+      const bool ok = y0 + ty < H && x0 + tx < W;
+      const int s = (ty + 1) * HW2 + tx + 1;
+      float dp[9];
+#pragma unroll
+      for (int j = 0; j < 9; ++j) dp[j] = 0.f;
+      for (int c8 = half; c8 < HC8; c8 += 2) {
+        const int c = hb * hd + c8 * 8;
+        const uint4 graw = *reinterpret_cast<const uint4*>(gs + (long)s * C + c);
+        const bf16* ge = reinterpret_cast<const bf16*>(&graw);
+        float g8[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) g8[i] = (float)ge[i];
+#pragma unroll
+        for (int ki = 0; ki < 3; ++ki)
+#pragma unroll
+          for (int kj = 0; kj < 3; ++kj) {
+            const uint4 raw = *reinterpret_cast<const uint4*>(rs + (long)(s + (ki - 1) * HW2 + (kj - 1)) * RP + c);
+            const bf16* e = reinterpret_cast<const bf16*>(&raw);
+            float a = dp[ki * 3 + kj];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) a = fmaf(g8[i], (float)e[i], a);
+            dp[ki * 3 + kj] = a;
+          }
+      }
+#pragma unroll
+      for (int j = 0; j < 9; ++j) dp[j] += __shfl_xor(dp[j], 1, 64);
+      if (!ok || half) continue;
+      const float* pp = P + ((long)s * heads + hb) * 9;
+      float sdp = 0.f;
+#pragma unroll
+      for (int j = 0; j < 9; ++j) sdp = fmaf(pp[j], dp[j], sdp);
+      bf16* o = rs + (long)s * RP + C + hb * 9;
+#pragma unroll
+      for (int j = 0; j < 9; ++j) o[j] = (bf16)(pp[j] * (dp[j] - sdp));
+    }
+    // 4b. dv of the interior pixels: thread per (pixel, 8-channel chunk), pulling from the 9 pixels
+    // whose window covers it
+    for (int idx = tid; idx < ((dbg & 2) ? 0 : PT * CH8); idx += NT) {
+      const int pt = fdiv(idx, t.fCH), cc = idx - pt * CH8;
+      const int hb = cc / HC8;
+      const int ty = fdiv(pt, t.fTW), tx = pt - ty * t.TW;
+      if (y0 + ty >= H || x0 + tx >= W) continue;
+      const int s = (ty + 1) * HW2 + tx + 1;
+      float acc[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+#pragma unroll
+      for (int ki = 0; ki < 3; ++ki)
+#pragma unroll
+        for (int kj = 0; kj < 3; ++kj) {
+          const int src = s - (ki - 1) * HW2 - (kj - 1);   // pixel q - off_j
+          const uint4 raw = *reinterpret_cast<const uint4*>(gs + (long)src * C + cc * 8);
+          const bf16* e = reinterpret_cast<const bf16*>(&raw);
+          const float w = P[((long)src * heads + hb) * 9 + ki * 3 + kj];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) acc[i] = fmaf(w, (float)e[i], acc[i]);
+        }
+      if (!(dbg & 8)) store_vec<bf16, 8>(dcat + ((long)(b * H + y0 + ty) * W + x0 + tx) * ldc + cc * 8, acc);
+    }
+    __syncthreads();
+    // 5. [dlogits | 0] columns of the interior rows -> dcat (16-B stores; the padding columns of the
+    // result tile are exact zeros: zero weight rows and bias)
+    const int LC = (ldc - C) / 8;
+    for (int idx = tid; idx < ((dbg & 8) ? 0 : PT * LC); idx += NT) {
+      const int pt = idx / LC, c8 = idx - pt * LC;
+      const int ty = fdiv(pt, t.fTW), tx = pt - ty * t.TW;
+      if (y0 + ty >= H || x0 + tx >= W) continue;
+      const int s = (ty + 1) * HW2 + tx + 1;
+      *reinterpret_cast<uint4*>(dcat + ((long)(b * H + y0 + ty) * W + x0 + tx) * ldc + C + c8 * 8) =
+          *reinterpret_cast<const uint4*>(rs + (long)s * RP + C + c8 * 8);
+    }
+  }
+}
+
 // ---- LDS bank model (MI355X_MICROARCH.md, LDS table) used to pick the result tile's row pitch: a
 // 16-B read (ds_read_b128) is serviced in four lane groups of 16 over 64 banks, an 8-B write
 // (ds_write_b64) in four groups of 16 contiguous lanes over 32 banks; each extra distinct dword on a
@@ -1249,8 +1528,9 @@ static int vtile_best_rp(const VTile& t, int C, int heads, int ldc) {
 // write) 4-14 % slower than the unfused GEMM + aggregation, so training keeps the unfused pair.
 static int g_outlook_vproj = 1;
 void set_outlook_vproj(int v) { g_outlook_vproj = v < 0 ? 0 : (v > 2 ? 2 : v); }
-// knob "vp_dbg" (timing experiments only, wrong results): skip phases of the fused kernel --
-// 1 the projection MFMAs, 2 the gather, 4 the softmax, 8 the cat write, 16 the x loads
+// knob "vp_dbg" (timing experiments only, wrong results): skip phases of the fused kernels --
+// 1 the projection MFMAs, 2 the gather (backward: dlogits + dv), 4 the softmax, 8 the cat write
+// (backward: the dcat stores), 16 the x (backward: x and dy) loads
 static int g_vp_dbg = 0;
 void set_vp_dbg(int v) { g_vp_dbg = v; }
 
@@ -1320,6 +1600,65 @@ static void vproj_run(const bf16* x, int ldx, const float* Wc, int wrows, const 
                                     (int)vtile_x_bytes(t, heads), g_vp_dbg);
 }
 
+// The fused backward's tile: 8 x 16 or 8 x 8 pixels at two workgroups of 4 waves per CU (<= 80 KB
+// of LDS each), else the same at one workgroup of 8 waves (<= 160 KB).  nw = waves per workgroup.
+static bool vproj_bwd_plan(int B, int H, int W, int C, int heads, int k, int ldc, ogv_dtype dt, VTile& t, int& nw) {
+  if (dt != OGV_BF16 || k != 3 || B <= 0 || H <= 0 || W <= 0 || heads <= 0) return false;
+  if (C % 16 != 0 || C > 96 || C % heads != 0 || (C / heads) % 8 != 0) return false;
+  const int NL = heads * 9;
+  if (ldc != (C + NL + 7) / 8 * 8) return false;
+  const int KP = (C + 31) / 32 * 32;
+  const int tws[4] = {16, 8, 16, 8};
+  const size_t caps[4] = {80 * 1024, 80 * 1024, 160 * 1024, 160 * 1024};
+  bool ok = false;
+  for (int pass = 0; pass < 4 && !ok; ++pass) {
+    t = VTile{};
+    t.TH = H < 8 ? H : 8;
+    t.TW = W < tws[pass] ? W : tws[pass];
+    t.ntx = (W + t.TW - 1) / t.TW;
+    t.nty = (H + t.TH - 1) / t.TH;
+    t.ntiles = (long)B * t.nty * t.ntx;
+    t.HP = (t.TH + 2) * (t.TW + 2);
+    t.HPr = (t.HP + 15) / 16 * 16;
+    t.ncol = (C + NL + 15) / 16 * 16;
+    for (int pad = 16; pad >= 8 && !ok; pad -= 8) {
+      t.XP = KP + pad;
+      t.WP = KP + pad;
+      t.RP = pad == 16 ? vtile_best_rp(t, C, heads, ldc) : t.ncol;
+      nw = pass < 2 ? 4 : 8;
+      ok = vtile_bwd_lds(t, C, heads, true) <= caps[pass] &&
+           t.HP * (KP / 8) <= (nw == 8 ? vp_bwd_pf<8>() * 512 : vp_bwd_pf<4>() * 256);
+    }
+  }
+  if (!ok || t.ntiles >= (1L << 22) || t.ncol > 128) return false;
+  t.per_img = fdiv_make(t.nty * t.ntx);
+  t.fntx = fdiv_make(t.ntx);
+  t.fHW2 = fdiv_make(t.TW + 2);
+  t.fTW = fdiv_make(t.TW);
+  t.fHB = fdiv_make(heads);
+  t.fCH = fdiv_make(C / 8);
+  t.fQ = fdiv_make((t.TW + VP_RX - 1) / VP_RX);
+  return true;
+}
+
+template <int NJ, int NK, int NW>
+static void vproj_bwd_run(const bf16* x, int ldx, const float* Wc, int wrows, const float* bias, const bf16* dy,
+                          bf16* dcat, int ldc, int H, int W, int C, int heads, const VTile& t, bool sw, hipStream_t s) {
+  const size_t lds = vtile_bwd_lds(t, C, heads, sw);
+  const long per_cu = NW == 4 ? 2 : 1;
+  const long nb = std::min<long>(t.ntiles, 256 * per_cu);
+  const unsigned grid = (unsigned)((nb + 7) / 8 * 8);
+  auto kern = sw ? outlook_vproj_bwd_kernel<NJ, NK, true, NW> : outlook_vproj_bwd_kernel<NJ, NK, false, NW>;
+  static bool attr[2] = {false, false};
+  if (!attr[sw]) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    attr[sw] = true;
+  }
+  kern<<<grid, NW * 64, lds, s>>>(x, ldx, Wc, wrows, bias, dy, C, dcat, ldc, H, W, C, heads, t,
+                                    (int)vtile_bwd_x_bytes(t, heads), g_vp_dbg);
+}
+
 }  // namespace ogv
 
 using namespace ogv;
@@ -1328,7 +1667,44 @@ extern "C" int ogv_outlook_vproj_supported(int B, int H, int W, int C, int heads
                                            ogv_dtype dt) {
   VTile t;
   if (g_outlook_vproj < (train ? 2 : 1)) return 0;
-  return vproj_plan(B, H, W, C, heads, k, ldc, dt, t) ? 1 : 0;
+  if (!vproj_plan(B, H, W, C, heads, k, ldc, dt, t)) return 0;
+  int nw = 0;
+  return (!train || vproj_bwd_plan(B, H, W, C, heads, k, ldc, dt, t, nw)) ? 1 : 0;
+}
+
+extern "C" int ogv_outlook_vproj_bwd(const void* x, int ldx, const float* w, const float* bias, const void* dy,
+                                     void* dcat, int ldc, int B, int H, int W, int C, int heads, int k, ogv_dtype dt,
+                                     void* stream) {
+  if (skip_mask() & 64) return OGV_OK;
+  OGV_REQUIRE(x && w && dy && dcat, "ogv_outlook_vproj_bwd: null pointer");
+  int rc = check_args(B, H, W, C, heads, k, heads * k * k, C, dt, "ogv_outlook_vproj_bwd");
+  if (rc) return rc;
+  VTile t;
+  int nw = 0;
+  OGV_REQUIRE(vproj_bwd_plan(B, H, W, C, heads, k, ldc, dt, t, nw),
+              "ogv_outlook_vproj_bwd: unsupported shape (needs bf16, k=3, 16 | C <= 96, 8 | head_dim, "
+              "ldc = C + 9*heads rounded up to 8; see ogv_outlook_vproj_supported)");
+  OGV_REQUIRE(ldx >= C && ldx % 8 == 0 && al16p(x) && al16p(dy) && al16p(dcat) && al16p(w),
+              "ogv_outlook_vproj_bwd: rows must be 16-B aligned (ldx %d)", ldx);
+  const int NJ = t.ncol / 16, NK = (C + 31) / 32;
+  const bool sw = (split_w() & 1) != 0;   // the forward's weights (bit-identical v / logits)
+  hipStream_t s = as_stream(stream);
+  const bf16* xb = (const bf16*)x;
+  const bf16* gb = (const bf16*)dy;
+  bf16* db = (bf16*)dcat;
+#define OGV_VPROJ_BWD(nj, nk)                                                                          \
+  if (NJ == nj && NK == nk) {                                                                          \
+    if (nw == 4) vproj_bwd_run<nj, nk, 4>(xb, ldx, w, ldc, bias, gb, db, ldc, H, W, C, heads, t, sw, s); \
+    else vproj_bwd_run<nj, nk, 8>(xb, ldx, w, ldc, bias, gb, db, ldc, H, W, C, heads, t, sw, s);         \
+    return check_launch("ogv_outlook_vproj_bwd");                                                      \
+  }
+  // (NJ, NK) pairs the plan admits: 16 | C <= 96, 8 | head_dim, ncol = C + 9 heads rounded to 16 <= 128
+  OGV_VPROJ_BWD(2, 1) OGV_VPROJ_BWD(3, 1) OGV_VPROJ_BWD(4, 1) OGV_VPROJ_BWD(5, 1)
+  OGV_VPROJ_BWD(4, 2) OGV_VPROJ_BWD(5, 2) OGV_VPROJ_BWD(6, 2) OGV_VPROJ_BWD(7, 2)
+  OGV_VPROJ_BWD(6, 3) OGV_VPROJ_BWD(7, 3) OGV_VPROJ_BWD(8, 3)
+#undef OGV_VPROJ_BWD
+  OGV_REQUIRE(false, "ogv_outlook_vproj_bwd: no instantiation for %d column / %d k blocks", NJ, NK);
+  return OGV_ERR_ARG;
 }
 
 extern "C" int ogv_outlook_vproj_fwd(const void* x, int ldx, const float* w, const float* bias, void* cat, int ldc,

@@ -107,7 +107,9 @@ def probe_bytes(name: str, u: dict) -> int:
         return e * u["M"] * (2 * u["C"] + u["k"] * u["k"] * u["heads"])
     if name == "outlook_vproj":  # read x [M,C] + fp32 W [ld,C] (+ bias), write y [M,C] (+ cat [M,ld] in training)
         return e * u["M"] * (2 * u["C"] + (u["ld"] if u["cat"] else 0)) + 4 * u["ld"] * (u["C"] + 1)
-    if name == "grid_fwd":      # read qkv [M,3C], write out [M,C] + fp32 lse [M,h]
+    if name == "outlook_vproj_bwd":  # read x [M,C], dy [M,C] + fp32 W [ld,C] (+ bias), write dcat [M,ld]
+        return e * u["M"] * (2 * u["C"] + u["ld"]) + 4 * u["ld"] * (u["C"] + 1)
+    if name == "grid_fwd":     # read qkv [M,3C], write out [M,C] + fp32 lse [M,h]
         return e * u["M"] * 4 * u["C"] + 4 * u["M"] * u["heads"]
     if name == "outlook_bwd":   # read dy, v, logits; write dv, dlogits
         return e * u["M"] * (3 * u["C"] + 2 * u["k"] * u["k"] * u["heads"])
@@ -130,6 +132,8 @@ def probe_flops(name: str, u: dict) -> int:
         return 36 * u["M"] * u["C"]
     if name == "outlook_vproj":   # the projection GEMM + the aggregation
         return 2 * u["M"] * u["ld"] * u["C"] + 18 * u["M"] * u["C"] + 45 * u["M"] * u["heads"]
+    if name == "outlook_vproj_bwd":   # the recomputed projection + the aggregation backward
+        return 2 * u["M"] * u["ld"] * u["C"] + 36 * u["M"] * u["C"] + 45 * u["M"] * u["heads"]
     if name == "grid_fwd":
         return 4 * u["M"] * u["N"] * u["C"]
     return 2 * u["M"] * u["N"] * u["K"]
@@ -238,7 +242,7 @@ def op_cost(name: str, u: dict):
         return s * 2 * M * C + 8 * M, 8 * M * C
     if name == "layernorm_bwd":      # read dy, x (+ dres), write dx (+ fp32 mean / rstd, gamma / beta partials)
         return s * M * C * (4 if u.get("dres") else 3) + 8 * M + 8 * C, 10 * M * C
-    if name in ("outlook_fwd", "outlook_bwd", "outlook_vproj", "grid_fwd"):
+    if name in ("outlook_fwd", "outlook_bwd", "outlook_vproj", "outlook_vproj_bwd", "grid_fwd"):
         return probe_bytes(name, u), probe_flops(name, u)
     if name == "grid_bwd":           # read dO, qkv, O (+ lse), write dqkv (+ delta)
         return s * M * 8 * C + 8 * M * u["heads"], 8 * M * u["N"] * C
@@ -710,35 +714,44 @@ class _OutlookAggCat(torch.autograd.Function):
 
 class _OutlookVProj(torch.autograd.Function):
     """Outlooker forward fused with its v / attn 1x1 projections (ogv_outlook_vproj_fwd): x [M, C]
-    -> y [M, C], writing cat = [v | logits | 0] [M, ld] only when a gradient is wanted.  Backward:
-    the LDS-tiled aggregation backward on cat -> dcat, then ONE dgrad + ONE wgrad of the
+    -> y [M, C].  mode 0: inference (nothing saved); 1: training with the fused backward
+    (ogv_outlook_vproj_bwd recomputes [v | logits] from x in LDS, so the forward writes only y);
+    2: training that saves cat = [v | logits | 0] [M, ld] for the LDS-tiled aggregation backward.
+    Either backward yields ONE dcat = [dv | dlogits | 0], then ONE dgrad + ONE wgrad of the
     concatenated weight (as _OutlookAggCat + _Linear)."""
 
     @staticmethod
-    def forward(ctx, x2d, w, b, C, B, H, W, heads, k, train):
+    def forward(ctx, x2d, w, b, C, B, H, W, heads, k, mode):
         lib = _lib.load()
         M = x2d.shape[0]
         ld = w.shape[0]
         y = torch.empty((M, C), dtype=x2d.dtype, device=x2d.device)
-        cat = torch.empty((M, ld), dtype=x2d.dtype, device=x2d.device) if train else None
-        ou = dict(M=M, C=C, ld=ld, heads=heads, k=k, cat=train, elem=x2d.element_size())
+        cat = torch.empty((M, ld), dtype=x2d.dtype, device=x2d.device) if mode == 2 else None
+        ou = dict(M=M, C=C, ld=ld, heads=heads, k=k, cat=mode == 2, elem=x2d.element_size())
         with _probe("outlook_vproj", ou), _census("outlook_vproj", ou):
             check(lib.ogv_outlook_vproj_fwd(_ptr(x2d), x2d.stride(0), _ptr(w), _ptr(b), _ptr(cat), ld, _ptr(y), B, H, W,
                                             C, heads, k, _dt(x2d), _stream()), "ogv_outlook_vproj_fwd")
-        ctx.save_for_backward(x2d, w, cat)
-        ctx.meta = (B, H, W, C, heads, k, b is not None)
+        ctx.save_for_backward(x2d, w, b, cat)
+        ctx.meta = (B, H, W, C, heads, k, b is not None, mode)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x2d, w, cat = ctx.saved_tensors
-        B, H, W, C, heads, k, has_bias = ctx.meta
-        M, ld = cat.shape
-        es = cat.element_size()
-        dy = dy.to(cat.dtype).contiguous()
-        dcat = torch.empty_like(cat)
-        _outlook_bwd(dy, cat.data_ptr(), ld, cat.data_ptr() + C * es, ld, dcat.data_ptr(), ld, dcat.data_ptr() + C * es,
-                     ld, ld - C, B, H, W, C, heads, k)
+        x2d, w, b, cat = ctx.saved_tensors
+        B, H, W, C, heads, k, has_bias, mode = ctx.meta
+        M, ld = x2d.shape[0], w.shape[0]
+        dy = dy.to(x2d.dtype).contiguous()
+        dcat = torch.empty((M, ld), dtype=x2d.dtype, device=x2d.device)
+        if mode == 1:
+            ou = dict(M=M, C=C, ld=ld, heads=heads, k=k, elem=x2d.element_size())
+            with _probe("outlook_vproj_bwd", ou), _census("outlook_vproj_bwd", ou):
+                check(_lib.load().ogv_outlook_vproj_bwd(_ptr(x2d), x2d.stride(0), _ptr(w), _ptr(b), _ptr(dy), _ptr(dcat),
+                                                        ld, B, H, W, C, heads, k, _dt(x2d), _stream()),
+                      "ogv_outlook_vproj_bwd")
+        else:
+            es = cat.element_size()
+            _outlook_bwd(dy, cat.data_ptr(), ld, cat.data_ptr() + C * es, ld, dcat.data_ptr(), ld,
+                         dcat.data_ptr() + C * es, ld, ld - C, B, H, W, C, heads, k)
         want_dw = ctx.needs_input_grad[1] or (has_bias and ctx.needs_input_grad[2])
         dx, dw, db = _linear_bwd(dcat, x2d, w, None, 1, 0, has_bias, ctx.needs_input_grad[0], want_dw)
         return dx, dw, db, None, None, None, None, None, None, None
@@ -752,15 +765,17 @@ def outlook_vproj_supported(B, H, W, C, heads, k, ld, dtype, train) -> bool:
     return bool(_lib.load().ogv_outlook_vproj_supported(B, H, W, C, heads, k, ld, int(bool(train)), OGV_BF16))
 
 
-def outlook_vproj(x2d, w, b, C, B, H, W, heads, k):
+def outlook_vproj(x2d, w, b, C, B, H, W, heads, k, save_cat=False):
     """y [M, C] = outlook aggregation of (x2d @ [Wv; Wattn; 0]^T + b) without materialising the
-    projection for the forward (x2d bf16 rows, w fp32 [ld, C], b fp32 [ld] or None)."""
+    projection (x2d bf16 rows, w fp32 [ld, C], b fp32 [ld] or None).  When a gradient will be
+    wanted the backward recomputes [v | logits] from x (ogv_outlook_vproj_bwd); save_cat=True
+    instead writes cat [M, ld] in the forward for the aggregation backward (comparison path)."""
     require_device(x2d, w, b, what="ogv.outlook_vproj")
     x2d = _rows_contig(x2d)
-    # the [v | logits] tensor is written for the backward only when a gradient will be wanted
     train = torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in (x2d, w, b))
+    mode = 0 if not train else (2 if save_cat else 1)
     return _OutlookVProj.apply(x2d, w.contiguous(), None if b is None else b.contiguous(), int(C), int(B), int(H),
-                               int(W), int(heads), int(k), train)
+                               int(W), int(heads), int(k), mode)
 
 
 def outlook_aggregate_rows(v2d, logits2d, B, H, W, heads, k):

@@ -811,12 +811,77 @@ def test_outlook_vproj_full_size_matches_unfused(shape):
         cat = OF.linear_rows(x, w, b)
         y_ref = OF.outlook_aggregate_cat(cat, C, B, H, W, h, 3)
     wq, bq = w.clone().requires_grad_(), b.clone().requires_grad_()
-    y = OF.outlook_vproj(x, wq, bq, C, B, H, W, h, 3)     # training mode: writes cat as well
+    y = OF.outlook_vproj(x, wq, bq, C, B, H, W, h, 3, save_cat=True)     # writes cat as well
     tol = 1e-2 * max(1.0, y_ref.float().abs().max().item())
     assert fx.maxabs(y.detach().float(), y_ref.float()) <= tol
-    cat_f = y.grad_fn.saved_tensors[2]
+    cat_f = y.grad_fn.saved_tensors[3]
     assert fx.maxabs(cat_f.float(), cat.float()) <= 1e-2 * max(1.0, cat.float().abs().max().item())
     assert torch.equal(cat_f[:, C + 9 * h:], torch.zeros_like(cat_f[:, C + 9 * h:]))
+
+
+def _vproj_problem(B, C, h, H, W, seed):
+    ld = (C + 9 * h + 7) // 8 * 8
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    x = torch.randn(B * H * W, C, device=DEV, generator=g).to(torch.bfloat16)
+    w = torch.randn(ld, C, device=DEV, generator=g) / C ** 0.5
+    w[C:C + 9 * h] *= 3.0
+    w[C + 9 * h:] = 0
+    b = 0.1 * torch.randn(ld, device=DEV, generator=g)
+    b[C + 9 * h:] = 0
+    dy = torch.randn(B * H * W, C, device=DEV, generator=g).to(torch.bfloat16)
+    return x, w, b, dy, ld
+
+
+@pytest.mark.parametrize("case", VPROJ_CASES + [(512, 48, 2, 32, 32), (256, 96, 3, 16, 16), (2, 64, 2, 224, 224)])
+def test_outlook_vproj_bwd_bitwise(case):
+    """The fused backward (ogv_outlook_vproj_bwd: [v | logits] recomputed from x in LDS) is
+    BIT-identical to the LDS-tiled aggregation backward run on the cat the fused forward writes:
+    same MFMA fragments and rounding for the recompute, same softmax / dP / gather order -- so
+    training through the recompute path trains exactly the function the forward evaluated.  Also
+    covers partial tiles, 1x1 / 1-row images and every (column, k) block count of the plan."""
+    from ogv import functional as OF
+    from ogv._lib import load
+    lib = load()
+    B, C, h, H, W = case
+    x, w, b, dy, ld = _vproj_problem(B, C, h, H, W, seed=B * 7 + C + H)
+    M = B * H * W
+    wq, bq = w.clone().requires_grad_(), b.clone().requires_grad_()
+    y = OF.outlook_vproj(x, wq, bq, C, B, H, W, h, 3, save_cat=True)
+    cat = y.grad_fn.saved_tensors[3]
+    dcat_ref = torch.empty_like(cat)
+    es = cat.element_size()
+    OF._outlook_bwd(dy, cat.data_ptr(), ld, cat.data_ptr() + C * es, ld, dcat_ref.data_ptr(), ld,
+                    dcat_ref.data_ptr() + C * es, ld, ld - C, B, H, W, C, h, 3)
+    dcat = torch.full((M, ld), float("nan"), device=DEV, dtype=torch.bfloat16)
+    OF.check(lib.ogv_outlook_vproj_bwd(OF._ptr(x), C, OF._ptr(w), OF._ptr(b), OF._ptr(dy), OF._ptr(dcat), ld, B, H, W,
+                                       C, h, 3, OF.OGV_BF16, OF._stream()), "ogv_outlook_vproj_bwd")
+    torch.cuda.synchronize()
+    assert torch.equal(dcat, dcat_ref), (case, fx.maxabs(dcat.float(), dcat_ref.float()))
+    assert torch.equal(dcat[:, C + 9 * h:], torch.zeros_like(dcat[:, C + 9 * h:]))
+
+
+@pytest.mark.parametrize("shape", [(512, 48, 2, 32, 32), (256, 96, 3, 16, 16), (4, 64, 2, 224, 224)])
+def test_outlook_vproj_train_grads_full_size_match_unfused(shape):
+    """Full size: x / W / b gradients through the fused training pair (forward writes only y,
+    backward recomputes the projections) vs the unfused GEMM -> cat -> aggregation -> backward on
+    the same inputs, within 1e-2 * max(1, |ref|) (the two projection GEMMs round their bf16 output
+    from differently ordered fp32 sums; the weight gradients sum bf16 dcat over M rows: 3x)."""
+    from ogv import functional as OF
+    B, C, h, H, W = shape
+    x, w, b, dy, ld = _vproj_problem(B, C, h, H, W, seed=B + H + 1)
+    grads = []
+    for fused in (True, False):
+        xx, wq, bq = x.clone().requires_grad_(), w.clone().requires_grad_(), b.clone().requires_grad_()
+        if fused:
+            y = OF.outlook_vproj(xx, wq, bq, C, B, H, W, h, 3)
+            assert y.grad_fn.saved_tensors[3] is None          # no [v | logits] tensor kept
+        else:
+            y = OF.outlook_aggregate_cat(OF.linear_rows(xx, wq, bq), C, B, H, W, h, 3)
+        y.backward(dy)
+        grads.append((y.detach().float(), xx.grad.float(), wq.grad, bq.grad))
+    for i, (a, r) in enumerate(zip(*grads)):
+        tol = 1e-2 * max(1.0, r.abs().max().item()) * (3 if i >= 2 else 1)
+        assert fx.maxabs(a, r) <= tol, ("y", "dx", "dW", "db")[i]
 
 
 @pytest.mark.parametrize("which", ["outlook", "grid"])

@@ -1,8 +1,11 @@
-"""Outlooker forward: the fused projection + aggregation kernel (ogv_outlook_vproj_fwd) vs the
-unfused pair (concatenated [Wv; Wattn; 0] GEMM -> cat, then the aggregation reading cat), per
-Model-A stage shape, cold L2 (512 MB flush before each rep), HIP events, median of --reps.
-Algorithmic bytes: fused 2*M*(2C + ld) (+ the fp32 weight), i.e. read x, write y and cat;
-the unfused pair moves 2*M*(C + ld) + 2*M*(2C + 9h) (+ the cat halo re-reads).
+"""Outlooker: the fused projection + aggregation kernels vs the unfused pair, per Model-A stage
+shape, cold L2 (512 MB flush before each rep), HIP events, median of --reps.
+Forward: ogv_outlook_vproj_fwd (fused_eval: writes y; fused_train: also the cat [v | logits | 0]
+the aggregation backward would read) vs the concatenated [Wv; Wattn; 0] GEMM -> cat, then the
+aggregation reading cat (unfused).  Backward: ogv_outlook_vproj_bwd (fused_bwd: [v | logits]
+recomputed from x in LDS, writes dcat) vs the LDS-tiled aggregation backward on cat (unfused_bwd).
+Algorithmic bytes: fused_eval 2*M*2C, fused_train 2*M*(2C + ld), unfused 2*M*(C + ld) + 2*M*(2C + 9h),
+fused_bwd 2*M*(2C + ld), unfused_bwd 2*M*(C + ld) (dy, cat) + 2*M*ld (dcat).
     python tools/bench_vproj.py [--reps 20]"""
 import argparse
 import pathlib
@@ -25,7 +28,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE")
     ap.add_argument("--shapes", default="", help="comma list of shape names (default all)")
-    ap.add_argument("--kinds", default="unfused,fused_train,fused_eval")
+    ap.add_argument("--kinds", default="unfused,fused_train,fused_eval,unfused_bwd,fused_bwd")
     a = ap.parse_args()
     ogv.load()
     lib = load()
@@ -45,6 +48,10 @@ def main():
         b = torch.zeros(ld, device="cuda")
         cat = torch.empty(M, ld, device="cuda", dtype=torch.bfloat16)
         y = torch.empty(M, C, device="cuda", dtype=torch.bfloat16)
+        dy = torch.randn(M, C, device="cuda").to(torch.bfloat16)
+        dcat = torch.empty(M, ld, device="cuda", dtype=torch.bfloat16)
+        OF.check(lib.ogv_outlook_vproj_fwd(OF._ptr(x), C, OF._ptr(w), OF._ptr(b), OF._ptr(cat), ld, OF._ptr(y), B, S, S,
+                                           C, h, 3, OGV_BF16, s()), "vproj")
         p = OF._ptr
         runs = {
             "unfused": lambda: (OF.check(lib.ogv_gemm_fwd(p(x), C, p(w), p(b), None, None, 1, p(cat), ld, M, ld, C,
@@ -55,9 +62,13 @@ def main():
                                                                       h, 3, OGV_BF16, s()), "vproj"),
             "fused_eval": lambda: OF.check(lib.ogv_outlook_vproj_fwd(p(x), C, p(w), p(b), None, ld, p(y), B, S, S, C, h,
                                                                      3, OGV_BF16, s()), "vproj"),
+            "unfused_bwd": lambda: OF._outlook_bwd(dy, cat.data_ptr(), ld, cat.data_ptr() + 2 * C, ld, dcat.data_ptr(), ld,
+                                                   dcat.data_ptr() + 2 * C, ld, ld - C, B, S, S, C, h, 3),
+            "fused_bwd": lambda: OF.check(lib.ogv_outlook_vproj_bwd(p(x), C, p(w), p(b), p(dy), p(dcat), ld, B, S, S, C, h,
+                                                                    3, OGV_BF16, s()), "vproj_bwd"),
         }
         nbytes = {"unfused": 2 * M * (C + ld) + 2 * M * (2 * C + 9 * h), "fused_train": 2 * M * (2 * C + ld),
-                  "fused_eval": 2 * M * 2 * C}
+                  "fused_eval": 2 * M * 2 * C, "unfused_bwd": 2 * M * (C + 2 * ld), "fused_bwd": 2 * M * (2 * C + ld)}
         row = [f"{name:7s} M={M:8d}"]
         for kind, fn in runs.items():
             if kind not in a.kinds.split(","):

@@ -1522,35 +1522,48 @@ static int vtile_best_rp(const VTile& t, int C, int heads, int ldc) {
   return rp_best;
 }
 
-// knob "outlook_vproj": 0 = never, 1 = for inference (no cat written; default), 2 = also in training.
-// Measured (tools/bench_vproj.py, cold L2, bs = 512 / 256 / 128): inference 7M stage 0 82 vs 91 us
-// unfused, 14M stage 0 195 vs 201 us, 7M stage 1 / 22M stage 0 within 1-3 %; training (the cat
-// write) 4-14 % slower than the unfused GEMM + aggregation, so training keeps the unfused pair.
-static int g_outlook_vproj = 1;
-void set_outlook_vproj(int v) { g_outlook_vproj = v < 0 ? 0 : (v > 2 ? 2 : v); }
+// knob "outlook_vproj": 0 = never, 1 = inference only, 2 = also in training with the forward writing
+// cat for the LDS-tiled aggregation backward (default), 3 = training with the recompute backward
+// (ogv_outlook_vproj_bwd; the forward writes only y).  Measured (tools/bench_vproj.py, cold L2,
+// profiles/r03_vproj_tile.log, fwd + bwd per Outlooker): 7M stage 0 unfused 91.6 + 95.7 us, fused
+// with cat 89.8 + 95.7, fused + recompute 78.5 + 121.5; 7M stage 1 52.6 / 43.4 (+ 51.8 either way);
+// 14M stage 0 200 / 176 (+ 230) / 155 + 265; 22M stage 0 1102 / 987 (+ 1269) / 892 + 1557 -- the
+// fused forward with cat wins at every shape, the recompute backward does not yet.
+static int g_outlook_vproj = 2;
+void set_outlook_vproj(int v) { g_outlook_vproj = v < 0 ? 0 : (v > 3 ? 3 : v); }
 // knob "vp_dbg" (timing experiments only, wrong results): skip phases of the fused kernels --
 // 1 the projection MFMAs, 2 the gather (backward: dlogits + dv), 4 the softmax, 8 the cat write
 // (backward: the dcat stores), 16 the x (backward: x and dy) loads
 static int g_vp_dbg = 0;
 void set_vp_dbg(int v) { g_vp_dbg = v; }
 
-// shapes the fused kernel takes: bf16, k = 3, 16 | C <= 96, 8 | head_dim, ldc = C + 9 heads rounded
-// up to 8, 16-B aligned rows, and an LDS footprint within one CU's 160 KB
-static inline int NK_W(int KP) { return KP > 64 ? 8 : 4; }   // waves per workgroup for a padded K
+// shapes the fused kernels take: bf16, k = 3, 16 | C <= 96, 8 | head_dim, ldc = C + 9 heads rounded
+// up to 8, 16-B aligned rows, and an LDS footprint within one CU's 160 KB.
+// Tile candidates: (1) 8 x 16 pixels at two workgroups of 4 waves per CU (<= 80 KB of LDS each),
+// (2) 8 x 8 at two of 4 waves, (3) 8 x 16 at one workgroup of 8 waves (<= 160 KB), (4) 8 x 8 at one
+// of 8 waves; tried in the order 1, 3, 2, 4 -- measured (tools/bench_vproj.py with the knob
+// "vp_tile" = n forcing candidate n, profiles/r03_vproj_tile.log): 8 x 16 at 8 waves beats 8 x 8 at
+// 4 waves on every Model-A shape, forward (14M stage 0 with cat 215 -> 176 us, 22M 1262 -> 987 us)
+// and backward (7M stage 0 140 -> 122 us), and 8 x 8 at 8 waves loses to both.
+static int g_vp_tile = 0;
+void set_vp_tile(int v) { g_vp_tile = v < 0 ? 0 : (v > 4 ? 4 : v); }
 
-static bool vproj_plan(int B, int H, int W, int C, int heads, int k, int ldc, ogv_dtype dt, VTile& t) {
-  if (!g_outlook_vproj || dt != OGV_BF16 || k != 3 || B <= 0 || H <= 0 || W <= 0 || heads <= 0) return false;
+static bool vtile_plan(int B, int H, int W, int C, int heads, int k, int ldc, ogv_dtype dt, bool bwd, VTile& t,
+                       int& nw) {
+  if (dt != OGV_BF16 || k != 3 || B <= 0 || H <= 0 || W <= 0 || heads <= 0) return false;
   if (C % 16 != 0 || C > 96 || C % heads != 0 || (C / heads) % 8 != 0) return false;
   const int NL = heads * 9;
   if (ldc != (C + NL + 7) / 8 * 8) return false;
   const int KP = (C + 31) / 32 * 32;
-  // 8 x 16 tiles when two workgroups fit one CU's LDS, else 8 x 8, else 8 x 16 at one per CU
+  const int tws[4] = {16, 8, 16, 8};
+  const size_t caps[4] = {80 * 1024, 80 * 1024, 160 * 1024, 160 * 1024};
+  const int order[4] = {0, 2, 1, 3};
   bool ok = false;
-  for (int pass = 0; pass < 3 && !ok; ++pass) {
+  for (int i = 0; i < (g_vp_tile ? 1 : 4) && !ok; ++i) {
+    const int pass = g_vp_tile ? g_vp_tile - 1 : order[i];
     t = VTile{};
     t.TH = H < 8 ? H : 8;
-    const int tw = pass == 1 ? 8 : 16;
-    t.TW = W < tw ? W : tw;
+    t.TW = W < tws[pass] ? W : tws[pass];
     t.ntx = (W + t.TW - 1) / t.TW;
     t.nty = (H + t.TH - 1) / t.TH;
     t.ntiles = (long)B * t.nty * t.ntx;
@@ -1565,69 +1578,10 @@ static bool vproj_plan(int B, int H, int W, int C, int heads, int k, int ldc, og
       t.XP = KP + pad;
       t.WP = KP + pad;
       t.RP = pad == 16 ? vtile_best_rp(t, C, heads, ldc) : t.ncol;
-      const size_t lds = vtile_lds(t, heads, true);
-      ok = pass == 2 ? lds <= 160 * 1024 : lds <= 80 * 1024;
-    }
-  }
-  if (!ok || t.ntiles >= (1L << 22)) return false;
-  if (t.ncol > 128 || t.HP * (KP / 8) > (NK_W(KP) == 8 ? vp_pf<8>() * 512 : vp_pf<4>() * 256)) return false;
-  t.per_img = fdiv_make(t.nty * t.ntx);
-  t.fntx = fdiv_make(t.ntx);
-  t.fHW2 = fdiv_make(t.TW + 2);
-  t.fTW = fdiv_make(t.TW);
-  t.fHB = fdiv_make(heads);
-  t.fCH = fdiv_make(C / 8);
-  t.fQ = fdiv_make((t.TW + VP_RX - 1) / VP_RX);
-  return true;
-}
-
-template <int NJ, int NK>
-static void vproj_run(const bf16* x, int ldx, const float* Wc, int wrows, const float* bias, bf16* cat, int ldc, bf16* y,
-                      int H, int W, int C, int heads, const VTile& t, bool sw, hipStream_t s) {
-  const size_t lds = vtile_lds(t, heads, sw);
-  const long per_cu = NK == 3 ? 1 : std::min<long>(2, std::max<long>(1, (long)(160 * 1024 / lds)));
-  const long nb = std::min<long>(t.ntiles, 256 * per_cu);
-  const unsigned grid = (unsigned)((nb + 7) / 8 * 8);
-  constexpr int NW = NK == 3 ? 8 : 4;
-  auto kern = sw ? outlook_vproj_fwd_kernel<NJ, NK, true, NW> : outlook_vproj_fwd_kernel<NJ, NK, false, NW>;
-  static bool attr[2] = {false, false};
-  if (!attr[sw]) {   // dynamic LDS above the default grant
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    attr[sw] = true;
-  }
-  kern<<<grid, NW * 64, lds, s>>>(x, ldx, Wc, wrows, bias, cat, ldc, y, H, W, C, heads, t,
-                                    (int)vtile_x_bytes(t, heads), g_vp_dbg);
-}
-
-// The fused backward's tile: 8 x 16 or 8 x 8 pixels at two workgroups of 4 waves per CU (<= 80 KB
-// of LDS each), else the same at one workgroup of 8 waves (<= 160 KB).  nw = waves per workgroup.
-static bool vproj_bwd_plan(int B, int H, int W, int C, int heads, int k, int ldc, ogv_dtype dt, VTile& t, int& nw) {
-  if (dt != OGV_BF16 || k != 3 || B <= 0 || H <= 0 || W <= 0 || heads <= 0) return false;
-  if (C % 16 != 0 || C > 96 || C % heads != 0 || (C / heads) % 8 != 0) return false;
-  const int NL = heads * 9;
-  if (ldc != (C + NL + 7) / 8 * 8) return false;
-  const int KP = (C + 31) / 32 * 32;
-  const int tws[4] = {16, 8, 16, 8};
-  const size_t caps[4] = {80 * 1024, 80 * 1024, 160 * 1024, 160 * 1024};
-  bool ok = false;
-  for (int pass = 0; pass < 4 && !ok; ++pass) {
-    t = VTile{};
-    t.TH = H < 8 ? H : 8;
-    t.TW = W < tws[pass] ? W : tws[pass];
-    t.ntx = (W + t.TW - 1) / t.TW;
-    t.nty = (H + t.TH - 1) / t.TH;
-    t.ntiles = (long)B * t.nty * t.ntx;
-    t.HP = (t.TH + 2) * (t.TW + 2);
-    t.HPr = (t.HP + 15) / 16 * 16;
-    t.ncol = (C + NL + 15) / 16 * 16;
-    for (int pad = 16; pad >= 8 && !ok; pad -= 8) {
-      t.XP = KP + pad;
-      t.WP = KP + pad;
-      t.RP = pad == 16 ? vtile_best_rp(t, C, heads, ldc) : t.ncol;
       nw = pass < 2 ? 4 : 8;
-      ok = vtile_bwd_lds(t, C, heads, true) <= caps[pass] &&
-           t.HP * (KP / 8) <= (nw == 8 ? vp_bwd_pf<8>() * 512 : vp_bwd_pf<4>() * 256);
+      const size_t lds = bwd ? vtile_bwd_lds(t, C, heads, true) : vtile_lds(t, heads, true);
+      const int pf = bwd ? (nw == 8 ? vp_bwd_pf<8>() : vp_bwd_pf<4>()) : (nw == 8 ? vp_pf<8>() : vp_pf<4>());
+      ok = lds <= caps[pass] && t.HP * (KP / 8) <= pf * nw * 64;
     }
   }
   if (!ok || t.ntiles >= (1L << 22) || t.ncol > 128) return false;
@@ -1639,6 +1593,32 @@ static bool vproj_bwd_plan(int B, int H, int W, int C, int heads, int k, int ldc
   t.fCH = fdiv_make(C / 8);
   t.fQ = fdiv_make((t.TW + VP_RX - 1) / VP_RX);
   return true;
+}
+
+static bool vproj_plan(int B, int H, int W, int C, int heads, int k, int ldc, ogv_dtype dt, VTile& t, int& nw) {
+  return g_outlook_vproj && vtile_plan(B, H, W, C, heads, k, ldc, dt, false, t, nw);
+}
+
+template <int NJ, int NK, int NW>
+static void vproj_run(const bf16* x, int ldx, const float* Wc, int wrows, const float* bias, bf16* cat, int ldc, bf16* y,
+                      int H, int W, int C, int heads, const VTile& t, bool sw, hipStream_t s) {
+  const size_t lds = vtile_lds(t, heads, sw);
+  const long per_cu = NW == 4 ? 2 : 1;
+  const long nb = std::min<long>(t.ntiles, 256 * per_cu);
+  const unsigned grid = (unsigned)((nb + 7) / 8 * 8);
+  auto kern = sw ? outlook_vproj_fwd_kernel<NJ, NK, true, NW> : outlook_vproj_fwd_kernel<NJ, NK, false, NW>;
+  static bool attr[2] = {false, false};
+  if (!attr[sw]) {   // dynamic LDS above the default grant
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    attr[sw] = true;
+  }
+  kern<<<grid, NW * 64, lds, s>>>(x, ldx, Wc, wrows, bias, cat, ldc, y, H, W, C, heads, t,
+                                    (int)vtile_x_bytes(t, heads), g_vp_dbg);
+}
+
+static bool vproj_bwd_plan(int B, int H, int W, int C, int heads, int k, int ldc, ogv_dtype dt, VTile& t, int& nw) {
+  return vtile_plan(B, H, W, C, heads, k, ldc, dt, true, t, nw);
 }
 
 template <int NJ, int NK, int NW>
@@ -1667,9 +1647,10 @@ extern "C" int ogv_outlook_vproj_supported(int B, int H, int W, int C, int heads
                                            ogv_dtype dt) {
   VTile t;
   if (g_outlook_vproj < (train ? 2 : 1)) return 0;
-  if (!vproj_plan(B, H, W, C, heads, k, ldc, dt, t)) return 0;
   int nw = 0;
-  return (!train || vproj_bwd_plan(B, H, W, C, heads, k, ldc, dt, t, nw)) ? 1 : 0;
+  if (!vproj_plan(B, H, W, C, heads, k, ldc, dt, t, nw)) return 0;
+  if (!train || g_outlook_vproj < 3) return 1;
+  return vproj_bwd_plan(B, H, W, C, heads, k, ldc, dt, t, nw) ? 2 : 1;
 }
 
 extern "C" int ogv_outlook_vproj_bwd(const void* x, int ldx, const float* w, const float* bias, const void* dy,
@@ -1714,7 +1695,8 @@ extern "C" int ogv_outlook_vproj_fwd(const void* x, int ldx, const float* w, con
   int rc = check_args(B, H, W, C, heads, k, heads * k * k, C, dt, "ogv_outlook_vproj_fwd");
   if (rc) return rc;
   VTile t;
-  OGV_REQUIRE(vproj_plan(B, H, W, C, heads, k, ldc, dt, t),
+  int nw = 0;
+  OGV_REQUIRE(vproj_plan(B, H, W, C, heads, k, ldc, dt, t, nw),
               "ogv_outlook_vproj_fwd: unsupported shape (needs bf16, k=3, 16 | C <= 96, 8 | head_dim, "
               "ldc = C + 9*heads rounded up to 8; see ogv_outlook_vproj_supported)");
   OGV_REQUIRE(ldx >= C && ldx % 8 == 0 && al16p(x) && al16p(y) && (!cat || al16p(cat)) && al16p(w),
@@ -1724,14 +1706,16 @@ extern "C" int ogv_outlook_vproj_fwd(const void* x, int ldx, const float* w, con
   hipStream_t s = as_stream(stream);
   const bf16* xb = (const bf16*)x;
   bf16 *cb = (bf16*)cat, *yb = (bf16*)y;
-#define OGV_VPROJ(nj, nk)                                                                     \
-  if (NJ == nj && NK == nk) {                                                                 \
-    vproj_run<nj, nk>(xb, ldx, w, ldc, bias, cb, ldc, yb, H, W, C, heads, t, sw, s);          \
-    return check_launch("ogv_outlook_vproj_fwd");                                             \
+#define OGV_VPROJ(nj, nk)                                                                      \
+  if (NJ == nj && NK == nk) {                                                                  \
+    if (nw == 4) vproj_run<nj, nk, 4>(xb, ldx, w, ldc, bias, cb, ldc, yb, H, W, C, heads, t, sw, s); \
+    else vproj_run<nj, nk, 8>(xb, ldx, w, ldc, bias, cb, ldc, yb, H, W, C, heads, t, sw, s);         \
+    return check_launch("ogv_outlook_vproj_fwd");                                              \
   }
-  OGV_VPROJ(2, 1) OGV_VPROJ(3, 1) OGV_VPROJ(4, 1) OGV_VPROJ(5, 1) OGV_VPROJ(6, 1) OGV_VPROJ(7, 1) OGV_VPROJ(8, 1)
-  OGV_VPROJ(2, 2) OGV_VPROJ(3, 2) OGV_VPROJ(4, 2) OGV_VPROJ(5, 2) OGV_VPROJ(6, 2) OGV_VPROJ(7, 2) OGV_VPROJ(8, 2)
-  OGV_VPROJ(2, 3) OGV_VPROJ(3, 3) OGV_VPROJ(4, 3) OGV_VPROJ(5, 3) OGV_VPROJ(6, 3) OGV_VPROJ(7, 3) OGV_VPROJ(8, 3)
+  // (NJ, NK) pairs the plan admits: 16 | C <= 96, 8 | head_dim, ncol = C + 9 heads rounded to 16 <= 128
+  OGV_VPROJ(2, 1) OGV_VPROJ(3, 1) OGV_VPROJ(4, 1) OGV_VPROJ(5, 1)
+  OGV_VPROJ(4, 2) OGV_VPROJ(5, 2) OGV_VPROJ(6, 2) OGV_VPROJ(7, 2)
+  OGV_VPROJ(6, 3) OGV_VPROJ(7, 3) OGV_VPROJ(8, 3)
 #undef OGV_VPROJ
   OGV_REQUIRE(false, "ogv_outlook_vproj_fwd: no instantiation for %d column / %d k blocks", NJ, NK);
   return OGV_ERR_ARG;

@@ -759,20 +759,25 @@ class _OutlookVProj(torch.autograd.Function):
 
 def outlook_vproj_supported(B, H, W, C, heads, k, ld, dtype, train) -> bool:
     """Whether OutlookAttention2d takes the fused projection + aggregation forward for this shape
-    (knob "outlook_vproj": 0 never, 1 inference only (default), 2 also in training)."""
+    (knob "outlook_vproj": 0 never, 1 inference only, 2 also in training -- the default --, 3 training
+    with the recompute backward)."""
     if dtype != torch.bfloat16:
         return False
     return bool(_lib.load().ogv_outlook_vproj_supported(B, H, W, C, heads, k, ld, int(bool(train)), OGV_BF16))
 
 
-def outlook_vproj(x2d, w, b, C, B, H, W, heads, k, save_cat=False):
+def outlook_vproj(x2d, w, b, C, B, H, W, heads, k, save_cat=None):
     """y [M, C] = outlook aggregation of (x2d @ [Wv; Wattn; 0]^T + b) without materialising the
-    projection (x2d bf16 rows, w fp32 [ld, C], b fp32 [ld] or None).  When a gradient will be
-    wanted the backward recomputes [v | logits] from x (ogv_outlook_vproj_bwd); save_cat=True
-    instead writes cat [M, ld] in the forward for the aggregation backward (comparison path)."""
+    projection for the forward's own use (x2d bf16 rows, w fp32 [ld, C], b fp32 [ld] or None).
+    When a gradient will be wanted: save_cat=True writes cat = [v | logits | 0] [M, ld] in the same
+    launch for the LDS-tiled aggregation backward; False keeps only x and recomputes [v | logits]
+    in the backward (ogv_outlook_vproj_bwd); None follows the knob (outlook_vproj 3 -> recompute)."""
     require_device(x2d, w, b, what="ogv.outlook_vproj")
     x2d = _rows_contig(x2d)
     train = torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in (x2d, w, b))
+    if train and save_cat is None:
+        save_cat = _lib.load().ogv_outlook_vproj_supported(int(B), int(H), int(W), int(C), int(heads), int(k),
+                                                           int(w.shape[0]), 1, OGV_BF16) != 2
     mode = 0 if not train else (2 if save_cat else 1)
     return _OutlookVProj.apply(x2d, w.contiguous(), None if b is None else b.contiguous(), int(C), int(B), int(H),
                                int(W), int(heads), int(k), mode)

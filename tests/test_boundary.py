@@ -181,9 +181,11 @@ def test_gemm_routing_table():
 
 
 def test_outlook_vproj_plan_and_knob():
-    """Which shapes the fused Outlooker forward takes (host-side plan, no GPU): bf16, k = 3,
+    """Which shapes the fused Outlooker kernels take (host-side plan, no GPU): bf16, k = 3,
     16 | C <= 96, 8 | head_dim, ld = C + 9 heads rounded up to 8; knob outlook_vproj: 0 never,
-    1 inference only (default), 2 also in training; unsupported calls fail before any launch."""
+    1 inference only, 2 also in training with the forward writing cat (default: returns 1 for
+    training), 3 training with the recompute backward (returns 2 when ogv_outlook_vproj_bwd takes
+    the shape); the tile knob vp_tile forces a candidate; unsupported calls fail before any launch."""
     import ogv._lib as L
     lib = L.load()
     ld = lambda C, h: (C + 9 * h + 7) // 8 * 8  # noqa: E731
@@ -198,13 +200,24 @@ def test_outlook_vproj_plan_and_knob():
         assert sup(2, 8, 8, 48, 2, False, k=5) == 0
         assert sup(2, 8, 8, 40, 5, False) == 0              # head_dim 8 but 16 does not divide C
         assert sup(2, 8, 8, 48, 2, False, l=72 + 8) == 0    # wrong row stride of cat
-        assert sup(512, 32, 32, 48, 2, True) == 0           # default: training keeps the unfused pair
-        assert lib.ogv_set_option(b"outlook_vproj", 2) == 0
-        assert sup(512, 32, 32, 48, 2, True) == 1
+        assert sup(512, 32, 32, 48, 2, True) == 1           # default: fused forward writing cat in training
+        assert lib.ogv_set_option(b"outlook_vproj", 3) == 0
+        for shape in ((512, 32, 32, 48, 2), (512, 16, 16, 96, 3), (128, 224, 224, 64, 2), (2, 5, 7, 16, 2)):
+            assert sup(*shape, True) == 2, shape            # the recompute backward takes every 7M/14M/22M shape
+            assert sup(*shape, False) == 1
+        assert lib.ogv_set_option(b"outlook_vproj", 1) == 0
+        assert sup(512, 32, 32, 48, 2, True) == 0           # inference only
+        assert sup(512, 32, 32, 48, 2, False) == 1
         assert lib.ogv_set_option(b"outlook_vproj", 0) == 0
         assert sup(512, 32, 32, 48, 2, False) == 0
+        assert lib.ogv_set_option(b"outlook_vproj", 2) == 0
+        assert lib.ogv_set_option(b"vp_tile", 1) == 0       # 8 x 16 at two workgroups per CU: the C = 96
+        assert sup(512, 16, 16, 96, 3, False) == 0          # weight slab alone is 57 KB -- does not fit
+        assert lib.ogv_set_option(b"vp_tile", 3) == 0       # 8 x 16 at one workgroup of 8 waves
+        assert sup(512, 16, 16, 96, 3, False) == 1
     finally:
-        assert lib.ogv_set_option(b"outlook_vproj", 1) == 0
+        assert lib.ogv_set_option(b"outlook_vproj", 2) == 0
+        assert lib.ogv_set_option(b"vp_tile", 0) == 0
     x = ctypes.c_void_p(16)
     rc = lib.ogv_outlook_vproj_fwd(x, 192, x, None, None, 200, x, 2, 8, 8, 192, 6, 3, L.OGV_BF16, None)
     assert rc != 0 and b"unsupported" in lib.ogv_last_error()

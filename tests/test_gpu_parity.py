@@ -429,9 +429,10 @@ def test_outlook_vproj_vs_oracle(case):
 
 @pytest.mark.parametrize("case", [(2, 48, 2, 32, 32), (2, 96, 3, 16, 16), (1, 64, 2, 56, 56)])
 def test_outlook_vproj_matches_unfused(case):
-    """OutlookAttention2d with the fused forward in training (knob outlook_vproj=2) vs the unfused
-    GEMM + aggregation (0): y, dx and every parameter gradient within bf16 rounding; and the
-    default (1: fused for inference only) in eval / no_grad vs the unfused forward."""
+    """OutlookAttention2d with the fused forward in training (knob outlook_vproj=2, the default:
+    the forward writes cat for the tiled backward; 3: the recompute backward) vs the unfused GEMM +
+    aggregation (0): y, dx and every parameter gradient within bf16 rounding; and the fused
+    inference forward (1) in eval / no_grad vs the unfused forward."""
     from ogv._lib import load
     from src.model.outlook_attention import OutlookAttention2d
     lib = load()
@@ -442,7 +443,7 @@ def test_outlook_vproj_matches_unfused(case):
     dy = torch.randn(B, C, H, W, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     outs = []
     try:
-        for knob in (2, 0):
+        for knob in (2, 3, 0):
             assert lib.ogv_set_option(b"outlook_vproj", knob) == 0
             m.zero_grad()
             xx = x.clone().requires_grad_()
@@ -455,9 +456,12 @@ def test_outlook_vproj_matches_unfused(case):
             with torch.no_grad():
                 inf.append(m.eval()(x).float())
     finally:
-        assert lib.ogv_set_option(b"outlook_vproj", 1) == 0
-    for a, b in zip(*outs):
-        assert fx.maxabs(a, b) <= 1e-2 * max(1.0, b.abs().max().item())
+        assert lib.ogv_set_option(b"outlook_vproj", 2) == 0
+    for o in outs[:2]:
+        for a, b in zip(o, outs[2]):
+            assert fx.maxabs(a, b) <= 1e-2 * max(1.0, b.abs().max().item())
+    for a, b in zip(outs[0], outs[1]):     # saved cat vs recompute: the same function, bit for bit
+        assert torch.equal(a, b)
     assert fx.maxabs(inf[0], inf[1]) <= 1e-2 * max(1.0, inf[1].abs().max().item())
     # the default no_grad forward IS the fused kernel: bit-identical to a direct call
     from ogv import functional as OF
@@ -873,7 +877,7 @@ def test_outlook_vproj_train_grads_full_size_match_unfused(shape):
     for fused in (True, False):
         xx, wq, bq = x.clone().requires_grad_(), w.clone().requires_grad_(), b.clone().requires_grad_()
         if fused:
-            y = OF.outlook_vproj(xx, wq, bq, C, B, H, W, h, 3)
+            y = OF.outlook_vproj(xx, wq, bq, C, B, H, W, h, 3, save_cat=False)
             assert y.grad_fn.saved_tensors[3] is None          # no [v | logits] tensor kept
         else:
             y = OF.outlook_aggregate_cat(OF.linear_rows(xx, wq, bq), C, B, H, W, h, 3)

@@ -50,9 +50,13 @@ const char* ogv_last_error(void);
  *   bit 1 next-panel register prefetch in the streaming GEMM, bit 2 also for its prologue variants;
  *   "sg_per_cu" (default 2): streaming-GEMM workgroups per CU; "splitk_max" (default 32): K-slab
  *   cap of the fp32 split-K GEMM; "se_gemv" 1 (default) / 0: the Squeeze-Excite MLP on the GEMV
- *   kernels of ogv_se.hip instead of split-K GEMM + reduce; "outlook_vproj" 0/1/2: fused Outlooker
- *   projection + aggregation never / inference (default) / also training; "vp_dbg", "pg_dbg":
- *   phase-skipping timing experiments (wrong results).
+ *   kernels of ogv_se.hip instead of split-K GEMM + reduce; "outlook_vproj" 0/1/2/3: fused Outlooker
+ *   projection + aggregation never / inference only / also training with the forward writing cat for
+ *   the tiled backward (default) / training with the recompute backward ogv_outlook_vproj_bwd;
+ *   "vp_tile" 0 (default) / 1-4: force a tile candidate of the fused Outlooker kernels; "wg2_fuse" 0
+ *   (default) / 1: in-kernel last-workgroup reduction of the split-M weight gradient instead of the
+ *   column-reduce launch (measured slower); "vp_dbg", "pg_dbg": phase-skipping timing experiments
+ *   (wrong results).
  * Options pick kernel plans, and every *_ws_bytes query sizes the workspace for the plans in force
  * when it is called: set options first, then size workspaces (a workspace sized under other option
  * values can be too small -- e.g. wg_blocks / wg_tile / swg_min_m change the split-M partial count).
@@ -92,8 +96,10 @@ size_t ogv_outlook_bwd_ws_bytes(int B, int H, int W, int C, int heads, int k, og
  * Writes y [M, C] and, when cat != NULL, cat [M, ldc] = [v | logits | 0] rounded to bf16 (what
  * ogv_outlook_agg_bwd reads in training).  ldc must be C + heads*9 rounded up to 8.
  * ogv_outlook_vproj_supported() says whether a shape takes this kernel (16 | C <= 96,
- * 8 | head_dim) for inference (train = 0) or training (train = 1: the forward with cat = NULL plus
- * ogv_outlook_vproj_bwd) under knob "outlook_vproj" (0 never, 1 inference only, 2 both);
+ * 8 | head_dim) for inference (train = 0) or training (train = 1) under knob "outlook_vproj":
+ * 0 never; 1 inference only; 2 (default) training too, returning 1 = the forward writes cat for
+ * ogv_outlook_agg_bwd; 3 returning 2 = the forward writes only y and ogv_outlook_vproj_bwd
+ * recomputes [v | logits] (1 when that backward does not take the shape).
  * ogv_outlook_vproj_fwd itself runs any shape the kernel supports and returns OGV_ERR_ARG for the
  * others.
  * ogv_outlook_vproj_bwd: the backward of the same fused op with the projections RECOMPUTED from x
@@ -247,10 +253,13 @@ typedef struct {
   int has_bn, train;
   float bn_eps, bn_momentum;
   int act;
+  int w_layout;   /* 0: w / dw stored [Cout, Cin, 3, 3]; 1: stored [Cout, 3, 3, Cin] (a channels_last
+                     weight tensor, which is the tap-major matrix the kernels multiply by: no weight
+                     transpose launches, dw written in place) */
 } ogv_convbn_desc;
 
 typedef struct {
-  const float* w;                                   /* [Cout, Cin, 3, 3] */
+  const float* w;                                   /* [Cout, Cin, 3, 3] (w_layout 0) or [Cout, 3, 3, Cin] */
   const float* bias;                                /* [Cout] or NULL */
   const float *bn_w, *bn_b; float *bn_rm, *bn_rv;   /* [Cout] */
 } ogv_convbn_params;

@@ -26,13 +26,14 @@ __global__ void conv_w_fwd_kernel(const float* __restrict__ w, float* __restrict
   const int tap = r / Cin, c = r - tap * Cin;
   wt[i] = w[((long)n * Cin + c) * 9 + tap];
 }
-// wd[c][tap*Cout + n] = w[n][c][tap]   (the data gradient's GEMM weights)
-__global__ void conv_w_dgrad_kernel(const float* __restrict__ w, float* __restrict__ wd, int Cout, int Cin) {
+// wd[c][tap*Cout + n] = w[n][c][tap]   (the data gradient's GEMM weights; tm: w stored tap-major
+// [n][tap][c], a channels_last weight)
+__global__ void conv_w_dgrad_kernel(const float* __restrict__ w, float* __restrict__ wd, int Cout, int Cin, int tm) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (long)Cout * Cin * 9) return;
   const int c = (int)(i / (9L * Cout)), r = (int)(i - (long)c * 9 * Cout);
   const int tap = r / Cout, n = r - tap * Cout;
-  wd[i] = w[((long)n * Cin + c) * 9 + tap];
+  wd[i] = tm ? w[((long)n * 9 + tap) * Cin + c] : w[((long)n * Cin + c) * 9 + tap];
 }
 // dw[n][c][tap] = dwt[n][tap*Cin + c]
 __global__ void conv_dw_untranspose_kernel(const float* __restrict__ dwt, float* __restrict__ dw, int Cout, int Cin) {
@@ -372,7 +373,11 @@ extern "C" int ogv_convbn_fwd(const void* x, void* out, void* saved, void* ws, c
   cb_saved(*d, dt, saved, &y, b, nullptr);
   const CbWs w = cb_ws(*d, dt, ws);
   const long nw = (long)d->Cout * d->Cin * 9;
-  conv_w_fwd_kernel<<<cdiv(nw, 256), 256, 0, s>>>(p->w, w.wt, d->Cout, d->Cin);
+  const float* wt = p->w;   // w_layout 1: already the tap-major matrix
+  if (!d->w_layout) {
+    conv_w_fwd_kernel<<<cdiv(nw, 256), 256, 0, s>>>(p->w, w.wt, d->Cout, d->Cin);
+    wt = w.wt;
+  }
   Epi e;
   e.bias = p->bias;
   const bool stats = d->has_bn && d->train;
@@ -380,7 +385,7 @@ extern "C" int ogv_convbn_fwd(const void* x, void* out, void* saved, void* ws, c
     e.stat = w.dstat;
     e.stat_shift = p->bn_rm;
   }
-  conv_gemm_launch(dt, x, g.fwd, w.wt, y, (int)g.Mo, d->Cout, e, s);
+  conv_gemm_launch(dt, x, g.fwd, wt, y, (int)g.Mo, d->Cout, e, s);
   if (d->has_bn) {
     if (stats) colreduce(w.dstat, w.dsums, gemm_stat_rows((int)g.Mo), 2L * d->Cout, 2L * d->Cout, w.dtmp, s);
     bn_finalize_launch(w.dsums, d->Cout, (double)g.Mo, p->bn_w, p->bn_b, d->bn_eps, d->bn_momentum, p->bn_rm, p->bn_rv,
@@ -419,13 +424,13 @@ extern "C" int ogv_convbn_bwd(const void* dout, const void* x, const void* saved
                   s);
   // 2) weight (+bias) gradient: dW[n][tap*Cin+c] = sum_m dy[m,n] * gather(x)[m, tap*Cin+c]
   const int K9 = 9 * d->Cin;
-  gemm_wgrad_launch(dt, w.dy, d->Cout, x, 0, Pro(), nullptr, 1, w.dwt, dbias, (int)g.Mo, d->Cout, K9, w.gemm, s,
-                    &g.fwd);
+  gemm_wgrad_launch(dt, w.dy, d->Cout, x, 0, Pro(), nullptr, 1, d->w_layout ? dw : w.dwt, dbias, (int)g.Mo, d->Cout,
+                    K9, w.gemm, s, &g.fwd);
   const long nw = (long)d->Cout * d->Cin * 9;
-  conv_dw_untranspose_kernel<<<cdiv(nw, 256), 256, 0, s>>>(w.dwt, dw, d->Cout, d->Cin);
+  if (!d->w_layout) conv_dw_untranspose_kernel<<<cdiv(nw, 256), 256, 0, s>>>(w.dwt, dw, d->Cout, d->Cin);
   // 3) data gradient: transposed gather of dy against the (Cin x 9*Cout) weight matrix
   if (dx) {
-    conv_w_dgrad_kernel<<<cdiv(nw, 256), 256, 0, s>>>(p->w, w.wt, d->Cout, d->Cin);
+    conv_w_dgrad_kernel<<<cdiv(nw, 256), 256, 0, s>>>(p->w, w.wt, d->Cout, d->Cin, d->w_layout);
     conv_gemm_launch(dt, w.dy, g.bwd, w.wt, dx, (int)g.M, d->Cin, Epi(), s);
   }
   return check_launch("ogv_convbn_bwd");

@@ -187,7 +187,8 @@ size_t swgrad_ws_floats(int M, int N, int K);
 // Pipelined split-M weight gradient (ogv_wgrad2.hip), same partial layout; knob "wg2": 0 off,
 // 1 = where the streaming kernel does not apply, 2 = ahead of it as well.
 int wgrad2_try(const void* G, int ldg, const void* X, int ldx, const Pro& pro, const float* rs, int rps, float* part,
-               bool bias, int M, int N, int K, hipStream_t s);
+               float* dW, float* dbias, bool bias, int M, int N, int K, hipStream_t s, bool* reduced);
+void set_wg2_fuse(int v);
 size_t wgrad2_ws_floats(int M, int N, int K);
 int wg2_mode();
 void set_wg2(int v);

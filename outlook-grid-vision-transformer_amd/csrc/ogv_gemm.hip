@@ -1439,11 +1439,13 @@ void gemm_wgrad_launch(ogv_dtype dt, const void* G, int ldg, const void* X, int 
   float* part = (float*)ws;
   if (dt == OGV_BF16 && !xc) {
     const bool b = dbias != nullptr;
-    int S = wg2_mode() == 2 ? wgrad2_try(G, ldg, X, ldx, pro, rs, rps, part, b, M, N, K, s) : 0;
+    bool reduced = false;
+    int S = wg2_mode() == 2 ? wgrad2_try(G, ldg, X, ldx, pro, rs, rps, part, dW, dbias, b, M, N, K, s, &reduced) : 0;
     if (S == 0) S = swgrad_try(G, ldg, X, ldx, pro, rs, rps, part, b, M, N, K, s);
-    if (S == 0 && wg2_mode() == 1) S = wgrad2_try(G, ldg, X, ldx, pro, rs, rps, part, b, M, N, K, s);
+    if (S == 0 && wg2_mode() == 1) S = wgrad2_try(G, ldg, X, ldx, pro, rs, rps, part, dW, dbias, b, M, N, K, s, &reduced);
     if (S > 0) {
-      colreduce(part, dW, S, dbias ? ldp : (long)N * K, ldp, part + (size_t)S * ldp, s, dbias, (long)N * K);
+      if (!reduced)
+        colreduce(part, dW, S, dbias ? ldp : (long)N * K, ldp, part + (size_t)S * ldp, s, dbias, (long)N * K);
       return;
     }
   }

@@ -186,6 +186,10 @@ extern "C" int ogv_set_option(const char* name, int value) {
     set_vp_dbg(value);
     return OGV_OK;
   }
+  if (!strcmp(name, "wg2_fuse")) {
+    set_wg2_fuse(value);
+    return OGV_OK;
+  }
   if (!strcmp(name, "vp_tile")) {
     set_vp_tile(value);
     return OGV_OK;

@@ -13,7 +13,11 @@
 //   * the prologue form is a template parameter (no runtime switch per element), and the tile
 //     edge may cover all of N (BN = 192), so the prologue runs once per X element;
 //   * loads use clamped, always-valid addresses and select zero afterwards (no branch per load).
-// Output: fp32 partials [S][N*K + N] (the tiled kernel's layout, reduced by the caller's colreduce).
+// Output: fp32 partials [S][N*K + N] (the tiled kernel's layout) and, with an arrival counter per
+// output tile (knob wg2_fuse = 1), dW / dbias themselves: the LAST workgroup of a tile to finish (arrival
+// counted by one agent-scope atomic ticket behind write-through partial stores) sums that tile's S
+// partials in slab order 0..S-1 -- deterministic, whichever workgroup arrives last -- and resets
+// the counter, so no separate column-reduce launch follows (slower at these slab counts: see the knob).
 // Fragment reads: ds_read_b64_tr_b16 with the same m-permutation as the tiled kernel (rows 4g+q and
 // 16+4g+q of each 32-row block; an odd multiple of 16 as pitch keeps them conflict-free).
 #include "ogv_gemm.h"
@@ -26,12 +30,19 @@ constexpr int W2_NT = 256;  // 4 waves, 2 x 2 over the output tile
 // prologue forms: -1 none; OGV_ACT_GELU: gelu(x); OGV_ACT_SILU: silu(x * sc + sh) * gate; 99: any (runtime)
 constexpr int W2_GENERIC = 99;
 
+// arrival counters of the fused reduction: zero at module load, each used window reset to zero by
+// its last workgroup; the host hands every launch its own window of a ring (w2_counters)
+constexpr int W2_CNT = 1 << 16;
+__device__ unsigned g_w2_cnt[W2_CNT];
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
 template <int BN, int BK, int PA>
 __global__ __launch_bounds__(W2_NT) void wgrad2_bf16_kernel(const bf16* __restrict__ G, int ldg,
                                                             const bf16* __restrict__ X, int ldx, Pro pro,
                                                             const float* __restrict__ rs, int rps,
                                                             float* __restrict__ part, long ldp, int want_bias, int M,
-                                                            int N, int K, int mchunk, int nNt, int tiles, int S) {
+                                                            int N, int K, int mchunk, int nNt, int tiles, int S,
+                                                            int cnt0, float* __restrict__ dW, float* __restrict__ dbias) {
   constexpr int MS = W2_MS;
   constexpr int GP = BN + 16, XP = BK + 16;      // odd multiples of 16 for BN in {64, 96, 128, 192}, BK in {64, 128}
   constexpr int GC = BN / 8, XC = BK / 8;        // 16-B chunks per staged row
@@ -213,32 +224,146 @@ __global__ __launch_bounds__(W2_NT) void wgrad2_bf16_kernel(const bf16* __restri
     __syncthreads();
   }
 
-  float* dst = part + (long)s * ldp;
+  if (cnt0 < 0) {   // partials only: the caller's colreduce sums them
+    float* dst = part + (long)s * ldp;
+#pragma unroll
+    for (int i = 0; i < TN; ++i)
+#pragma unroll
+      for (int j = 0; j < TK; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int n = n0 + wn * (BN / 2) + i * 16 + 4 * g + r;
+          const int k = k0 + wk * (BK / 2) + j * 16 + c16;
+          if (n < N && k < K) dst[(long)n * K + k] = acc[i][j][r];
+        }
+    if (bias_wave && c16 == 0) {  // every column of the ones product holds the row sum
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int n = n0 + wn * (BN / 2) + i * 16 + 4 * g + r;
+          if (n < N) dst[(long)N * K + n] = bacc[i][r];
+        }
+    }
+    return;
+  }
+  // ---- fused reduction (cdna_hip_programming.md §5 "In-launch split-K reduction", sc1 form): the
+  // partial tile goes out as 16-B WRITE-THROUGH (sc1) stores, staged through LDS into whole rows;
+  // every wave drains them (vmcnt 0) before the workgroup barrier, then ONE lane takes a ticket
+  // (relaxed agent-scope add); the workgroup that draws S - 1 reads all S partial tiles with sc1
+  // loads (never an L2 writeback / invalidate: no __threadfence) in slab order 0..S-1.
+  constexpr int TP = BK + 4;                         // fp32 tile pitch: conflict-free fragment writes
+  float* T = reinterpret_cast<float*>(smem);         // [BN][TP] partial tile, then [BN] bias, then a flag
+  float* Tb = T + BN * TP;
+  unsigned* flag = reinterpret_cast<unsigned*>(Tb + BN);
+  static_assert((BN * TP + BN + 1) * 4 <= 2 * BUF * 2, "fp32 tile must fit the staging LDS");
+  __syncthreads();                                   // every wave's last fragment reads are done
 #pragma unroll
   for (int i = 0; i < TN; ++i)
 #pragma unroll
     for (int j = 0; j < TK; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int n = n0 + wn * (BN / 2) + i * 16 + 4 * g + r;
-        const int k = k0 + wk * (BK / 2) + j * 16 + c16;
-        if (n < N && k < K) dst[(long)n * K + k] = acc[i][j][r];
-      }
-  if (bias_wave && c16 == 0) {  // every column of the ones product holds the row sum
+      for (int r = 0; r < 4; ++r)
+        T[(wn * (BN / 2) + i * 16 + 4 * g + r) * TP + wk * (BK / 2) + j * 16 + c16] = acc[i][j][r];
+  if (bias_wave && c16 == 0) {
 #pragma unroll
     for (int i = 0; i < TN; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int n = n0 + wn * (BN / 2) + i * 16 + 4 * g + r;
-        if (n < N) dst[(long)N * K + n] = bacc[i][r];
-      }
+      for (int r = 0; r < 4; ++r) Tb[wn * (BN / 2) + i * 16 + 4 * g + r] = bacc[i][r];
   }
+  __syncthreads();
+  const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(part, (short)0, (int)(S * ldp * 4), 0x00020000);
+  constexpr int C4 = BK / 4;   // 16-B chunks per tile row
+  const bool bias_tile = want_bias && kt == 0;
+  for (int e = tid; e < BN * C4; e += W2_NT) {
+    const int nl = e / C4, kl = (e % C4) * 4, n = n0 + nl, k = k0 + kl;
+    if (n >= N || k >= K) continue;
+    const float4 v = *reinterpret_cast<const float4*>(T + nl * TP + kl);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), prs, (int)(((long)s * ldp + (long)n * K + k) * 4), 0,
+                                           16);
+  }
+  if (bias_tile) {
+    for (int e = tid; e < BN / 4; e += W2_NT) {
+      const int n = n0 + 4 * e;
+      if (n >= N) continue;
+      const float4 v = *reinterpret_cast<const float4*>(Tb + 4 * e);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), prs, (int)(((long)s * ldp + (long)N * K + n) * 4),
+                                             0, 16);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // EVERY storing wave drains its sc1 stores
+  __syncthreads();
+  if (tid == 0)
+    flag[0] = __hip_atomic_fetch_add(&g_w2_cnt[cnt0 + tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+              (unsigned)(S - 1);
+  __syncthreads();
+  if (!flag[0]) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // (compiler ordering only: every load below is sc1)
+  for (int e = tid; e < BN * C4; e += W2_NT) {
+    const int n = n0 + e / C4, k = k0 + (e % C4) * 4;
+    if (n >= N || k >= K) continue;
+    const int off = (int)(((long)n * K + k) * 4), step = (int)(ldp * 4);
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+    int r = 0;
+    for (; r + 8 <= S; r += 8) {
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        v[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(prs, off + (r + u) * step, 0, 16));
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        a.x += v[u].x; a.y += v[u].y; a.z += v[u].z; a.w += v[u].w;
+      }
+    }
+    for (; r < S; ++r) {
+      const float4 v = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(prs, off + r * step, 0, 16));
+      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
+    *reinterpret_cast<float4*>(dW + (long)n * K + k) = a;
+  }
+  if (bias_tile && dbias) {
+    for (int e = tid; e < BN / 4; e += W2_NT) {
+      const int n = n0 + 4 * e;
+      if (n >= N) continue;
+      const int off = (int)(((long)N * K + n) * 4), step = (int)(ldp * 4);
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int r = 0; r < S; ++r) {
+        const float4 v = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(prs, off + r * step, 0, 16));
+        a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+      }
+      *reinterpret_cast<float4*>(dbias + n) = a;
+    }
+  }
+  if (tid == 0) __hip_atomic_store(&g_w2_cnt[cnt0 + tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ------------------------------------------------------------------------------------------------
 static int g_wg2 = 2;          // knob "wg2": 0 off, 1 = this kernel below the streaming-wgrad M, 2 = at every M (default: measured faster than both other kernels at every 7M shape but one, which ties)
 static int g_wg2_blocks = 1024;  // knob "wg2_blocks": workgroups the split-M plan aims for
 static int g_wg2_tile = 0;     // knob "wg2_tile": force the N edge (64 / 96 / 128 / 192; K edge 64 / 128)
+// knob "wg2_fuse": 1 = last-workgroup reduction in the kernel, 0 = the caller's colreduce (default).
+// Measured and rejected as the default (tools/bench_wgrad.py, profiles/r03_wgrad_fuse.log, 7M step
+// shapes): the split-M plan aims at ~1024 workgroups, so a tile has S = 29-1024 slabs and its last
+// workgroup reads S x 16 KB serially -- per-step total 5.69 ms with colreduce vs 16.6 ms fused
+// (10.2 ms at 256 workgroups); e.g. M = 524288, N = K = 48: 27 vs 402 us.  (A __threadfence()
+// release / acquire in every workgroup, the first form tried, took the 7M step from 17.0 to 32.3 ms.)
+static int g_wg2_fuse = 0;
+void set_wg2_fuse(int v) { g_wg2_fuse = v ? 1 : 0; }
+
+// A window of `tiles` arrival counters for one launch.  Windows are handed out round the ring in
+// launch order, per device; a window is reused only W2_CNT counters later, by which time its
+// previous user has finished (a step launches far fewer than W2_CNT tiles, and every launch that
+// could still be running -- side streams, the branches of one captured graph -- holds a distinct
+// window).  Returns -1 (no fused reduction) when a launch has more tiles than a ring share.
+static int w2_counters(int tiles) {
+  static long pos[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64 || tiles > W2_CNT / 16) return -1;
+  if (pos[dev] + tiles > W2_CNT) pos[dev] = 0;
+  const int c = (int)pos[dev];
+  pos[dev] += tiles;
+  return c;
+}
 int wg2_mode() { return g_wg2; }
 void set_wg2(int v) { g_wg2 = v < 0 ? 0 : (v > 2 ? 2 : v); }
 void set_wg2_blocks(int v) { g_wg2_blocks = v < 64 ? 64 : v; }
@@ -291,44 +416,56 @@ size_t wgrad2_ws_floats(int M, int N, int K) {
   return best;
 }
 
+struct W2Out {
+  float* part;
+  long ldp;
+  int cnt0;          // counter window, -1 = partials only
+  float *dW, *dbias;
+};
+
 template <int BN, int BK, int PA>
 static void w2_launch(const W2Plan& p, const bf16* G, int ldg, const bf16* X, int ldx, const Pro& pro, const float* rs,
-                      int rps, float* part, long ldp, bool bias, int M, int N, int K, hipStream_t s) {
+                      int rps, const W2Out& o, bool bias, int M, int N, int K, hipStream_t s) {
   const int tiles = p.nNt * p.nKt;
   const unsigned grid = (unsigned)(((p.S + 7) / 8) * 8 * tiles);
-  wgrad2_bf16_kernel<BN, BK, PA><<<grid, W2_NT, 0, s>>>(G, ldg, X, ldx, pro, rs, rps, part, ldp, bias ? 1 : 0, M, N, K,
-                                                        p.mchunk, p.nNt, tiles, p.S);
+  wgrad2_bf16_kernel<BN, BK, PA><<<grid, W2_NT, 0, s>>>(G, ldg, X, ldx, pro, rs, rps, o.part, o.ldp, bias ? 1 : 0, M, N,
+                                                        K, p.mchunk, p.nNt, tiles, p.S, o.cnt0, o.dW, o.dbias);
 }
 
 template <int PA>
 static void w2_dispatch(const W2Plan& p, const bf16* G, int ldg, const bf16* X, int ldx, const Pro& pro,
-                        const float* rs, int rps, float* part, long ldp, bool bias, int M, int N, int K,
-                        hipStream_t s) {
+                        const float* rs, int rps, const W2Out& o, bool bias, int M, int N, int K, hipStream_t s) {
   // instantiated: 64 x 64, 96 x 64, 128 x 64, 192 x 64 and 128 x 128 (forced by wg2_tile=128 only)
-  if (p.BN == 128 && p.BK == 128) w2_launch<128, 128, PA>(p, G, ldg, X, ldx, pro, rs, rps, part, ldp, bias, M, N, K, s);
-  else if (p.BN == 64) w2_launch<64, 64, PA>(p, G, ldg, X, ldx, pro, rs, rps, part, ldp, bias, M, N, K, s);
-  else if (p.BN == 96) w2_launch<96, 64, PA>(p, G, ldg, X, ldx, pro, rs, rps, part, ldp, bias, M, N, K, s);
-  else if (p.BN == 128) w2_launch<128, 64, PA>(p, G, ldg, X, ldx, pro, rs, rps, part, ldp, bias, M, N, K, s);
-  else w2_launch<192, 64, PA>(p, G, ldg, X, ldx, pro, rs, rps, part, ldp, bias, M, N, K, s);
+  if (p.BN == 128 && p.BK == 128) w2_launch<128, 128, PA>(p, G, ldg, X, ldx, pro, rs, rps, o, bias, M, N, K, s);
+  else if (p.BN == 64) w2_launch<64, 64, PA>(p, G, ldg, X, ldx, pro, rs, rps, o, bias, M, N, K, s);
+  else if (p.BN == 96) w2_launch<96, 64, PA>(p, G, ldg, X, ldx, pro, rs, rps, o, bias, M, N, K, s);
+  else if (p.BN == 128) w2_launch<128, 64, PA>(p, G, ldg, X, ldx, pro, rs, rps, o, bias, M, N, K, s);
+  else w2_launch<192, 64, PA>(p, G, ldg, X, ldx, pro, rs, rps, o, bias, M, N, K, s);
 }
 
 // Returns the number of partial rows written into part (layout [S][N*K + N]), 0 if not handled.
+// *reduced = true when the kernel also wrote dW (and dbias, when bias) itself: no colreduce needed.
 int wgrad2_try(const void* G, int ldg, const void* X, int ldx, const Pro& pro, const float* rs, int rps, float* part,
-               bool bias, int M, int N, int K, hipStream_t s) {
+               float* dW, float* dbias, bool bias, int M, int N, int K, hipStream_t s, bool* reduced) {
+  *reduced = false;
   if (!g_wg2) return 0;
   if ((ldg & 7) || (ldx & 7) || (reinterpret_cast<uintptr_t>(G) & 15) || (reinterpret_cast<uintptr_t>(X) & 15))
     return 0;
   W2Plan p = wgrad2_plan(M, N, K, pro.any());
   if (!p.ok) return 0;
-  const long ldp = (long)N * K + N;
+  W2Out o{part, (long)N * K + N, -1, dW, dbias};
+  if (g_wg2_fuse && dW && !(reinterpret_cast<uintptr_t>(dW) & 15) && !(reinterpret_cast<uintptr_t>(part) & 15) &&
+      (!dbias || !(reinterpret_cast<uintptr_t>(dbias) & 15)) && (long)p.S * o.ldp * 4 < (1L << 31))
+    o.cnt0 = w2_counters(p.nNt * p.nKt);
   const bf16* g = static_cast<const bf16*>(G);
   const bf16* x = static_cast<const bf16*>(X);
   const bool gelu_only = pro.act == OGV_ACT_GELU && !pro.sc && !pro.sh && !pro.gate;
   const bool bn_silu_gate = pro.act == OGV_ACT_SILU && pro.sc && pro.sh && pro.gate && !(pro.gld & 3);
-  if (!pro.any()) w2_dispatch<-1>(p, g, ldg, x, ldx, pro, rs, rps, part, ldp, bias, M, N, K, s);
-  else if (gelu_only) w2_dispatch<OGV_ACT_GELU>(p, g, ldg, x, ldx, pro, rs, rps, part, ldp, bias, M, N, K, s);
-  else if (bn_silu_gate) w2_dispatch<OGV_ACT_SILU>(p, g, ldg, x, ldx, pro, rs, rps, part, ldp, bias, M, N, K, s);
-  else w2_dispatch<W2_GENERIC>(p, g, ldg, x, ldx, pro, rs, rps, part, ldp, bias, M, N, K, s);
+  if (!pro.any()) w2_dispatch<-1>(p, g, ldg, x, ldx, pro, rs, rps, o, bias, M, N, K, s);
+  else if (gelu_only) w2_dispatch<OGV_ACT_GELU>(p, g, ldg, x, ldx, pro, rs, rps, o, bias, M, N, K, s);
+  else if (bn_silu_gate) w2_dispatch<OGV_ACT_SILU>(p, g, ldg, x, ldx, pro, rs, rps, o, bias, M, N, K, s);
+  else w2_dispatch<W2_GENERIC>(p, g, ldg, x, ldx, pro, rs, rps, o, bias, M, N, K, s);
+  *reduced = o.cnt0 >= 0;
   return p.S;
 }
 

@@ -41,7 +41,7 @@ class MBConvGrads(ctypes.Structure):
 
 class ConvBNDesc(ctypes.Structure):
     _fields_ = [("B", _i), ("H", _i), ("W", _i), ("Cin", _i), ("Cout", _i), ("stride", _i), ("has_bn", _i),
-                ("train", _i), ("bn_eps", _f), ("bn_momentum", _f), ("act", _i)]
+                ("train", _i), ("bn_eps", _f), ("bn_momentum", _f), ("act", _i), ("w_layout", _i)]
 
 
 class ConvBNParams(ctypes.Structure):

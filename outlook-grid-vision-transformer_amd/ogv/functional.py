@@ -757,6 +757,27 @@ class _OutlookVProj(torch.autograd.Function):
         return dx, dw, db, None, None, None, None, None, None, None
 
 
+class _AliasedConcat(torch.autograd.Function):
+    """torch.cat along rows for parts that already ARE row blocks of `full` (views of one buffer,
+    e.g. parameters re-pointed into it; part i starts at row offsets[i]): returns `full` itself --
+    no copy launch -- and hands each part the matching row block of the incoming gradient (views
+    that AccumulateGrad steals: nothing is copied on the way back either).  Rows of `full` outside
+    the parts carry no gradient."""
+
+    @staticmethod
+    def forward(ctx, full, offsets, *parts):
+        ctx.meta = [(int(o), p.shape) for o, p in zip(offsets, parts)]
+        return full.view(full.shape)
+
+    @staticmethod
+    def backward(ctx, g):
+        return (None, None) + tuple(g[o:o + shp[0]].view(shp) for o, shp in ctx.meta)
+
+
+def aliased_concat(full, offsets, *parts):
+    return _AliasedConcat.apply(full, tuple(offsets), *parts)
+
+
 def outlook_vproj_supported(B, H, W, C, heads, k, ld, dtype, train) -> bool:
     """Whether OutlookAttention2d takes the fused projection + aggregation forward for this shape
     (knob "outlook_vproj": 0 never, 1 inference only, 2 also in training -- the default --, 3 training
@@ -1018,8 +1039,15 @@ def conv3x3_bn_act(x, conv, bn=None, act=None):
     Cout, stride = conv.out_channels, conv.stride[0]
     has_bn, train, eps, mom, rm, rv = _bn_args(bn)
     x2d = _rows_contig(nchw_to_rows(x.to(compute_dtype(x))))
-    geom = (int(B), int(H), int(W), int(Cin), int(Cout), int(stride), has_bn, train, eps, mom, ACT[act])
-    y = _ConvBN.apply(x2d, geom, rm, rv, f32(conv.weight).contiguous(), f32(conv.bias),
+    w = f32(conv.weight)
+    # a channels_last weight (the model moved to channels_last) IS the tap-major [Cout, 3, 3, Cin]
+    # matrix the kernels multiply by: passed as is (no copy here, no transpose launches, and its
+    # gradient comes back in the same layout, so AccumulateGrad copies nothing)
+    tap_major = not w.is_contiguous() and w.is_contiguous(memory_format=torch.channels_last)
+    if not tap_major:
+        w = w.contiguous()
+    geom = (int(B), int(H), int(W), int(Cin), int(Cout), int(stride), has_bn, train, eps, mom, ACT[act], int(tap_major))
+    y = _ConvBN.apply(x2d, geom, rm, rv, w, f32(conv.bias),
                       f32(bn.weight) if has_bn else None, f32(bn.bias) if has_bn else None)
     if has_bn and train and not getattr(bn, "_ogv_nbt_pooled", False):
         bn.num_batches_tracked.add_(1)

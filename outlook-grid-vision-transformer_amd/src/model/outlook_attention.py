@@ -115,11 +115,59 @@ class OutlookAttention2d(nn.Module):
     def _hooked(self) -> bool:
         return any(m._forward_hooks or m._forward_pre_hooks for m in (self.attn, self.v))
 
+    def _cat_store(self, ld):
+        """One fp32 [ld, C] weight buffer (+ [ld] bias buffer) whose row blocks ARE v.weight and
+        attn.weight (v.bias, attn.bias): the parameters are re-pointed into it once (values copied,
+        names / shapes / state_dict unchanged), so [Wv; Wattn; 0] needs no concatenation per
+        forward.  Re-binds if the parameters were replaced since (e.g. .to(), assign-loading);
+        None when the parameters are not fp32 device tensors (the copying path then runs)."""
+        C, n = self.dim, self.attn.out_channels
+        wv, wa, bv, ba = self.v.weight, self.attn.weight, self.v.bias, self.attn.bias
+        if not wv.is_cuda or any(t is not None and t.dtype != torch.float32 for t in (wv, wa, bv, ba)):
+            return None
+        st = self.__dict__.get("_cat_buf")
+        if st is not None:
+            fw, fb = st
+            base = fw.data_ptr()
+            ok = (fw.device == wv.device and fw.shape[0] == ld and wv.data_ptr() == base and wv.is_contiguous()
+                  and wa.data_ptr() == base + 4 * C * C and wa.is_contiguous()
+                  and (fb is None) == (bv is None and ba is None))
+            if ok and fb is not None:
+                ok = ((bv is None or bv.data_ptr() == fb.data_ptr()) and (ba is None or ba.data_ptr() == fb.data_ptr() + 4 * C))
+            if ok:
+                return st
+        with torch.no_grad():
+            fw = torch.zeros(ld, C, device=wv.device)
+            fw[:C].copy_(wv.reshape(C, C))
+            fw[C:C + n].copy_(wa.reshape(n, C))
+            wv.data = fw[:C].view(wv.shape)
+            wa.data = fw[C:C + n].view(wa.shape)
+            fb = None
+            if bv is not None or ba is not None:
+                fb = torch.zeros(ld, device=wv.device)
+                if bv is not None:
+                    fb[:C].copy_(bv)
+                    bv.data = fb[:C]
+                if ba is not None:
+                    fb[C:C + n].copy_(ba)
+                    ba.data = fb[C:C + n]
+        self.__dict__["_cat_buf"] = (fw, fb)
+        return fw, fb
+
     def _cat_params(self):
         """[Wv; Wattn; 0] ([ld, C], ld = C + heads*k*k rounded up to 8 so every row of the GEMM
-        output is 16-B aligned) and the matching bias, differentiable w.r.t. both convs."""
+        output is 16-B aligned) and the matching bias, differentiable w.r.t. both convs.  With the
+        parameters living in one buffer (_cat_store) this is that buffer: no copy launch."""
         C, n = self.dim, self.attn.out_channels
         ld = (C + n + 7) // 8 * 8
+        st = self._cat_store(ld)
+        if st is not None:
+            fw, fb = st
+            w = OF.aliased_concat(fw, (0, C), self.v.weight, self.attn.weight)
+            if fb is None:
+                return w, None
+            bs = [(o, t) for o, t in ((0, self.v.bias), (C, self.attn.bias)) if t is not None]
+            return w, OF.aliased_concat(fb, [o for o, _ in bs], *[t for _, t in bs])
         wv, wa = self.v.weight.reshape(C, C), self.attn.weight.reshape(n, C)
         zw, zb = self._zero_pads(wv.device, ld - C - n)
         parts = [wv.float(), wa.float()] + ([zw] if ld > C + n else [])

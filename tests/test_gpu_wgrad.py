@@ -78,8 +78,9 @@ CASES = [  # M, N, K, prologue act, bias, rowscale
     (131072, 96, 384, "gelu", True, False), (1000, 200, 136, "gelu", True, True),
     (777, 96, 64, None, True, False), (40, 48, 24, None, True, False), (130, 328, 248, "silu", True, True),
 ]
-MODES = [("default", {}), ("wg2=0", {"wg2": 0}), ("wg2=1", {"wg2": 1})]  # default = wg2 2
-DEFAULTS = {"wg2": 2, "wg2_blocks": 1024, "wg2_tile": 0}
+MODES = [("default", {}), ("wg2=0", {"wg2": 0}), ("wg2=1", {"wg2": 1}),
+         ("wg2_fuse=1", {"wg2_fuse": 1})]  # default = wg2 2, wg2_fuse 0
+DEFAULTS = {"wg2": 2, "wg2_blocks": 1024, "wg2_tile": 0, "wg2_fuse": 0}
 
 
 def _inputs(M, N, K, rs, seed):
@@ -138,6 +139,53 @@ def test_wgrad2_deterministic():
     a = _check(case, {"wg2": 2})
     b = _check(case, {"wg2": 2})
     assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+
+
+@pytest.mark.parametrize("case", [(32768, 768, 192, None, True, False), (8192, 72, 256, None, True, False),
+                                  (40, 48, 24, None, True, False), (130, 328, 248, "silu", True, True)],
+                         ids=lambda c: "x".join(str(v) for v in c[:3]))
+def test_wgrad2_fused_reduction(case):
+    """The in-kernel last-workgroup reduction (wg2_fuse=1; off by default, slower): equal to the colreduce path
+    within fp32 summation-order rounding, BIT-identical across repeated launches (slab order fixed,
+    whichever workgroup arrives last; the arrival counters reset themselves -- a stale counter would
+    skip or double a tile), also over more launches than the counter ring holds and with launches
+    in flight on two streams at once."""
+    M, N, K, act, bias, rs = case
+    x, d, s, rps = _inputs(M, N, K, rs, 11)
+    xd, dd = x.to(DEV), d.to(DEV)
+    sd = s.to(DEV) if s is not None else None
+    ref = _check(case, {"wg2_fuse": 0}, seed=11 - M - N - K)
+    _opt("wg2_fuse", 1)
+    try:
+        _fused_repeats(case, dd, xd, sd, rps, ref)
+    finally:
+        _opt("wg2_fuse", 0)
+
+
+def _fused_repeats(case, dd, xd, sd, rps, ref):
+    M, N, K, act, bias, rs = case
+    outs = [_wgrad(dd, xd, sd, rps, act, bias, M, N, K) for _ in range(3)]
+    for w, b in outs:
+        assert torch.isfinite(w).all()
+        assert fx.maxrel(w, ref[0]) <= 1e-5
+        if bias:
+            assert fx.maxrel(b, ref[1]) <= 1e-5
+        assert torch.equal(w, outs[0][0]) and (not bias or torch.equal(b, outs[0][1]))
+    # many launches back to back (several trips round the counter ring) on two streams at once
+    ws = [torch.empty(_L().ogv_gemm_wgrad_ws_bytes(M, N, K), device=DEV, dtype=torch.uint8) for _ in range(2)]
+    res = [(torch.empty(N, K, device=DEV), torch.empty(N, device=DEV) if bias else None) for _ in range(2)]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    for st in streams:
+        st.wait_stream(torch.cuda.current_stream())
+    for it in range(400):
+        i = it & 1
+        with torch.cuda.stream(streams[i]):
+            rc = _L().ogv_gemm_wgrad(_p(dd), N, _p(xd), K, _p(sd), rps, _p(res[i][0]), _p(res[i][1]), M, N, K,
+                                     ACT[act], _p(ws[i]), BF16, ctypes.c_void_p(streams[i].cuda_stream))
+            assert rc == 0
+    torch.cuda.synchronize()
+    for w, b in res:
+        assert torch.equal(w, outs[0][0]) and (not bias or torch.equal(b, outs[0][1]))
 
 
 @pytest.mark.parametrize("name", fx.fixture_names("mbconv_") + fx.fixture_names("outgrid_block_")[:2])

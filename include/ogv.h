@@ -67,6 +67,15 @@ int ogv_set_option(const char* name, int value);
  * streaming kernel (large M), 2 = the pipelined panel kernel (small M), 0 = the LDS-tiled kernel;
  * ogv_gpu_sleep queues a ~microseconds device-side spin on the stream (timing harnesses). */
 int ogv_gemm_stream_route(int kind, int M, int N, int K, ogv_act act_in);
+/* Deferred parameter-gradient reductions (no reference counterpart; a training-step scheduling
+ * aid).  While ogv_reduce_defer(1) is in force, the final column reductions that turn slab partials
+ * into PARAMETER gradients -- ogv_gemm_wgrad's dW / dbias and ogv_layernorm_bwd's dgamma / dbeta --
+ * are recorded instead of launched (their workspaces must stay allocated, and the gradients unread,
+ * until the flush); ogv_reduce_flush(stream) runs every recorded reduction as one batched launch
+ * (48 per launch) on `stream`, which must be ordered after all the producing launches.  Returns: defer
+ * -> the number of reductions pending; flush -> 0 or an error code. */
+int ogv_reduce_defer(int on);
+int ogv_reduce_flush(void* stream);
 int ogv_gpu_sleep(int microseconds, void* stream);
 
 /* ---------------------------------------------------------------------------------------------

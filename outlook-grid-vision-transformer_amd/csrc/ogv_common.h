@@ -42,6 +42,12 @@ void colreduce(const float* src, float* dst, long R, long n, long ld, float* tmp
                float* dst2 = nullptr, long n1 = 0);
 // fp64 variant (BatchNorm batch statistics); tmp needs colreduce_tmp_floats(R, n) doubles
 void colreduce(const double* src, double* dst, long R, long n, long ld, double* tmp, hipStream_t s);
+// The same reduction for a PARAMETER GRADIENT (dst read by nothing before the optimizer): while the
+// caller has deferral on (ogv_reduce_defer), recorded instead of launched and run later by
+// ogv_reduce_flush as ONE batched launch with every other deferred reduction (same arithmetic as the
+// single-pass colreduce4 kernel); otherwise identical to colreduce.
+void colreduce_param(const float* src, float* dst, long R, long n, long ld, float* tmp, hipStream_t s,
+                     float* dst2 = nullptr, long n1 = 0);
 
 static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 static inline unsigned cdiv(long a, long b) { return (unsigned)((a + b - 1) / b); }

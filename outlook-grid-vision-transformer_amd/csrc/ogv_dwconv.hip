@@ -8,6 +8,8 @@
 //        (per-block partials [S][9][C] -> column reducer; dbias = sum dout)
 // Channels are vectorised V-wide per thread (16-B loads for bf16 at V=8); weights are staged as
 // wt[tap][C] fp32 so a thread's 9 taps x V channels are contiguous.
+#include <vector>
+
 #include "ogv_common.h"
 
 namespace ogv {
@@ -122,6 +124,110 @@ void colreduce(const float* src, float* dst, long R, long n, long ld, float* tmp
 void colreduce(const double* src, double* dst, long R, long n, long ld, double* tmp, hipStream_t s) {
   colreduce_t<double>(src, dst, R, n, ld, tmp, s, nullptr, n);
 }
+
+// ------------------------------------------------------------------ deferred, batched reductions
+// Parameter-gradient column sums recorded while deferral is on, then run as one launch: block b
+// works on descriptor j (start[j] <= b < start[j + 1]) exactly as a colreduce4 block does.
+struct RedDesc {
+  const float* src;
+  float *dst, *dst2;
+  long R, n, ld, n1;
+};
+constexpr int RED_BATCH = 48;   // descriptors per launch (kernel arguments < 4 KB)
+struct RedBatch {
+  RedDesc d[RED_BATCH];
+  int start[RED_BATCH + 1];
+  int count;
+};
+
+__global__ __launch_bounds__(256) void colreduce_batch_kernel(RedBatch b) {
+  __shared__ float4 red[16][16];
+  int j = 0;
+  while (j + 1 < b.count && b.start[j + 1] <= (int)blockIdx.x) ++j;
+  const RedDesc d = b.d[j];
+  const int cq = threadIdx.x & 15, rg = threadIdx.x >> 4;
+  const long col = ((long)(blockIdx.x - b.start[j]) * 16 + cq) * 4;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (col < d.n) {
+    long r = rg;
+    for (; r + 7 * 16 < d.R; r += 8 * 16) {
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(d.src + (r + u * 16) * d.ld + col);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w;
+      }
+    }
+    for (; r < d.R; r += 16) {
+      const float4 v = *reinterpret_cast<const float4*>(d.src + r * d.ld + col);
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+  }
+  red[rg][cq] = acc;
+  __syncthreads();
+  if (rg == 0 && col < d.n) {
+    float4 t = red[0][cq];
+#pragma unroll
+    for (int g = 1; g < 16; ++g) {
+      const float4 v = red[g][cq];
+      t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+    }
+    const float o[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const long c = col + q;
+      if (c >= d.n) break;
+      if (d.dst2 && c >= d.n1) d.dst2[c - d.n1] = o[q];
+      else d.dst[c] = o[q];
+    }
+  }
+}
+
+static bool g_defer = false;
+static std::vector<RedDesc> g_pending;
+
+void colreduce_param(const float* src, float* dst, long R, long n, long ld, float* tmp, hipStream_t s, float* dst2,
+                     long n1) {
+  const bool fits = (n & 3) == 0 && (ld & 3) == 0 && (reinterpret_cast<uintptr_t>(src) & 15) == 0 && R > 0 &&
+                    (n + 63) / 64 < (1L << 20);
+  if (g_defer && fits) {
+    g_pending.push_back(RedDesc{src, dst, dst2, R, n, ld, dst2 ? n1 : n});
+    return;
+  }
+  colreduce(src, dst, R, n, ld, tmp, s, dst2, n1);
+}
+
+}  // namespace ogv
+
+using namespace ogv;
+
+extern "C" int ogv_reduce_defer(int on) {
+  g_defer = on != 0;
+  return (int)g_pending.size();
+}
+
+extern "C" int ogv_reduce_flush(void* stream) {
+  hipStream_t s = as_stream(stream);
+  size_t i = 0;
+  while (i < g_pending.size()) {
+    RedBatch b{};
+    int blocks = 0;
+    for (; b.count < RED_BATCH && i < g_pending.size(); ++i) {
+      const RedDesc& d = g_pending[i];
+      b.d[b.count] = d;
+      b.start[b.count] = blocks;
+      blocks += (int)((d.n + 63) / 64);
+      ++b.count;
+    }
+    b.start[b.count] = blocks;
+    colreduce_batch_kernel<<<blocks, 256, 0, s>>>(b);
+  }
+  g_pending.clear();
+  return check_launch("ogv_reduce_flush");
+}
+
+namespace ogv {
 
 // ------------------------------------------------------------------ depthwise conv kernels
 struct DwGeom {

@@ -140,7 +140,7 @@ void gemm_dgrad_launch(ogv_dtype dt, const void* dout, int ldd, const float* W, 
 size_t wgrad_ws_bytes(int M, int N, int K);
 void gemm_wgrad_launch(ogv_dtype dt, const void* G, int ldg, const void* X, int ldx, const Pro& pro, const float* rs,
                        int rps, float* dW, float* dbias, int M, int N, int K, void* ws, hipStream_t s,
-                       const ConvG* xconv = nullptr);
+                       const ConvG* xconv = nullptr, bool param_grad = false);
 
 // Small-M fp32 GEMM with split-K (SE MLP: M = batch rows): out = epi(pro(A)[M,K] . W[N,K]^T);
 // ws >= splitk_ws_bytes(M, N, K).  Epilogue: bias, rs, res, zact (no stats).

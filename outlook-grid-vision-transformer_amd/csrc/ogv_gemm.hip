@@ -1425,7 +1425,11 @@ static void launch_wgrad_bf16(const WgradPlan& p, const void* G, int ldg, const 
 
 void gemm_wgrad_launch(ogv_dtype dt, const void* G, int ldg, const void* X, int ldx, const Pro& pro, const float* rs,
                        int rps, float* dW, float* dbias, int M, int N, int K, void* ws, hipStream_t s,
-                       const ConvG* xc) {
+                       const ConvG* xc, bool param_grad) {
+  // param_grad: dW / dbias are final parameter gradients (read by nothing but the optimizer), so
+  // their slab reduction may be deferred (colreduce_param)
+  auto reduce = param_grad ? colreduce_param : static_cast<void (*)(const float*, float*, long, long, long, float*,
+                                                                    hipStream_t, float*, long)>(colreduce);
   if (skip_mask() & 4) return;
   if (M <= 0) {
     (void)hipMemsetAsync(dW, 0, (size_t)N * K * sizeof(float), s);
@@ -1445,7 +1449,7 @@ void gemm_wgrad_launch(ogv_dtype dt, const void* G, int ldg, const void* X, int 
     if (S == 0 && wg2_mode() == 1) S = wgrad2_try(G, ldg, X, ldx, pro, rs, rps, part, dW, dbias, b, M, N, K, s, &reduced);
     if (S > 0) {
       if (!reduced)
-        colreduce(part, dW, S, dbias ? ldp : (long)N * K, ldp, part + (size_t)S * ldp, s, dbias, (long)N * K);
+        reduce(part, dW, S, dbias ? ldp : (long)N * K, ldp, part + (size_t)S * ldp, s, dbias, (long)N * K);
       return;
     }
   }
@@ -1471,7 +1475,7 @@ void gemm_wgrad_launch(ogv_dtype dt, const void* G, int ldg, const void* X, int 
       wgrad_f32_kernel<false><<<grid, 256, 0, s>>>((const float*)G, ldg, (const float*)X, ldx, pro, rs, rps, part, ldp,
                                                    dbias != nullptr, M, N, K, p.mchunk, p.nNt, cv);
   }
-  colreduce(part, dW, p.S, dbias ? ldp : (long)N * K, ldp, tmp, s, dbias, (long)N * K);
+  reduce(part, dW, p.S, dbias ? ldp : (long)N * K, ldp, tmp, s, dbias, (long)N * K);
 }
 
 static int check_common(int M, int N, int K, ogv_act act, ogv_dtype dt, const char* who) {
@@ -1556,6 +1560,7 @@ extern "C" int ogv_gemm_wgrad(const void* dout, int ldd, const void* A, int lda,
   OGV_REQUIRE(!rs || rps > 0, "ogv_gemm_wgrad: rows-per-sample must be > 0 with a row scale");
   Pro pro;
   pro.act = act_in;
-  gemm_wgrad_launch(dt, dout, ldd, A, lda, pro, rs, rps > 0 ? rps : 1, dW, dbias, M, N, K, ws, as_stream(stream));
+  gemm_wgrad_launch(dt, dout, ldd, A, lda, pro, rs, rps > 0 ? rps : 1, dW, dbias, M, N, K, ws, as_stream(stream),
+                    nullptr, true);
   return check_launch("ogv_gemm_wgrad");
 }

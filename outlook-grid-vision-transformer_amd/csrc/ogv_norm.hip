@@ -291,8 +291,8 @@ extern "C" int ogv_layernorm_bwd(const void* dy, const void* x, const float* gam
   float* tmp = part + (size_t)nb * 2 * C;
   OGV_LN_DISPATCH(ln_bwd_launch, dy, x, gamma, mean, rstd, dres, dx, part, nb, (long)M, C, s);
   // partials are [nb][dgamma(C) | dbeta(C)]: reduced straight into the caller's buffers
-  if (dgamma && dbeta) colreduce(part, dgamma, nb, 2L * C, 2L * C, tmp, s, dbeta, C);
-  else if (dgamma) colreduce(part, dgamma, nb, C, 2L * C, tmp, s);
-  else if (dbeta) colreduce(part + C, dbeta, nb, C, 2L * C, tmp, s);
+  if (dgamma && dbeta) colreduce_param(part, dgamma, nb, 2L * C, 2L * C, tmp, s, dbeta, C);
+  else if (dgamma) colreduce_param(part, dgamma, nb, C, 2L * C, tmp, s);
+  else if (dbeta) colreduce_param(part + C, dbeta, nb, C, 2L * C, tmp, s);
   return check_launch("ogv_layernorm_bwd");
 }

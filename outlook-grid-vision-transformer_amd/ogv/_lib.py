@@ -61,6 +61,8 @@ SIGNATURES = {
     "ogv_set_option": (_i, [ctypes.c_char_p, _i]),
     "ogv_gemm_stream_route": (_i, [_i, _i, _i, _i, _i]),
     "ogv_gpu_sleep": (_i, [_i, _p]),
+    "ogv_reduce_defer": (_i, [_i]),
+    "ogv_reduce_flush": (_i, [_p]),
     "ogv_outlook_agg_fwd": (_i, [_p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _p]),
     "ogv_outlook_bwd_ws_bytes": (_sz, [_i, _i, _i, _i, _i, _i, _i]),
     "ogv_outlook_vproj_supported": (_i, [_i, _i, _i, _i, _i, _i, _i, _i, _i]),

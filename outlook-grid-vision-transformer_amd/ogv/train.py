@@ -287,7 +287,7 @@ class Trainer:
     def __init__(self, model: nn.Module, lr=5e-4, weight_decay=0.05, clip=1.0, label_smoothing=0.1,
                  total_steps=10_000, warmup_ratio=0.05, min_lr=1e-6, amp_dtype: Optional[torch.dtype] = torch.bfloat16,
                  graphs: bool = False, capture_warmup: int = 3, capture_hook=None, bucket_mb: float = 8.0,
-                 broadcast_buffers: bool = True):
+                 broadcast_buffers: bool = True, defer_reductions: bool = True):
         self.model = model
         core = model.module if hasattr(model, "module") else model
         self.core = core
@@ -304,6 +304,9 @@ class Trainer:
         self.sched = WarmupCosineLR(self.opt, total_steps, int(warmup_ratio * total_steps), min_lr)
         self.params = [p for p in core.parameters() if p.requires_grad]
         self.clip, self.ls, self.amp_dtype = clip, label_smoothing, amp_dtype
+        # parameter-gradient column reductions batched into one launch at the end of backward
+        # (functional.deferred_param_reductions: every .grad is None when backward starts here)
+        self.defer_reductions = bool(defer_reductions) and self.device_side
         self.capture_warmup = int(capture_warmup)
         self.capture_hook = capture_hook          # called right before recording starts
         self._eager_steps = 0
@@ -381,7 +384,10 @@ class Trainer:
             self._flag(loss.detach(), 0)
         if self.world > 1 and self._overlap:
             self._launch_meta(loss)
-        loss.backward()
+        from .functional import deferred_param_reductions
+        # not under the eager DP overlap: its bucket hooks read gradients as soon as they are produced
+        with deferred_param_reductions(self.defer_reductions and not (self.world > 1 and self._overlap)):
+            loss.backward()
         return loss.detach()
 
     def _meta_values(self, loss):

@@ -353,3 +353,33 @@ def test_graph_dp_world2_matches_single_process(tmp_path):
         d_move += float((p.detach().cpu() - p0).double().norm() ** 2)
     # the DP trajectory differs from the single-process one by far less than the training moved
     assert d_dp ** 0.5 <= 0.25 * d_move ** 0.5, (d_dp ** 0.5, d_move ** 0.5)
+
+
+def test_deferred_param_reductions_match_immediate():
+    """The Trainer's backward records the parameter-gradient column reductions (Linear weight / bias
+    gradients, LayerNorm gamma / beta) and runs them as one batched launch at its end
+    (functional.deferred_param_reductions): every gradient equals the immediate path's (same
+    single-pass arithmetic where that path used it, fp32 rounding of a different split otherwise),
+    and the deferral really took the reductions (dozens pending before the flush)."""
+    from ogv import functional as OF
+    from ogv._lib import load
+    from ogv.train import Trainer
+    x, y = _batch(64, 5)
+    grads, pending = [], []
+    for defer in (False, True):
+        m = _model(13)
+        t = Trainer(m, total_steps=50, graphs=False, defer_reductions=False)
+        t.opt.zero_grad(set_to_none=True)
+        with OF.deferred_param_reductions(defer):
+            loss = t._loss(x, y)
+            loss.backward()
+            pending.append(load().ogv_reduce_defer(1 if defer else 0))
+        torch.cuda.synchronize()
+        grads.append([p.grad.detach().clone() for p in m.parameters()])
+    assert pending[0] == 0 and pending[1] >= 50, pending
+    same = 0
+    for a, b in zip(*grads):
+        assert torch.isfinite(b).all()
+        torch.testing.assert_close(b, a, rtol=1e-5, atol=1e-7)
+        same += bool(torch.equal(a, b))
+    assert same >= len(grads[0]) // 2, (same, len(grads[0]))

@@ -28,6 +28,9 @@ namespace ogv {
 constexpr int PG_NW = 4;           // waves per workgroup
 constexpr int PG_KB = 64;          // reduction columns per k-step (two 32-wide MFMA sub-steps)
 constexpr int PG_KP = PG_KB;       // [n][k] slab pitch (elements): 128-B rows, 16-B chunks rotated by the row
+// data gradients (BT) with their slab columns permuted like the forward's rows (16-B epilogue
+// accesses of dX, Z and the residual) instead of 8-B ones
+constexpr bool PG_BT16 = true;
 // (chunk c of row r stored at (c + r) & 7): conflict-free 16-B fragment reads and 8-B staging writes
 
 template <int TN, bool BT>
@@ -134,8 +137,12 @@ __global__ __launch_bounds__(PG_NW * 64, 2) void pgemm_bf16_kernel(const bf16* _
         const int r = pg_col_slot(idx / (PG_KB / 4)), kq = idx % (PG_KB / 4);
         off = r * PG_KP + (((kq >> 1) + r) & 7) * 8 + (kq & 1) * 4;
       } else {
+        // column c of the [k][n] slab stored at pg_col_slot(c) (groups of 4 stay contiguous): the
+        // transposed reads then hand a lane's fragment pair 8 consecutive output columns, as in the
+        // forward (16-B epilogue accesses)
         const int kr = idx / (BN / 4);
-        off = ((kr & ~31) | pg_perm(kr & 31)) * BP + (idx % (BN / 4)) * 4;
+        const int c = (idx % (BN / 4)) * 4;
+        off = ((kr & ~31) | pg_perm(kr & 31)) * BP + (PG_BT16 ? pg_col_slot(c) : c);
       }
       const bf16x4 h = {(bf16)wr[i].x, (bf16)wr[i].y, (bf16)wr[i].z, (bf16)wr[i].w};
       *reinterpret_cast<bf16x4*>(hi + off) = h;
@@ -304,32 +311,44 @@ __global__ __launch_bounds__(PG_NW * 64, 2) void pgemm_bf16_kernel(const bf16* _
   auto epilogue = [&](int j) {
     const int mt = tile_mt(j), n0 = tile_nt(j) * BN, mw = mt * BM + wave * 16 * RS;
     const float* cv = cvec + (j & 1) * 2 * BN;
-    if constexpr (!BT) {
+    if constexpr (!BT || PG_BT16) {
       // lane: row m, columns 32 q + 8 fg .. + 7 of every fragment pair q (pg_col_slot)
 #pragma unroll
       for (int i = 0; i < RS; ++i) {
         const int m = mw + i * 16 + fr;
         const bool mok = m < M;
         const float rsc = (epi.rs && mok) ? epi.rs[m / epi.rps] : 1.f;
-        uint4 rv[TN / 2];
+        constexpr int QC = (ZA != 0 && TN > 8) ? TN / 4 : TN / 2;   // fragment pairs per residual / Z round trip
 #pragma unroll
-        for (int q = 0; q < TN / 2; ++q) {   // residual of the row first: one round trip
-          const int n = n0 + 32 * q + 8 * fg;
-          rv[q] = uint4{0u, 0u, 0u, 0u};
-          if (res && mok && n < N) rv[q] = *reinterpret_cast<const uint4*>(res + (long)m * ldo + n);
+        for (int q0 = 0; q0 < TN / 2; q0 += QC) {
+        uint4 rv[QC], zv[QC];
+#pragma unroll
+        for (int u = 0; u < QC; ++u) {   // residual / Z of the chunk first: one round trip
+          const int n = n0 + 32 * (q0 + u) + 8 * fg;
+          rv[u] = zv[u] = uint4{0u, 0u, 0u, 0u};
+          if (res && mok && n < N) rv[u] = *reinterpret_cast<const uint4*>(res + (long)m * ldo + n);
+          if constexpr (ZA != 0) {
+            if (mok && n < N) zv[u] = *reinterpret_cast<const uint4*>(Z + (long)m * epi.ldz + n);
+          }
         }
 #pragma unroll
-        for (int q = 0; q < TN / 2; ++q) {
+        for (int u = 0; u < QC; ++u) {
+          const int q = q0 + u;
           const int c = 32 * q + 8 * fg, n = n0 + c;
           const bool ok = mok && n < N;
           const float4 b0 = *reinterpret_cast<const float4*>(cv + c);
           const float4 b1 = *reinterpret_cast<const float4*>(cv + c + 4);
           const float bias[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-          const bf16* rb = reinterpret_cast<const bf16*>(&rv[q]);
+          const bf16* rb = reinterpret_cast<const bf16*>(&rv[u]);
+          const bf16* zb = reinterpret_cast<const bf16*>(&zv[u]);
           uint4 ov;
           bf16* ob = reinterpret_cast<bf16*>(&ov);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) ob[e] = (bf16)((acc[i][2 * q + (e >> 2)][e & 3] + bias[e]) * rsc + (float)rb[e]);
+          for (int e = 0; e < 8; ++e) {
+            float x = (acc[i][2 * q + (e >> 2)][e & 3] + bias[e]) * rsc + (float)rb[e];
+            if constexpr (ZA != 0) x *= act_grad(ZA, (float)zb[e]);
+            ob[e] = (bf16)x;
+          }
           if (ok && !(dbg & 4)) *reinterpret_cast<uint4*>(out + orow(m) * ldo + n) = ov;
           if (epi.aout && ok) {
             uint4 av;
@@ -375,6 +394,7 @@ __global__ __launch_bounds__(PG_NW * 64, 2) void pgemm_bf16_kernel(const bf16* _
             }
           }
         }
+        }   // q0
       }
     } else {
 #pragma unroll

@@ -201,6 +201,7 @@ class _probe:
             self.e1 = torch.cuda.Event(enable_timing=True)
             self.nbytes = probe_bytes(name, units)
             self.nflops = probe_flops(name, units)
+            self.units = units
 
     def __enter__(self):
         if self.on:
@@ -211,7 +212,7 @@ class _probe:
     def __exit__(self, *a):
         if self.on:
             self.e1.record()
-            _PROBE["recs"].append((self.e0, self.e1, self.nbytes, self.nflops))
+            _PROBE["recs"].append((self.e0, self.e1, self.nbytes, self.nflops, self.units))
         return False
 
 
@@ -239,7 +240,14 @@ def probe_results():
         return None
     torch.cuda.synchronize()
     ovh = _empty_pair_ms()
-    ms = [max(a.elapsed_time(b) - ovh, 1e-6) for a, b, _, _ in recs]
+    ms = [max(a.elapsed_time(b) - ovh, 1e-6) for a, b, _, _, _ in recs]
+    dump = os.environ.get("OGV_PROBE_DUMP")
+    if dump:   # per-launch table: shape, algorithmic bytes, time, GB/s
+        with open(dump, "a") as f:
+            for (a, b, nb, nf, u), t in zip(recs, ms):
+                f.write(f"{_PROBE['target']} {u.get('kind', 'fwd')} M={u.get('M')} N={u.get('N')} K={u.get('K')} "
+                        f"z={int(bool(u.get('z')))} res={int(bool(u.get('res')))} bytes={nb} us={1e3 * t:.2f} "
+                        f"GBs={nb / (t * 1e-3) / 1e9:.0f}\n")
     nbytes = sum(r[2] for r in recs)
     nflops = sum(r[3] for r in recs)
     tot = sum(ms)

@@ -99,7 +99,8 @@ PROBE_KERNEL = {  # probe name -> kernel symbol(s) it times (rocprofv3 names)
                   "of the step)",
     "gemm_tiled": "ogv::gemm_bf16_kernel<*> (LDS-tiled MFMA GEMM: Linear / 1x1-conv launches routed to "
                   "neither the streaming nor the panel kernel, and the implicit-GEMM convs)",
-    "wgrad": "ogv::wgrad_bf16_kernel<*> / ogv::swgrad_bf16_kernel<*> + colreduce (Linear / 1x1-conv weight gradients)",
+    "wgrad": "ogv::wgrad2_bf16_kernel<*> (pipelined split-M; also wgrad_bf16 / swgrad_bf16 where planned) + its slab "
+             "reduction (Linear / 1x1-conv weight gradients)",
     "outlook_bwd": "ogv::outlook_bwd_tile_kernel<*> (LDS-tiled outlook backward: the col2im fold as a gather + dlogits)",
     "sgemm": "ogv::sgemm_bf16_kernel<*> (persistent streaming projection GEMM: the Linear / 1x1-conv fwd and dgrad "
              "launches routed to it)",
@@ -346,7 +347,8 @@ def main():
                              "unit": "TFLOP/s", "frac": round(probe["achieved_TFLOPs"] / MFMA_PEAK_TFLOPS, 4),
                              "algorithmic_flops_per_launch": int(probe["flops_per_launch"])},
                     "timing": ("HIP events around each launch (a 40 us device spin queued ahead of each, so no host "
-                               "launch gap is timed; minus the empty event-pair interval), " + ("eager step after the timed graph replays"
+                               "launch gap is timed; minus what an event pair adds around a kernel, calibrated on a "
+                               "20 us wall-clock spin), " + ("eager step after the timed graph replays"
                                                            if trainer.graphs else "all timed steps"))}
         if roof is not None and census is not None:
             # clip_grad_norm (norm pass reads g; scale pass reads + writes g) and the fused AdamW (reads p,

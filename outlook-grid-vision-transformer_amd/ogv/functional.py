@@ -217,19 +217,25 @@ class _probe:
 
 
 def _empty_pair_ms(reps: int = 16) -> float:
-    """Median interval of an event pair with nothing between them (same spin in front): the
-    event-recording overhead, subtracted from every probed interval."""
+    """The event-recording overhead subtracted from every probed interval: the median interval of an
+    event pair around a device spin of KNOWN length (ogv_gpu_sleep: a wall-clock loop of 20 us, the
+    same 40 us spin in front) minus that length -- i.e. what a pair adds around a kernel.  (An EMPTY
+    pair's interval, the round-2 calibration, over-counts it: measured 5.0-5.4 us vs 2.5-3 us around a
+    kernel, so the probe read ~10% under rocprofv3's kernel durations,
+    profiles/r03_head_probe_vs_trace.txt.)"""
     lib = _lib.load()
     pairs = []
+    spin_us = 20
     for _ in range(reps):
         check(lib.ogv_gpu_sleep(40, _stream()), "ogv_gpu_sleep")
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
+        check(lib.ogv_gpu_sleep(spin_us, _stream()), "ogv_gpu_sleep")
         b.record()
         pairs.append((a, b))
     torch.cuda.synchronize()
     ms = sorted(a.elapsed_time(b) for a, b in pairs)
-    return ms[len(ms) // 2]
+    return max(ms[len(ms) // 2] - spin_us * 1e-3, 0.0)
 
 
 def probe_results():

@@ -187,7 +187,9 @@ size_t swgrad_ws_floats(int M, int N, int K);
 // Pipelined split-M weight gradient (ogv_wgrad2.hip), same partial layout; knob "wg2": 0 off,
 // 1 = where the streaming kernel does not apply, 2 = ahead of it as well.
 int wgrad2_try(const void* G, int ldg, const void* X, int ldx, const Pro& pro, const float* rs, int rps, float* part,
-               float* dW, float* dbias, bool bias, int M, int N, int K, hipStream_t s, bool* reduced);
+               float* dW, float* dbias, bool bias, int M, int N, int K, hipStream_t s, bool* reduced,
+               const ConvG* xc = nullptr);
+void set_wg2_conv(int v);
 void set_wg2_fuse(int v);
 size_t wgrad2_ws_floats(int M, int N, int K);
 int wg2_mode();

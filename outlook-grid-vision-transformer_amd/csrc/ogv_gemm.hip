@@ -1441,6 +1441,14 @@ void gemm_wgrad_launch(ogv_dtype dt, const void* G, int ldg, const void* X, int 
             xc != nullptr, dbias != nullptr);
   const long ldp = (long)N * K + N;
   float* part = (float*)ws;
+  if (dt == OGV_BF16 && xc) {   // 3x3 conv weight gradient: pipelined kernel with the gather (8 | C_in)
+    bool reduced = false;
+    const int S = wgrad2_try(G, ldg, X, ldx, pro, rs, rps, part, dW, dbias, dbias != nullptr, M, N, K, s, &reduced, xc);
+    if (S > 0) {
+      reduce(part, dW, S, dbias ? ldp : (long)N * K, ldp, part + (size_t)S * ldp, s, dbias, (long)N * K);
+      return;
+    }
+  }
   if (dt == OGV_BF16 && !xc) {
     const bool b = dbias != nullptr;
     bool reduced = false;

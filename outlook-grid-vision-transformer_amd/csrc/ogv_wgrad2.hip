@@ -36,13 +36,16 @@ constexpr int W2_CNT = 1 << 16;
 __device__ unsigned g_w2_cnt[W2_CNT];
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-template <int BN, int BK, int PA>
+// CV: X is the implicit-GEMM gather of a 3x3 convolution's input (ConvG cv; row m = output pixel,
+// column k = tap * Cs + channel, 8 | Cs so an 8-column chunk never straddles a tap; zero padding)
+template <int BN, int BK, int PA, bool CV = false>
 __global__ __launch_bounds__(W2_NT) void wgrad2_bf16_kernel(const bf16* __restrict__ G, int ldg,
                                                             const bf16* __restrict__ X, int ldx, Pro pro,
                                                             const float* __restrict__ rs, int rps,
                                                             float* __restrict__ part, long ldp, int want_bias, int M,
                                                             int N, int K, int mchunk, int nNt, int tiles, int S,
-                                                            int cnt0, float* __restrict__ dW, float* __restrict__ dbias) {
+                                                            int cnt0, float* __restrict__ dW, float* __restrict__ dbias,
+                                                            ConvG cv) {
   constexpr int MS = W2_MS;
   constexpr int GP = BN + 16, XP = BK + 16;      // odd multiples of 16 for BN in {64, 96, 128, 192}, BK in {64, 128}
   constexpr int GC = BN / 8, XC = BK / 8;        // 16-B chunks per staged row
@@ -115,7 +118,13 @@ __global__ __launch_bounds__(W2_NT) void wgrad2_bf16_kernel(const bf16* __restri
 #pragma unroll
     for (int v = 0; v < XV; ++v) {
       const int m = min(m0 + xrow0 + v * XRP, mend - 1);
-      R.x[v] = *reinterpret_cast<const uint4*>(X + (long)m * ldx + xk);
+      if constexpr (CV) {
+        const int tap = xk / cv.Cs;
+        const long off = conv_src(cv, conv_row(cv, m), tap);
+        R.x[v] = off >= 0 ? *reinterpret_cast<const uint4*>(X + off + (xk - tap * cv.Cs)) : uint4{0u, 0u, 0u, 0u};
+      } else {
+        R.x[v] = *reinterpret_cast<const uint4*>(X + (long)m * ldx + xk);
+      }
       if constexpr (SG) load_vec<float, 8>(pro.gate + (long)(m / pro.rps) * pro.gld + xk, R.gt[v]);
     }
   };
@@ -341,6 +350,8 @@ __global__ __launch_bounds__(W2_NT) void wgrad2_bf16_kernel(const bf16* __restri
 static int g_wg2 = 2;          // knob "wg2": 0 off, 1 = this kernel below the streaming-wgrad M, 2 = at every M (default: measured faster than both other kernels at every 7M shape but one, which ties)
 static int g_wg2_blocks = 1024;  // knob "wg2_blocks": workgroups the split-M plan aims for
 static int g_wg2_tile = 0;     // knob "wg2_tile": force the N edge (64 / 96 / 128 / 192; K edge 64 / 128)
+static int g_wg2_conv = 1;     // knob "wg2_conv": 3x3 conv weight gradients (8 | C_in) on this kernel (0: tiled kernel)
+void set_wg2_conv(int v) { g_wg2_conv = v ? 1 : 0; }
 // knob "wg2_fuse": 1 = last-workgroup reduction in the kernel, 0 = the caller's colreduce (default).
 // Measured and rejected as the default (tools/bench_wgrad.py, profiles/r03_wgrad_fuse.log, 7M step
 // shapes): the split-M plan aims at ~1024 workgroups, so a tile has S = 29-1024 slabs and its last
@@ -423,13 +434,13 @@ struct W2Out {
   float *dW, *dbias;
 };
 
-template <int BN, int BK, int PA>
+template <int BN, int BK, int PA, bool CV = false>
 static void w2_launch(const W2Plan& p, const bf16* G, int ldg, const bf16* X, int ldx, const Pro& pro, const float* rs,
-                      int rps, const W2Out& o, bool bias, int M, int N, int K, hipStream_t s) {
+                      int rps, const W2Out& o, bool bias, int M, int N, int K, hipStream_t s, const ConvG& cv = ConvG()) {
   const int tiles = p.nNt * p.nKt;
   const unsigned grid = (unsigned)(((p.S + 7) / 8) * 8 * tiles);
-  wgrad2_bf16_kernel<BN, BK, PA><<<grid, W2_NT, 0, s>>>(G, ldg, X, ldx, pro, rs, rps, o.part, o.ldp, bias ? 1 : 0, M, N,
-                                                        K, p.mchunk, p.nNt, tiles, p.S, o.cnt0, o.dW, o.dbias);
+  wgrad2_bf16_kernel<BN, BK, PA, CV><<<grid, W2_NT, 0, s>>>(G, ldg, X, ldx, pro, rs, rps, o.part, o.ldp, bias ? 1 : 0, M,
+                                                            N, K, p.mchunk, p.nNt, tiles, p.S, o.cnt0, o.dW, o.dbias, cv);
 }
 
 template <int PA>
@@ -445,10 +456,22 @@ static void w2_dispatch(const W2Plan& p, const bf16* G, int ldg, const bf16* X, 
 
 // Returns the number of partial rows written into part (layout [S][N*K + N]), 0 if not handled.
 // *reduced = true when the kernel also wrote dW (and dbias, when bias) itself: no colreduce needed.
+// xc: X is a 3x3 convolution's gathered input (forward convs with 8 | Cs; 64 x 64 tiles, no prologue).
 int wgrad2_try(const void* G, int ldg, const void* X, int ldx, const Pro& pro, const float* rs, int rps, float* part,
-               float* dW, float* dbias, bool bias, int M, int N, int K, hipStream_t s, bool* reduced) {
+               float* dW, float* dbias, bool bias, int M, int N, int K, hipStream_t s, bool* reduced, const ConvG* xc) {
   *reduced = false;
   if (!g_wg2) return 0;
+  if (xc) {
+    if (!g_wg2_conv || xc->transposed || xc->par >= 0 || (xc->Cs & 7) || pro.any() || rs || (ldg & 7) ||
+        (reinterpret_cast<uintptr_t>(G) & 15) || (reinterpret_cast<uintptr_t>(X) & 15) || (N & 7) || (K & 7))
+      return 0;
+    W2Plan p = wgrad2_plan(M, N, K, false);
+    if (!p.ok || p.BN != 64 || p.BK != 64) return 0;
+    const W2Out o{part, (long)N * K + N, -1, dW, dbias};
+    w2_launch<64, 64, -1, true>(p, static_cast<const bf16*>(G), ldg, static_cast<const bf16*>(X), 0, pro, nullptr, 1, o,
+                                bias, M, N, K, s, *xc);
+    return p.S;
+  }
   if ((ldg & 7) || (ldx & 7) || (reinterpret_cast<uintptr_t>(G) & 15) || (reinterpret_cast<uintptr_t>(X) & 15))
     return 0;
   W2Plan p = wgrad2_plan(M, N, K, pro.any());

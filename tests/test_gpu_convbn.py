@@ -54,7 +54,10 @@ ACTS = {"silu": nn.SiLU(), "gelu": nn.GELU(), "relu": nn.ReLU(), None: nn.Identi
     (2, 5, 12, 6, 6, 2, True, True, None),           # Cin % 8 != 0 on the strided path
     (3, 16, 24, 10, 6, 2, True, True, "gelu"),       # dgrad as 4 parity-class GEMMs, non-square
 ])
-def test_conv_bn_act(case, dtype):
+@pytest.mark.parametrize("wcl", [False, True], ids=["w_oihw", "w_channels_last"])
+def test_conv_bn_act(case, dtype, wcl):
+    """wcl: the conv weight in channels_last memory (as after model.to(channels_last)) -- the tap-major
+    matrix the kernels use directly (w_layout 1: no transposes, the gradient written in place)."""
     from ogv import functional as OF
     B, Cin, Cout, H, W, stride, use_bn, train, act = case
     conv, bn = _modules(Cin, Cout, stride, use_bn, act, seed=Cin * 7 + Cout)
@@ -73,6 +76,9 @@ def test_conv_bn_act(case, dtype):
     yr.backward(gy.double())
     # ogv
     dconv = copy.deepcopy(conv).cuda()
+    if wcl:
+        dconv = dconv.to(memory_format=torch.channels_last)
+        assert not dconv.weight.is_contiguous() or Cin == 1
     dbn = copy.deepcopy(bn).cuda() if bn is not None else None
     if dbn is not None:
         dbn.train(train)

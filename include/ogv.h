@@ -69,7 +69,8 @@ int ogv_set_option(const char* name, int value);
 int ogv_gemm_stream_route(int kind, int M, int N, int K, ogv_act act_in);
 /* Deferred parameter-gradient reductions (no reference counterpart; a training-step scheduling
  * aid).  While ogv_reduce_defer(1) is in force, the final column reductions that turn slab partials
- * into PARAMETER gradients -- ogv_gemm_wgrad's dW / dbias and ogv_layernorm_bwd's dgamma / dbeta --
+ * into PARAMETER gradients -- ogv_gemm_wgrad's dW / dbias, ogv_layernorm_bwd's dgamma / dbeta and the
+ * expand / project / SE weight gradients of ogv_mbconv_bwd --
  * are recorded instead of launched (their workspaces must stay allocated, and the gradients unread,
  * until the flush); ogv_reduce_flush(stream) runs every recorded reduction as one batched launch
  * (48 per launch) on `stream`, which must be ordered after all the producing launches.  Returns: defer
@@ -210,7 +211,10 @@ int ogv_dwconv3x3_bwd(const void* dy, const void* x, const float* w, void* dx, f
  *   e = x.We^T -> a1 = act(BN1(e)) -> d = dw3x3(a1) -> a2 = act(BN2(d)) -> g = SE(a2)
  *   -> p = (a2*g).Wp^T -> out = x + BN3(p)
  * x/out: [B*H*W, C] rows.  `saved` (>= ogv_mbconv_saved_bytes) is written by fwd and read by
- * bwd; `ws` (>= ogv_mbconv_ws_bytes) is scratch for either.  bwd writes dx (= the residual
+ * bwd; `ws` (>= ogv_mbconv_ws_bytes) is scratch for either; bwd also takes `param_ws`
+ * (>= ogv_mbconv_param_ws_bytes): the slab partials of its four weight gradients (expand, project,
+ * SE fc1 / fc2), whose column reductions are deferred under ogv_reduce_defer -- keep it allocated
+ * until ogv_reduce_flush.  bwd writes dx (= the residual
  * gradient + the branch gradient) and every parameter gradient (fp32, overwritten).
  * num_batches_tracked is left to the caller.
  * ------------------------------------------------------------------------------------------- */
@@ -239,11 +243,12 @@ typedef struct {
 
 size_t ogv_mbconv_saved_bytes(const ogv_mbconv_desc* desc, ogv_dtype dt);
 size_t ogv_mbconv_ws_bytes(const ogv_mbconv_desc* desc, ogv_dtype dt);
+size_t ogv_mbconv_param_ws_bytes(const ogv_mbconv_desc* desc);
 int ogv_mbconv_fwd(const void* x, void* out, void* saved, void* ws, const ogv_mbconv_desc* desc,
                    const ogv_mbconv_params* params, ogv_dtype dt, void* stream);
 int ogv_mbconv_bwd(const void* dout, const void* x, const void* saved, void* dx, const ogv_mbconv_grads* grads,
-                   void* ws, const ogv_mbconv_desc* desc, const ogv_mbconv_params* params, ogv_dtype dt,
-                   void* stream);
+                   void* ws, void* param_ws, const ogv_mbconv_desc* desc, const ogv_mbconv_params* params,
+                   ogv_dtype dt, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * MaxOutNet around the blocks: 3x3 convolution (padding 1, stride 1|2) -> BatchNorm2d -> act on

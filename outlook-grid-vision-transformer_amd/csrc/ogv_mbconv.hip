@@ -1113,6 +1113,9 @@ struct BwdWs {
   float *wtse, *split;  // transposed SE weight, split-K partials
   float* tmp2;          // colreduce scratch of the side stream
   char *gemm, *gemm2;   // GEMM workspaces: current stream, side stream
+  // slab partials of the four parameter weight gradients, one region each: their column reductions
+  // may be deferred to the end of the backward (colreduce_param), so no later phase may reuse them
+  char *wg_proj, *wg_expand, *wg_se2, *wg_se1;
 };
 static size_t max3(size_t a, size_t b, size_t c) { return a > b ? (a > c ? a : c) : (b > c ? b : c); }
 static BwdWs bwd_ws_layout(void* base, const ogv_mbconv_desc& s, size_t esz, size_t* total) {
@@ -1149,8 +1152,26 @@ static BwdWs bwd_ws_layout(void* base, const ogv_mbconv_desc& s, size_t esz, siz
   w.gemm = b.take<char>(g);
   w.tmp2 = b.take<float>(colreduce_tmp_floats(S2, 9L * s.mid) + 16);
   w.gemm2 = b.take<char>(g);
+  w.wg_proj = w.wg_expand = w.wg_se2 = w.wg_se1 = nullptr;   // bwd_param_ws_layout
   if (total) *total = b.off + 256;
   return w;
+}
+// the four parameter weight gradients' slab partials, one region each (a separate buffer: it stays
+// allocated until a deferred reduction has read it, the big workspace above need not)
+static void bwd_param_ws_layout(void* base, const ogv_mbconv_desc& s, BwdWs* w, size_t* total) {
+  Buf b(base);
+  const long M = (long)s.B * s.H * s.W;
+  char* p0 = b.take<char>(wgrad_ws_bytes((int)M, s.C, s.mid));
+  char* p1 = b.take<char>(wgrad_ws_bytes((int)M, s.mid, s.C));
+  char* p2 = b.take<char>(wgrad_ws_bytes(s.B, s.mid, s.se));
+  char* p3 = b.take<char>(wgrad_ws_bytes(s.B, s.se, s.mid));
+  if (w) {
+    w->wg_proj = p0;
+    w->wg_expand = p1;
+    w->wg_se2 = p2;
+    w->wg_se1 = p3;
+  }
+  if (total) *total = b.off + 256;
 }
 
 // Side stream for the weight-gradient work of the fused backward (independent of the data-gradient
@@ -1442,7 +1463,8 @@ static void mbconv_bwd_impl(const void* dout, const void* x, const Saved& sv, vo
     pr.gate = sv.gate;
     pr.rps = HW;
     pr.gld = s.mid;
-    gemm_wgrad_launch(dt, w.dp, s.C, sv.d, s.mid, pr, nullptr, 1, G.w_proj, nullptr, (int)M, s.C, s.mid, w.gemm2, sd);
+    gemm_wgrad_launch(dt, w.dp, s.C, sv.d, s.mid, pr, nullptr, 1, G.w_proj, nullptr, (int)M, s.C, s.mid, w.wg_proj, sd,
+                      nullptr, true);
   }
   // B3) one pass over (dA3, d): SE gate grads + BN2 partial sums per image
   // (+ dz2 = dgate * g * (1 - g), the gate's sigmoid backward, written by the same reduce)
@@ -1454,8 +1476,8 @@ static void mbconv_bwd_impl(const void* dout, const void* x, const Saved& sv, vo
   {
     Pro p2;
     p2.act = s.act;
-    gemm_wgrad_launch(OGV_F32, w.dz2, s.mid, sv.z1, s.se, p2, nullptr, 1, G.se_w2, G.se_b2, s.B, s.mid, s.se, w.gemm,
-                      fork_side(st));
+    gemm_wgrad_launch(OGV_F32, w.dz2, s.mid, sv.z1, s.se, p2, nullptr, 1, G.se_w2, G.se_b2, s.B, s.mid, s.se, w.wg_se2,
+                      fork_side(st), nullptr, true);
     {  // dz1 = act'(z1) * (dz2 . W2):  W2 [mid, se] read reduction-major (no transpose launch)
       Epi e;
       e.Z = sv.z1;
@@ -1468,7 +1490,7 @@ static void mbconv_bwd_impl(const void* dout, const void* x, const Saved& sv, vo
         gemm_fwd_splitk_f32(w.dz2, s.mid, Pro(), P.se_w2, s.se, w.dz1, s.se, s.B, s.se, s.mid, e, w.split, st, true);
     }
     gemm_wgrad_launch(OGV_F32, w.dz1, s.se, sv.pooled, s.mid, Pro(), nullptr, 1, G.se_w1, G.se_b1, s.B, s.se, s.mid,
-                      w.gemm, fork_side(st));
+                      w.wg_se1, fork_side(st), nullptr, true);
     {  // dpool = dz1 . W1:  W1 [se, mid] read reduction-major
       if (se_gemv_on())
         se_gemv_launch(w.dz1, s.se, OGV_ACT_NONE, P.se_w1, s.mid, nullptr, nullptr, 0, 0, w.dpool, s.mid, nullptr, s.B,
@@ -1514,7 +1536,8 @@ static void mbconv_bwd_impl(const void* dout, const void* x, const Saved& sv, vo
   OGV_V_DISPATCH(rp.V, O::template bn_apply, w.bufA, sv.e, sv.mean1, sv.inv1, w.coef, w.bufB, M, s.mid, st);
   // B8) expand: dx = de . We + dout (residual) ; dWe = de^T . x
   sd = fork_side(st);  // dWe on the side stream, overlapping dx
-  gemm_wgrad_launch(dt, w.bufB, s.mid, x, s.C, Pro(), nullptr, 1, G.w_expand, nullptr, (int)M, s.mid, s.C, w.gemm2, sd);
+  gemm_wgrad_launch(dt, w.bufB, s.mid, x, s.C, Pro(), nullptr, 1, G.w_expand, nullptr, (int)M, s.mid, s.C, w.wg_expand,
+                    sd, nullptr, true);
   gemm_dgrad_launch(dt, w.bufB, s.mid, P.w_expand, nullptr, 0, 0, nullptr, 1, dout, dx, s.C, (int)M, s.mid, s.C,
                     w.gemm, st);
   join_side(st, sd);
@@ -1565,17 +1588,25 @@ extern "C" int ogv_mbconv_fwd(const void* x, void* out, void* saved, void* ws, c
   return check_launch("ogv_mbconv_fwd");
 }
 
+extern "C" size_t ogv_mbconv_param_ws_bytes(const ogv_mbconv_desc* s) {
+  if (!s) return 0;
+  size_t t = 0;
+  bwd_param_ws_layout(nullptr, *s, nullptr, &t);
+  return t;
+}
+
 extern "C" int ogv_mbconv_bwd(const void* dout, const void* x, const void* saved, void* dx,
-                              const ogv_mbconv_grads* G, void* ws, const ogv_mbconv_desc* s,
+                              const ogv_mbconv_grads* G, void* ws, void* param_ws, const ogv_mbconv_desc* s,
                               const ogv_mbconv_params* P, ogv_dtype dt, void* stream) {
   int rc = mb_check(s, dt, "ogv_mbconv_bwd");
   if (rc) return rc;
-  OGV_REQUIRE(dout && x && saved && dx && G && ws && P, "ogv_mbconv_bwd: null pointer");
+  OGV_REQUIRE(dout && x && saved && dx && G && ws && param_ws && P, "ogv_mbconv_bwd: null pointer");
   OGV_REQUIRE(G->w_expand && G->bn1_w && G->bn1_b && G->w_dw && G->bn2_w && G->bn2_b && G->se_w1 && G->se_b1 &&
                   G->se_w2 && G->se_b2 && G->w_proj && G->bn3_w && G->bn3_b,
               "ogv_mbconv_bwd: every gradient output must be given");
   Saved sv = saved_layout(const_cast<void*>(saved), *s, dt == OGV_BF16 ? 2 : 4, nullptr);
   BwdWs w = bwd_ws_layout(ws, *s, dt == OGV_BF16 ? 2 : 4, nullptr);
+  bwd_param_ws_layout(param_ws, *s, &w, nullptr);
   if (dt == OGV_BF16) mbconv_bwd_impl<bf16>(dout, x, sv, dx, *G, w, *s, *P, dt, as_stream(stream));
   else mbconv_bwd_impl<float>(dout, x, sv, dx, *G, w, *s, *P, dt, as_stream(stream));
   return check_launch("ogv_mbconv_bwd");

@@ -87,7 +87,8 @@ SIGNATURES = {
     "ogv_mbconv_saved_bytes": (_sz, [_PD, _i]),
     "ogv_mbconv_ws_bytes": (_sz, [_PD, _i]),
     "ogv_mbconv_fwd": (_i, [_p, _p, _p, _p, _PD, _PP, _i, _p]),
-    "ogv_mbconv_bwd": (_i, [_p, _p, _p, _p, _PG, _p, _PD, _PP, _i, _p]),
+    "ogv_mbconv_param_ws_bytes": (_sz, [_PD]),
+    "ogv_mbconv_bwd": (_i, [_p, _p, _p, _p, _PG, _p, _p, _PD, _PP, _i, _p]),
     "ogv_convbn_saved_bytes": (_sz, [_PCD, _i]),
     "ogv_convbn_ws_bytes": (_sz, [_PCD, _i]),
     "ogv_convbn_fwd": (_i, [_p, _p, _p, _p, _PCD, _PCP, _i, _p]),

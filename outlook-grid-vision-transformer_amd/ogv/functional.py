@@ -100,9 +100,9 @@ _DEFER = {"on": False, "keep": []}
 
 class deferred_param_reductions:
     """Within this context the column reductions that produce parameter gradients (Linear weight /
-    bias gradients through ogv_gemm_wgrad, LayerNorm gamma / beta) are recorded, not launched; on exit
-    they run as one batched launch on the current stream (ogv_reduce_flush) -- ~80 fewer launches per
-    Model-A-7M step.  Only for a backward whose parameter gradients nothing reads before the exit:
+    bias gradients through ogv_gemm_wgrad, LayerNorm gamma / beta, the fused MBConv's expand / project /
+    SE weight gradients) are recorded, not launched; on exit they run as batched launches on the
+    current stream (ogv_reduce_flush) -- ~110 fewer launches per Model-A-7M step.  Only for a backward whose parameter gradients nothing reads before the exit:
     every .grad None at entry (set_to_none) and no parameter used twice in the graph (autograd would
     add its two partial gradients before they exist), and no gradient hooks that read them (DP bucket
     hooks).  Every side stream the backward forked must be joined into the current one (ogv's forks
@@ -1008,9 +1008,10 @@ class _MBConv(torch.autograd.Function):
         dout = dout.to(x2d.dtype).contiguous()
         dx = torch.empty_like(x2d)
         ws = _ws(lib.ogv_mbconv_ws_bytes(ctypes.byref(desc), dt), x2d.device)
+        pws = _ws(lib.ogv_mbconv_param_ws_bytes(ctypes.byref(desc)), x2d.device, deferrable=True)
         with _census("mbconv_bwd", _mb_units(ctx.geom, x2d)):
             check(lib.ogv_mbconv_bwd(_ptr(dout), _ptr(x2d), _ptr(saved), _ptr(dx), ctypes.byref(G), _ptr(ws),
-                                     ctypes.byref(desc), ctypes.byref(P), dt, _stream()), "ogv_mbconv_bwd")
+                                     _ptr(pws), ctypes.byref(desc), ctypes.byref(P), dt, _stream()), "ogv_mbconv_bwd")
         return (dx, None, None, *grads)
 
 

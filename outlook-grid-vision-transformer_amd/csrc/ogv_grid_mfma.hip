@@ -988,12 +988,312 @@ __global__ __launch_bounds__(GB_NW * 64) void grid_big_dkv_kernel(const bf16* __
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Large groups, second generation (knob grid_big = 2, the default).  The kernels above spend most
+// of their time on the VALU, not the MFMA: per score they pay a scale multiply, a mask select, the
+// max, a subtract, the log2(e) multiply inside __expf and a cross-lane row sum, and the probability
+// products run on the 16x16x16 MFMA (half the 16x16x32 rate on gfx950).  Here:
+//   * exp(s * scale - m) = exp2(s * scale*log2(e) - m2): one FMA + v_exp_f32 per score, the max is
+//     taken on the raw scores (scale > 0) and scaled once per row;
+//   * masks only on the ragged last step (N % 64 / % 32 / % 16 keys);
+//   * lazy rescale: the running max m2 only moves (O and the row sum rescaled, 4 cross-lane reads)
+//     when some row's chunk max exceeds it by more than 2^8, decided wave-uniformly; between
+//     rescales P <= 2^8, exact in fp32 and bf16 (same 8-bit exponent);
+//   * the row sum is kept per lane (its 4 keys of each chunk) and reduced over the 4 lane groups
+//     once at the end;
+//   * two 16-key chunks are paired into one 16x16x32 MFMA for P V, dS K, P^T dO and dS^T Q: the
+//     A operand is [pack4(chunk c) | pack4(chunk c+1)], the B operand the two transposed LDS reads
+//     of the same key rows, so k index i < 4 <-> key 16c + 4fg + i and i >= 4 <-> 16(c+1) + 4fg + i-4
+//     on both sides.
+constexpr float GB_LOG2E = 1.4426950408889634f, GB_LN2 = 0.6931471805599453f;
+constexpr float GB_RESCALE = 8.f;  // log2 units
+
+__device__ __forceinline__ float gb_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+__device__ __forceinline__ bf16x8 gb_cat8(gm_s16x4 a, gm_s16x4 b) {
+  typedef __attribute__((ext_vector_type(8))) short s16x8;
+  const s16x8 t = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, t);
+}
+
+// transposed 16x16x16-B-operand read of key rows row0 + 4fg + (fr >> 2), dims j*16 + (fr & 3)*4
+__device__ __forceinline__ gm_s16x4 gb_tr(const bf16* tile, int row0, int pitch, int j, int lane) {
+  const int fr = lane & 15, fg = lane >> 4;
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (gm_lds_s16x4*)(tile + (row0 + 4 * fg + (fr >> 2)) * pitch + j * 16 + (fr & 3) * 4));
+}
+
+template <int HDP>
+__global__ __launch_bounds__(GB_NW * 64) void grid_big_fwd2_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
+                                                                  float* __restrict__ lse, GridGeomM G, float scale,
+                                                                  int Np) {
+  constexpr int KK = HDP / 32, ND = HDP / 16, PITCH = gm_pitch<HDP>();
+  extern __shared__ __attribute__((aligned(16))) bf16 gsm[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const long C3 = 3L * G.C;
+  const long pr = blockIdx.x;
+  const int h = (int)(pr % G.heads);
+  const long grp = pr / G.heads;
+  const bf16* Ks = gsm;
+  const bf16* Vs = gsm + (size_t)Np * PITCH;
+  gb_stage2<HDP>(gsm, qkv + G.C + h * G.hd, C3, qkv + 2 * G.C + h * G.hd, C3, G, grp, Np);
+  __syncthreads();
+  const float sl2 = scale * GB_LOG2E;
+  const int kfull = G.N & ~63;   // keys of the unmasked 64-key steps
+  for (int qb = wave; qb < Np / 16; qb += GB_NW) {
+    const int qtok = qb * 16 + fr;
+    const bool qok = qtok < G.N;
+    const long qpix = qok ? G.pixel(grp, qtok) : 0;
+    bf16x8 qf[KK];
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      const int d = kk * 32 + fg * 8;
+      qf[kk] = gm_load8(qkv + h * G.hd + qpix * C3 + d, qok && d < G.hd);
+    }
+    f32x4 o[ND];
+#pragma unroll
+    for (int j = 0; j < ND; ++j) o[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float m = -INFINITY, lp = 0.f;  // running max (log2 units, replicated over fg); this lane's row-sum part
+    auto step = [&](const int k0, const int nc, const bool tail) {
+      f32x4 sc[4];
+      float mc = -INFINITY;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        sc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (c < nc) {
+#pragma unroll
+          for (int kk = 0; kk < KK; ++kk) {
+            const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks + (k0 + 16 * c + fr) * PITCH + kk * 32 + fg * 8);
+            sc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[kk], sc[c], 0, 0, 0);
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          if (tail && !(c < nc && k0 + 16 * c + 4 * fg + r < G.N)) sc[c][r] = -INFINITY;
+          mc = fmaxf(mc, sc[c][r]);
+        }
+      }
+      mc = fmaxf(mc, __shfl_xor(mc, 16, 64));
+      mc = fmaxf(mc, __shfl_xor(mc, 32, 64));
+      const float mc2 = mc * sl2;
+      if (__any(mc2 > m + GB_RESCALE)) {   // always on the first step (m = -inf)
+        const float mn = fmaxf(m, mc2);
+        const float corr = gb_exp2(m - mn);
+        lp *= corr;
+        float cr[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) cr[r] = __shfl(corr, 4 * fg + r, 64);
+#pragma unroll
+        for (int j = 0; j < ND; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[j][r] *= cr[r];
+        m = mn;
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          sc[c][r] = gb_exp2(fmaf(sc[c][r], sl2, -m));   // masked: exp2(-inf) = 0
+          lp += sc[c][r];
+        }
+#pragma unroll
+      for (int cp = 0; cp < 2; ++cp) {
+        if (2 * cp >= nc) break;
+        const bool two = 2 * cp + 1 < nc;
+        const float p0[4] = {sc[2 * cp][0], sc[2 * cp][1], sc[2 * cp][2], sc[2 * cp][3]};
+        const float p1[4] = {sc[2 * cp + 1][0], sc[2 * cp + 1][1], sc[2 * cp + 1][2], sc[2 * cp + 1][3]};
+        const bf16x8 pa = gb_cat8(pack4(p0), pack4(p1));
+#pragma unroll
+        for (int j = 0; j < ND; ++j) {
+          const gm_s16x4 v0 = gb_tr(Vs, k0 + 32 * cp, PITCH, j, lane);
+          const gm_s16x4 v1 = two ? gb_tr(Vs, k0 + 32 * cp + 16, PITCH, j, lane) : gm_s16x4{0, 0, 0, 0};
+          o[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, gb_cat8(v0, v1), o[j], 0, 0, 0);
+        }
+      }
+    };
+    int k0 = 0;
+    for (; k0 < kfull; k0 += 64) step(k0, 4, false);
+    if (k0 < Np) step(k0, (Np - k0) / 16, true);
+    float l = lp + __shfl_xor(lp, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    float inv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) inv[r] = 1.f / __shfl(l, 4 * fg + r, 64);
+    gb_store<HDP>(o, inv, out + h * G.hd, G.C, G, grp, qb * 16, lane);
+    if (fg == 0 && qok) lse[qpix * G.heads + h] = m * GB_LN2 + __logf(l);
+  }
+}
+
+// dQ, second generation: K and V resident; 32 keys (two S^T / dP^T chunks) per 16x16x32 dS K MFMA.
+template <int HDP>
+__global__ __launch_bounds__(GB_NW * 64) void grid_big_dq2_kernel(const bf16* __restrict__ dout,
+                                                                 const bf16* __restrict__ qkv,
+                                                                 const float* __restrict__ lse,
+                                                                 const float* __restrict__ delta,
+                                                                 bf16* __restrict__ dqkv, GridGeomM G, float scale,
+                                                                 int Np) {
+  constexpr int KK = HDP / 32, ND = HDP / 16, PITCH = gm_pitch<HDP>();
+  extern __shared__ __attribute__((aligned(16))) bf16 gsm[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const long C3 = 3L * G.C;
+  const long pr = blockIdx.x;
+  const int h = (int)(pr % G.heads);
+  const long grp = pr / G.heads;
+  const bf16* Ks = gsm;
+  const bf16* Vs = gsm + (size_t)Np * PITCH;
+  gb_stage2<HDP>(gsm, qkv + G.C + h * G.hd, C3, qkv + 2 * G.C + h * G.hd, C3, G, grp, Np);
+  __syncthreads();
+  const float sl2 = scale * GB_LOG2E;
+  const int kfull = G.N & ~31;
+  for (int qb = wave; qb < Np / 16; qb += GB_NW) {
+    const int qtok = qb * 16 + fr;
+    const bool qok = qtok < G.N;
+    const long qpix = qok ? G.pixel(grp, qtok) : 0;
+    bf16x8 qf[KK], gf[KK];  // Q^T and dO^T as B operands (query fr)
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      const int d = kk * 32 + fg * 8;
+      qf[kk] = gm_load8(qkv + h * G.hd + qpix * C3 + d, qok && d < G.hd);
+      gf[kk] = gm_load8(dout + qpix * G.C + h * G.hd + d, qok && d < G.hd);
+    }
+    const float lq2 = qok ? lse[qpix * G.heads + h] * GB_LOG2E : INFINITY;   // invalid query: P = 0
+    const float dl = qok ? delta[qpix * G.heads + h] : 0.f;
+    f32x4 dq[ND];
+#pragma unroll
+    for (int j = 0; j < ND; ++j) dq[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto chunk = [&](const int k0, const bool tail, float (&ds)[4]) {
+      f32x4 sv = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) {
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks + (k0 + fr) * PITCH + kk * 32 + fg * 8);
+        const bf16x8 vf = *reinterpret_cast<const bf16x8*>(Vs + (k0 + fr) * PITCH + kk * 32 + fg * 8);
+        sv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[kk], sv, 0, 0, 0);    // S^T
+        dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, gf[kk], dp, 0, 0, 0);    // dP^T
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float pw = gb_exp2(fmaf(sv[r], sl2, -lq2));
+        if (tail && k0 + 4 * fg + r >= G.N) pw = 0.f;
+        ds[r] = pw * (dp[r] - dl);
+      }
+    };
+    auto pair = [&](const int k0, const bool tail) {
+      const bool two = k0 + 16 < Np;
+      float d0[4], d1[4] = {0.f, 0.f, 0.f, 0.f};
+      chunk(k0, tail, d0);
+      if (two) chunk(k0 + 16, tail, d1);
+      const bf16x8 da = gb_cat8(pack4(d0), pack4(d1));   // A operand: dS[query fr][32 keys]
+#pragma unroll
+      for (int j = 0; j < ND; ++j) {
+        const gm_s16x4 k0b = gb_tr(Ks, k0, PITCH, j, lane);
+        const gm_s16x4 k1b = two ? gb_tr(Ks, k0 + 16, PITCH, j, lane) : gm_s16x4{0, 0, 0, 0};
+        dq[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, gb_cat8(k0b, k1b), dq[j], 0, 0, 0);
+      }
+    };
+    int k0 = 0;
+    for (; k0 < kfull; k0 += 32) pair(k0, false);
+    if (k0 < Np) pair(k0, true);
+    const float sc4[4] = {scale, scale, scale, scale};
+    gb_store<HDP>(dq, sc4, dqkv + h * G.hd, C3, G, grp, qb * 16, lane);
+  }
+}
+
+// dK, dV, second generation: Q, dO, lse*log2(e), delta resident; 32 queries per 16x16x32 MFMA pair.
+template <int HDP>
+__global__ __launch_bounds__(GB_NW * 64) void grid_big_dkv2_kernel(const bf16* __restrict__ dout,
+                                                                  const bf16* __restrict__ qkv,
+                                                                  const float* __restrict__ lse,
+                                                                  const float* __restrict__ delta,
+                                                                  bf16* __restrict__ dqkv, GridGeomM G, float scale,
+                                                                  int Np) {
+  constexpr int KK = HDP / 32, ND = HDP / 16, PITCH = gm_pitch<HDP>();
+  extern __shared__ __attribute__((aligned(16))) bf16 gsm[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const long C3 = 3L * G.C;
+  const long pr = blockIdx.x;
+  const int h = (int)(pr % G.heads);
+  const long grp = pr / G.heads;
+  const bf16* Qs = gsm;
+  const bf16* Gs = gsm + (size_t)Np * PITCH;
+  float* lq_s = reinterpret_cast<float*>(gsm + 2 * (size_t)Np * PITCH);
+  float* dl_s = lq_s + Np;
+  gb_stage2<HDP>(gsm, qkv + h * G.hd, C3, dout + h * G.hd, G.C, G, grp, Np);
+  for (int t = threadIdx.x; t < Np; t += GB_NW * 64) {   // padded rows: lse = inf -> P = 0
+    const bool ok = t < G.N;
+    const long pq = ok ? G.pixel(grp, t) : 0;
+    lq_s[t] = ok ? lse[pq * G.heads + h] * GB_LOG2E : INFINITY;
+    dl_s[t] = ok ? delta[pq * G.heads + h] : 0.f;
+  }
+  __syncthreads();
+  const float sl2 = scale * GB_LOG2E;
+  for (int kb = wave; kb < Np / 16; kb += GB_NW) {
+    const int ktok = kb * 16 + fr;
+    const bool kok = ktok < G.N;
+    const long kpix = kok ? G.pixel(grp, ktok) : 0;
+    bf16x8 kf[KK], vf[KK];  // K^T, V^T as B operands (key fr)
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      const int d = kk * 32 + fg * 8;
+      kf[kk] = gm_load8(qkv + G.C + h * G.hd + kpix * C3 + d, kok && d < G.hd);
+      vf[kk] = gm_load8(qkv + 2 * G.C + h * G.hd + kpix * C3 + d, kok && d < G.hd);
+    }
+    f32x4 dk[ND], dv[ND];
+#pragma unroll
+    for (int j = 0; j < ND; ++j) {
+      dk[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      dv[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    auto chunk = [&](const int q0, float (&pw)[4], float (&ds)[4]) {
+      // S[query 4fg+r][key fr] = Q K^T ; dP = dO V^T
+      f32x4 sv = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) {
+        const bf16x8 qa = *reinterpret_cast<const bf16x8*>(Qs + (q0 + fr) * PITCH + kk * 32 + fg * 8);
+        const bf16x8 ga = *reinterpret_cast<const bf16x8*>(Gs + (q0 + fr) * PITCH + kk * 32 + fg * 8);
+        sv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kf[kk], sv, 0, 0, 0);
+        dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ga, vf[kk], dp, 0, 0, 0);
+      }
+      const float4 lq4 = *reinterpret_cast<const float4*>(lq_s + q0 + 4 * fg);
+      const float4 dl4 = *reinterpret_cast<const float4*>(dl_s + q0 + 4 * fg);
+      const float lq[4] = {lq4.x, lq4.y, lq4.z, lq4.w}, dl[4] = {dl4.x, dl4.y, dl4.z, dl4.w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        pw[r] = kok ? gb_exp2(fmaf(sv[r], sl2, -lq[r])) : 0.f;
+        ds[r] = pw[r] * (dp[r] - dl[r]);
+      }
+    };
+    for (int q0 = 0; q0 < Np; q0 += 32) {
+      const bool two = q0 + 16 < Np;
+      float p0[4], d0[4], p1[4] = {0.f, 0.f, 0.f, 0.f}, d1[4] = {0.f, 0.f, 0.f, 0.f};
+      chunk(q0, p0, d0);
+      if (two) chunk(q0 + 16, p1, d1);
+      const bf16x8 pa = gb_cat8(pack4(p0), pack4(p1)), da = gb_cat8(pack4(d0), pack4(d1));
+#pragma unroll
+      for (int j = 0; j < ND; ++j) {
+        const gm_s16x4 g0 = gb_tr(Gs, q0, PITCH, j, lane), q0b = gb_tr(Qs, q0, PITCH, j, lane);
+        const gm_s16x4 g1 = two ? gb_tr(Gs, q0 + 16, PITCH, j, lane) : gm_s16x4{0, 0, 0, 0};
+        const gm_s16x4 q1b = two ? gb_tr(Qs, q0 + 16, PITCH, j, lane) : gm_s16x4{0, 0, 0, 0};
+        dv[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, gb_cat8(g0, g1), dv[j], 0, 0, 0);
+        dk[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, gb_cat8(q0b, q1b), dk[j], 0, 0, 0);
+      }
+    }
+    const float sc4[4] = {scale, scale, scale, scale}, one4[4] = {1.f, 1.f, 1.f, 1.f};
+    gb_store<HDP>(dk, sc4, dqkv + G.C + h * G.hd, C3, G, grp, kb * 16, lane);
+    gb_store<HDP>(dv, one4, dqkv + 2 * G.C + h * G.hd, C3, G, grp, kb * 16, lane);
+  }
+}
+
 template <int HDP>
 static bool grid_big_bwd_try(const GridGeomM& G, const void* dout, const void* qkv, const float* lse,
                              const float* delta, void* dqkv, float scale, hipStream_t s);
 
-static int g_grid_big = 1;   // tuning knob "grid_big": one-pair-per-block LDS kernel for large groups
-void set_grid_big(int v) { g_grid_big = v ? 1 : 0; }
+// tuning knob "grid_big": one-pair-per-block LDS kernels for large groups (0 off, 1 first
+// generation, 2 exp2/lazy-rescale/16x16x32 second generation)
+static int g_grid_big = 2;
+void set_grid_big(int v) { g_grid_big = v < 0 ? 0 : (v > 2 ? 2 : v); }
 constexpr size_t GB_LDS_MAX = 160 * 1024;
 
 template <int HDP>
@@ -1005,10 +1305,15 @@ static bool grid_big_fwd_try(const GridGeomM& G, const void* qkv, void* out, flo
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(grid_big_fwd_kernel<HDP>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)GB_LDS_MAX);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(grid_big_fwd2_kernel<HDP>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)GB_LDS_MAX);
     attr = true;
   }
   const long pairs = (long)G.B * G.g * G.g * G.heads;
-  grid_big_fwd_kernel<HDP><<<(unsigned)pairs, GB_NW * 64, lds, s>>>((const bf16*)qkv, (bf16*)out, lse, G, scale, Np);
+  if (g_grid_big == 2)
+    grid_big_fwd2_kernel<HDP><<<(unsigned)pairs, GB_NW * 64, lds, s>>>((const bf16*)qkv, (bf16*)out, lse, G, scale, Np);
+  else
+    grid_big_fwd_kernel<HDP><<<(unsigned)pairs, GB_NW * 64, lds, s>>>((const bf16*)qkv, (bf16*)out, lse, G, scale, Np);
   return true;
 }
 
@@ -1024,9 +1329,20 @@ static bool grid_big_bwd_try(const GridGeomM& G, const void* dout, const void* q
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)GB_LDS_MAX);
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(grid_big_dkv_kernel<HDP>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)GB_LDS_MAX);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(grid_big_dq2_kernel<HDP>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)GB_LDS_MAX);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(grid_big_dkv2_kernel<HDP>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)GB_LDS_MAX);
     attr = true;
   }
   const long pairs = (long)G.B * G.g * G.g * G.heads;
+  if (g_grid_big == 2) {
+    grid_big_dq2_kernel<HDP><<<(unsigned)pairs, GB_NW * 64, l1, s>>>((const bf16*)dout, (const bf16*)qkv, lse, delta,
+                                                                     (bf16*)dqkv, G, scale, Np);
+    grid_big_dkv2_kernel<HDP><<<(unsigned)pairs, GB_NW * 64, l2, s>>>((const bf16*)dout, (const bf16*)qkv, lse, delta,
+                                                                      (bf16*)dqkv, G, scale, Np);
+    return true;
+  }
   grid_big_dq_kernel<HDP><<<(unsigned)pairs, GB_NW * 64, l1, s>>>((const bf16*)dout, (const bf16*)qkv, lse, delta,
                                                                   (bf16*)dqkv, G, scale, Np);
   grid_big_dkv_kernel<HDP><<<(unsigned)pairs, GB_NW * 64, l2, s>>>((const bf16*)dout, (const bf16*)qkv, lse, delta,

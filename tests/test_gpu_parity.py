@@ -164,9 +164,12 @@ def test_golden_bf16(name):
     assert e <= bound, f"{name} bf16 fwd max|d| {e:.3e} > {bound:.3e} (torch {e_torch:.3e})"
     e = fx.maxabs(dx.float(), arr["dx"])
     assert e <= _tol(arr["dx"], 3e-2), f"{name} bf16 dx max|d| {e:.3e}"
-    # the trained quantity: bf16-path weight gradients (full or sketched) at 3e-2 of |ref|
+    # the trained quantity: bf16-path weight gradients (full or sketched) at 3e-2 of |ref|, or twice
+    # the reference's own bf16-autocast deviation on that tensor where the fixture records it and it
+    # is larger (outgrid_block_224_s0_*: the BatchNorm weight / bias gradients of the MBConv expand
+    # conv are sums over every pixel, and the reference's own bf16 path is 3.2% off on them)
     grads = {k: p.grad for k, p in mod.named_parameters()}
-    assert fx.compare_grads(grads, arr, BF16_GRAD, 1e-4, name + " bf16") > 0
+    assert fx.compare_grads(grads, arr, BF16_GRAD, 1e-4, name + " bf16", floor_tag="bf16", floor_scale=2.0) > 0
 
 
 def test_capture_attn_hook():
@@ -546,6 +549,44 @@ def test_grid_mfma_vs_oracle(case):
     y0, gq0 = outs[0]
     assert fx.maxabs(y, y0) <= 1e-2 * max(1, y0.abs().max().item())
     assert fx.maxabs(gq, gq0) <= 2e-2 * max(1, gq0.abs().max().item())
+
+
+GRID_BIG_CASES = [(2, 28, 28, 64, 2, 1), (1, 20, 20, 64, 2, 1), (1, 14, 14, 128, 2, 1), (1, 18, 18, 32, 1, 1),
+                  (1, 19, 19, 64, 2, 1)]   # N = 784 / 400 / 196 (hd 64) / 324 / 361 (ragged 16-chunk)
+
+
+@pytest.mark.parametrize("case", GRID_BIG_CASES)
+def test_grid_big_generations(case):
+    """Both large-group kernel generations (knob grid_big = 1: per-step rescale, 16x16x16 P V; = 2:
+    exp2 + lazy rescale + paired 16x16x32 products) against the fp32 oracle, forward and dq/dk/dv,
+    and against each other."""
+    from ogv import functional as OF
+    from ogv._lib import load
+    B, H, W, C, h, g = case
+    gen = torch.Generator().manual_seed(hash(case) & 0xFFFF)
+    qkv = torch.randn(B, H, W, 3 * C, generator=gen).to(torch.bfloat16).float()
+    dy = torch.randn(B, H, W, C, generator=gen).to(torch.bfloat16).float()
+    q_r = qkv.clone().requires_grad_()
+    y_r, _ = orc.grid_core(q_r, h, g, want_probs=True)
+    y_r.backward(dy)
+    lib = load()
+    outs = {}
+    try:
+        for knob in (1, 2):
+            assert lib.ogv_set_option(b"grid_big", knob) == 0
+            qd = qkv.to(DEV, torch.bfloat16).requires_grad_()
+            y, _ = OF.grid_attention_rows(qd.reshape(-1, 3 * C), B, H, W, h, g, (C // h) ** -0.5)
+            y.backward(dy.to(DEV, torch.bfloat16).reshape(-1, C))
+            outs[knob] = (y.float().view(B, H, W, C).cpu(), qd.grad.float().cpu())
+    finally:
+        assert lib.ogv_set_option(b"grid_big", 2) == 0
+    gref = q_r.grad
+    for knob, (y, gq) in outs.items():
+        assert fx.maxabs(y, y_r) <= 1e-2 * max(1, y_r.abs().max().item()), knob
+        assert fx.maxabs(gq, gref) <= 2e-2 * max(1, gref.abs().max().item()), knob
+    (y1, g1), (y2, g2) = outs[1], outs[2]
+    assert fx.maxabs(y1, y2) <= 1e-2 * max(1, y1.abs().max().item())
+    assert fx.maxabs(g1, g2) <= 2e-2 * max(1, g1.abs().max().item())
 
 
 GEMM_CASES = [  # M, N, K, act, bias, residual, rowscale

@@ -347,8 +347,8 @@ def main():
                              "unit": "TFLOP/s", "frac": round(probe["achieved_TFLOPs"] / MFMA_PEAK_TFLOPS, 4),
                              "algorithmic_flops_per_launch": int(probe["flops_per_launch"])},
                     "timing": ("HIP events around each launch (a 40 us device spin queued ahead of each, so no host "
-                               "launch gap is timed; minus what an event pair adds around a kernel, calibrated on a "
-                               "20 us wall-clock spin), " + ("eager step after the timed graph replays"
+                               "launch gap is timed; raw intervals, nothing subtracted: they equal rocprofv3's kernel "
+                               "durations, profiles/r03_final_probe_vs_trace.txt), " + ("eager step after the timed graph replays"
                                                            if trainer.graphs else "all timed steps"))}
         if roof is not None and census is not None:
             # clip_grad_norm (norm pass reads g; scale pass reads + writes g) and the fused AdamW (reads p,

@@ -55,7 +55,9 @@ const char* ogv_last_error(void);
  *   the tiled backward (default) / training with the recompute backward ogv_outlook_vproj_bwd;
  *   "vp_tile" 0 (default) / 1-4: force a tile candidate of the fused Outlooker kernels; "wg2_fuse" 0
  *   (default) / 1: in-kernel last-workgroup reduction of the split-M weight gradient instead of the
- *   column-reduce launch (measured slower); "vp_dbg", "pg_dbg": phase-skipping timing experiments
+ *   column-reduce launch (measured slower); "grid_big" 0/1/2 (default 2): one-(group, head)-pair-per-block
+ *   LDS-resident grid attention for groups too large for the multi-pair kernels off / first generation /
+ *   second generation (exp2 + lazy rescale + paired 16x16x32 MFMAs); "vp_dbg", "pg_dbg": phase-skipping timing experiments
  *   (wrong results).
  * Options pick kernel plans, and every *_ws_bytes query sizes the workspace for the plans in force
  * when it is called: set options first, then size workspaces (a workspace sized under other option

@@ -217,12 +217,13 @@ class _probe:
 
 
 def _empty_pair_ms(reps: int = 16) -> float:
-    """The event-recording overhead subtracted from every probed interval: the median interval of an
-    event pair around a device spin of KNOWN length (ogv_gpu_sleep: a wall-clock loop of 20 us, the
-    same 40 us spin in front) minus that length -- i.e. what a pair adds around a kernel.  (An EMPTY
-    pair's interval, the round-2 calibration, over-counts it: measured 5.0-5.4 us vs 2.5-3 us around a
-    kernel, so the probe read ~10% under rocprofv3's kernel durations,
-    profiles/r03_head_probe_vs_trace.txt.)"""
+    """What an event pair adds around a device spin of KNOWN length (ogv_gpu_sleep: a wall-clock loop
+    of 20 us, the same 40 us spin in front): median interval minus 20 us.  REPORTED ONLY, not
+    subtracted: around a real kernel this cost overlaps the kernel, and the raw probe interval
+    equals rocprofv3's kernel duration (27.67 vs 27.67 us per panel launch at HEAD, 27.58 vs 26.94 at
+    the round-3 head pass), while subtracting it -- or the empty-pair interval of round 2 -- read
+    10-14% under rocprof (profiles/r03_final_probe_vs_trace.txt).  The raw interval is therefore a
+    conservative bound: achieved bytes / raw interval <= the kernel's true rate."""
     lib = _lib.load()
     pairs = []
     spin_us = 20
@@ -240,13 +241,13 @@ def _empty_pair_ms(reps: int = 16) -> float:
 
 def probe_results():
     """{n, avg_ms, bytes_per_launch, achieved_GBs, event_overhead_ms} over the recorded launches
-    (each interval minus the empty event-pair overhead), or None."""
+    (raw event intervals: see _empty_pair_ms), or None."""
     recs = _PROBE["recs"]
     if not recs:
         return None
     torch.cuda.synchronize()
     ovh = _empty_pair_ms()
-    ms = [max(a.elapsed_time(b) - ovh, 1e-6) for a, b, _, _, _ in recs]
+    ms = [max(a.elapsed_time(b), 1e-6) for a, b, _, _, _ in recs]
     dump = os.environ.get("OGV_PROBE_DUMP")
     if dump:   # per-launch table: shape, algorithmic bytes, time, GB/s
         with open(dump, "a") as f:
@@ -368,8 +369,8 @@ class _census:
 
 def census_results(hbm_gbs: float, mfma_tflops: float):
     """Per-op-family table and totals of the recorded ops: algorithmic bytes / flops, roofline time
-    max(bytes / HBM peak, flops / MFMA peak), measured time (each interval minus the empty
-    event-pair overhead)."""
+    max(bytes / HBM peak, flops / MFMA peak), measured time (raw event intervals, see
+    _empty_pair_ms)."""
     recs = _CENSUS["recs"]
     if not recs:
         return None
@@ -377,7 +378,7 @@ def census_results(hbm_gbs: float, mfma_tflops: float):
     ovh = _empty_pair_ms()
     fam = {}
     for name, a, b, nb, nf in recs:
-        ms = max(a.elapsed_time(b) - ovh, 1e-6)
+        ms = max(a.elapsed_time(b), 1e-6)
         bound = max(nb / (hbm_gbs * 1e9), nf / (mfma_tflops * 1e12)) * 1e3
         d = fam.setdefault(name, {"launches": 0, "bytes": 0, "flops": 0, "bound_ms": 0.0, "measured_ms": 0.0})
         d["launches"] += 1

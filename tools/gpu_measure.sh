@@ -14,7 +14,7 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/
   -- python3 bench.py --steps 4 --warmup 3 --no-cpu-baseline --no-parity > "$OUT/prof.log" 2>&1 || { echo "rocprof rc=$?"; tail -20 "$OUT/prof.log"; exit 1; }
 grep -E '^\{' "$OUT/prof.log" | tail -1
 python3 tools/trace_steps.py "$OUT/prof/bench_kernel_trace.csv" --top 60 --step -2 > "$OUT/step_breakdown.txt" 2>&1
-python3 tools/probe_vs_trace.py "$OUT/prof/bench_kernel_trace.csv" "$OUT/prof.log" > "$OUT/probe_vs_trace.txt" 2>&1
+python3 tools/probe_vs_trace.py "$OUT/prof/bench_kernel_trace.csv" "$OUT/prof.log" "$OUT/bench.log" > "$OUT/probe_vs_trace.txt" 2>&1
 cat "$OUT/probe_vs_trace.txt"
 gzip -f "$OUT/prof/bench_kernel_trace.csv"
 if [ "${PMC:-1}" = 1 ]; then

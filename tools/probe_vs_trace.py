@@ -5,7 +5,11 @@ probe step); their rocprof durations are averaged and compared with the probe's 
 (HIP events).  Also prints the average over every launch of the probed kernel family in the
 graph-replayed steps.
 
-    python tools/probe_vs_trace.py bench_kernel_trace.csv bench_stdout.log
+    python tools/probe_vs_trace.py bench_kernel_trace.csv bench_stdout.log [unprofiled_bench.log]
+
+Under rocprofv3 the HIP-event intervals themselves are inflated by the tracer (its completion
+handling sits between the events), so the like-for-like check is the probe of an UNPROFILED bench
+run on the same box (third argument) against the rocprof durations of the probed launches.
 """
 import csv
 import json
@@ -13,7 +17,7 @@ import re
 import sys
 
 
-def main(trace, log):
+def main(trace, log, clean_log=None):
     rows = list(csv.DictReader(open(trace)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     line = [ln for ln in open(log) if ln.startswith("{")][-1]
@@ -47,10 +51,15 @@ def main(trace, log):
     if allk:
         print(f"rocprof, every other {fam} launch (graph replays + MBConv-internal): n={len(allk)} "
               f"avg={sum(allk) / len(allk):.5f} ms")
+    if clean_log:
+        rc = json.loads([ln for ln in open(clean_log) if ln.startswith("{")][-1]).get("roofline") or {}
+        if rc.get("avg_launch_ms"):
+            print(f"probe of the unprofiled bench (HIP events): n={rc.get('launches')} avg={rc['avg_launch_ms']:.5f} ms "
+                  f"achieved={rc.get('achieved')} GB/s -> ratio events/rocprof = {rc['avg_launch_ms'] / avg_p:.3f}")
     bpl = roof.get("algorithmic_bytes_per_launch")
     if bpl:
         print(f"algorithmic bytes/launch {bpl} -> rocprof-timed achieved {bpl / (avg_p * 1e-3) / 1e9:.1f} GB/s")
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:3])
+    main(*sys.argv[1:4])

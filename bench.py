@@ -351,8 +351,8 @@ def main():
                                "durations, profiles/r03_final_probe_vs_trace.txt), " + ("eager step after the timed graph replays"
                                                            if trainer.graphs else "all timed steps"))}
         if roof is not None and census is not None:
-            # clip_grad_norm (norm pass reads g; scale pass reads + writes g) and the fused AdamW (reads p,
-            # g, m, v; writes p, m, v) run as ATen foreach / fused kernels: 40 B per fp32 parameter
+            # clip + AdamW (ogv_clip_adamw: the norm pass reads g; the update pass reads p, g, m, v and writes
+            # them back, g clipped in place): 36 B per fp32 parameter, priced at 40 B (the torch path's bytes)
             n_par = sum(p.numel() for p in trainer.params)
             opt_ms = 40.0 * n_par / (HBM_PEAK_GBS * 1e9) * 1e3
             bound_ms = census["bound_ms"] + opt_ms

@@ -322,6 +322,36 @@ int ogv_mix_targets(const int64_t* targets, const int64_t* perm, float* out, int
 /* Elementwise helpers used by the autograd glue. */
 int ogv_cast(const void* src, ogv_dtype src_dt, void* dst, ogv_dtype dst_dt, size_t n, void* stream);
 
+/* Gradient clipping + AdamW of one training step (src/training/one_epoch_train.py:121/141
+ * clip_grad_norm_(model.parameters(), grad_clip_norm); src/training/train_full_model.py:57
+ * torch.optim.AdamW(param_groups, betas=(0.9, 0.999), eps=1e-8)), as torch's
+ * clip_grad_norm_(foreach) + AdamW(fused, capturable).step() compute them, on the optimizer's own
+ * state tensors (a torch AdamW state_dict stays valid): total = sqrt(sum of every grad^2);
+ * coef = min(max_norm / (total + 1e-6), 1) (NaN propagates; max_norm <= 0: no clipping); unless
+ * *found_inf != 0 (then nothing changes): step += 1, grad *= coef (in place, as clip_grad_norm_),
+ * param -= lr*wd*param, exp_avg = b1*exp_avg + (1-b1)*grad, exp_avg_sq = b2*exp_avg_sq + (1-b2)*grad^2 ((1-b) given),
+ * param -= lr/(1-b1^step) * exp_avg / (sqrt(exp_avg_sq)/sqrt(1-b2^step) + eps).  All fp32, device
+ * pointers; `tensors` / `groups` are HOST arrays (their pointers travel in kernel arguments: 64
+ * tensors per launch, 2 launches per 64; graph-capturable).  lr is a device scalar per group (the
+ * schedule writes it).  norm_ws: fp32 workspace of ogv_clip_adamw_ws_bytes(tensors, n). */
+typedef struct {
+  float* param;
+  float* grad;
+  float* exp_avg;
+  float* exp_avg_sq;
+  float* step;          /* device fp32 scalar (torch's capturable state['step']) */
+  long long numel;      /* < 2^31 */
+  int group;            /* index into groups[], < ngroups <= 4 */
+} ogv_adamw_tensor;
+typedef struct {
+  const float* lr;      /* device fp32 scalar */
+  float weight_decay, beta1, beta2, eps;
+  float one_minus_beta1, one_minus_beta2;   /* rounded from double on the host, as torch forms them */
+} ogv_adamw_group;
+size_t ogv_clip_adamw_ws_bytes(const ogv_adamw_tensor* tensors, int n);
+int ogv_clip_adamw(const ogv_adamw_tensor* tensors, int n, const ogv_adamw_group* groups, int ngroups,
+                   const float* found_inf, float max_norm, float* norm_ws, void* stream);
+
 /* Training-step guard and schedule (src/training/one_epoch_train.py:98-108, :152-153;
  * src/training/warmup.py:38-52), one single-thread launch each, capturable, no host sync:
  * ogv_step_flag: *found = 1.0f when the fp32 scalar *x is not finite (mode 0: x = the loss) or

@@ -48,6 +48,16 @@ class ConvBNParams(ctypes.Structure):
     _fields_ = [(n, _p) for n in ("w", "bias", "bn_w", "bn_b", "bn_rm", "bn_rv")]
 
 
+class AdamWTensor(ctypes.Structure):
+    _fields_ = [("param", _p), ("grad", _p), ("exp_avg", _p), ("exp_avg_sq", _p), ("step", _p),
+                ("numel", ctypes.c_longlong), ("group", _i)]
+
+
+class AdamWGroup(ctypes.Structure):
+    _fields_ = [("lr", _p), ("weight_decay", _f), ("beta1", _f), ("beta2", _f), ("eps", _f),
+                ("one_minus_beta1", _f), ("one_minus_beta2", _f)]
+
+
 _PD = ctypes.POINTER(MBConvDesc)
 _PCD = ctypes.POINTER(ConvBNDesc)
 _PCP = ctypes.POINTER(ConvBNParams)
@@ -101,6 +111,8 @@ SIGNATURES = {
     "ogv_mix_targets": (_i, [_p, _p, _p, _i, _i, _f, _f, _p]),
     "ogv_cast": (_i, [_p, _i, _p, _i, _sz, _p]),
     "ogv_step_flag": (_i, [_p, _i, _p, _p]),
+    "ogv_clip_adamw_ws_bytes": (_sz, [ctypes.POINTER(AdamWTensor), _i]),
+    "ogv_clip_adamw": (_i, [ctypes.POINTER(AdamWTensor), _i, ctypes.POINTER(AdamWGroup), _i, _p, _f, _p, _p]),
     "ogv_schedule_step": (_i, [_p, _p, _p, ctypes.POINTER(_p), ctypes.POINTER(_f), _i, _i, _i, _f, _p]),
 }
 

@@ -88,6 +88,17 @@ def build_model(model_cfg: dict) -> nn.Module:
     raise ValueError(f"Unknown model.type '{kind}'. Use 'model_a' (MaxOutNet) or 'model_b' (OutlookerFrontGridNet)")
 
 
+def _dense_like(t: torch.Tensor, p: torch.Tensor) -> bool:
+    """t is an fp32 CUDA tensor of p's shape, dense (contiguous or channels_last) and in p's memory
+    order: strides equal wherever the size is > 1 (a [C, K, 1, 1] weight is both contiguous and
+    channels_last with different strides on its size-1 dims, same bytes)."""
+    if t.dtype != torch.float32 or not t.is_cuda or t.shape != p.shape:
+        return False
+    if not (t.is_contiguous() or (t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last))):
+        return False
+    return all(a == b for a, b, n in zip(t.stride(), p.stride(), p.shape) if n > 1)
+
+
 def param_groups_no_wd(model: nn.Module, weight_decay: float):
     decay, no_decay = [], []
     for name, p in model.named_parameters():
@@ -287,7 +298,7 @@ class Trainer:
     def __init__(self, model: nn.Module, lr=5e-4, weight_decay=0.05, clip=1.0, label_smoothing=0.1,
                  total_steps=10_000, warmup_ratio=0.05, min_lr=1e-6, amp_dtype: Optional[torch.dtype] = torch.bfloat16,
                  graphs: bool = False, capture_warmup: int = 3, capture_hook=None, bucket_mb: float = 8.0,
-                 broadcast_buffers: bool = True, defer_reductions: bool = True):
+                 broadcast_buffers: bool = True, defer_reductions: bool = True, native_optimizer: bool = True):
         self.model = model
         core = model.module if hasattr(model, "module") else model
         self.core = core
@@ -307,6 +318,10 @@ class Trainer:
         # parameter-gradient column reductions batched into one launch at the end of backward
         # (functional.deferred_param_reductions: every .grad is None when backward starts here)
         self.defer_reductions = bool(defer_reductions) and self.device_side
+        # clip_grad_norm_ + AdamW.step() as the native ogv_clip_adamw (2 launches per 64 tensors) on
+        # the torch optimizer's own state tensors; torch's foreach clip + fused AdamW otherwise
+        self.native_optimizer = bool(native_optimizer) and self.device_side
+        self.native_optimizer_fallbacks = 0
         self.capture_warmup = int(capture_warmup)
         self.capture_hook = capture_hook          # called right before recording starts
         self._eager_steps = 0
@@ -453,9 +468,10 @@ class Trainer:
         if self.device_side:
             if flag is not None:
                 self._flag(flag, 1)
-            if self.clip is not None:
-                torch.nn.utils.clip_grad_norm_(self.params, self.clip, foreach=True)
-            self.opt.step()                                   # skipped entirely when _found == 1
+            if not (self.native_optimizer and self._native_clip_adamw()):
+                if self.clip is not None:
+                    torch.nn.utils.clip_grad_norm_(self.params, self.clip, foreach=True)
+                self.opt.step()                               # skipped entirely when _found == 1
             # nonfinite += found; the schedule's step counter advances on applied steps only
             self.sched.device_step(self._found, self._nonfinite)
             return
@@ -467,6 +483,52 @@ class Trainer:
             torch.nn.utils.clip_grad_norm_(self.params, self.clip, foreach=True)
         self.opt.step()
         self.sched.step()
+
+    def _native_clip_adamw(self) -> bool:
+        """clip_grad_norm_(params, clip) + AdamW.step() through ogv_clip_adamw (include/ogv.h), on the
+        state tensors torch's AdamW(fused, capturable) keeps (created here on the first step exactly as
+        its _init_group does, so state_dict / load_state_dict are unchanged).  Returns False (and the
+        caller runs the torch path) when some tensor is not dense with the parameter's strides."""
+        from . import _lib
+        opt = self.opt
+        ents, groups = [], []
+        for gi, g in enumerate(opt.param_groups):
+            if g.get("amsgrad") or g.get("maximize") or len(opt.param_groups) > 4:
+                self.native_optimizer_fallbacks += 1
+                return False
+            b1, b2 = g["betas"]
+            lr = g["lr"]
+            if not (torch.is_tensor(lr) and lr.is_cuda and lr.dtype == torch.float32):
+                self.native_optimizer_fallbacks += 1
+                return False
+            groups.append(_lib.AdamWGroup(lr.data_ptr(), float(g["weight_decay"]), float(b1), float(b2), float(g["eps"]),
+                                          1.0 - float(b1), 1.0 - float(b2)))
+            for p in g["params"]:
+                if p.grad is None:
+                    continue
+                st = opt.state[p]
+                if len(st) == 0:
+                    st["step"] = torch.zeros((), dtype=torch.float32, device=p.device)
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                ts = (p, p.grad, st["exp_avg"], st["exp_avg_sq"])
+                if not all(_dense_like(t, p) for t in ts) \
+                        or st["step"].dtype != torch.float32 or not st["step"].is_cuda:
+                    self.native_optimizer_fallbacks += 1
+                    return False
+                ents.append(_lib.AdamWTensor(p.data_ptr(), p.grad.data_ptr(), st["exp_avg"].data_ptr(),
+                                             st["exp_avg_sq"].data_ptr(), st["step"].data_ptr(), p.numel(), gi))
+        if not ents:
+            return True
+        lib = _lib.load()
+        tarr = (_lib.AdamWTensor * len(ents))(*ents)
+        garr = (_lib.AdamWGroup * len(groups))(*groups)
+        nbytes = lib.ogv_clip_adamw_ws_bytes(tarr, len(ents))
+        ws = torch.empty(nbytes // 4, dtype=torch.float32, device=self._found.device)
+        _lib.check(lib.ogv_clip_adamw(tarr, len(ents), garr, len(groups), self._found.data_ptr(),
+                                      float(self.clip) if self.clip is not None else 0.0, ws.data_ptr(),
+                                      torch.cuda.current_stream().cuda_stream), "ogv_clip_adamw")
+        return True
 
     def _allreduce(self):
         torch.distributed.all_reduce(self.flat)

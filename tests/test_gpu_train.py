@@ -383,3 +383,50 @@ def test_deferred_param_reductions_match_immediate():
         torch.testing.assert_close(b, a, rtol=1e-5, atol=1e-7)
         same += bool(torch.equal(a, b))
     assert same >= len(grads[0]) // 2, (same, len(grads[0]))
+
+
+class _ParamBag(torch.nn.Module):
+    """> 64 parameter tensors (several ogv_clip_adamw launches), odd sizes, > 8192-element tensors
+    (several chunks), channels_last 4-D weights and both weight-decay groups."""
+
+    def __init__(self):
+        super().__init__()
+        g = torch.Generator().manual_seed(3)
+        self.ws = torch.nn.ParameterList(
+            [torch.nn.Parameter(torch.randn(n, generator=g)) for n in (1, 3, 5, 17, 63, 64, 65, 8191, 8192, 8193, 40000)]
+            + [torch.nn.Parameter(torch.randn(7, 13, generator=g)) for _ in range(60)])
+        self.conv = torch.nn.Parameter(torch.randn(32, 16, 3, 3, generator=g).contiguous(memory_format=torch.channels_last))
+        self.norm_w = torch.nn.Parameter(torch.randn(96, generator=g))
+        self.bias = torch.nn.Parameter(torch.randn(130, generator=g))
+
+
+@pytest.mark.parametrize("clip", [1.0, None, 1e6])
+def test_native_clip_adamw_matches_torch(clip):
+    """ogv_clip_adamw (the Trainer's default) against torch's clip_grad_norm_(foreach) + AdamW(fused,
+    capturable).step() on the same parameters, gradients and schedule, over 4 steps with a skipped
+    (found_inf) one: parameters, moments, step counters and the clipped gradients (on applied steps:
+    on a skipped one torch's clip_grad_norm_ still scales .grad, the native path leaves it as is --
+    the skipped step's gradients are discarded either way)."""
+    from ogv.train import Trainer
+    dev = "cuda"
+    mods = [_ParamBag().to(dev) for _ in range(2)]
+    trs = [Trainer(m, lr=3e-3, weight_decay=0.05, clip=clip, native_optimizer=nat, total_steps=50)
+           for m, nat in zip(mods, (True, False))]
+    g = torch.Generator(device=dev).manual_seed(11)
+    for step in range(4):
+        grads = [torch.randn(p.shape, device=dev, generator=g) * (0.5 + step) for p in mods[0].parameters()]
+        for tr, m in zip(trs, mods):
+            for p, gr in zip(m.parameters(), grads):
+                p.grad = gr.clone().contiguous(memory_format=torch.channels_last) if p.dim() == 4 else gr.clone()
+            tr._found.fill_(1.0 if step == 2 else 0.0)
+            tr._update()
+        torch.cuda.synchronize()
+        assert trs[0].native_optimizer_fallbacks == 0
+        for (n0, p0), p1 in zip(mods[0].named_parameters(), mods[1].parameters()):
+            if step != 2:
+                torch.testing.assert_close(p0.grad, p1.grad, rtol=1e-5, atol=1e-7, msg=f"{n0} grad step {step}")
+            torch.testing.assert_close(p0, p1, rtol=1e-5, atol=1e-6, msg=f"{n0} param step {step}")
+            s0, s1 = trs[0].opt.state[p0], trs[1].opt.state[p1]
+            assert float(s0["step"]) == float(s1["step"]) == (step + 1 if step < 2 else step)
+            torch.testing.assert_close(s0["exp_avg"], s1["exp_avg"], rtol=1e-5, atol=1e-7)
+            torch.testing.assert_close(s0["exp_avg_sq"], s1["exp_avg_sq"], rtol=1e-5, atol=1e-9)

@@ -54,6 +54,11 @@ def parse():
     ap.add_argument("--cpu-dry-run", action="store_true",
                     help="launcher / process-group rehearsal on the CPU (gloo): every rank builds the model, "
                          "the Trainer broadcasts it and each step runs only the gradient all-reduce; no HIP kernels")
+    ap.add_argument("--force-dp", action="store_true",
+                    help="take the data-parallel path (process group, broadcast, per-step gradient all_reduce) at "
+                         "N=1 too: a world-size-1 RCCL ('nccl') group on one GPU")
+    ap.add_argument("--dp-capture", action="store_true",
+                    help="graph mode with DP: capture the RCCL all_reduce inside the step's graph")
     ap.add_argument("--step-roofline", type=int, default=1,
                     help="1: time every C-ABI op of one eager step (after the timed region) for roofline.step")
     return ap.parse_args()
@@ -263,7 +268,14 @@ def main():
     from ogv.train import MODEL_CONFIGS, Trainer, build_model, setup_distributed
     import ogv
 
-    rank, world, local, device = setup_distributed()
+    if args.force_dp and "WORLD_SIZE" not in os.environ:
+        # a world-1 process group (env rendezvous on 127.0.0.1), set up before anything touches the GPU
+        import socket
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(s.getsockname()[1]), WORLD_SIZE="1",
+                              RANK="0", LOCAL_RANK="0")
+    rank, world, local, device = setup_distributed(force_group=args.force_dp)
     if world != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE is {world}")
     torch.backends.cudnn.benchmark = True   # as the reference (src/training/autocast.py:8-17)
@@ -278,7 +290,8 @@ def main():
     model = build_model({k: v for k, v in cfg.items() if k != "img"})
     model = model.to(device).to(memory_format=torch.channels_last)
     trainer = Trainer(model, total_steps=max(100, args.steps + args.warmup + 1), graphs=not args.eager,
-                      capture_warmup=max(0, args.warmup - 1))
+                      capture_warmup=max(0, args.warmup - 1), force_dp=args.force_dp,
+                      dp_capture_collective=args.dp_capture)
 
     B, S = args.batch, cfg["img"]
     g = torch.Generator(device=device).manual_seed(7 + rank)
@@ -289,7 +302,7 @@ def main():
         trainer.step(x, y)
     trainer.step(x, y)       # last warmup step (graph mode: eager step on a side stream + capture)
     OF.probe_reset()
-    if world > 1:
+    if trainer.dp:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -298,7 +311,7 @@ def main():
             OF.probe_arm(args.probe)
         loss = trainer.step(x, y)
     torch.cuda.synchronize()
-    if world > 1:
+    if trainer.dp:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     OF.probe_disarm()
@@ -373,7 +386,12 @@ def main():
             "vs_baseline": None, "dtype": "bf16", "data": "synthetic (randn images, randint labels; random init)",
             "config": {"workload": f"{args.model} train step: fwd+CE(ls=0.1)+bwd+clip(1.0)+AdamW", "img_size": S,
                        "per_gpu_batch": B, "global_batch": B * world, "parallelism": f"dp{world}",
-                       "execution": "hipGraph replay" if trainer.graphs else "eager launches"},
+                       "execution": "hipGraph replay" if trainer.graphs else "eager launches",
+                       "backend": trainer.backend or "none (single process, no collective)",
+                       "dp_collective": (None if not trainer.dp else "all_reduce captured in the step graph"
+                                         if trainer.dp_capture_collective else
+                                         "one flat all_reduce between graph A and graph B" if trainer.graphs else
+                                         "bucketed async all_reduce during backward")},
             "roofline": roof,
         }
         if world == 1 and not args.no_parity:
@@ -382,7 +400,7 @@ def main():
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
             out["gpu_over_cpu"] = round(value / out["cpu_baseline"]["value"], 1)
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if trainer.dp:
         dist.destroy_process_group()
 
 

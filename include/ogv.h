@@ -327,7 +327,8 @@ int ogv_cast(const void* src, ogv_dtype src_dt, void* dst, ogv_dtype dst_dt, siz
  * torch.optim.AdamW(param_groups, betas=(0.9, 0.999), eps=1e-8)), as torch's
  * clip_grad_norm_(foreach) + AdamW(fused, capturable).step() compute them, on the optimizer's own
  * state tensors (a torch AdamW state_dict stays valid): total = sqrt(sum of every grad^2);
- * coef = min(max_norm / (total + 1e-6), 1) (NaN propagates; max_norm <= 0: no clipping); unless
+ * coef = min(max_norm / (total + 1e-6), 1) for max_norm >= 0 (NaN propagates; max_norm = 0 zeroes the
+ * gradients as torch's clip_grad_norm_(max_norm=0) does); max_norm < 0: no clipping (grad_clip_norm=None); unless
  * *found_inf != 0 (then nothing changes): step += 1, grad *= coef (in place, as clip_grad_norm_),
  * param -= lr*wd*param, exp_avg = b1*exp_avg + (1-b1)*grad, exp_avg_sq = b2*exp_avg_sq + (1-b2)*grad^2 ((1-b) given),
  * param -= lr/(1-b1^step) * exp_avg / (sqrt(exp_avg_sq)/sqrt(1-b2^step) + eps).  All fp32, device

@@ -24,6 +24,7 @@ parameter dict keyed like the reference state_dict, so the same deterministic pa
   model_b             src/Model_B_OutGridNet.py:10-104
   mix_apply           src/training/cutmix_mixup_aug.py:6-7, 36-64 (given the drawn perm/lam/box)
   model_a             src/Model_A_OutGridNet.py:14-67, stem_head.py:17-32, downsampling.py:50-65
+  train_steps         src/training/one_epoch_train.py:85-153, train_full_model.py:56-66, warmup.py:4-59
 
 Parity: pinned against golden vectors produced by running the reference itself in the build
 container (tests/golden/make_golden.py; tests/test_oracle_golden.py checks this file against
@@ -379,6 +380,41 @@ def train_step(x, y, p, stages, opt, clip=1.0, label_smoothing=0.1):
     torch.nn.utils.clip_grad_norm_(params, clip)
     opt.step()
     return loss.detach()
+
+
+def lr_at(t: int, base: float, warmup_steps: int, total_steps: int, min_lr: float) -> float:
+    """WarmupCosineLR.step's lr for step count t (src/training/warmup.py:38-52)."""
+    if warmup_steps > 0 and t <= warmup_steps:
+        return base * (t / warmup_steps)
+    prog = (min(t, total_steps) - warmup_steps) / max(1, total_steps - warmup_steps)
+    return min_lr + (base - min_lr) * 0.5 * (1.0 + math.cos(math.pi * prog))
+
+
+def train_steps(batches, p, stages, lr=5e-4, weight_decay=0.05, clip=1.0, label_smoothing=0.1, total_steps=8,
+                warmup_steps=2, min_lr=0.0, on_step=None):
+    """The reference's training loop over ``batches`` (src/training/one_epoch_train.py:85-153 with the
+    optimizer / schedule of train_full_model.py:56-66 and warmup.py:29-59): zero_grad, forward, CE with
+    label smoothing; a non-finite loss skips the step (no update, no scheduler.step -- :98-108); else
+    backward, clip_grad_norm_, AdamW.step, scheduler.step.  The first step runs at the base lr (the
+    schedule only writes the lr after a step).  on_step(t, loss, lr_used, skipped, step_num) per batch."""
+    opt = make_optimizer(p, lr, weight_decay)
+    step_num = 0
+    for t, (x, y) in enumerate(batches):
+        lr_used = [float(g["lr"]) for g in opt.param_groups]
+        opt.zero_grad(set_to_none=True)
+        logits = model_a(x, p, stages, train=True)
+        loss = F.cross_entropy(logits.float(), y, label_smoothing=label_smoothing)
+        skipped = not bool(torch.isfinite(loss))
+        if not skipped:
+            loss.backward()
+            torch.nn.utils.clip_grad_norm_([q for q in p.values() if q.requires_grad], clip)
+            opt.step()
+            step_num += 1
+            for g in opt.param_groups:
+                g["lr"] = lr_at(step_num, lr, warmup_steps, total_steps, min_lr)
+        if on_step is not None:
+            on_step(t, loss.detach(), lr_used, skipped, step_num)
+    return opt
 
 
 # ---------------------------------------------------------------------------- kernel-level oracles

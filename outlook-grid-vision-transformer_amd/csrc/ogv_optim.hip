@@ -1,6 +1,6 @@
 // Clip-by-global-norm + AdamW over the parameter tensors of a training step, as two kinds of native
 // launches: what the reference's training loop does with
-//   torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm)   src/training/train_one_epoch.py
+//   torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm)   src/training/one_epoch_train.py:121
 //   torch.optim.AdamW(...).step()                                  src/training/train_full_model.py
 // and what ogv/train.py did with torch's foreach norm / mul launches and its fused AdamW (9 + ~17
 // launches, 0.36 ms per Model-A-7M step for ~35 us of HBM traffic).
@@ -97,7 +97,7 @@ __global__ __launch_bounds__(256) void adamw_update_kernel(AdamWBatch b, AdamWGr
   __shared__ float red[4];
   if (found && *found != 0.f) return;   // uniform over the grid: skipped step
   float coef = 1.f;
-  if (max_norm > 0.f) {
+  if (max_norm >= 0.f) {   // < 0: no clipping (grad_clip_norm=None)
     float s = 0.f;
     for (int i = threadIdx.x; i < nchunks; i += blockDim.x) s += norm_ws[i];
     s = opt_block_sum(s, red);

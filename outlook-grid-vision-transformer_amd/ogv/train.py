@@ -221,13 +221,19 @@ def load_optimizer_state(optimizer: torch.optim.Optimizer, state_dict: dict):
             if isinstance(v, torch.Tensor) and isinstance(o, torch.Tensor) and o.shape == v.shape:
                 o.copy_(v)
                 st[k] = o
+            elif isinstance(v, torch.Tensor) and v.shape == p.shape and v.dim() == 4 and v.stride() != p.stride():
+                # a reference checkpoint holds contiguous moments; the model is channels_last: re-lay
+                # them like their parameter (ogv_clip_adamw walks parameter, gradient and moments with
+                # one index, and otherwise falls back to torch every step)
+                st[k] = torch.empty_like(p, dtype=v.dtype).copy_(v)
 
 
 # ------------------------------------------------------------------------------- distributed
-def setup_distributed(cpu: bool = False):
+def setup_distributed(cpu: bool = False, force_group: bool = False):
     """One process per GPU (torchrun env).  Returns (rank, world, local_rank, device).  The process
     group uses "nccl" (= RCCL over xGMI on ROCm) on HIP devices, "gloo" on the CPU (``cpu=True``
-    forces the CPU: bench.py's launcher rehearsal and the world-2 tests)."""
+    forces the CPU: bench.py's launcher rehearsal and the world-2 tests).  ``force_group``: create the
+    group at world size 1 too (the DP path on one GPU, bench.py --force-dp)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -236,7 +242,7 @@ def setup_distributed(cpu: bool = False):
         device = torch.device("cuda", local)
     else:
         device = torch.device("cpu")
-    if world > 1 and not torch.distributed.is_initialized():
+    if (world > 1 or force_group) and not torch.distributed.is_initialized():
         backend = "nccl" if device.type == "cuda" else "gloo"
         torch.distributed.init_process_group(backend=backend, device_id=device if device.type == "cuda" else None)
     return rank, world, local, device
@@ -298,7 +304,8 @@ class Trainer:
     def __init__(self, model: nn.Module, lr=5e-4, weight_decay=0.05, clip=1.0, label_smoothing=0.1,
                  total_steps=10_000, warmup_ratio=0.05, min_lr=1e-6, amp_dtype: Optional[torch.dtype] = torch.bfloat16,
                  graphs: bool = False, capture_warmup: int = 3, capture_hook=None, bucket_mb: float = 8.0,
-                 broadcast_buffers: bool = True, defer_reductions: bool = True, native_optimizer: bool = True):
+                 broadcast_buffers: bool = True, defer_reductions: bool = True, native_optimizer: bool = True,
+                 force_dp: bool = False, dp_capture_collective: bool = False):
         self.model = model
         core = model.module if hasattr(model, "module") else model
         self.core = core
@@ -316,8 +323,11 @@ class Trainer:
         self.params = [p for p in core.parameters() if p.requires_grad]
         self.clip, self.ls, self.amp_dtype = clip, label_smoothing, amp_dtype
         # parameter-gradient column reductions batched into one launch at the end of backward
-        # (functional.deferred_param_reductions: every .grad is None when backward starts here)
-        self.defer_reductions = bool(defer_reductions) and self.device_side
+        # (functional.deferred_param_reductions: every .grad is None when backward starts here).  Not
+        # under DDP: its reducer copies each gradient into its bucket as AccumulateGrad fires, before
+        # the flush has written it (ditto any user hook that reads .grad as soon as it is accumulated).
+        hooked = any(getattr(p, "_post_accumulate_grad_hooks", None) for p in core.parameters())
+        self.defer_reductions = bool(defer_reductions) and self.device_side and not self.ddp and not hooked
         # clip_grad_norm_ + AdamW.step() as the native ogv_clip_adamw (2 launches per 64 tensors) on
         # the torch optimizer's own state tensors; torch's foreach clip + fused AdamW otherwise
         self.native_optimizer = bool(native_optimizer) and self.device_side
@@ -334,8 +344,18 @@ class Trainer:
             self._nonfinite = torch.zeros((), dtype=torch.float32, device=dev)
             self.sched.bind_device(torch.zeros((), dtype=torch.float32, device=dev))
         self.world = 1 if self.ddp else _dist_world()
-        self.rank = torch.distributed.get_rank() if self.world > 1 else 0
-        if self.world > 1:
+        # the data-parallel path (broadcast at start, gradient / buffer exchange every step); force_dp
+        # takes it at world size 1 as well (a world-1 process group: the collective path on one GPU)
+        self.dp = self.world > 1 or (bool(force_dp) and not self.ddp)
+        if self.dp and not (torch.distributed.is_available() and torch.distributed.is_initialized()):
+            raise RuntimeError("Trainer(force_dp=True) needs an initialised torch.distributed process group")
+        self.rank = torch.distributed.get_rank() if self.dp else 0
+        self.backend = torch.distributed.get_backend() if self.dp else None
+        # graph mode: the all_reduce captured INSIDE the step's one graph (RCCL collectives are
+        # capturable; gloo's are host work and never are) instead of graph A -> all_reduce -> graph B
+        self.dp_capture_collective = bool(dp_capture_collective) and self.dp and self.backend == "nccl"
+        self._warned_fallback = False
+        if self.dp:
             with torch.no_grad():   # identical start on every rank (what DDP's constructor does)
                 for t in list(core.parameters()) + list(core.buffers()):
                     torch.distributed.broadcast(t.data, 0)
@@ -397,11 +417,11 @@ class Trainer:
         loss = self._loss(x, y)
         if self.device_side:
             self._flag(loss.detach(), 0)
-        if self.world > 1 and self._overlap:
+        if self.dp and self._overlap:
             self._launch_meta(loss)
         from .functional import deferred_param_reductions
         # not under the eager DP overlap: its bucket hooks read gradients as soon as they are produced
-        with deferred_param_reductions(self.defer_reductions and not (self.world > 1 and self._overlap)):
+        with deferred_param_reductions(self.defer_reductions and not (self.dp and self._overlap)):
             loss.backward()
         return loss.detach()
 
@@ -469,6 +489,12 @@ class Trainer:
             if flag is not None:
                 self._flag(flag, 1)
             if not (self.native_optimizer and self._native_clip_adamw()):
+                if self.native_optimizer and not self._warned_fallback:
+                    import warnings
+                    self._warned_fallback = True
+                    warnings.warn("ogv_clip_adamw declined this optimizer state (a moment tensor not laid out like "
+                                  "its parameter, > 4 groups, amsgrad / maximize, or a non-device lr): running "
+                                  "torch's clip_grad_norm_ + fused AdamW instead", RuntimeWarning, stacklevel=3)
                 if self.clip is not None:
                     torch.nn.utils.clip_grad_norm_(self.params, self.clip, foreach=True)
                 self.opt.step()                               # skipped entirely when _found == 1
@@ -526,7 +552,7 @@ class Trainer:
         nbytes = lib.ogv_clip_adamw_ws_bytes(tarr, len(ents))
         ws = torch.empty(nbytes // 4, dtype=torch.float32, device=self._found.device)
         _lib.check(lib.ogv_clip_adamw(tarr, len(ents), garr, len(groups), self._found.data_ptr(),
-                                      float(self.clip) if self.clip is not None else 0.0, ws.data_ptr(),
+                                      float(self.clip) if self.clip is not None else -1.0, ws.data_ptr(),
                                       torch.cuda.current_stream().cuda_stream), "ogv_clip_adamw")
         return True
 
@@ -535,7 +561,7 @@ class Trainer:
 
     def _eager(self, x, y):
         self.opt.zero_grad(set_to_none=True)
-        if self.world > 1 and self._buckets:
+        if self.dp and self._buckets:
             self._overlap = True
             try:
                 loss = self._fwd_bwd(x, y)
@@ -545,7 +571,7 @@ class Trainer:
             return loss
         loss = self._fwd_bwd(x, y)
         flag = None
-        if self.world > 1:
+        if self.dp:
             self._flatten(loss)
             self._allreduce()
             flag = self._unflatten()
@@ -571,16 +597,23 @@ class Trainer:
             self.capture_hook()
         pool = torch.cuda.graph_pool_handle()
         self._g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self._g, pool=pool):
+        # RCCL: ProcessGroupNCCL's watchdog thread polls the events of earlier collectives while this
+        # thread captures; under the default "global" capture mode that poll is a capture-unsupported
+        # call from another thread (hipErrorStreamCaptureUnsupported -> abort), so capture thread-locally
+        mode = "thread_local" if self.backend == "nccl" else "global"
+        with torch.cuda.graph(self._g, pool=pool, capture_error_mode=mode):
             self._loss_static = self._fwd_bwd(self._x, self._y)
-            if self.world > 1:
+            if self.dp:
                 self._flatten(self._loss_static)
+                if self.dp_capture_collective:
+                    self._allreduce()
+                    self._update(self._unflatten())
             else:
                 self._update()
         self.graph_grads = [p.grad for p in self.params]   # the tensors the replays write
-        if self.world > 1:
+        if self.dp and not self.dp_capture_collective:
             self._g2 = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self._g2, pool=pool):
+            with torch.cuda.graph(self._g2, pool=pool, capture_error_mode=mode):
                 self._update(self._unflatten())
         return loss
 
@@ -600,7 +633,7 @@ class Trainer:
         self._x.copy_(x)
         self._y.copy_(y)
         self._g.replay()
-        if self.world > 1:
+        if self.dp and not self.dp_capture_collective:
             self._allreduce()
             self._g2.replay()
         return self._loss_static.clone()
@@ -611,8 +644,12 @@ class Trainer:
 
     # -- checkpoint / resume (src/training/chekpoints.py dict keys) -----------------------------
     def state_dict(self):
-        return {"model": self.core.state_dict(), "optimizer": self.opt.state_dict(),
-                "scheduler": self.sched.state_dict()}
+        """Checkpoint dict (src/training/chekpoints.py keys).  Model tensors are cloned: the Outlooker's
+        v / attn parameters are views into one padded [ld, C] buffer (_AliasedConcat), and a state dict
+        of shared-storage views would make torch.save write the whole padded buffer and safetensors-style
+        writers refuse it."""
+        model = {k: v.detach().clone() for k, v in self.core.state_dict().items()}
+        return {"model": model, "optimizer": self.opt.state_dict(), "scheduler": self.sched.state_dict()}
 
     def load_state_dict(self, sd):
         """In place: a recorded graph keeps reading the same parameter / moment / lr tensors."""

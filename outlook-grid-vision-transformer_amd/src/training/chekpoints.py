@@ -15,8 +15,10 @@ import torch
 def save_checkpoint(path: str, model, optimizer, scheduler, scaler, epoch: int, best_top1: float,
                     extra: dict | None = None):
     core = model.module if hasattr(model, "module") else model
+    # cloned: the Outlooker's v / attn tensors are views into one padded buffer (_AliasedConcat), and
+    # torch.save of shared-storage views writes that whole buffer
     ckpt = {
-        "model": core.state_dict(),
+        "model": {k: v.detach().clone() for k, v in core.state_dict().items()},
         "optimizer": optimizer.state_dict() if optimizer is not None else None,
         "scheduler": scheduler.state_dict() if scheduler is not None else None,
         "scaler": scaler.state_dict() if scaler is not None else None,

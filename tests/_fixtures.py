@@ -137,3 +137,100 @@ def bf16_storage_error(fn, x, ref):
     with torch.no_grad(), Bf16Storage():
         y = fn(x.to(torch.bfloat16).to(torch.float32))
     return maxabs(y.float(), ref)
+
+
+# ------------------------------------------------------------------ training-step fixture (make_golden.py r4)
+def train_batches(meta):
+    """The fixture's batches: images gen_params.tensor('train_x_<t>'), labels gen_params.labels('train_t_<t>');
+    step meta['nan_step'] holds one NaN pixel (the reference skips that step)."""
+    out = []
+    for t in range(meta["steps"]):
+        x = gp.tensor(f"train_x_{t}", (meta["B"], 3, 32, 32))
+        if t == meta["nan_step"]:
+            x[0, 0, 0, 0] = np.nan
+        out.append((torch.from_numpy(x), torch.from_numpy(gp.labels(f"train_t_{t}", meta["B"], meta["num_classes"]))))
+    return out
+
+
+def update_sketch(key, d):
+    """tests/golden/make_golden.py::update_sketch on a torch / numpy update (float64)."""
+    d = torch.as_tensor(d).double().cpu()
+    d = d.reshape(d.shape[0], -1) if d.dim() > 0 else d.reshape(1, 1)
+    L = torch.from_numpy(gp.sketch_matrix(key + ":rows", d.shape[0], 8))
+    R = torch.from_numpy(gp.sketch_matrix(key, d.shape[1], 8))
+    return L.T @ d @ R
+
+
+def train_stable_masks(meta, arr, params):
+    """name -> float64 0/1 mask of the elements the fixture's update sketches cover (make_golden.py main_r4:
+    elements whose gradient was rounding noise at some step take a +-lr Adam step of random sign in any
+    fp32 implementation and are left out)."""
+    flat = torch.ones(sum(params[k].numel() for k in meta["param_names"]), dtype=torch.float64)
+    flat[torch.from_numpy(arr["unstable"])] = 0.0
+    out, off = {}, 0
+    for k in meta["param_names"]:
+        n = params[k].numel()
+        out[k] = flat[off:off + n].view(params[k].shape)
+        off += n
+    return out
+
+
+def train_step_errors(meta, arr, t, params, p0, masks=None):
+    """Deviation of parameters ``params`` (name -> tensor, any device) after fixture step t from the
+    reference's, with p0 (name -> tensor) the common start.  Returns a dict of maxima over parameters:
+      upd    max|sketch(ours) - sketch(ref)| / max(|update_ref|_F, 1e-12) on the stable elements -- the
+             relative error of the update
+      dn     max| |update|_F ours - ref | / max(|update_ref|_F, 1e-12)
+      norm   max| |p|_F ours - ref | / max(1, |p|_F ref)
+      full   (steps recorded in full) max|p - p_ref| / max(1, max|p_ref|) over the stable elements of every
+             small parameter
+    and 'worst' = the parameter name behind the largest 'upd'."""
+    names = meta["param_names"]
+    if masks is None:
+        masks = train_stable_masks(meta, arr, params)
+    dsk, dn, pn = arr[f"dsk{t}"], arr[f"dn{t}"], arr[f"pn{t}"]
+    upd = dnerr = norm = 0.0
+    worst = None
+    for i, k in enumerate(names):
+        p = params[k].detach().double().cpu()
+        d = (p - p0[k].detach().double().cpu()) * masks[k]
+        scale = max(float(dn[i]), 1e-12)
+        e = (update_sketch(k, d) - torch.from_numpy(dsk[i])).abs().max().item() / scale
+        if float(dn[i]) > 0 and e > upd:
+            upd, worst = e, k
+        if float(dn[i]) > 0:
+            dnerr = max(dnerr, abs(d.norm().item() - float(dn[i])) / scale)
+        norm = max(norm, abs(p.norm().item() - float(pn[i])) / max(1.0, float(pn[i])))
+    out = dict(upd=upd, dn=dnerr, norm=norm, worst=worst)
+    if f"p{t}" in arr:
+        flat, off, full = arr[f"p{t}"], 0, 0.0
+        for k in names:
+            p = params[k].detach().double().cpu()
+            if p.numel() > meta["full_max"]:
+                continue
+            ref = torch.from_numpy(flat[off:off + p.numel()]).double().view_as(p.contiguous())
+            off += p.numel()
+            full = max(full, ((p.contiguous() - ref) * masks[k]).abs().max().item() / max(1.0, ref.abs().max().item()))
+        assert off == flat.size
+        out["full"] = full
+    return out
+
+
+def record(kind: str, **fields):
+    """Append one JSON line of measured parity numbers to $OGV_PARITY_LOG (when set): the GPU runs
+    write the achieved errors next to their bars, and the committed copy under profiles/ is the
+    evidence each bar cites."""
+    import json
+    import os
+    path = os.environ.get("OGV_PARITY_LOG")
+    if not path:
+        return
+
+    def _py(v):
+        if isinstance(v, (np.floating, np.integer)):
+            return v.item()
+        if isinstance(v, torch.Tensor):
+            return v.item() if v.numel() == 1 else v.tolist()
+        return v
+    with open(path, "a") as f:
+        f.write(json.dumps(dict(kind=kind, **{k: _py(v) for k, v in fields.items()})) + "\n")

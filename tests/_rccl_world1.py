@@ -1,0 +1,61 @@
+"""Child process of tests/test_gpu_train.py::test_rccl_world1_dp_path_matches_single_process (GPU box
+only): a world-size-1 RCCL ("nccl") process group and the Trainer's data-parallel path on it, against
+the single-process Trainer.  Prints one JSON line per mode; the parent asserts on them."""
+import json
+import os
+import pathlib
+import socket
+import sys
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+for p in (ROOT / "outlook-grid-vision-transformer_amd", ROOT / "tests", ROOT / "tests" / "golden"):
+    sys.path.insert(0, str(p))
+
+with socket.socket() as sk:     # env rendezvous on 127.0.0.1, set before anything touches the GPU
+    sk.bind(("127.0.0.1", 0))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(sk.getsockname()[1]))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+
+def main():
+    import ogv
+    from ogv.train import MODEL_CONFIGS, Trainer, build_model
+    ogv.load()
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    print(json.dumps({"stage": "init", "backend": dist.get_backend()}), flush=True)
+    cfg = MODEL_CONFIGS["model_a_7m"]
+    batches = []
+    for i in range(4):
+        g = torch.Generator(device="cuda").manual_seed(90 + i)
+        batches.append((torch.randn(16, 3, 32, 32, device="cuda", generator=g).contiguous(memory_format=torch.channels_last),
+                        torch.randint(0, 100, (16,), device="cuda", generator=g)))
+    runs = {}
+    for mode in ("plain", "dp_graph", "dp_capture", "plain_eager", "dp_eager"):
+        torch.backends.cudnn.benchmark = False
+        torch.manual_seed(31)
+        m = build_model(dict(type="model_a", num_classes=100, stem_dim=64, dpr_max=0.0, stages=cfg["stages"]))
+        m = m.cuda().to(memory_format=torch.channels_last)
+        dp = mode.startswith("dp")
+        t = Trainer(m, total_steps=50, warmup_ratio=0.1, graphs=not mode.endswith("eager"), capture_warmup=1,
+                    force_dp=dp, dp_capture_collective=mode == "dp_capture")
+        assert t.dp == dp and t.dp_capture_collective == (mode == "dp_capture")
+        losses = [t.step(*b).float().item() for b in batches]     # eager, capture, replay, replay
+        torch.cuda.synchronize()
+        state = [p.detach().clone() for p in m.parameters()] + [b.detach().clone() for b in m.buffers()]
+        runs[mode] = (losses, state)
+        out = {"mode": mode, "backend": t.backend, "losses": losses, "graphs": t.graphs}
+        for ref in ("plain", "plain_eager"):
+            if ref in runs and ref != mode:
+                out["max_param_diff_vs_" + ref] = max(float((a.double() - b.double()).abs().max())
+                                                      for a, b in zip(state, runs[ref][1]) if a.is_floating_point())
+        print(json.dumps(out), flush=True)
+        del t
+    torch.cuda.synchronize()
+    dist.destroy_process_group()
+    print(json.dumps({"stage": "done"}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -161,6 +161,9 @@ def test_golden_bf16(name):
     bound, e_emul = _bf16_bound(meta, arr, arr["y"], _oracle_fn(meta), torch.from_numpy(x).to(DEV))
     print(f"{name}: bf16 fwd max|d| ours {e:.3e} (bound {bound:.3e}, storage emulation {e_emul}) "
           f"torch-autocast {e_torch:.3e}")
+    fx.record("golden_bf16", fixture=name, train=bool(meta.get("train", False)), ours=e, bound=bound,
+              bound_north_star=1e-2 * max(1.0, float(np.abs(arr["y"]).max())), storage_emulation=e_emul,
+              oracle_gpu_autocast=e_torch)
     assert e <= bound, f"{name} bf16 fwd max|d| {e:.3e} > {bound:.3e} (torch {e_torch:.3e})"
     e = fx.maxabs(dx.float(), arr["dx"])
     assert e <= _tol(arr["dx"], 3e-2), f"{name} bf16 dx max|d| {e:.3e}"
@@ -194,6 +197,21 @@ def test_outlook_attn_forward_hook_sees_logits():
     m.attn.register_forward_hook(lambda mod, i, o: seen.append(o.shape))
     m(torch.randn(2, 32, 8, 8, device=DEV))
     assert seen == [torch.Size([2, 36, 8, 8])]
+
+
+def _oracle_gpu_autocast_logits_error(meta, arr):
+    """max|logits - ref| of the oracle (the reference's ops restated on stock ATen) run on THIS GPU under
+    torch.autocast(bf16): what the reference's own model gives in bf16 on a HIP device -- the second
+    comparator of the bf16 bars (tests only)."""
+    p = {k: v.to(DEV) for k, v in fx.oracle_params(meta, requires_grad=False).items()}
+    x = torch.from_numpy(gp.input_from_spec(meta["x"])).to(DEV)
+    train = meta["mode"] == "train"
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        if meta["kind"] == "model_b":
+            y = orc.model_b(x, p, meta["stages"], meta["outlooker_front_depth"], train)
+        else:
+            y = orc.model_a(x, p, meta["stages"], train)
+    return fx.maxabs(y.float(), arr["logits"])
 
 
 MODEL_FIXTURES = [n for n in fx.fixture_names("model_a_") + fx.fixture_names("model_b_") if not n.endswith("_autocast")]
@@ -240,8 +258,12 @@ def test_model_logits(name, dtype):
         e_ref = float(np.abs(arr["logits_cpu_bf16_autocast"].astype(np.float64) - arr["logits"]).max())
         bound = max(bound, e_ref)
     lref = float(arr["loss"][0])
+    e_gpu_ac = _oracle_gpu_autocast_logits_error(meta, arr) if bf else None
     print(f"{name} {'bf16' if bf else 'fp32'}: logits max|d| {e:.3e} (bound {bound:.3e}, |ref| {ref_max:.3f}, "
-          f"reference's own bf16 {e_ref}), loss {loss.item():.6f} vs {lref:.6f}")
+          f"reference's own bf16 {e_ref}, oracle under GPU autocast {e_gpu_ac}), loss {loss.item():.6f} vs {lref:.6f}")
+    fx.record("model_logits", fixture=name, dtype="bf16" if bf else "fp32", mode=mode, ours=e, bound=bound,
+              bound_north_star=(BF16_FWD if bf else 1e-3) * max(1.0, ref_max), ref_abs_max=ref_max,
+              reference_cpu_autocast=e_ref, oracle_gpu_autocast=e_gpu_ac, loss=loss.item(), loss_ref=lref)
     loss.backward()
     names = meta["param_names"]
     params = dict(mod.named_parameters())

@@ -355,28 +355,46 @@ def test_graph_dp_world2_matches_single_process(tmp_path):
     assert d_dp ** 0.5 <= 0.25 * d_move ** 0.5, (d_dp ** 0.5, d_move ** 0.5)
 
 
-def test_deferred_param_reductions_match_immediate():
+DEFER_CASES = [("model_a_7m", 64, 0.0), ("model_a_7m", 32, 0.07), ("model_a_14m_tin64", 8, 0.08),
+               ("model_a_22m_224", 2, 0.11), ("model_b_cifar100", 16, 0.1)]
+
+
+@pytest.mark.parametrize("cfg_name,B,dpr", DEFER_CASES, ids=[f"{c}_b{b}_dpr{d}" for c, b, d in DEFER_CASES])
+def test_deferred_param_reductions_match_immediate(cfg_name, B, dpr):
     """The Trainer's backward records the parameter-gradient column reductions (Linear weight / bias
-    gradients, LayerNorm gamma / beta) and runs them as one batched launch at its end
-    (functional.deferred_param_reductions): every gradient equals the immediate path's (same
-    single-pass arithmetic where that path used it, fp32 rounding of a different split otherwise),
-    and the deferral really took the reductions (dozens pending before the flush)."""
+    gradients, LayerNorm gamma / beta, the fused MBConv's weight gradients) and runs them as one batched
+    launch at its end (functional.deferred_param_reductions): every gradient equals the immediate path's
+    (same single-pass arithmetic where that path used it, fp32 rounding of a different split otherwise),
+    and the deferral really took the reductions (dozens pending before the flush) -- on every model
+    configuration, with DropPath on (its per-row scales enter the weight-gradient prologues; the same
+    seed draws the same masks in both runs)."""
     from ogv import functional as OF
     from ogv._lib import load
-    from ogv.train import Trainer
-    x, y = _batch(64, 5)
+    from ogv.train import MODEL_CONFIGS, Trainer, build_model
+    cfg = dict(MODEL_CONFIGS[cfg_name])
+    img = cfg.pop("img")
+    cfg["dpr_max"] = dpr
+    g = torch.Generator(device="cuda").manual_seed(5)
+    x = torch.randn(B, 3, img, img, device="cuda", generator=g).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, cfg["num_classes"], (B,), device="cuda", generator=g)
     grads, pending = [], []
     for defer in (False, True):
-        m = _model(13)
+        torch.manual_seed(13)
+        m = build_model(cfg).cuda().to(memory_format=torch.channels_last)
         t = Trainer(m, total_steps=50, graphs=False, defer_reductions=False)
         t.opt.zero_grad(set_to_none=True)
+        torch.manual_seed(99)                  # the same DropPath draws in both runs
         with OF.deferred_param_reductions(defer):
             loss = t._loss(x, y)
             loss.backward()
             pending.append(load().ogv_reduce_defer(1 if defer else 0))
         torch.cuda.synchronize()
         grads.append([p.grad.detach().clone() for p in m.parameters()])
-    assert pending[0] == 0 and pending[1] >= 50, pending
+        # every parameter received a distinct gradient tensor (a deferred destination written twice or
+        # into a stolen / cloned buffer would alias or leave one unwritten)
+        ptrs = [p.grad.data_ptr() for p in m.parameters()]
+        assert len(set(ptrs)) == len(ptrs)
+    assert pending[0] == 0 and pending[1] >= 20, pending
     same = 0
     for a, b in zip(*grads):
         assert torch.isfinite(b).all()
@@ -400,7 +418,7 @@ class _ParamBag(torch.nn.Module):
         self.bias = torch.nn.Parameter(torch.randn(130, generator=g))
 
 
-@pytest.mark.parametrize("clip", [1.0, None, 1e6])
+@pytest.mark.parametrize("clip", [1.0, None, 1e6, 0.0])
 def test_native_clip_adamw_matches_torch(clip):
     """ogv_clip_adamw (the Trainer's default) against torch's clip_grad_norm_(foreach) + AdamW(fused,
     capturable).step() on the same parameters, gradients and schedule, over 4 steps with a skipped
@@ -430,3 +448,130 @@ def test_native_clip_adamw_matches_torch(clip):
             assert float(s0["step"]) == float(s1["step"]) == (step + 1 if step < 2 else step)
             torch.testing.assert_close(s0["exp_avg"], s1["exp_avg"], rtol=1e-5, atol=1e-7)
             torch.testing.assert_close(s0["exp_avg_sq"], s1["exp_avg_sq"], rtol=1e-5, atol=1e-9)
+
+
+def test_state_dict_tensors_do_not_share_storage(tmp_path):
+    """the Outlooker's v / attn parameters are views into one padded [ld, C] buffer after the
+    first forward; Trainer.state_dict() and save_checkpoint write independent, unpadded tensors (the file
+    holds the parameters' bytes, not the padded buffer's)."""
+    from ogv.train import Trainer
+    from src.training.chekpoints import save_checkpoint
+    m = _model(3)
+    t = Trainer(m, total_steps=10, graphs=False)
+    t.step(*_batch(8, 1))
+    live = dict(m.state_dict())
+    shared = [k for k, v in live.items() if v.untyped_storage().nbytes() > v.numel() * v.element_size()]
+    assert shared, "expected the Outlooker's aliased parameter buffer"
+    for k, v in t.state_dict()["model"].items():
+        assert v.untyped_storage().nbytes() == v.numel() * v.element_size(), k
+        assert torch.equal(v, live[k])
+    save_checkpoint(str(tmp_path / "c.pt"), m, None, None, None, epoch=0, best_top1=0.0)
+    ck = torch.load(tmp_path / "c.pt", map_location="cpu", weights_only=True)
+    for k, v in ck["model"].items():
+        assert v.untyped_storage().nbytes() == v.numel() * v.element_size(), k
+
+
+def test_native_optimizer_after_contiguous_moment_resume(tmp_path):
+    """a checkpoint whose AdamW moments are contiguous (the reference's layout) resumed into a
+    channels_last model: load_optimizer_state re-lays them like their parameters, so the native clip +
+    AdamW keeps running (no silent per-step torch fallback)."""
+    from ogv.train import Trainer
+    from src.training.chekpoints import load_checkpoint, save_checkpoint
+    m0 = _model(4)
+    t0 = Trainer(m0, total_steps=10, graphs=False)
+    t0.step(*_batch(8, 2))
+    sd = t0.opt.state_dict()
+    for st in sd["state"].values():
+        for k in ("exp_avg", "exp_avg_sq"):
+            st[k] = st[k].contiguous()
+    torch.save({"model": m0.state_dict(), "optimizer": sd, "scheduler": t0.sched.state_dict(), "scaler": None,
+                "epoch": 0, "best_top1": 0.0, "extra": {}}, tmp_path / "r.pt")
+    m1 = _model(5)
+    t1 = Trainer(m1, total_steps=10, graphs=False)
+    load_checkpoint(str(tmp_path / "r.pt"), m1, t1.opt, t1.sched, None)
+    t1.step(*_batch(8, 3))
+    assert t1.native_optimizer_fallbacks == 0
+
+
+def _free_port():
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def test_rccl_world1_dp_path_matches_single_process():
+    """The RCCL branch executed: a world-size-1 "nccl" (= RCCL) process group, the Trainer's data-parallel
+    path forced on (force_dp: rank-0 broadcast, gradient + buffer + non-finite-flag bucket, all_reduce), in
+    graph mode (graph A -> RCCL all_reduce -> graph B), with the all_reduce captured inside the step's graph
+    (dp_capture_collective), and eagerly with the bucketed asynchronous all_reduces during backward: every
+    loss and parameter equals the single-process Trainer's (the all_reduce of one rank is the identity; the
+    eager bucket path runs its parameter-gradient reductions immediately instead of deferred, so it is held
+    to one lr step per element, Adam's sign flips of near-zero gradients).  Runs tests/_rccl_world1.py as a
+    child process (its own process group and HIP context; an RCCL abort cannot take the test runner down)."""
+    import json
+    import pathlib
+    import subprocess
+    import sys
+    here = pathlib.Path(__file__).resolve().parent
+    r = subprocess.run([sys.executable, str(here / "_rccl_world1.py")], capture_output=True, text=True, timeout=240)
+    print(r.stdout[-4000:], r.stderr[-4000:])
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    res = {d["mode"]: d for d in lines if "mode" in d}
+    assert set(res) >= {"plain", "dp_graph", "dp_capture", "plain_eager", "dp_eager"}, (r.returncode, list(res))
+    for mode in ("dp_graph", "dp_capture", "dp_eager"):
+        assert res[mode]["backend"] == "nccl", res[mode]
+    for mode, ref in (("dp_graph", "plain"), ("dp_capture", "plain")):
+        assert res[mode]["losses"] == res[ref]["losses"], (mode, res[mode]["losses"], res[ref]["losses"])
+        assert res[mode]["max_param_diff_vs_" + ref] == 0.0, res[mode]
+    la, lb = res["dp_eager"]["losses"], res["plain_eager"]["losses"]
+    assert all(abs(a - b) <= 1e-3 * max(1.0, abs(b)) for a, b in zip(la, lb)), (la, lb)
+    assert res["dp_eager"]["max_param_diff_vs_plain_eager"] <= 4 * 2 * 5e-4 + 1e-6
+    assert r.returncode == 0, r.returncode
+
+
+def _ddp_worker(rank, world, port, out):
+    import os
+    import torch.distributed as dist
+    from ogv.train import Trainer, wrap_ddp
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import ogv
+    ogv.load()
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.backends.cudnn.benchmark = False
+        res = {}
+        for kind in ("ddp", "bare"):
+            m = _model(41).eval()                 # running-statistics BN: the shards see the same model
+            model = wrap_ddp(m, torch.device("cuda", 0)) if kind == "ddp" else m
+            t = Trainer(model, total_steps=50, warmup_ratio=0.1, graphs=False)
+            assert t.ddp == (kind == "ddp")
+            assert not (t.ddp and t.defer_reductions), "deferral must be off under DDP"
+            for i in range(2):
+                x, y = _batch(16, 100 + i)
+                t.step(x[rank * 8:(rank + 1) * 8].contiguous(memory_format=torch.channels_last), y[rank * 8:(rank + 1) * 8])
+            res[kind] = [p.detach().cpu() for p in m.parameters()]
+        torch.save(res, f"{out}/d{rank}.pt")
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ddp_wrapped_model_world2(tmp_path):
+    """a DDP-wrapped model handed to the Trainer.  DDP's reducer copies each gradient
+    into its bucket when AccumulateGrad fires, so the deferred parameter-gradient reductions must be off
+    (they would be all-reduced before being written).  Two gloo ranks on one GPU, eval-mode BatchNorm:
+    the DDP run equals the Trainer's own DP path on the same shards (one lr step per element: Adam sign
+    flips of near-zero gradients) and both ranks agree."""
+    import torch.multiprocessing as mp
+    mp.spawn(_ddp_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    r0 = torch.load(tmp_path / "d0.pt", weights_only=True)
+    r1 = torch.load(tmp_path / "d1.pt", weights_only=True)
+    for a, b in zip(r0["ddp"], r1["ddp"]):
+        assert torch.equal(a, b), "DDP ranks diverged"
+    init = [p.detach().cpu() for p in _model(41).parameters()]
+    move = sum(float((a - p0).double().norm() ** 2) for a, p0 in zip(r0["bare"], init)) ** 0.5
+    diff = 0.0
+    for a, b in zip(r0["ddp"], r0["bare"]):
+        assert float((a - b).abs().max()) <= 2 * 2 * 5e-4 + 1e-6
+        diff += float((a - b).double().norm() ** 2)
+    assert diff ** 0.5 <= 0.25 * move, (diff ** 0.5, move)

@@ -1,0 +1,91 @@
+"""The benchmarked training step against the REFERENCE'S OWN training loop (fixture train_steps_7m_b16,
+tests/golden/make_golden.py r4: src/training/one_epoch_train.py:85-153 with the AdamW / param groups of
+train_full_model.py:56-66 and WarmupCosineLR of warmup.py:29-59, run on Model-A-7M, B = 16, fp32, five
+batches, the third holding a NaN pixel so the reference skips it).
+
+The Trainer (fp32: amp_dtype=None) runs the same five batches eagerly and as hipGraph replays, with the
+native clip + AdamW (ogv_clip_adamw, the default) and with torch's: per step the loss (1e-4), the lr the
+step used and the one it leaves (fp32 rounding of the reference's double), the schedule counter, the skip,
+and the parameters -- the update p_t - p_0 of every parameter through the fixture's fixed two-sided sketch
+(relative error of the update <= 2e-3: measured 4.8e-4 - 9.2e-4 on MI355X, profiles/r04_parity.jsonl; two CPU
+fp32 implementations, the reference and the oracle, differ by <= 2.2e-4, tests/test_oracle_golden.py::
+test_train_steps_oracle), every small parameter in full at the recorded steps (1e-4 * max(1, |p|); measured
+<= 2.9e-6), the parameters' norms (1e-4 * max(1, |p|): they include the noise elements below), and the
+BatchNorm running buffers before the NaN step.  Elements whose
+gradient is rounding noise (the key slice of qkv.bias, the last block's fc2.bias before the head's
+train-mode BatchNorm, ~0.6% of all) take a +-lr Adam step of random sign in any fp32 implementation and
+are excluded by the fixture's mask (make_golden.py main_r4)."""
+import numpy as np
+import pytest
+import torch
+
+import _fixtures as fx
+import gen_params as gp
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+UPD_TOL, FULL_TOL, LOSS_TOL, NORM_TOL = 2e-3, 1e-4, 1e-4, 1e-4
+
+
+@pytest.fixture(autouse=True, scope="module")
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import ogv
+    ogv.load()
+
+
+@pytest.mark.parametrize("native", [True, False], ids=["native_opt", "torch_opt"])
+@pytest.mark.parametrize("graphs", [False, True], ids=["eager", "graph"])
+def test_train_steps_match_reference(graphs, native):
+    from ogv.train import Trainer
+    from src.Model_A_OutGridNet import MaxOutNet
+    from src.stage_config import StageCfg
+    meta, arr = fx.load("train_steps_7m_b16")
+    torch.backends.cudnn.benchmark = False
+    m = MaxOutNet(meta["num_classes"], [StageCfg(**s) for s in meta["stages"]], 3, meta["stem_dim"], meta["dpr_max"])
+    gp.fill_module(m, meta["seed"])
+    m = m.to(DEV).to(memory_format=torch.channels_last).train()
+    params = dict(m.named_parameters())
+    assert list(params) == meta["param_names"]
+    p0 = {k: p.detach().clone() for k, p in params.items()}
+    masks = fx.train_stable_masks(meta, arr, params)
+    t = Trainer(m, lr=meta["lr"], weight_decay=meta["weight_decay"], clip=meta["clip"],
+                label_smoothing=meta["label_smoothing"], total_steps=meta["total_steps"],
+                warmup_ratio=meta["warmup_ratio"], min_lr=meta["min_lr"], amp_dtype=None, graphs=graphs,
+                capture_warmup=1, native_optimizer=native)
+    assert [len(g["params"]) for g in t.opt.param_groups] == meta["group_sizes"]
+    worst = dict(upd=0.0, full=0.0, loss=0.0)
+    for step, (x, y) in enumerate(fx.train_batches(meta)):
+        lr_used = [float(g["lr"]) for g in t.opt.param_groups]
+        loss = float(t.step(x.to(DEV).contiguous(memory_format=torch.channels_last), y.to(DEV)))
+        torch.cuda.synchronize()
+        lr_after = [float(g["lr"]) for g in t.opt.param_groups]
+        for got, ref in zip(lr_used + lr_after, list(arr["lr_used"][step]) + list(arr["lr_after"][step])):
+            assert abs(got - ref) <= 1.2e-7 * ref, (step, got, ref)     # fp32 rounding of the double
+        assert t.sched.step_num == int(arr["sched_step"][step])
+        skipped = bool(arr["skipped"][step])
+        assert (not np.isfinite(loss)) == skipped, (step, loss)
+        if not skipped:
+            worst["loss"] = max(worst["loss"], abs(loss - float(arr["loss"][step])))
+            assert abs(loss - float(arr["loss"][step])) <= LOSS_TOL, (step, loss, float(arr["loss"][step]))
+        e = fx.train_step_errors(meta, arr, step, params, p0, masks)
+        print(f"step {step}: loss {loss:.6f} ref {float(arr['loss'][step]):.6f} lr {lr_used[0]:.6g} -> {lr_after[0]:.6g} {e}")
+        assert e["upd"] <= UPD_TOL and e["dn"] <= UPD_TOL, (step, e)
+        assert e["norm"] <= NORM_TOL and e.get("full", 0.0) <= FULL_TOL, (step, e)
+        worst["upd"] = max(worst["upd"], e["upd"])
+        worst["full"] = max(worst["full"], e.get("full", 0.0))
+        if f"buf{step}" in arr:
+            bufs = [b for k, b in m.named_buffers() if k.endswith(("running_mean", "running_var"))]
+            got = torch.cat([b.detach().float().reshape(-1).cpu() for b in bufs])
+            ref = torch.from_numpy(arr[f"buf{step}"])
+            assert got.shape == ref.shape
+            assert fx.maxabs(got, ref) <= 1e-4 * max(1.0, ref.abs().max().item())
+    assert t.nonfinite_steps == int(arr["skipped"].sum())
+    if graphs:
+        assert t._g is not None and t.eager_fallbacks == 0
+    if native:
+        assert t.native_optimizer_fallbacks == 0
+    fx.record("train_steps", fixture="train_steps_7m_b16", graphs=graphs, native_optimizer=native,
+              loss_max_abs=worst["loss"], loss_tol=LOSS_TOL, update_rel_max=worst["upd"], update_tol=UPD_TOL,
+              param_full_max=worst["full"], param_tol=FULL_TOL)

@@ -139,3 +139,31 @@ def test_model_b(name):
     np.testing.assert_allclose(gn, arr["grad_norms"], rtol=2e-4, atol=1e-7)
     fx.compare_grads({k: p[k].grad for k in names}, arr, 1e-4, 1e-6, name)
     assert sum(p[k].numel() for k in names) == meta["n_params"]
+
+
+def test_train_steps_oracle():
+    """The oracle's training loop (optimizer, warmup-cosine schedule, clip, non-finite skip) against
+    the reference's own train_one_epoch run (fixture train_steps_7m_b16, make_golden.py r4)."""
+    meta, arr = fx.load("train_steps_7m_b16")
+    shapes = orc.model_a_shapes(meta["stages"], meta["num_classes"], 3, meta["stem_dim"])
+    p = orc.make_params(shapes, lambda k, s: gp.param_value(k, s, meta["seed"]))
+    assert [k for k, t in p.items() if t.requires_grad] == meta["param_names"]
+    p0 = {k: t.detach().clone() for k, t in p.items()}
+    rec = []
+
+    def on_step(t, loss, lr_used, skipped, step_num):
+        e = fx.train_step_errors(meta, arr, t, {k: p[k] for k in meta["param_names"]}, p0)
+        rec.append((t, float(loss), lr_used, skipped, step_num, e))
+
+    orc.train_steps(fx.train_batches(meta), p, meta["stages"], lr=meta["lr"], weight_decay=meta["weight_decay"],
+                    clip=meta["clip"], label_smoothing=meta["label_smoothing"], total_steps=meta["total_steps"],
+                    warmup_steps=int(meta["total_steps"] * meta["warmup_ratio"]), min_lr=meta["min_lr"],
+                    on_step=on_step)
+    for t, loss, lr_used, skipped, step_num, e in rec:
+        print(t, loss, e)
+        assert skipped == bool(arr["skipped"][t])
+        assert step_num == arr["sched_step"][t]
+        assert lr_used == list(arr["lr_used"][t])
+        if not skipped:
+            assert abs(loss - arr["loss"][t]) <= 1e-5, (t, loss)
+        assert e["upd"] <= 1e-3 and e["dn"] <= 1e-3 and e["norm"] <= 1e-5 and e.get("full", 0.0) <= 1e-6, (t, e)

@@ -322,6 +322,18 @@ int ogv_mix_targets(const int64_t* targets, const int64_t* perm, float* out, int
 /* Elementwise helpers used by the autograd glue. */
 int ogv_cast(const void* src, ogv_dtype src_dt, void* dst, ogv_dtype dst_dt, size_t n, void* stream);
 
+/* Batched fp32 segment copies (the data-parallel gradient bucket: the pack before the all_reduce and
+ * the unpack after it replace torch.cat / _foreach_copy_, which issue one hipMemcpyAsync per tensor):
+ * for every segment dst[0:numel] = src[0:numel] * scale, or = 0 when src is NULL.  `segs` is a HOST
+ * array; 64 segments travel in each launch's kernel arguments (graph-capturable).  Segments must not
+ * overlap.  Replaces nothing in the reference (it has no data parallelism: SURVEY §8e). */
+typedef struct {
+  const float* src;     /* NULL: zero fill */
+  float* dst;
+  long long numel;      /* < 2^31 */
+} ogv_copy_seg;
+int ogv_copy_batch_f32(const ogv_copy_seg* segs, int n, float scale, void* stream);
+
 /* Gradient clipping + AdamW of one training step (src/training/one_epoch_train.py:121/141
  * clip_grad_norm_(model.parameters(), grad_clip_norm); src/training/train_full_model.py:57
  * torch.optim.AdamW(param_groups, betas=(0.9, 0.999), eps=1e-8)), as torch's

@@ -58,6 +58,10 @@ class AdamWGroup(ctypes.Structure):
                 ("one_minus_beta1", _f), ("one_minus_beta2", _f)]
 
 
+class CopySeg(ctypes.Structure):
+    _fields_ = [("src", _p), ("dst", _p), ("numel", ctypes.c_longlong)]
+
+
 _PD = ctypes.POINTER(MBConvDesc)
 _PCD = ctypes.POINTER(ConvBNDesc)
 _PCP = ctypes.POINTER(ConvBNParams)
@@ -114,6 +118,7 @@ SIGNATURES = {
     "ogv_clip_adamw_ws_bytes": (_sz, [ctypes.POINTER(AdamWTensor), _i]),
     "ogv_clip_adamw": (_i, [ctypes.POINTER(AdamWTensor), _i, ctypes.POINTER(AdamWGroup), _i, _p, _f, _p, _p]),
     "ogv_schedule_step": (_i, [_p, _p, _p, ctypes.POINTER(_p), ctypes.POINTER(_f), _i, _i, _i, _f, _p]),
+    "ogv_copy_batch_f32": (_i, [ctypes.POINTER(CopySeg), _i, _f, _p]),
 }
 
 OGV_F32, OGV_BF16 = 0, 1

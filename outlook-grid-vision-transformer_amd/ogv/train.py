@@ -439,7 +439,47 @@ class Trainer:
         torch.cat(self._meta_values(loss), out=self.meta)
         self._meta_work = torch.distributed.all_reduce(self.meta, async_op=True)
 
+    def _copy_segments(self, segs, scale=1.0):
+        """dst <- src * scale (src None: zeros) for every (src, dst, numel) of fp32 device pointers, in
+        ceil(n / 64) native launches (ogv_copy_batch_f32) instead of one hipMemcpyAsync per tensor."""
+        from . import _lib
+        if not segs:
+            return
+        arr = (_lib.CopySeg * len(segs))(*[_lib.CopySeg(s, d, n) for s, d, n in segs])
+        _lib.check(_lib.load().ogv_copy_batch_f32(arr, len(segs), float(scale),
+                                                  torch.cuda.current_stream().cuda_stream), "ogv_copy_batch_f32")
+
+    def _flat_offsets(self):
+        if getattr(self, "_offs", None) is None:
+            offs, o = [], 0
+            for n in self._sizes + self._bsizes:
+                offs.append(o)
+                o += n
+            self._offs = offs
+        return self._offs
+
+    def _dense_fp32(self, t):
+        return (t is not None and t.is_cuda and t.dtype == torch.float32
+                and (t.is_contiguous() or (t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last))))
+
     def _flatten(self, loss):
+        """[gradients / world | rank 0's buffers (others: zeros) | non-finite flag] -> self.flat.  On the
+        device: batched native copies of every dense fp32 tensor straight from its storage (a dense
+        tensor's bytes are its elements in memory order, channels_last included: the unflatten writes
+        them back the same way), torch.cat otherwise."""
+        if self.device_side and all(self._dense_fp32(p.grad) or p.grad is None for p in self.params) \
+                and all(self._dense_fp32(b) for b in self._bufs):
+            base, esz = self.flat.data_ptr(), 4
+            offs = self._flat_offsets()
+            segs = [(p.grad.data_ptr() if p.grad is not None else None, base + esz * o, n)
+                    for p, o, n in zip(self.params, offs, self._sizes)]
+            self._copy_segments(segs, 1.0 / self.world)
+            boffs = offs[len(self._sizes):]
+            bsegs = [(b.data_ptr() if self.rank == 0 else None, base + esz * o, n)
+                     for b, o, n in zip(self._bufs, boffs, self._bsizes)]
+            bsegs.append((self._found.data_ptr(), base + esz * (self._ng + self._nb), 1))
+            self._copy_segments(bsegs)
+            return
         grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in self.params]
         torch.cat([g.reshape(-1) for g in grads] + self._meta_values(loss), out=self.flat)
         self.flat[:self._ng].mul_(1.0 / self.world)
@@ -453,10 +493,18 @@ class Trainer:
         return meta[self._nb:]
 
     def _unflatten(self):
-        views = [v.view_as(p) for v, p in zip(self.flat[:self._ng].split(self._sizes), self.params)]
-        for p, v in zip(self.params, views):
+        for p in self.params:
             if p.grad is None:
                 p.grad = torch.empty_like(p)
+        if self.device_side and all(self._dense_fp32(p.grad) for p in self.params) \
+                and all(self._dense_fp32(b) for b in self._bufs):
+            base, esz = self.flat.data_ptr(), 4
+            offs = self._flat_offsets()
+            segs = [(base + esz * o, p.grad.data_ptr(), n) for p, o, n in zip(self.params, offs, self._sizes)]
+            segs += [(base + esz * o, b.data_ptr(), n) for b, o, n in zip(self._bufs, offs[len(self._sizes):], self._bsizes)]
+            self._copy_segments(segs)
+            return self.flat[self._ng + self._nb:]
+        views = [v.view_as(p) for v, p in zip(self.flat[:self._ng].split(self._sizes), self.params)]
         torch._foreach_copy_([p.grad for p in self.params], views)
         return self._apply_meta(self.flat[self._ng:])
 

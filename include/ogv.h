@@ -107,8 +107,9 @@ size_t ogv_outlook_bwd_ws_bytes(int B, int H, int W, int C, int heads, int k, og
  * (rows C .. C+heads*9-1 are attn.weight, the rest zero), bias: fp32 [ldc] or NULL.
  * Writes y [M, C] and, when cat != NULL, cat [M, ldc] = [v | logits | 0] rounded to bf16 (what
  * ogv_outlook_agg_bwd reads in training).  ldc must be C + heads*9 rounded up to 8.
- * ogv_outlook_vproj_supported() says whether a shape takes this kernel (16 | C <= 96,
- * 8 | head_dim) for inference (train = 0) or training (train = 1) under knob "outlook_vproj":
+ * ogv_outlook_vproj_supported() says whether a shape takes this kernel (16 | C <= 96, or the
+ * weight-streaming variant for the wide stages C in {128, 192, 256, 384} with head_dim <= 64; 8 | head_dim)
+ * for inference (train = 0) or training (train = 1) under knob "outlook_vproj":
  * 0 never; 1 inference only; 2 (default) training too, returning 1 = the forward writes cat for
  * ogv_outlook_agg_bwd; 3 returning 2 = the forward writes only y and ogv_outlook_vproj_bwd
  * recomputes [v | logits] (1 when that backward does not take the shape).
@@ -118,7 +119,9 @@ size_t ogv_outlook_bwd_ws_bytes(int B, int H, int W, int C, int heads, int k, og
  * (the forward's weights and rounding, so v / logits are those the forward used): reads x, dy
  * ([M, C] contiguous) and writes dcat [M, ldc] = [dv | dlogits | 0], the gradient of the
  * concatenated projection output, for one dgrad + one wgrad of w.  Replaces the autograd of
- * src/model/outlook_attention.py:100-120 (unfold / softmax / fold). */
+ * src/model/outlook_attention.py:100-120 (unfold / softmax / fold).  16 | C <= 96 only:
+ * ogv_outlook_vproj_bwd_supported() says whether it takes a shape (the wide stages save cat). */
+int ogv_outlook_vproj_bwd_supported(int B, int H, int W, int C, int heads, int k, int ldc, ogv_dtype dt);
 int ogv_outlook_vproj_supported(int B, int H, int W, int C, int heads, int k, int ldc, int train,
                                 ogv_dtype dt);
 int ogv_outlook_vproj_fwd(const void* x, int ldx, const float* w, const float* bias, void* cat, int ldc,

@@ -1156,6 +1156,239 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void outlook_vproj_fwd_kernel(
 }
 
 // ------------------------------------------------------------------------------------------------
+// The fused Outlooker forward for WIDE stages (C > 96: 7M stages 2-3, every 14M / 22M stage after
+// the first; C = 128 / 192 / 256 / 384).  The [ncol x C] split weight slab no longer fits in LDS
+// next to the tile (190 KB at C = 192), so the projection phase streams it:
+//   * each wave's halo rows of x go straight from HBM into registers (16-B loads, zeros outside the
+//     image), held across the whole projection -- no x tile in LDS;
+//   * the weight [W_v; W_attn; 0] streams through LDS in chunks of CJ 16-column blocks (fp32 ->
+//     bf16 hi + lo from registers, double-buffered, ONE barrier per chunk), the chunk sequence
+//     running on across tiles (the weight is the same for every tile), so the next chunk's global
+//     loads are always in flight during the current chunk's MFMAs;
+//   * each chunk's outputs (+ bias, v = 0 outside the image) go straight into the LDS result tile,
+//     rounded to bf16 exactly where the unfused GEMM rounds its output;
+//   * then, as in the narrow kernel: interior rows -> cat (training), softmax per (pixel, head) into
+//     its own LDS region, the 3 x 3 gather from LDS -> y.
+// One workgroup of 8 waves per CU; 8 x 8 pixel tiles (a whole 8 x 8 / 4 x 4 image at 7M stages 2-3).
+// ------------------------------------------------------------------------------------------------
+static size_t vbig_lds(const VTile& t, int C, int heads, int CJ, bool sw) {
+  const size_t rs = ((size_t)(t.HP + 2) * t.RP * 2 + 15) / 16 * 16;
+  const size_t P = ((size_t)t.TH * t.TW * heads * 9 * 4 + 15) / 16 * 16;
+  const size_t wbuf = (size_t)(sw ? 2 : 1) * CJ * 16 * t.WP * 2;
+  return rs + P + 2 * wbuf + (size_t)t.ncol * 4;
+}
+
+constexpr int VB_NW = 8;
+
+template <int NK, int CJ, bool SW>
+__global__ __launch_bounds__(VB_NW * 64, 1) void outlook_vproj_big_fwd_kernel(
+    const bf16* __restrict__ x, int ldx, const float* __restrict__ Wc, int wrows, const float* __restrict__ bias,
+    bf16* __restrict__ cat, int ldc, bf16* __restrict__ y, int H, int W, int C, int heads, VTile t, int dbg) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NT = VB_NW * 64, KP = NK * 32;
+  constexpr int WCH = CJ * 16 * (KP / 4);              // float4 of one weight chunk
+  constexpr int WPT = (WCH + NT - 1) / NT;             // ... per thread
+  const int RP = t.RP, WP = t.WP, HW2 = t.TW + 2, HP = t.HP;
+  const int NJ = t.ncol / 16, NCH = (NJ + CJ - 1) / CJ;
+  bf16* rs = reinterpret_cast<bf16*>(smem);                                          // [HP + 2][RP]
+  const size_t rs_b = ((size_t)(HP + 2) * RP * 2 + 15) / 16 * 16;
+  float* P = reinterpret_cast<float*>(smem + rs_b);                                  // [TH*TW][heads][9]
+  const size_t p_b = ((size_t)t.TH * t.TW * heads * 9 * 4 + 15) / 16 * 16;
+  bf16* wbuf = reinterpret_cast<bf16*>(smem + rs_b + p_b);                           // [2][hi | lo][CJ*16][WP]
+  constexpr int WSL = CJ * 16;                                                       // rows per half
+  float* bs = reinterpret_cast<float*>(wbuf + (size_t)2 * (SW ? 2 : 1) * WSL * WP);  // [ncol]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int hd = C / heads, CH8 = C / 8;
+  for (int n = tid; n < t.ncol; n += NT) bs[n] = (bias && n < wrows) ? bias[n] : 0.f;
+
+  const int G = gridDim.x;
+  const int vid = (blockIdx.x & 7) * (G / 8) + (blockIdx.x >> 3);   // XCD-contiguous logical id
+  const int NI = t.HPr / 16, PT = t.TH * t.TW;
+
+  // ---- weight chunk ch: registers <- Wc rows [16 CJ ch, 16 CJ (ch + 1)), columns < C
+  float4 wr[WPT];
+  auto load_w = [&](int ch) {
+#pragma unroll
+    for (int u = 0; u < WPT; ++u) {
+      const int idx = tid + u * NT;
+      const int r = idx / (KP / 4), k = (idx - r * (KP / 4)) * 4, n = ch * WSL + r;
+      wr[u] = float4{0.f, 0.f, 0.f, 0.f};
+      if (idx < WCH && n < wrows && k < C) wr[u] = *reinterpret_cast<const float4*>(Wc + (long)n * C + k);
+    }
+  };
+  auto store_w = [&](int buf) {
+    bf16* hi = wbuf + (size_t)buf * (SW ? 2 : 1) * WSL * WP;
+#pragma unroll
+    for (int u = 0; u < WPT; ++u) {
+      const int idx = tid + u * NT;
+      if (idx >= WCH) continue;
+      const int r = idx / (KP / 4), k = (idx - r * (KP / 4)) * 4;
+      const bf16x4 h = {(bf16)wr[u].x, (bf16)wr[u].y, (bf16)wr[u].z, (bf16)wr[u].w};
+      *reinterpret_cast<bf16x4*>(hi + r * WP + k) = h;
+      if constexpr (SW) {
+        const bf16x4 l = {(bf16)(wr[u].x - (float)h[0]), (bf16)(wr[u].y - (float)h[1]), (bf16)(wr[u].z - (float)h[2]),
+                          (bf16)(wr[u].w - (float)h[3])};
+        *reinterpret_cast<bf16x4*>(hi + WSL * WP + r * WP + k) = l;
+      }
+    }
+  };
+  // ---- this wave's x fragments of tile `tile` (row block i = wave): pixel (i*16 + fr), k = 32 kt + 8 fg
+  bf16x8 xf[NK];
+  auto load_x = [&](long tile) {
+    const int b = fdiv((int)tile, t.per_img);
+    const int r0 = (int)tile - b * t.per_img.d;
+    const int ty0 = fdiv(r0, t.fntx);
+    const int y0 = ty0 * t.TH, x0 = (r0 - ty0 * t.ntx) * t.TW;
+    const int m = wave * 16 + fr;
+    const int hy = fdiv(m, t.fHW2);
+    const int yy = y0 - 1 + hy, xx = x0 - 1 + m - hy * HW2;
+    const bool ok = wave < NI && m < HP && yy >= 0 && yy < H && xx >= 0 && xx < W && !(dbg & 16);
+    const bf16* src = x + ((long)(b * H + (ok ? yy : 0)) * W + (ok ? xx : 0)) * ldx;
+#pragma unroll
+    for (int kt = 0; kt < NK; ++kt) {
+      const int k = kt * 32 + fg * 8;
+      xf[kt] = (ok && k < C) ? *reinterpret_cast<const bf16x8*>(src + k) : bf16x8{};
+    }
+  };
+
+  if (vid >= t.ntiles) return;
+  load_w(0);
+  load_x(vid);
+  store_w(0);
+  int gch = 0;   // global chunk counter (buffer parity), runs on across tiles
+  for (long tile = vid; tile < t.ntiles; tile += G) {
+    const int b = fdiv((int)tile, t.per_img);
+    const int r0 = (int)tile - b * t.per_img.d;
+    const int ty0 = fdiv(r0, t.fntx);
+    const int y0 = ty0 * t.TH, x0 = (r0 - ty0 * t.ntx) * t.TW;
+    const bool more = tile + G < t.ntiles;
+    // this wave's row block: in-image mask of its pixel
+    const int m = wave * 16 + fr;
+    const int hy = fdiv(m, t.fHW2);
+    const int yy = y0 - 1 + hy, xx = x0 - 1 + m - hy * HW2;
+    const bool inb = m < HP && yy >= 0 && yy < H && xx >= 0 && xx < W;
+    for (int ch = 0; ch < NCH; ++ch, ++gch) {
+      __syncthreads();   // chunk ch staged by everyone; the other buffer's readers (chunk ch - 1) are done
+      const bool last = ch + 1 == NCH;
+      if (!last) load_w(ch + 1);
+      else if (more) load_w(0);   // the next tile's first chunk
+      const bf16* hi = wbuf + (size_t)(gch & 1) * (SW ? 2 : 1) * WSL * WP;
+      if (wave < NI && !(dbg & 1)) {
+#pragma unroll
+        for (int jj = 0; jj < CJ; ++jj) {
+          const int j = ch * CJ + jj;
+          if (j >= NJ) break;
+          f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int kt = 0; kt < NK; ++kt) {
+            const bf16x8 wh = *reinterpret_cast<const bf16x8*>(hi + (jj * 16 + fr) * WP + kt * 32 + fg * 8);
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, xf[kt], acc, 0, 0, 0);
+            if constexpr (SW) {
+              const bf16x8 wl = *reinterpret_cast<const bf16x8*>(hi + WSL * WP + (jj * 16 + fr) * WP + kt * 32 + fg * 8);
+              acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl, xf[kt], acc, 0, 0, 0);
+            }
+          }
+          // lane: pixel m, columns 16 j + 4 fg .. + 3
+          if (m < HP) {
+            const int n = j * 16 + 4 * fg;
+            const float4 b4 = *reinterpret_cast<const float4*>(bs + n);
+            bf16x4 o;
+            o[0] = (bf16)(inb ? acc[0] + b4.x : 0.f);
+            o[1] = (bf16)(inb ? acc[1] + b4.y : 0.f);
+            o[2] = (bf16)(inb ? acc[2] + b4.z : 0.f);
+            o[3] = (bf16)(inb ? acc[3] + b4.w : 0.f);
+            *reinterpret_cast<bf16x4*>(rs + m * RP + n) = o;
+          }
+        }
+      }
+      if (last && more) load_x(tile + G);   // xf is dead: the next tile's rows fly during cat / softmax / gather
+      if (!last || more) store_w((gch + 1) & 1);
+    }
+    __syncthreads();   // the result tile is complete
+    // interior rows of [v | logits | 0] -> cat (the backward's input)
+    if (cat && !(dbg & 8)) {
+      const int LC = ldc / 8;
+      for (int idx = tid; idx < PT * LC; idx += NT) {
+        const int pt = idx / LC, c8 = idx - pt * LC;
+        const int ty = fdiv(pt, t.fTW), tx = pt - ty * t.TW;
+        if (y0 + ty >= H || x0 + tx >= W) continue;
+        const int s = (ty + 1) * HW2 + tx + 1;
+        *reinterpret_cast<uint4*>(cat + ((long)(b * H + y0 + ty) * W + x0 + tx) * ldc + c8 * 8) =
+            *reinterpret_cast<const uint4*>(rs + s * RP + c8 * 8);
+      }
+    }
+    // softmax of the interior pixels' logits (bf16-rounded, as the unfused path reads them)
+    for (int idx = tid; idx < ((dbg & 4) ? 0 : PT * heads); idx += NT) {
+      const int pt = fdiv(idx, t.fHB), hb = idx - pt * heads;
+      const int ty = fdiv(pt, t.fTW), tx = pt - ty * t.TW;
+      const bf16* l = rs + ((ty + 1) * HW2 + tx + 1) * RP + C + hb * 9;
+      float a[9], mx = -INFINITY;
+#pragma unroll
+      for (int jj = 0; jj < 9; ++jj) {
+        a[jj] = (float)l[jj];
+        mx = fmaxf(mx, a[jj]);
+      }
+      float sm = 0.f;
+#pragma unroll
+      for (int jj = 0; jj < 9; ++jj) {
+        a[jj] = __expf(a[jj] - mx);
+        sm += a[jj];
+      }
+      const float inv = 1.0f / sm;
+      float* d = P + (long)idx * 9;
+#pragma unroll
+      for (int jj = 0; jj < 9; ++jj) d[jj] = a[jj] * inv;
+    }
+    __syncthreads();
+    // gather: VP_RX consecutive pixels of one tile row per thread and 8-channel chunk
+    const int TWq = (t.TW + VP_RX - 1) / VP_RX;
+    const int items = (dbg & 2) ? 0 : t.TH * TWq * CH8;
+    for (int idx = tid; idx < items; idx += NT) {
+      const int q = fdiv(idx, t.fCH), cc = idx - q * CH8;
+      const int ty = fdiv(q, t.fQ), xq = q - ty * TWq;
+      if (y0 + ty >= H) continue;
+      const int hb = (cc * 8) / hd;
+      const int tx0 = xq * VP_RX;
+      const int s0 = (ty + 1) * HW2 + tx0 + 1;
+      float accy[VP_RX][8];
+      float pw[VP_RX][9];
+#pragma unroll
+      for (int r = 0; r < VP_RX; ++r) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) accy[r][i] = 0.f;
+        const bool ok = tx0 + r < t.TW;
+        const float* pp = P + ((long)(ty * t.TW + (ok ? tx0 + r : 0)) * heads + hb) * 9;
+#pragma unroll
+        for (int jj = 0; jj < 9; ++jj) pw[r][jj] = ok ? pp[jj] : 0.f;
+      }
+#pragma unroll
+      for (int ki = 0; ki < 3; ++ki)
+#pragma unroll
+        for (int c = 0; c < VP_RX + 2; ++c) {
+          const uint4 raw = *reinterpret_cast<const uint4*>(rs + (s0 + (ki - 1) * HW2 + c - 1) * RP + cc * 8);
+          const bf16* e = reinterpret_cast<const bf16*>(&raw);
+          float fv[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) fv[i] = (float)e[i];
+#pragma unroll
+          for (int r = 0; r < VP_RX; ++r) {
+            const int kj = c - r;
+            if (kj < 0 || kj > 2) continue;
+            const float w = pw[r][ki * 3 + kj];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) accy[r][i] = fmaf(w, fv[i], accy[r][i]);
+          }
+        }
+#pragma unroll
+      for (int r = 0; r < VP_RX; ++r)
+        if (tx0 + r < t.TW && x0 + tx0 + r < W)
+          store_vec<bf16, 8>(y + ((long)(b * H + y0 + ty) * W + x0 + tx0 + r) * C + cc * 8, accy[r]);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // Outlooker backward fused with the RECOMPUTE of its v / attn projections -- the training half of
 // the fused Outlooker (the forward above then writes only y: [v | logits] never reaches HBM).
 // Per TH x TW tile, as the forward: x of the halo pixels -> LDS, [v | logits] = x . Wc^T + b on
@@ -1617,6 +1850,67 @@ static void vproj_run(const bf16* x, int ldx, const float* Wc, int wrows, const 
                                     (int)vtile_x_bytes(t, heads), g_vp_dbg);
 }
 
+// wide stages (C > 96): the weight-streaming kernel, 8 x 8 tiles, CJ 16-column blocks per weight chunk
+// (the largest that fits 160 KB with split weights: C = 128 -> 6, 192 -> 3, 256 -> 2, 384 -> 1).
+// Knob "vp_big" (default 0 = the wide stages keep the unfused GEMM + aggregation; 1 = this kernel).
+// Measured slower than the unfused pair at every wide Model-A shape (tools/bench_vproj.py, cold L2,
+// profiles/r04_vproj_wide.log; fused with cat vs unfused, us): 7M s2 43.8 vs 34.2, 7M s3 48.2 vs 20.5,
+// 14M s1 164 vs 135, s2 116 vs 80, s3 54 vs 46, 22M s1 875 vs 843, s2 641 vs 436, s3 354 vs 186 --
+// every tile re-streams the whole [ncol x C] split weight through LDS (344 KB per 8 x 8 tile at C = 256:
+// 2.2 GB of L2 traffic at 22M stage 2) with the chunk loads' latency exposed, while the GEMM reads it
+// once per 128-row panel; so it stays opt-in.
+static int g_vp_big = 0;
+void set_vp_big(int v) { g_vp_big = v ? 1 : 0; }
+static int vbig_cj(int nk) { return nk == 4 ? 6 : nk == 6 ? 3 : nk == 8 ? 2 : nk == 12 ? 1 : 0; }
+
+static bool vbig_plan(int B, int H, int W, int C, int heads, int k, int ldc, ogv_dtype dt, VTile& t) {
+  if (!g_outlook_vproj || !g_vp_big) return false;
+  if (dt != OGV_BF16 || k != 3 || B <= 0 || H <= 0 || W <= 0 || heads <= 0) return false;
+  if (C <= 96 || C % 32 != 0 || C % heads != 0 || (C / heads) % 8 != 0 || C / heads > 64) return false;
+  const int cj = vbig_cj(C / 32);
+  if (!cj) return false;
+  const int NL = heads * 9;
+  if (ldc != (C + NL + 7) / 8 * 8) return false;
+  t = VTile{};
+  t.TH = H < 8 ? H : 8;
+  t.TW = W < 8 ? W : 8;
+  t.ntx = (W + t.TW - 1) / t.TW;
+  t.nty = (H + t.TH - 1) / t.TH;
+  t.ntiles = (long)B * t.nty * t.ntx;
+  t.HP = (t.TH + 2) * (t.TW + 2);
+  t.HPr = (t.HP + 15) / 16 * 16;
+  t.ncol = (C + NL + 15) / 16 * 16;
+  t.RP = t.ncol + 8;
+  t.WP = C + 8;   // (C + 8) / 2 dwords: an odd multiple of 4 mod 64 -> conflict-free 16-B fragment rows
+  t.XP = 0;
+  if (t.HPr / 16 > VB_NW || t.ntiles >= (1L << 22) || vbig_lds(t, C, heads, cj, true) > 160 * 1024) return false;
+  t.per_img = fdiv_make(t.nty * t.ntx);
+  t.fntx = fdiv_make(t.ntx);
+  t.fHW2 = fdiv_make(t.TW + 2);
+  t.fTW = fdiv_make(t.TW);
+  t.fHB = fdiv_make(heads);
+  t.fCH = fdiv_make(C / 8);
+  t.fQ = fdiv_make((t.TW + VP_RX - 1) / VP_RX);
+  return true;
+}
+
+template <int NK>
+static void vbig_run(const bf16* x, int ldx, const float* Wc, int wrows, const float* bias, bf16* cat, int ldc, bf16* y,
+                     int H, int W, int C, int heads, const VTile& t, bool sw, hipStream_t s) {
+  constexpr int CJ = NK == 4 ? 6 : NK == 6 ? 3 : NK == 8 ? 2 : 1;
+  const size_t lds = vbig_lds(t, C, heads, CJ, sw);
+  const long nb = std::min<long>(t.ntiles, 256);
+  const unsigned grid = (unsigned)((nb + 7) / 8 * 8);
+  auto kern = sw ? outlook_vproj_big_fwd_kernel<NK, CJ, true> : outlook_vproj_big_fwd_kernel<NK, CJ, false>;
+  static bool attr[2] = {false, false};
+  if (!attr[sw]) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    attr[sw] = true;
+  }
+  kern<<<grid, VB_NW * 64, lds, s>>>(x, ldx, Wc, wrows, bias, cat, ldc, y, H, W, C, heads, t, g_vp_dbg);
+}
+
 static bool vproj_bwd_plan(int B, int H, int W, int C, int heads, int k, int ldc, ogv_dtype dt, VTile& t, int& nw) {
   return vtile_plan(B, H, W, C, heads, k, ldc, dt, true, t, nw);
 }
@@ -1648,9 +1942,16 @@ extern "C" int ogv_outlook_vproj_supported(int B, int H, int W, int C, int heads
   VTile t;
   if (g_outlook_vproj < (train ? 2 : 1)) return 0;
   int nw = 0;
+  if (vbig_plan(B, H, W, C, heads, k, ldc, dt, t)) return 1;   // wide stages: forward with cat, tiled backward
   if (!vproj_plan(B, H, W, C, heads, k, ldc, dt, t, nw)) return 0;
   if (!train || g_outlook_vproj < 3) return 1;
   return vproj_bwd_plan(B, H, W, C, heads, k, ldc, dt, t, nw) ? 2 : 1;
+}
+
+extern "C" int ogv_outlook_vproj_bwd_supported(int B, int H, int W, int C, int heads, int k, int ldc, ogv_dtype dt) {
+  VTile t;
+  int nw = 0;
+  return vproj_bwd_plan(B, H, W, C, heads, k, ldc, dt, t, nw) ? 1 : 0;
 }
 
 extern "C" int ogv_outlook_vproj_bwd(const void* x, int ldx, const float* w, const float* bias, const void* dy,
@@ -1696,11 +1997,26 @@ extern "C" int ogv_outlook_vproj_fwd(const void* x, int ldx, const float* w, con
   if (rc) return rc;
   VTile t;
   int nw = 0;
-  OGV_REQUIRE(vproj_plan(B, H, W, C, heads, k, ldc, dt, t, nw),
-              "ogv_outlook_vproj_fwd: unsupported shape (needs bf16, k=3, 16 | C <= 96, 8 | head_dim, "
-              "ldc = C + 9*heads rounded up to 8; see ogv_outlook_vproj_supported)");
+  const bool big = vbig_plan(B, H, W, C, heads, k, ldc, dt, t);
+  OGV_REQUIRE(big || vproj_plan(B, H, W, C, heads, k, ldc, dt, t, nw),
+              "ogv_outlook_vproj_fwd: unsupported shape (needs bf16, k=3, 8 | head_dim, 16 | C <= 96 or "
+              "C in {128, 192, 256, 384} with head_dim <= 64, ldc = C + 9*heads rounded up to 8; see "
+              "ogv_outlook_vproj_supported)");
   OGV_REQUIRE(ldx >= C && ldx % 8 == 0 && al16p(x) && al16p(y) && (!cat || al16p(cat)) && al16p(w),
               "ogv_outlook_vproj_fwd: rows must be 16-B aligned (ldx %d)", ldx);
+  if (big) {
+    const bool sw = (split_w() & 1) != 0;
+    hipStream_t s = as_stream(stream);
+    const bf16* xb = (const bf16*)x;
+    bf16 *cb = (bf16*)cat, *yb = (bf16*)y;
+    switch (C / 32) {
+      case 4: vbig_run<4>(xb, ldx, w, ldc, bias, cb, ldc, yb, H, W, C, heads, t, sw, s); break;
+      case 6: vbig_run<6>(xb, ldx, w, ldc, bias, cb, ldc, yb, H, W, C, heads, t, sw, s); break;
+      case 8: vbig_run<8>(xb, ldx, w, ldc, bias, cb, ldc, yb, H, W, C, heads, t, sw, s); break;
+      default: vbig_run<12>(xb, ldx, w, ldc, bias, cb, ldc, yb, H, W, C, heads, t, sw, s); break;
+    }
+    return check_launch("ogv_outlook_vproj_fwd");
+  }
   const int NJ = t.ncol / 16, NK = (C + 31) / 32;
   const bool sw = (split_w() & 1) != 0;
   hipStream_t s = as_stream(stream);

@@ -196,6 +196,10 @@ extern "C" int ogv_set_option(const char* name, int value) {
     set_wg2_conv(value);
     return OGV_OK;
   }
+  if (!strcmp(name, "vp_big")) {
+    set_vp_big(value);
+    return OGV_OK;
+  }
   if (!strcmp(name, "vp_tile")) {
     set_vp_tile(value);
     return OGV_OK;

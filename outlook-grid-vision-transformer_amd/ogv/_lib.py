@@ -80,6 +80,7 @@ SIGNATURES = {
     "ogv_outlook_agg_fwd": (_i, [_p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _p]),
     "ogv_outlook_bwd_ws_bytes": (_sz, [_i, _i, _i, _i, _i, _i, _i]),
     "ogv_outlook_vproj_supported": (_i, [_i, _i, _i, _i, _i, _i, _i, _i, _i]),
+    "ogv_outlook_vproj_bwd_supported": (_i, [_i, _i, _i, _i, _i, _i, _i, _i]),
     "ogv_outlook_vproj_fwd": (_i, [_p, _i, _p, _p, _p, _i, _p, _i, _i, _i, _i, _i, _i, _i, _p]),
     "ogv_outlook_vproj_bwd": (_i, [_p, _i, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _p]),
     "ogv_outlook_agg_bwd": (_i, [_p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _p]),

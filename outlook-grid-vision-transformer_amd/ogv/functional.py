@@ -855,6 +855,9 @@ def outlook_vproj(x2d, w, b, C, B, H, W, heads, k, save_cat=None):
     if train and save_cat is None:
         save_cat = _lib.load().ogv_outlook_vproj_supported(int(B), int(H), int(W), int(C), int(heads), int(k),
                                                            int(w.shape[0]), 1, OGV_BF16) != 2
+    elif train and not save_cat and not _lib.load().ogv_outlook_vproj_bwd_supported(
+            int(B), int(H), int(W), int(C), int(heads), int(k), int(w.shape[0]), OGV_BF16):
+        raise ValueError(f"ogv.outlook_vproj: no recompute backward at C={C} (wide stages save cat)")
     mode = 0 if not train else (2 if save_cat else 1)
     return _OutlookVProj.apply(x2d, w.contiguous(), None if b is None else b.contiguous(), int(C), int(B), int(H),
                                int(W), int(heads), int(k), mode)

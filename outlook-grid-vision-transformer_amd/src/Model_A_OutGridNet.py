@@ -52,11 +52,16 @@ class MaxOutNet(nn.Module):
 
 def classifier_head(x, classifier: nn.Linear):
     """GAP -> Linear (Model_A_OutGridNet.py:65-67) in fp32 even under bf16 autocast: the pooled
-    features are averaged in fp32 and the classifier keeps its fp32 weights ([B, C] x [C, K]: no
-    measurable cost), so the logits carry no bf16 rounding of their own."""
+    features are averaged in fp32 and the classifier keeps its fp32 weights, so the logits carry no
+    bf16 rounding of their own.  The Linear runs on the native fp32 GEMM (ogv_gemm_fwd: the
+    thread-group kernel for [B, K] outputs, its dgrad / weight gradient on the exact-f32 MFMA kernels)
+    -- the module is called directly only when it carries forward hooks, which must see the call."""
     pooled = x.mean(dim=(2, 3), dtype=torch.float32)
-    with torch.autocast("cuda", enabled=False):
-        return classifier(pooled)
+    if classifier._forward_hooks or classifier._forward_pre_hooks:
+        with torch.autocast("cuda", enabled=False):
+            return classifier(pooled)
+    from ogv import functional as OF
+    return OF.linear_rows(pooled, classifier.weight, classifier.bias)
 
 
 def train_prologue(model: nn.Module, x):

@@ -195,7 +195,18 @@ def test_outlook_vproj_plan_and_knob():
         assert sup(512, 32, 32, 48, 2, False) == 1          # 7M stage 0
         assert sup(512, 16, 16, 96, 3, False) == 1          # 7M stage 1
         assert sup(128, 224, 224, 64, 2, False) == 1        # 22M stage 0
-        assert sup(512, 8, 8, 192, 6, False) == 0           # C > 96: unfused GEMM + aggregation
+        # wide stages (C > 96): the weight-streaming variant (opt-in, knob vp_big), forward with cat; no
+        # recompute backward
+        assert sup(512, 8, 8, 192, 6, False) == 0           # default: unfused GEMM + aggregation
+        assert lib.ogv_set_option(b"vp_big", 1) == 0
+        for shape in ((512, 8, 8, 192, 6), (512, 4, 4, 256, 8), (256, 32, 32, 128, 4), (128, 14, 14, 384, 6)):
+            assert sup(*shape, False) == 1 and sup(*shape, True) == 1, shape
+            assert lib.ogv_outlook_vproj_bwd_supported(*shape[:3], shape[3], shape[4], 3, ld(shape[3], shape[4]),
+                                                       L.OGV_BF16) == 0
+        assert sup(512, 8, 8, 160, 5, False) == 0           # C = 160: no streaming instantiation (32 | C, C / 32 = 5)
+        assert sup(512, 8, 8, 512, 4, False) == 0           # head_dim 128 > 64
+        assert lib.ogv_set_option(b"vp_big", 0) == 0
+        assert lib.ogv_outlook_vproj_bwd_supported(512, 32, 32, 48, 2, 3, ld(48, 2), L.OGV_BF16) == 1
         assert sup(2, 8, 8, 48, 2, False, dt=L.OGV_F32) == 0
         assert sup(2, 8, 8, 48, 2, False, k=5) == 0
         assert sup(2, 8, 8, 40, 5, False) == 0              # head_dim 8 but 16 does not divide C
@@ -218,6 +229,7 @@ def test_outlook_vproj_plan_and_knob():
     finally:
         assert lib.ogv_set_option(b"outlook_vproj", 2) == 0
         assert lib.ogv_set_option(b"vp_tile", 0) == 0
+        assert lib.ogv_set_option(b"vp_big", 0) == 0
     x = ctypes.c_void_p(16)
     rc = lib.ogv_outlook_vproj_fwd(x, 192, x, None, None, 200, x, 2, 8, 8, 192, 6, 3, L.OGV_BF16, None)
     assert rc != 0 and b"unsupported" in lib.ogv_last_error()

@@ -229,9 +229,9 @@ def test_model_logits(name, dtype):
 
     fp32: logits 1e-3 * max(1, |ref|), gradients 5e-3.  bf16: gradients (every parameter's norm, the
     sketched first / last block weight gradients) at 3e-2; logits at the north-star 1e-2 * max(1, |ref|),
-    except where the REFERENCE'S OWN bf16 path (its CPU autocast forward, recorded by make_golden.py
-    r3 on the same weights and input) is itself further than that from its fp32 logits: there the bar
-    is the reference's own bf16 error, with no allowance (ours <= it).  That is every train-mode
+    except where the REFERENCE'S OWN bf16 path is itself further than that from its fp32 logits: there
+    the bar is the smaller of its CPU-autocast error (recorded by make_golden.py r3 on the same weights
+    and input) and its ops' error under this GPU's autocast (the oracle), with no allowance.  That is every train-mode
     model fixture: batch-statistics BatchNorm normalises the logits down to |ref| ~ 1-2 while the bf16
     storage noise of the ~30 layers stays ~0.05-0.09 absolute -- measured: an fp32 emulation of bf16
     storage of every activation gives 0.086 on model_a_7m_train_b16 (vs its 0.018 bound) and keeping
@@ -254,11 +254,16 @@ def test_model_logits(name, dtype):
     ref_max = float(np.abs(arr["logits"]).max())
     bound = (BF16_FWD if bf else 1e-3) * max(1.0, ref_max)
     e_ref = None
-    if bf and "logits_cpu_bf16_autocast" in arr:
-        e_ref = float(np.abs(arr["logits_cpu_bf16_autocast"].astype(np.float64) - arr["logits"]).max())
-        bound = max(bound, e_ref)
-    lref = float(arr["loss"][0])
     e_gpu_ac = _oracle_gpu_autocast_logits_error(meta, arr) if bf else None
+    if bf and "logits_cpu_bf16_autocast" in arr:
+        # train-mode fixtures: no bf16 storage meets the plain bound; the bar is the
+        # reference's OWN bf16 error -- the SMALLER of its CPU-autocast run (recorded by make_golden.py r3)
+        # and its ops under this GPU's autocast (the oracle, measured here): ours must be at least as
+        # accurate as the reference's own bf16 path on either device.  Measured values per fixture:
+        # profiles/r04_parity.jsonl (ours 0.63-0.83x of this bar)
+        e_ref = float(np.abs(arr["logits_cpu_bf16_autocast"].astype(np.float64) - arr["logits"]).max())
+        bound = max(bound, min(e_ref, e_gpu_ac))
+    lref = float(arr["loss"][0])
     print(f"{name} {'bf16' if bf else 'fp32'}: logits max|d| {e:.3e} (bound {bound:.3e}, |ref| {ref_max:.3f}, "
           f"reference's own bf16 {e_ref}, oracle under GPU autocast {e_gpu_ac}), loss {loss.item():.6f} vs {lref:.6f}")
     fx.record("model_logits", fixture=name, dtype="bf16" if bf else "fp32", mode=mode, ours=e, bound=bound,
@@ -290,6 +295,9 @@ def test_model_logits(name, dtype):
         w = int(np.argmax(rel))
         print(f"{name}: grad-norm relative deviation RMS {rms:.4f} (reference bf16 {rms_ref:.4f}), worst {rel[w]:.4f} "
               f"({names[w]}; reference bf16 worst {rel_ref.max():.4f})")
+        fx.record("model_grad_norms_bf16", fixture=name, rms=rms, rms_reference_bf16=rms_ref, worst=float(rel[w]),
+                  worst_param=names[w], worst_reference_bf16=float(rel_ref.max()),
+                  rms_bar=max(BF16_GRAD, 1.5 * rms_ref), worst_bar=max(0.1, 2.0 * rel_ref.max()))
         assert rms <= max(BF16_GRAD, 1.5 * rms_ref), (name, rms, rms_ref)
         assert rel.max() <= max(0.1, 2.0 * rel_ref.max()), (name, names[w], rel[w], rel_ref.max())
     else:
@@ -410,11 +418,25 @@ VPROJ_CASES = [  # B, C, heads, H, W: 7M stage 0 / 1, 14M / 22M stage 0 (C = 64)
     # 1-row images, head_dim 8 (NL = 36), K not a multiple of 32 (C = 16 / 48 / 80)
     (2, 48, 2, 32, 32), (2, 96, 3, 16, 16), (1, 64, 2, 56, 56), (2, 16, 2, 5, 7), (1, 32, 4, 9, 33),
     (3, 48, 2, 1, 1), (2, 80, 2, 1, 19), (2, 64, 2, 8, 8),
+    # wide stages (C > 96, the weight-streaming kernel): 7M stages 2 / 3, 14M stages 1-3, 22M stages 2 / 3
+    # (partial 8 x 8 tiles at 28 / 14 / 12 x 10), head_dim 32 and 64
+    (8, 192, 6, 8, 8), (16, 256, 8, 4, 4), (2, 128, 4, 32, 32), (2, 256, 8, 16, 16), (2, 384, 6, 8, 8),
+    (1, 384, 6, 14, 14), (1, 256, 8, 28, 28), (2, 192, 6, 12, 10), (3, 128, 4, 5, 11),
 ]
 
 
+@pytest.fixture
+def vp_big():
+    """The wide-stage fused Outlooker (C > 96) is opt-in (knob vp_big): on for the test."""
+    from ogv._lib import load
+    lib = load()
+    assert lib.ogv_set_option(b"vp_big", 1) == 0
+    yield
+    assert lib.ogv_set_option(b"vp_big", 0) == 0
+
+
 @pytest.mark.parametrize("case", VPROJ_CASES)
-def test_outlook_vproj_vs_oracle(case):
+def test_outlook_vproj_vs_oracle(case, vp_big):
     """Outlooker forward fused with the v / attn projections (ogv_outlook_vproj_fwd, bf16) vs the
     oracle on the same bf16-valued x and fp32 weights: y, the saved [v | logits | 0] tensor, and the
     gradients of x, W and b through the fused op's backward, within 1e-2 * max(1, |ref|)."""
@@ -444,7 +466,10 @@ def test_outlook_vproj_vs_oracle(case):
     y.backward(dy.to(DEV, torch.bfloat16))
     tol = lambda r: 1e-2 * max(1.0, r.abs().max().item())
     assert fx.maxabs(y.float(), yr.detach()) <= tol(yr), "y"
-    assert fx.maxabs(xd.grad.float(), xr.grad) <= tol(xr.grad), "dx"
+    # dx = dcat . W sums ld = C + 9 heads bf16-stored gradient columns: at the wide stages (C > 96) the
+    # bf16 noise grows with that length -- measured 0.098 of |ref| 6.7 at C = 192 (fused and unfused
+    # paths alike: test_outlook_vproj_matches_unfused), so the bar scales with C / 96 there
+    assert fx.maxabs(xd.grad.float(), xr.grad) <= max(1.0, C / 96) * tol(xr.grad), "dx"
     assert fx.maxabs(wd.grad, wr.grad) <= tol(wr.grad) * 3, "dW"      # bf16 dcat summed over M rows
     assert fx.maxabs(bd.grad, br.grad) <= tol(br.grad) * 3, "db"
     with torch.no_grad():       # inference: no cat written, same y
@@ -452,8 +477,9 @@ def test_outlook_vproj_vs_oracle(case):
     assert torch.equal(y2, y.detach())
 
 
-@pytest.mark.parametrize("case", [(2, 48, 2, 32, 32), (2, 96, 3, 16, 16), (1, 64, 2, 56, 56)])
-def test_outlook_vproj_matches_unfused(case):
+@pytest.mark.parametrize("case", [(2, 48, 2, 32, 32), (2, 96, 3, 16, 16), (1, 64, 2, 56, 56), (8, 192, 6, 8, 8),
+                                  (8, 256, 8, 4, 4), (2, 384, 6, 8, 8), (2, 128, 4, 32, 32)])
+def test_outlook_vproj_matches_unfused(case, vp_big):
     """OutlookAttention2d with the fused forward in training (knob outlook_vproj=2, the default:
     the forward writes cat for the tiled backward; 3: the recompute backward) vs the unfused GEMM +
     aggregation (0): y, dx and every parameter gradient within bf16 rounding; and the fused
@@ -859,8 +885,8 @@ def test_outgrid_block_with_dropouts():
         assert torch.equal(drop.eval()(x), ref.eval()(x))
 
 
-@pytest.mark.parametrize("shape", [(512, 48, 2, 32, 32), (4, 64, 2, 224, 224)])
-def test_outlook_vproj_full_size_matches_unfused(shape):
+@pytest.mark.parametrize("shape", [(512, 48, 2, 32, 32), (4, 64, 2, 224, 224), (512, 192, 6, 8, 8), (512, 256, 8, 4, 4)])
+def test_outlook_vproj_full_size_matches_unfused(shape, vp_big):
     """Full-size property (7M stage 0 at bs=512; 22M stage 0 at 224^2): the fused projection +
     aggregation kernel equals the unfused GEMM -> cat -> aggregation pair on the same inputs within
     bf16 output rounding, and the cat it writes for training equals the GEMM's [v | logits | 0]."""
@@ -899,7 +925,8 @@ def _vproj_problem(B, C, h, H, W, seed):
     return x, w, b, dy, ld
 
 
-@pytest.mark.parametrize("case", VPROJ_CASES + [(512, 48, 2, 32, 32), (256, 96, 3, 16, 16), (2, 64, 2, 224, 224)])
+@pytest.mark.parametrize("case", [c for c in VPROJ_CASES if c[1] <= 96]
+                         + [(512, 48, 2, 32, 32), (256, 96, 3, 16, 16), (2, 64, 2, 224, 224)])
 def test_outlook_vproj_bwd_bitwise(case):
     """The fused backward (ogv_outlook_vproj_bwd: [v | logits] recomputed from x in LDS) is
     BIT-identical to the LDS-tiled aggregation backward run on the cat the fused forward writes:
@@ -986,3 +1013,28 @@ def test_attn_drop_materialising_path(which):
     assert torch.equal(outs[0], outs[1]) and not torch.equal(outs[0], y_ref.detach())
     with torch.no_grad():
         assert torch.equal(drop.eval()(x), ref.eval()(x))
+
+
+@pytest.mark.parametrize("shape", [(512, 192, 6, 8, 8), (512, 256, 8, 4, 4), (64, 384, 6, 14, 14)])
+def test_outlook_vproj_wide_train_grads_full_size_match_unfused(shape, vp_big):
+    """Full size, wide stages (the weight-streaming fused forward writing cat, then the LDS-tiled
+    aggregation backward): y, x / W / b gradients vs the unfused GEMM -> cat -> aggregation pair within
+    1e-2 * max(1, |ref|) (3x for the weight gradients: bf16 dcat summed over M rows); the wide shapes
+    have no recompute backward, so an explicit save_cat=False is refused."""
+    from ogv import functional as OF
+    B, C, h, H, W = shape
+    x, w, b, dy, ld = _vproj_problem(B, C, h, H, W, seed=B + H + 3)
+    outs = []
+    for fused in (True, False):
+        xx, wq, bq = x.clone().requires_grad_(), w.clone().requires_grad_(), b.clone().requires_grad_()
+        if fused:
+            y = OF.outlook_vproj(xx, wq, bq, C, B, H, W, h, 3)
+            assert y.grad_fn.saved_tensors[3] is not None
+        else:
+            y = OF.outlook_aggregate_cat(OF.linear_rows(xx, wq, bq), C, B, H, W, h, 3)
+        y.backward(dy)
+        outs.append((y.detach().float(), xx.grad.float(), wq.grad, bq.grad))
+    for i, (a, r) in enumerate(zip(*outs)):
+        assert fx.maxabs(a, r) <= (3 if i >= 2 else 1) * 1e-2 * max(1.0, r.abs().max().item()), (shape, i)
+    with pytest.raises(ValueError):
+        OF.outlook_vproj(x.clone().requires_grad_(), w, b, C, B, H, W, h, 3, save_cat=False)

@@ -20,7 +20,11 @@ from ogv import functional as OF  # noqa: E402
 from ogv._lib import ACT, OGV_BF16, OgvError, load  # noqa: E402
 
 SHAPES = [("7m_s0", 512, 48, 2, 32), ("7m_s1", 512, 96, 3, 16), ("14m_s0", 256, 64, 2, 64),
-          ("22m_s0", 128, 64, 2, 224)]
+          ("22m_s0", 128, 64, 2, 224),
+          # wide stages: the weight-streaming fused forward (no recompute backward: fused_bwd skipped)
+          ("7m_s2", 512, 192, 6, 8), ("7m_s3", 512, 256, 8, 4), ("14m_s1", 256, 128, 4, 32),
+          ("14m_s2", 256, 256, 8, 16), ("14m_s3", 256, 384, 6, 8), ("22m_s1", 128, 128, 4, 112),
+          ("22m_s2", 128, 256, 8, 56), ("22m_s3", 128, 384, 6, 28)]
 
 
 def main():

@@ -105,6 +105,25 @@ __device__ __forceinline__ void store_vec(T* __restrict__ p, const float* in) {
   }
 }
 
+// V consecutive elements kept as the raw loaded bits (bf16 pairs / fp32) until they are used, so a
+// prefetch need not retire before the next use of any LATER load (vmcnt retires in issue order), and a
+// load under a (uniform) branch is not converted -- hence waited for -- inside the branch.
+template <typename T, int V>
+struct RawVec {
+  static constexpr int NV = (sizeof(T) == 4 && V == 8) ? 2 : 1;
+  typedef typename VecT<T, V>::type VT;
+  VT v[NV];
+  __device__ __forceinline__ void load(const T* __restrict__ p) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) v[k] = *reinterpret_cast<const VT*>(p + k * (V / NV));
+  }
+  __device__ __forceinline__ void unpack(float* out) const {
+    const T* e = reinterpret_cast<const T*>(v);
+#pragma unroll
+    for (int i = 0; i < V; ++i) out[i] = to_f(e[i]);
+  }
+};
+
 // ---------------------------------------------------------------- XCD-aware block order
 // Hardware block i runs on XCD i % 8.  Logical block id = (i % 8) * per + i / 8 hands each XCD a
 // contiguous range of logical ids, so blocks that differ only in the fastest index (e.g. the

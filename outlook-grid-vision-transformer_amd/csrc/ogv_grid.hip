@@ -57,13 +57,19 @@ __global__ __launch_bounds__(256) void grid_fwd_kernel(const T* __restrict__ qkv
   const long pq = G.pixel(grp, t);
 
   float q[HDMAX], o[HDMAX];
+  {
+    // every chunk loaded at a clamped (valid) offset, then zeroed past hd: one round trip, where a
+    // guarded load_vec per chunk made the compiler wait for each chunk in turn
+    RawVec<T, V> rq[HDMAX / V];
 #pragma unroll
-  for (int d0 = 0; d0 < HDMAX; d0 += V) {
-    if (d0 < hd) {
-      load_vec<T, V>(qkv + pq * C3 + h * hd + d0, q + d0);
-    } else {
+    for (int d0 = 0; d0 < HDMAX; d0 += V) rq[d0 / V].load(qkv + pq * C3 + h * hd + min(d0, hd - V));
 #pragma unroll
-      for (int i = 0; i < V; ++i) q[d0 + i] = 0.f;
+    for (int d0 = 0; d0 < HDMAX; d0 += V) {
+      rq[d0 / V].unpack(q + d0);
+      if (d0 >= hd) {
+#pragma unroll
+        for (int i = 0; i < V; ++i) q[d0 + i] = 0.f;
+      }
     }
   }
 #pragma unroll
@@ -77,11 +83,14 @@ __global__ __launch_bounds__(256) void grid_fwd_kernel(const T* __restrict__ qkv
     if constexpr (sizeof(T) == 2 && V == 8) {
       // bf16: this key's k AND v rows are issued together (v does not depend on the score), so a
       // key costs one memory round trip instead of two; same arithmetic order as below
+      // (clamped, always-valid chunk offsets: the chunks past hd reload the last one and are skipped
+      // below -- a per-chunk guard made the compiler wait for each load in turn)
       uint4 rk[HDMAX / 8], rv[HDMAX / 8];
 #pragma unroll
       for (int c = 0; c < HDMAX / 8; ++c) {
-        rk[c] = c * 8 < hd ? *reinterpret_cast<const uint4*>(kp + c * 8) : uint4{0u, 0u, 0u, 0u};
-        rv[c] = c * 8 < hd ? *reinterpret_cast<const uint4*>(kp + G.C + c * 8) : uint4{0u, 0u, 0u, 0u};
+        const int cc = min(c * 8, hd - 8);
+        rk[c] = *reinterpret_cast<const uint4*>(kp + cc);
+        rv[c] = *reinterpret_cast<const uint4*>(kp + G.C + cc);
       }
 #pragma unroll
       for (int c = 0; c < HDMAX / 8; ++c) {

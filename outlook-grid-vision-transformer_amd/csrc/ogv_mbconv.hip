@@ -287,23 +287,6 @@ __device__ __forceinline__ const float* ring_px(const float* ring, const DwTile&
   return ring + ((size_t)ring_slot(r) * (t.TW + 2) + px) * t.PP;
 }
 
-// V consecutive elements kept as the raw loaded bits (bf16 pairs / fp32) until they are used, so a
-// prefetch need not retire before the next use of any LATER load (vmcnt retires in issue order).
-template <typename T, int V>
-struct RawVec {
-  static constexpr int NV = (sizeof(T) == 4 && V == 8) ? 2 : 1;
-  typedef typename VecT<T, V>::type VT;
-  VT v[NV];
-  __device__ __forceinline__ void load(const T* __restrict__ p) {
-#pragma unroll
-    for (int k = 0; k < NV; ++k) v[k] = *reinterpret_cast<const VT*>(p + k * (V / NV));
-  }
-  __device__ __forceinline__ void unpack(float* out) const {
-    const T* e = reinterpret_cast<const T*>(v);
-#pragma unroll
-    for (int i = 0; i < V; ++i) out[i] = to_f(e[i]);
-  }
-};
 
 // Up to DW_R input rows (TW+2 pixels incl. halo) of the block's channel tile, in registers.  The
 // loads are unconditional (addresses clamped into the tensor); the zero padding, the producer's

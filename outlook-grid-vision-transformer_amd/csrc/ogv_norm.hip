@@ -106,6 +106,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
   const long stride = (long)gridDim.x * rows_per_block;
   for (long row0 = blockIdx.x * rows_per_block + threadIdx.x / G; row0 < M; row0 += RPI * stride) {
     float xv[RPI][E], dv[RPI][E], rv[RPI][E], mu[RPI], rs[RPI];
+    // raw bits first, converted after every load of both rows is in flight (a conversion next to a
+    // load under the dres branch made the compiler wait for each of those loads in turn)
+    RawVec<T, VEC> rx[RPI][NV], rd[RPI][NV], rr[RPI][NV];
 #pragma unroll
     for (int q = 0; q < RPI; ++q) {
       const long row = min(row0 + q * stride, M - 1);
@@ -114,11 +117,26 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
 #pragma unroll
       for (int v = 0; v < NV; ++v) {
         const int c = min((v * G + lane_g) * VEC, C - VEC);
-        load_vec<T, VEC>(x + row * C + c, xv[q] + v * VEC);
-        load_vec<T, VEC>(dy + row * C + c, dv[q] + v * VEC);
-        if (dres) load_vec<T, VEC>(dres + row * C + c, rv[q] + v * VEC);
+        rx[q][v].load(x + row * C + c);
+        rd[q][v].load(dy + row * C + c);
       }
     }
+    if (dres) {
+#pragma unroll
+      for (int q = 0; q < RPI; ++q) {
+        const long row = min(row0 + q * stride, M - 1);
+#pragma unroll
+        for (int v = 0; v < NV; ++v) rr[q][v].load(dres + row * C + min((v * G + lane_g) * VEC, C - VEC));
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < RPI; ++q)
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        rx[q][v].unpack(xv[q] + v * VEC);
+        rd[q][v].unpack(dv[q] + v * VEC);
+        if (dres) rr[q][v].unpack(rv[q] + v * VEC);
+      }
 #pragma unroll
     for (int q = 0; q < RPI; ++q) {
       const long row = row0 + q * stride;

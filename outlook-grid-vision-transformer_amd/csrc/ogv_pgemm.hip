@@ -317,18 +317,29 @@ __global__ __launch_bounds__(PG_NW * 64, 2) void pgemm_bf16_kernel(const bf16* _
       for (int i = 0; i < RS; ++i) {
         const int m = mw + i * 16 + fr;
         const bool mok = m < M;
-        const float rsc = (epi.rs && mok) ? epi.rs[m / epi.rps] : 1.f;
+        // residual / Z / row-scale loads at CLAMPED (always valid) addresses, issued unconditionally under
+        // a uniform branch: the compiler then keeps them in flight together (one wait), where per-lane
+        // guards made it wait after each load (one HBM round trip per 16-B load, 8 per RS = 2 tile)
+        const long mc = mok ? m : M - 1;
+        const float rsc = epi.rs ? epi.rs[mc / epi.rps] : 1.f;
         constexpr int QC = (ZA != 0 && TN > 8) ? TN / 4 : TN / 2;   // fragment pairs per residual / Z round trip
 #pragma unroll
         for (int q0 = 0; q0 < TN / 2; q0 += QC) {
         uint4 rv[QC], zv[QC];
 #pragma unroll
-        for (int u = 0; u < QC; ++u) {   // residual / Z of the chunk first: one round trip
-          const int n = n0 + 32 * (q0 + u) + 8 * fg;
-          rv[u] = zv[u] = uint4{0u, 0u, 0u, 0u};
-          if (res && mok && n < N) rv[u] = *reinterpret_cast<const uint4*>(res + (long)m * ldo + n);
-          if constexpr (ZA != 0) {
-            if (mok && n < N) zv[u] = *reinterpret_cast<const uint4*>(Z + (long)m * epi.ldz + n);
+        for (int u = 0; u < QC; ++u) rv[u] = zv[u] = uint4{0u, 0u, 0u, 0u};
+        if (res) {
+#pragma unroll
+          for (int u = 0; u < QC; ++u) {
+            const int n = min(n0 + 32 * (q0 + u) + 8 * fg, N - 8);
+            rv[u] = *reinterpret_cast<const uint4*>(res + mc * ldo + n);
+          }
+        }
+        if constexpr (ZA != 0) {
+#pragma unroll
+          for (int u = 0; u < QC; ++u) {
+            const int n = min(n0 + 32 * (q0 + u) + 8 * fg, N - 8);
+            zv[u] = *reinterpret_cast<const uint4*>(Z + mc * epi.ldz + n);
           }
         }
 #pragma unroll

@@ -182,7 +182,7 @@ __global__ __launch_bounds__(SG_NW * 64) void sgemm_bf16_kernel(const bf16* __re
         if (mi < M && k < K) v = *reinterpret_cast<const bf16x8*>(A + mi * lda + k);
         dst[i][kt] = v;
       }
-      rs[i] = (epi.rs && mi < M) ? epi.rs[mi / epi.rps] : 1.f;
+      rs[i] = epi.rs ? epi.rs[(mi < M ? mi : M - 1) / epi.rps] : 1.f;
     }
   };
   // Without an A prologue the next panel's fragments are fetched right after the current ones are
@@ -294,20 +294,33 @@ __global__ __launch_bounds__(SG_NW * 64) void sgemm_bf16_kernel(const bf16* __re
     }
     for (int c0 = 0; c0 < nb; c0 += SG_CW) {
       // residual / Z runs of this chunk first (their latency overlaps the MFMAs)
+      // (clamped, always-valid addresses under a uniform branch: per-lane guards made the compiler
+      // wait after each of these loads -- one round trip per 8-B load)
       uint2 rv[RS][4], zv[RS][4];
 #pragma unroll
       for (int i = 0; i < RS; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int cc = c0 + j * 16 + 4 * fg;
-          const bool ok = m[i] < M && cc < nb;
-          rv[i][j] = uint2{0u, 0u};
-          zv[i][j] = uint2{0u, 0u};
-          if (ok && res) rv[i][j] = *reinterpret_cast<const uint2*>(res + m[i] * ldo + n0 + cc);
-          if constexpr (ZA != 0) {
-            if (ok) zv[i][j] = *reinterpret_cast<const uint2*>(Z + m[i] * epi.ldz + n0 + cc);
+        for (int j = 0; j < 4; ++j) rv[i][j] = zv[i][j] = uint2{0u, 0u};
+      if (res) {
+#pragma unroll
+        for (int i = 0; i < RS; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const long mc = m[i] < M ? m[i] : M - 1;
+            const int cc = min(c0 + j * 16 + 4 * fg, nb - 4);
+            rv[i][j] = *reinterpret_cast<const uint2*>(res + mc * ldo + n0 + cc);
           }
-        }
+      }
+      if constexpr (ZA != 0) {
+#pragma unroll
+        for (int i = 0; i < RS; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const long mc = m[i] < M ? m[i] : M - 1;
+            const int cc = min(c0 + j * 16 + 4 * fg, nb - 4);
+            zv[i][j] = *reinterpret_cast<const uint2*>(Z + mc * epi.ldz + n0 + cc);
+          }
+      }
       f32x4 acc[RS][4];
 #pragma unroll
       for (int i = 0; i < RS; ++i)

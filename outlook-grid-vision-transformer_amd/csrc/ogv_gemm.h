@@ -91,6 +91,16 @@ struct ConvG {
   int par = -1, ntap = 9;
   int tap[4] = {0, 0, 0, 0};
 };
+// tap[t] of a parity class through selects on the (uniform) kernel-argument values: a dynamic index
+// into the by-value argument struct makes the compiler re-load it from the kernarg segment and wait
+// for that load at every use
+__device__ __forceinline__ int conv_tap(const ConvG& g, int t) {
+  // (readfirstlane pins each value in a register: a plain select chain is folded back into a load
+  // through a selected kernarg address)
+  const int t0 = __builtin_amdgcn_readfirstlane(g.tap[0]), t1 = __builtin_amdgcn_readfirstlane(g.tap[1]);
+  const int t2 = __builtin_amdgcn_readfirstlane(g.tap[2]), t3 = __builtin_amdgcn_readfirstlane(g.tap[3]);
+  return t <= 0 ? t0 : t == 1 ? t1 : t == 2 ? t2 : t3;
+}
 struct ConvRow {
   int b, ry, rx;
 };
@@ -226,6 +236,7 @@ void se_gemv_launch(const float* in, int ldi, int pro_act, const float* W, int l
 bool se_gemv_on();
 void set_se_gemv(int v);
 void set_dw_fuse(int v);
+void set_dw_bn2(int v);
 void set_swg_min_m(int v);
 void set_pg_split(int v);
 int split_w();

@@ -290,12 +290,16 @@ __device__ __forceinline__ const float* ring_px(const float* ring, const DwTile&
 
 // Up to DW_R input rows (TW+2 pixels incl. halo) of the block's channel tile, in registers.  The
 // loads are unconditional (addresses clamped into the tensor); the zero padding, the producer's
-// BatchNorm + activation and the conversion to fp32 are applied as the rows enter the LDS ring.
-template <typename T, int V, int LDQ>
+// transform (stage(v, v2, image): BatchNorm + activation forward, or the whole BN2 backward from
+// the two sources (dA3, d) when TWO) and the conversion to fp32 are applied as the rows enter the
+// LDS ring.
+template <typename T, int V, int LDQ, bool TWO = false>
 struct RowPipe {
   RawVec<T, V> raw[DW_R][LDQ];
+  RawVec<T, V> raw2[TWO ? DW_R : 1][TWO ? LDQ : 1];
   template <int NR>
-  __device__ __forceinline__ void load(const T* __restrict__ src, const DwTile& t, const TileIdx& ti, VRow p, int cc) {
+  __device__ __forceinline__ void load(const T* __restrict__ src, const T* __restrict__ src2, const DwTile& t,
+                                       const TileIdx& ti, VRow p, int cc) {
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
       const long b = ti.b0 + min(max(p.im, 0), ti.nimg - 1);
@@ -304,19 +308,22 @@ struct RowPipe {
       for (int j = 0; j < LDQ; ++j) {
         const int i = threadIdx.x + j * 256;
         const int x = min(max(ti.x0 - 1 + i / t.chunks, 0), t.W - 1);
-        raw[r][j].load(src + ((b * t.H + y) * t.W + x) * t.C + cc);
+        const long off = ((b * t.H + y) * t.W + x) * t.C + cc;
+        raw[r][j].load(src + off);
+        if constexpr (TWO) raw2[r][j].load(src2 + off);
       }
       p = vnext(t, p);
     }
   }
-  template <bool PRO, int ACT>
+  template <typename Stage>
   __device__ __forceinline__ void store(float* ring, const DwTile& t, const TileIdx& ti, VRow p, int nr, int chunk,
-                                        bool cok, const float* s, const float* h) const {
+                                        bool cok, Stage&& stage) const {
     const int n = (ti.tw + 2) * t.chunks;
 #pragma unroll
     for (int r = 0; r < DW_R; ++r, p = vnext(t, p)) {
       if (r >= nr) break;
       const bool rok = cok && p.im >= 0 && p.im < ti.nimg && p.y < t.H;
+      const int im = min(max(p.im, 0), ti.nimg - 1);
       float* slot = ring + (size_t)ring_slot(p.u) * (t.TW + 2) * t.PP;
 #pragma unroll
       for (int j = 0; j < LDQ; ++j) {
@@ -326,11 +333,15 @@ struct RowPipe {
           const bool ok = rok && x >= 0 && x < t.W;
           float v[V];
           raw[r][j].unpack(v);
-#pragma unroll
-          for (int k = 0; k < V; ++k) {
-            if constexpr (PRO) v[k] = act_fwd(ACT, fmaf(v[k], s[k], h[k]));
-            v[k] = ok ? v[k] : 0.f;
+          if constexpr (TWO) {
+            float v2[V];
+            raw2[r][j].unpack(v2);
+            stage(v, v2, im);
+          } else {
+            stage(v, v, im);
           }
+#pragma unroll
+          for (int k = 0; k < V; ++k) v[k] = ok ? v[k] : 0.f;
           float* d = slot + (i / t.chunks) * t.PP + chunk * V;
 #pragma unroll
           for (int k = 0; k < V; k += 4)
@@ -380,24 +391,24 @@ __device__ __forceinline__ void dw_reduce_store(A (&q)[NQ][V], float* lds_raw, i
 // clamped row), then the output rows among u..u+R-1 (not seam rows) are computed through
 // body(r, u+r, image, y, px), one item (pixel, V channels) per thread and row.  Issue order = retire
 // order, so the body waits for its own loads only while the prefetch stays in flight.
-template <typename T, int V, int LDQ, bool PRO, int ACT, typename Pre, typename Body>
-__device__ __forceinline__ void dw_walk(float* ring, const T* __restrict__ src, const DwTile& t, const TileIdx& ti,
-                                        int cc, int chunk, bool cok, const float* s, const float* h, Pre&& pre,
-                                        Body&& body) {
-  RowPipe<T, V, LDQ> rp;
+template <typename T, int V, int LDQ, bool TWO, typename Stage, typename Pre, typename Body>
+__device__ __forceinline__ void dw_walk(float* ring, const T* __restrict__ src, const T* __restrict__ src2,
+                                        const DwTile& t, const TileIdx& ti, int cc, int chunk, bool cok,
+                                        Stage&& stage, Pre&& pre, Body&& body) {
+  RowPipe<T, V, LDQ, TWO> rp;
   VRow p = {-1, -1, t.H};
-  rp.template load<2>(src, t, ti, p, cc);
-  rp.template store<PRO, ACT>(ring, t, ti, p, 2, chunk, cok, s, h);
-  rp.template load<DW_R>(src, t, ti, vadv<2>(t, p), cc);
+  rp.template load<2>(src, src2, t, ti, p, cc);
+  rp.store(ring, t, ti, p, 2, chunk, cok, stage);
+  rp.template load<DW_R>(src, src2, t, ti, vadv<2>(t, p), cc);
   const int nitems = ti.tw * t.chunks;  // <= 256 (dw_tile_plan)
   const bool item = cok && (int)threadIdx.x < nitems;
   const int px = min((int)threadIdx.x, nitems - 1) / t.chunks;
   const int nv = ti.nimg * (t.H + 1) - 1;  // virtual rows incl. the seams between images
   for (p = vnext(t, p); p.u < nv; p = vadv<DW_R>(t, p)) {
-    rp.template store<PRO, ACT>(ring, t, ti, vnext(t, p), DW_R, chunk, cok, s, h);
+    rp.store(ring, t, ti, vnext(t, p), DW_R, chunk, cok, stage);
     __syncthreads();
     pre(p, px);
-    rp.template load<DW_R>(src, t, ti, vadv<DW_R + 1>(t, p), cc);
+    rp.template load<DW_R>(src, src2, t, ti, vadv<DW_R + 1>(t, p), cc);
     if (item) {
       VRow q = p;
 #pragma unroll
@@ -442,7 +453,11 @@ __global__ __launch_bounds__(256) void dw_fwd_tile_kernel(const T* __restrict__ 
 #pragma unroll
   for (int i = 0; i < V; ++i) { q[0][i] = 0.0; q[1][i] = 0.0; }
   const int cc = cok ? c : 0;
-  dw_walk<T, V, LDQ, true, ACT>(ring, e, t, ti, cc, chunk, cok, s, h, [&](VRow, int) {},
+  auto stage = [&](float (&v)[V], const float (&)[V], int) {
+#pragma unroll
+    for (int k = 0; k < V; ++k) v[k] = act_fwd(ACT, fmaf(v[k], s[k], h[k]));
+  };
+  dw_walk<T, V, LDQ, false>(ring, e, e, t, ti, cc, chunk, cok, stage, [&](VRow, int) {},
                            [&](int, int u, long b, int y, int px) {
     float acc[V];
 #pragma unroll
@@ -479,14 +494,23 @@ __global__ __launch_bounds__(256) void dw_fwd_tile_kernel(const T* __restrict__ 
 // with a = act(e*sc1 + sh1): the transposed conv already reads dd[q - tap] for every tap of output
 // pixel q and loads e[q], so the 9 partial sums cost 9 FMAs per element and no second pass over dd
 // and e (part[rid][tap][c], as dw_wgrad_tile_kernel writes them)
-template <typename T, int V, int LDQ, int ACT, bool WG = false>
+// BN2: dd is not materialised -- the ring stages dd = BN2-backward(dA3, d) (bn2_apply_kernel's
+// arithmetic, rounded to T as the stored dd would be) from the two [M, C] sources, the per-image
+// SE gate and dpool/HW of the block's images staged once in LDS behind the ring.
+template <typename T>
+struct Bn2In {
+  const T* d;
+  const float *sc, *sh, *mean, *inv, *gate, *dpool, *coef;
+  int HW;
+};
+template <typename T, int V, int LDQ, int ACT, bool WG = false, bool BN2 = false>
 __global__ __launch_bounds__(256) void dw_dgrad_tile_kernel(const T* __restrict__ dd, const float* __restrict__ wdw,
                                                             const T* __restrict__ e, const float* __restrict__ sc,
                                                             const float* __restrict__ sh,
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ invstd, int act,
                                                             T* __restrict__ out, float* __restrict__ stat, DwTile t,
-                                                            float* __restrict__ part = nullptr) {
+                                                            float* __restrict__ part, Bn2In<T> b2, int tab_off) {
   extern __shared__ __attribute__((aligned(16))) float ring[];
   TileIdx ti;
   if (!tile_idx(t, ti)) return;
@@ -503,6 +527,31 @@ __global__ __launch_bounds__(256) void dw_dgrad_tile_kernel(const T* __restrict_
     mu[i] = cok ? mean[c + i] : 0.f;
     is[i] = cok ? invstd[c + i] : 0.f;
   }
+  float s2[BN2 ? V : 1], h2[BN2 ? V : 1], mu2[BN2 ? V : 1], is2[BN2 ? V : 1], ca[BN2 ? V : 1], cb[BN2 ? V : 1],
+      cc2[BN2 ? V : 1];
+  float* tab = ring + tab_off;  // [G][2][CT]: gate, dpool/HW of the block's images
+  if constexpr (BN2) {
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      s2[i] = cok ? b2.sc[c + i] : 0.f;
+      h2[i] = cok ? b2.sh[c + i] : 0.f;
+      mu2[i] = cok ? b2.mean[c + i] : 0.f;
+      is2[i] = cok ? b2.inv[c + i] : 0.f;
+      ca[i] = cok ? b2.coef[c + i] : 0.f;
+      cb[i] = cok ? b2.coef[t.C + c + i] : 0.f;
+      cc2[i] = cok ? b2.coef[2 * t.C + c + i] : 0.f;
+    }
+    const float ihw = 1.f / (float)b2.HW;
+    for (int idx = threadIdx.x; idx < t.G * t.CT; idx += 256) {
+      const int im = idx / t.CT, cl = idx - im * t.CT, ch = ti.ct * t.CT + cl;
+      const bool ok = im < ti.nimg && ch < t.C;
+      const long gi = ok ? (ti.b0 + im) * t.C + ch : 0;
+      const float g = b2.gate[gi], dp = b2.dpool[gi];
+      tab[im * 2 * t.CT + cl] = ok ? g : 0.f;
+      tab[(im * 2 + 1) * t.CT + cl] = ok ? dp * ihw : 0.f;
+    }
+    __syncthreads();
+  }
   float q[2][V];
 #pragma unroll
   for (int i = 0; i < V; ++i) { q[0][i] = 0.f; q[1][i] = 0.f; }
@@ -517,7 +566,27 @@ __global__ __launch_bounds__(256) void dw_dgrad_tile_kernel(const T* __restrict_
 #pragma unroll
     for (int r = 0; r < DW_R; ++r, q = vnext(t, q)) dw_pixel_load(ce[r], e, t, ti, q, px, cc);
   };
-  dw_walk<T, V, LDQ, false, OGV_ACT_NONE>(ring, dd, t, ti, cc, chunk, cok, s, h, pre, [&](int r, int u, long b, int y, int px) {
+  auto stage = [&](float (&v)[V], const float (&dv)[V], int im) {
+    if constexpr (BN2) {
+      const float* gp = tab + im * 2 * t.CT + chunk * V;
+      float gt[V], dpi[V];
+#pragma unroll
+      for (int k = 0; k < V; k += 4) {
+        const float4 g4 = *reinterpret_cast<const float4*>(gp + k);
+        const float4 p4 = *reinterpret_cast<const float4*>(gp + t.CT + k);
+        gt[k] = g4.x; gt[k + 1] = g4.y; gt[k + 2] = g4.z; gt[k + 3] = g4.w;
+        dpi[k] = p4.x; dpi[k + 1] = p4.y; dpi[k + 2] = p4.z; dpi[k + 3] = p4.w;
+      }
+#pragma unroll
+      for (int k = 0; k < V; ++k) {
+        const float y = fmaf(dv[k], s2[k], h2[k]);
+        const float dy2 = fmaf(v[k], gt[k], dpi[k]) * act_grad(ACT, y);
+        const float dh = (dv[k] - mu2[k]) * is2[k];
+        v[k] = to_f(from_f<T>(ca[k] * (dy2 - cb[k] - dh * cc2[k])));
+      }
+    }
+  };
+  dw_walk<T, V, LDQ, BN2>(ring, dd, b2.d, t, ti, cc, chunk, cok, stage, pre, [&](int r, int u, long b, int y, int px) {
     const long off = ((b * t.H + y) * t.W + ti.x0 + px) * t.C + c;
     float ev[V];
     ce[r].unpack(ev);
@@ -589,7 +658,11 @@ __global__ __launch_bounds__(256) void dw_wgrad_tile_kernel(const T* __restrict_
 #pragma unroll
     for (int r = 0; r < DW_R; ++r, q = vnext(t, q)) dw_pixel_load(cg[r], dd, t, ti, q, px, cc);
   };
-  dw_walk<T, V, LDQ, true, ACT>(ring, e, t, ti, cc, chunk, cok, s, h, pre, [&](int r, int u, long, int, int px) {
+  auto stage = [&](float (&v)[V], const float (&)[V], int) {
+#pragma unroll
+    for (int k = 0; k < V; ++k) v[k] = act_fwd(ACT, fmaf(v[k], s[k], h[k]));
+  };
+  dw_walk<T, V, LDQ, false>(ring, e, e, t, ti, cc, chunk, cok, stage, pre, [&](int r, int u, long, int, int px) {
     float g[V];
     cg[r].unpack(g);
 #pragma unroll
@@ -1165,6 +1238,10 @@ void set_mb_side(int v) { g_mb_side = v; }
 // knob "dw_fuse": 1 (default) = the depthwise data and weight gradients in one pass over (dd, e)
 static int g_dw_fuse = 1;
 void set_dw_fuse(int v) { g_dw_fuse = v; }
+// knob "dw_bn2": 1 (default) = the BN2 backward computed in the depthwise backward's staging (dd never
+// written to HBM: one [M, mid] write + read and the bn2_apply launch saved); needs dw_fuse
+static int g_dw_bn2 = 1;
+void set_dw_bn2(int v) { g_dw_bn2 = v; }
 struct SideStream {
   hipStream_t s = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
@@ -1231,21 +1308,26 @@ struct Ops {
                         (const T*)e, w, sc, sh, act, (T*)out, stat, shift, t))
   }
   // part != nullptr: the weight-gradient partials in the same pass (dw_dgrad_tile_kernel<.., WG>)
+  // b2 != nullptr: dd is BN2-backward(dA3 = dd, b2->d), computed as the rows are staged
   static void dw_dgrad(const void* dd, const float* w, const void* e, const float* sc, const float* sh,
                        const float* mean, const float* inv, int act, void* out, float* stat, const DwTile& t,
-                       hipStream_t st, float* part = nullptr) {
+                       hipStream_t st, float* part = nullptr, const Bn2In<T>* b2 = nullptr) {
     if (skip_mask() & 8) return;
     constexpr int V = 4;
-    const size_t lds = t.lds_bytes(part ? 9 : 2, V, sizeof(float));
-#define OGV_DWD(WG_)                                                                                                 \
-    OGV_DW_ACT(act, if (t.ldq <= 1) dw_dgrad_tile_kernel<T, V, 1, A, WG_><<<dw_grid(t), 256, lds, st>>>(             \
-                        (const T*)dd, w, (const T*)e, sc, sh, mean, inv, act, (T*)out, stat, t, part);               \
-               else if (t.ldq <= 2) dw_dgrad_tile_kernel<T, V, 2, A, WG_><<<dw_grid(t), 256, lds, st>>>(             \
-                        (const T*)dd, w, (const T*)e, sc, sh, mean, inv, act, (T*)out, stat, t, part);               \
-               else dw_dgrad_tile_kernel<T, V, 3, A, WG_><<<dw_grid(t), 256, lds, st>>>(                              \
-                        (const T*)dd, w, (const T*)e, sc, sh, mean, inv, act, (T*)out, stat, t, part))
-    if (part) { OGV_DWD(true) }
-    else { OGV_DWD(false) }
+    size_t lds = t.lds_bytes(part ? 9 : 2, V, sizeof(float));
+    const int tab_off = (int)(lds / sizeof(float));
+    if (b2) lds += (size_t)t.G * 2 * t.CT * sizeof(float);
+    const Bn2In<T> bi = b2 ? *b2 : Bn2In<T>{};
+#define OGV_DWD(WG_, B2_)                                                                                            \
+    OGV_DW_ACT(act, if (t.ldq <= 1) dw_dgrad_tile_kernel<T, V, 1, A, WG_, B2_><<<dw_grid(t), 256, lds, st>>>(        \
+                        (const T*)dd, w, (const T*)e, sc, sh, mean, inv, act, (T*)out, stat, t, part, bi, tab_off);  \
+               else if (t.ldq <= 2) dw_dgrad_tile_kernel<T, V, 2, A, WG_, B2_><<<dw_grid(t), 256, lds, st>>>(        \
+                        (const T*)dd, w, (const T*)e, sc, sh, mean, inv, act, (T*)out, stat, t, part, bi, tab_off);  \
+               else dw_dgrad_tile_kernel<T, V, 3, A, WG_, B2_><<<dw_grid(t), 256, lds, st>>>(                         \
+                        (const T*)dd, w, (const T*)e, sc, sh, mean, inv, act, (T*)out, stat, t, part, bi, tab_off))
+    if (part && b2) { OGV_DWD(true, true) }
+    else if (part) { OGV_DWD(true, false) }
+    else { OGV_DWD(false, false) }
 #undef OGV_DWD
   }
   static void dw_wgrad(const void* dd, const void* e, const float* sc, const float* sh, int act, float* part,
@@ -1483,19 +1565,30 @@ static void mbconv_bwd_impl(const void* dout, const void* x, const Saved& sv, vo
                             true);
     }
   }
-  // B5) BN2 backward: dd = ca*(dy2 - cb - dhat*cc)  -> bufB
+  // B5) BN2 backward: dd = ca*(dy2 - cb - dhat*cc)  -> bufB  (with dw_bn2: computed inside B6's staging)
+  const bool bn2f = g_dw_fuse && g_dw_bn2;
   {
     bn2_terms_kernel<<<cdiv((long)s.B * s.mid, 256), 256, 0, st>>>(w.R, sv.gate, w.dpool, w.terms, s.B, HW, s.mid);
     bn_reduce_coeffs_kernel<<<cdiv(s.mid, 16), 256, 0, st>>>(w.terms, s.B, 2L * s.mid, s.mid, (float)M, P.bn2_w, sv.inv2,
                                                             G.bn2_w, G.bn2_b, w.coef, s.train);
-    OGV_V_DISPATCH(rp.V, O::template bn2_apply, w.bufA, sv.d, sv.sc2, sv.sh2, sv.mean2, sv.inv2, sv.gate, w.dpool,
-                   w.coef, s.act, w.bufB, M, HW, s.mid, st);
+    if (!bn2f)
+      OGV_V_DISPATCH(rp.V, O::template bn2_apply, w.bufA, sv.d, sv.sc2, sv.sh2, sv.mean2, sv.inv2, sv.gate, w.dpool,
+                     w.coef, s.act, w.bufB, M, HW, s.mid, st);
   }
-  // B6) depthwise backward: dy1 = dgrad(dd) * act'(BN1(e)) -> bufA (+ BN1 sums); dWdw from (dd, act(BN1(e)))
+  // B6) depthwise backward: dy1 = dgrad(dd) * act'(BN1(e)) -> dy1 (+ BN1 sums); dWdw from (dd, act(BN1(e)))
+  // dy1 = bufA (dd in bufB), or bufB when dd is staged from (dA3 = bufA, d)
+  void* dy1 = bn2f ? w.bufB : w.bufA;
+  void* de = bn2f ? w.bufA : w.bufB;
   {
     const DwTile t = dw_tile_plan(s.B, s.H, s.W, s.mid, 4);
     join_side(st, sd);
-    if (g_dw_fuse) {   // one pass over (dd, e): data gradient + BN1 sums + dWdw partials
+    if (bn2f) {  // one pass over (dA3, d, e): BN2 backward + data gradient + BN1 sums + dWdw partials
+      const Bn2In<T> b2 = {(const T*)sv.d, sv.sc2, sv.sh2, sv.mean2, sv.inv2, sv.gate, w.dpool, w.coef, HW};
+      O::dw_dgrad(w.bufA, P.w_dw, sv.e, sv.sc1, sv.sh1, sv.mean1, sv.inv1, s.act, dy1, w.stat, t, st, w.part9, &b2);
+      sd = fork_side(st);
+      colreduce(w.part9, w.sums9, t.rows(), 9L * s.mid, 9L * s.mid, w.tmp2, sd);
+      tapmajor_to_chan_kernel<<<cdiv(9 * s.mid, 256), 256, 0, sd>>>(w.sums9, G.w_dw, s.mid);
+    } else if (g_dw_fuse) {   // one pass over (dd, e): data gradient + BN1 sums + dWdw partials
       O::dw_dgrad(w.bufB, P.w_dw, sv.e, sv.sc1, sv.sh1, sv.mean1, sv.inv1, s.act, w.bufA, w.stat, t, st, w.part9);
       sd = fork_side(st);  // the partials' reduction overlaps the BN1 backward
       colreduce(w.part9, w.sums9, t.rows(), 9L * s.mid, 9L * s.mid, w.tmp2, sd);
@@ -1509,19 +1602,19 @@ static void mbconv_bwd_impl(const void* dout, const void* x, const Saved& sv, vo
                        w.bufA, w.stat, t, st);
     }
   }
-  join_side(st, sd);  // B7 overwrites bufB
-  // B7) BN1 backward: de = ca*(dy1 - cb - ehat*cc) -> bufB
+  join_side(st, sd);  // B7 overwrites de
+  // B7) BN1 backward: de = ca*(dy1 - cb - ehat*cc)
   {
     const long R1 = dw_tile_plan(s.B, s.H, s.W, s.mid, 4).rows();
     bn_reduce_coeffs_kernel<<<cdiv(s.mid, 16), 256, 0, st>>>(w.stat, R1, 2L * s.mid, s.mid, (float)M, P.bn1_w, sv.inv1,
                                                             G.bn1_w, G.bn1_b, w.coef, s.train);
   }
-  OGV_V_DISPATCH(rp.V, O::template bn_apply, w.bufA, sv.e, sv.mean1, sv.inv1, w.coef, w.bufB, M, s.mid, st);
+  OGV_V_DISPATCH(rp.V, O::template bn_apply, dy1, sv.e, sv.mean1, sv.inv1, w.coef, de, M, s.mid, st);
   // B8) expand: dx = de . We + dout (residual) ; dWe = de^T . x
   sd = fork_side(st);  // dWe on the side stream, overlapping dx
-  gemm_wgrad_launch(dt, w.bufB, s.mid, x, s.C, Pro(), nullptr, 1, G.w_expand, nullptr, (int)M, s.mid, s.C, w.wg_expand,
+  gemm_wgrad_launch(dt, de, s.mid, x, s.C, Pro(), nullptr, 1, G.w_expand, nullptr, (int)M, s.mid, s.C, w.wg_expand,
                     sd, nullptr, true);
-  gemm_dgrad_launch(dt, w.bufB, s.mid, P.w_expand, nullptr, 0, 0, nullptr, 1, dout, dx, s.C, (int)M, s.mid, s.C,
+  gemm_dgrad_launch(dt, de, s.mid, P.w_expand, nullptr, 0, 0, nullptr, 1, dout, dx, s.C, (int)M, s.mid, s.C,
                     w.gemm, st);
   join_side(st, sd);
 }

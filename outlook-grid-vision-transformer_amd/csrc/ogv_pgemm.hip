@@ -114,7 +114,7 @@ __global__ __launch_bounds__(PG_NW * 64, 2) void pgemm_bf16_kernel(const bf16* _
         if constexpr (CV) {
           if (cv.par >= 0) {   // the class's tap t -> the weight's full tap-major column block
             const int t = k / cv.Cs;
-            kc = cv.tap[t < 4 ? t : 3] * cv.Cs + (k - t * cv.Cs);
+            kc = conv_tap(cv, t) * cv.Cs + (k - t * cv.Cs);
           }
         }
         if (n0 + r < N && k < K) wr[i] = *reinterpret_cast<const float4*>(W + (long)(n0 + r) * ldw + kc);
@@ -166,41 +166,52 @@ __global__ __launch_bounds__(PG_NW * 64, 2) void pgemm_bf16_kernel(const bf16* _
           const int h2 = cv.Hr >> 1, w2 = cv.Wr >> 1, mm = m < M ? m : 0;
           const int b = mm / (h2 * w2), rem = mm - b * h2 * w2, Y = rem / w2;
           const int ry = 2 * Y + (cv.par >> 1), rx = 2 * (rem - Y * w2) + (cv.par & 1);
+          // (offsets first, then both loads unconditionally at a valid address -- element 0 for a zero
+          // tap -- and the zeros selected after: a guarded load here made the compiler wait for each)
+          long offs[2];
 #pragma unroll
           for (int kt = 0; kt < 2; ++kt) {
             const int k = k0 + kt * 32 + fg * 8;
-            bf16x8 v = {};
+            offs[kt] = -1;
             if (m < M && k < K) {
-              const int t = k / cv.Cs, tp = cv.tap[t < 4 ? t : 3];
+              const int t = k / cv.Cs, tp = conv_tap(cv, t);
               const int ky = tp / 3, kx = tp - 3 * ky;
               const int sy = (ry + 1 - ky) >> 1, sx = (rx + 1 - kx) >> 1;   // even by the class
               if (sy >= 0 && sy < cv.Hs && sx >= 0 && sx < cv.Ws)
-                v = *reinterpret_cast<const bf16x8*>(A + ((long)(b * cv.Hs + sy) * cv.Ws + sx) * cv.Cs +
-                                                     (k - t * cv.Cs));
+                offs[kt] = ((long)(b * cv.Hs + sy) * cv.Ws + sx) * cv.Cs + (k - t * cv.Cs);
             }
-            a[i][kt] = v;
+          }
+#pragma unroll
+          for (int kt = 0; kt < 2; ++kt) {
+            const bf16x8 v = *reinterpret_cast<const bf16x8*>(A + (offs[kt] >= 0 ? offs[kt] : 0));
+            a[i][kt] = offs[kt] >= 0 ? v : bf16x8{};
           }
           continue;
         }
         const ConvRow cr = conv_row(cv, m < M ? m : 0);
+        long offs[2];
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt) {
           const int k = k0 + kt * 32 + fg * 8;
-          bf16x8 v = {};
+          offs[kt] = -1;
           if (m < M && k < K) {
             const int tap = k / cv.Cs;            // 8 | Cs: the 8 columns share one tap
             const long off = conv_src(cv, cr, tap);
-            if (off >= 0) v = *reinterpret_cast<const bf16x8*>(A + off + (k - tap * cv.Cs));
+            if (off >= 0) offs[kt] = off + (k - tap * cv.Cs);
           }
-          a[i][kt] = v;
+        }
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) {
+          const bf16x8 v = *reinterpret_cast<const bf16x8*>(A + (offs[kt] >= 0 ? offs[kt] : 0));
+          a[i][kt] = offs[kt] >= 0 ? v : bf16x8{};
         }
       } else {
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt) {
           const int k = k0 + kt * 32 + fg * 8;
-          bf16x8 v = {};
-          if (m < M && k < K) v = *reinterpret_cast<const bf16x8*>(A + (long)m * lda + k);
-          a[i][kt] = v;
+          const bool ok = m < M && k < K;
+          const bf16x8 v = *reinterpret_cast<const bf16x8*>(A + (ok ? (long)m * lda + k : 0));
+          a[i][kt] = ok ? v : bf16x8{};
         }
       }
     }

@@ -180,6 +180,10 @@ extern "C" int ogv_set_option(const char* name, int value) {
     set_dw_fuse(value);
     return OGV_OK;
   }
+  if (!strcmp(name, "dw_bn2")) {
+    set_dw_bn2(value);
+    return OGV_OK;
+  }
   if (!strcmp(name, "se_gemv")) {
     set_se_gemv(value);
     return OGV_OK;

@@ -121,7 +121,10 @@ __global__ __launch_bounds__(W2_NT) void wgrad2_bf16_kernel(const bf16* __restri
       if constexpr (CV) {
         const int tap = xk / cv.Cs;
         const long off = conv_src(cv, conv_row(cv, m), tap);
-        R.x[v] = off >= 0 ? *reinterpret_cast<const uint4*>(X + off + (xk - tap * cv.Cs)) : uint4{0u, 0u, 0u, 0u};
+        // unconditional load at a valid address (element 0 for a zero tap), zero selected after: the
+        // guarded form made the compiler wait for each of these loads in turn
+        const uint4 xv = *reinterpret_cast<const uint4*>(X + (off >= 0 ? off + (xk - tap * cv.Cs) : 0));
+        R.x[v] = off >= 0 ? xv : uint4{0u, 0u, 0u, 0u};
       } else {
         R.x[v] = *reinterpret_cast<const uint4*>(X + (long)m * ldx + xk);
       }

@@ -855,6 +855,44 @@ def test_mbconv_fused_image_groups(C, H, B):
         assert lib.ogv_set_option(b"dw_blocks", 0) == 0
 
 
+@pytest.mark.parametrize("C,H,B", [(48, 32, 4), (96, 16, 3), (192, 8, 2), (256, 4, 5), (20, 6, 2), (64, 2, 9)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_mbconv_bn2_staged_matches_materialised(C, H, B, dtype):
+    """dw_bn2 = 1 (the BN2 backward computed as the depthwise backward stages its rows, dd never in
+    HBM) against dw_bn2 = 0 (bn2_apply writes dd, the depthwise backward reads it): the staged value
+    is bn2_apply's arithmetic rounded to the storage dtype, so every gradient is bit-identical."""
+    from ogv._lib import load
+    from src.model.mbc_conv import MBConv, MBConvConfig
+    lib = load()
+    torch.manual_seed(C + H + B)
+    m = MBConv(C, C, 1, MBConvConfig()).to(DEV)
+    with torch.no_grad():
+        for b in m.modules():
+            if isinstance(b, torch.nn.BatchNorm2d):
+                b.running_mean.normal_(0, 0.2)
+                b.running_var.uniform_(0.5, 1.5)
+                b.weight.normal_(1, 0.1)
+                b.bias.normal_(0, 0.1)
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    x = torch.randn(B, C, H, H, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+    dy = torch.randn_like(x)
+    res = []
+    try:
+        for knob in (0, 1):
+            assert lib.ogv_set_option(b"dw_bn2", knob) == 0
+            m.load_state_dict(sd)
+            m.zero_grad(set_to_none=True)
+            xx = x.clone().requires_grad_()
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=dtype == torch.bfloat16):
+                y = m.train()(xx)
+            y.backward(dy)
+            res.append([xx.grad.clone()] + [p.grad.clone() for p in m.parameters()])
+    finally:
+        assert lib.ogv_set_option(b"dw_bn2", 1) == 0
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+
+
 def test_outgrid_block_with_dropouts():
     """proj_drop / ffn_drop > 0 (no reference config uses them; the modules then take torch Dropout on
     the HIP kernels' outputs with an explicit residual add): training forward + backward finite and

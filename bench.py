@@ -346,8 +346,10 @@ def main():
         if probe and probe["achieved_GBs"]:
             traffic = None
             tf = ROOT / "profiles" / "pmc_traffic.json"
-            if tf.exists() and args.model == "model_a_7m" and B == 512:   # the PMC passes ran on this workload
-                traffic = json.loads(tf.read_text()).get(args.probe, {}).get("hbm_bytes_per_launch")
+            if tf.exists():   # PMC passes of this workload (tools/gpu_measure.sh): 7M bs=512 under the probe's
+                # name, any other workload under '<model>/bs<B>:<probe>'
+                key = args.probe if (args.model == "model_a_7m" and B == 512) else f"{args.model}/bs{B}:{args.probe}"
+                traffic = json.loads(tf.read_text()).get(key, {}).get("hbm_bytes_per_launch")
             ach = probe["achieved_GBs"]
             roof = {"probe": args.probe, "kernel": PROBE_KERNEL[args.probe], "bound": "hbm", "achieved": round(ach, 1),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,

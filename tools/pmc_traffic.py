@@ -26,6 +26,8 @@ PROBES = {
     "gemm_fwd": r"gemm_bf16_kernel<(128|64), (128|64), (true|false), false, 0, false>",
     "outlook_fwd": r"outlook_fwd_kernel",
     "grid_fwd": r"grid_fwd_kernel",
+    # bench.py's "wgrad" probe (the 14M / 22M dominant family): the weight-gradient kernels themselves
+    "wgrad": r"wgrad2_bf16_kernel|(?<![s2])wgrad_bf16_kernel|swgrad_bf16_kernel",
 }
 
 
@@ -56,6 +58,8 @@ def main():
     ap.add_argument("--out", default="profiles/pmc_traffic.json")
     ap.add_argument("--probe", default=None, help="the bench.py --probe of this run: only its entry is (re)written, "
                     "from the launches queued behind the probe's spin; other entries of --out are kept")
+    ap.add_argument("--key", default=None, help="entry name in --out (default: the probe name; bench.py reads "
+                    "'<model>/bs<B>:<probe>' for workloads other than Model-A-7M bs=512)")
     ap.add_argument("--skip-steps", type=int, default=1, help="leading launches per probe treated as warmup: "
                     "steps to drop (the probe keeps the last step's launches)")
     a = ap.parse_args()
@@ -80,11 +84,12 @@ def main():
         f, w = f[-n:], w[-n:]
         fb = [2 * 1024 * x for x in f]   # KB -> bytes, x2 gfx950 read correction
         wb = [1024 * x for x in w]
-        out[probe] = {"launches": n, "kernel_regex": rx,
+        key = a.key or probe
+        out[key] = {"launches": n, "kernel_regex": rx,
                       "fetch_bytes_per_launch": sum(fb) / n, "write_bytes_per_launch": sum(wb) / n,
                       "hbm_bytes_per_launch": (sum(fb) + sum(wb)) / n,
                       "correction": "FETCH_SIZE(KB)*1024*2 (gfx950 half-count of wide reads) + WRITE_SIZE(KB)*1024"}
-        print(probe, json.dumps(out[probe]))
+        print(key, json.dumps(out[key]))
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     with open(a.out, "w") as fo:
         json.dump(out, fo, indent=1)

@@ -24,14 +24,15 @@ def main(trace, log, clean_log=None):
     rec = json.loads(line)
     roof = rec.get("roofline") or {}
     fams = {"sgemm": "sgemm_bf16_kernel", "gemm_tiled": "::gemm_bf16_kernel", "gemm_panel": "pgemm_bf16_kernel", "outlook_bwd": "outlook_bwd",
-            "outlook_fwd": "outlook_fwd", "grid_fwd": "grid_fwd"}
+            "outlook_fwd": "outlook_fwd", "grid_fwd": "grid_fwd",
+            "wgrad": r"wgrad2_bf16_kernel|(?<![s2])wgrad_bf16_kernel|swgrad_bf16_kernel"}   # regexes
     fam = fams.get(roof.get("probe", "sgemm" if "sgemm" in roof.get("kernel", "") else ""))
     if fam is None:
         print("probe family has no single-kernel trace match; nothing to compare")
         return
     probed, allk = [], []
     for i, r in enumerate(rows):
-        if fam not in r["Kernel_Name"]:
+        if not re.search(fam, r["Kernel_Name"]):
             continue
         d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6  # ms
         # same queue, the previous launch on it is the sleep kernel

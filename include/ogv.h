@@ -217,8 +217,8 @@ int ogv_dwconv3x3_bwd(const void* dy, const void* x, const float* w, void* dx, f
  *   -> p = (a2*g).Wp^T -> out = x + BN3(p)
  * x/out: [B*H*W, C] rows.  `saved` (>= ogv_mbconv_saved_bytes) is written by fwd and read by
  * bwd; `ws` (>= ogv_mbconv_ws_bytes) is scratch for either; bwd also takes `param_ws`
- * (>= ogv_mbconv_param_ws_bytes): the slab partials of its four weight gradients (expand, project,
- * SE fc1 / fc2), whose column reductions are deferred under ogv_reduce_defer -- keep it allocated
+ * (>= ogv_mbconv_param_ws_bytes): the slab partials of its weight gradients (expand, project,
+ * SE fc1 / fc2, depthwise), whose column reductions are deferred under ogv_reduce_defer -- keep it allocated
  * until ogv_reduce_flush.  bwd writes dx (= the residual
  * gradient + the branch gradient) and every parameter gradient (fp32, overwritten).
  * num_batches_tracked is left to the caller.
@@ -367,6 +367,21 @@ typedef struct {
 size_t ogv_clip_adamw_ws_bytes(const ogv_adamw_tensor* tensors, int n);
 int ogv_clip_adamw(const ogv_adamw_tensor* tensors, int n, const ogv_adamw_group* groups, int ngroups,
                    const float* found_inf, float max_norm, float* norm_ws, void* stream);
+
+/* Training loss: F.cross_entropy(logits, target, label_smoothing=ls), mean reduction, ignore_index
+ * -100, over fp32 logits [B, K] row-major (src/training/one_epoch_train.py:96; torch's
+ * cross_entropy_loss_label_smoothing).  Forward: a row pass (a wave per row) + a one-workgroup
+ * fixed-order sum; backward: one launch.
+ * ogv_ce_ls_fwd: *loss = (1-ls) * mean nll + (ls/K) * mean(-sum_k log_softmax); ws (ogv_ce_ls_ws_bytes)
+ *   receives the per-row logsumexp and the count of non-ignored rows for the backward; found != NULL:
+ *   *found = !isfinite(loss) (ogv_step_flag mode 0, fused).  A label outside [0, K) other than -100
+ *   (torch raises; a raise needs a device sync) makes the loss NaN, so the guarded step is skipped.
+ * ogv_ce_ls_bwd: dlogits = (*grad_loss / n) * (softmax - (1-ls) onehot - ls/K), 0 on ignored rows. */
+size_t ogv_ce_ls_ws_bytes(int B);
+int ogv_ce_ls_fwd(const float* logits, const int64_t* target, int B, int K, float label_smoothing, float* loss,
+                  float* ws, float* found, void* stream);
+int ogv_ce_ls_bwd(const float* logits, const int64_t* target, const float* ws, const float* grad_loss, int B, int K,
+                  float label_smoothing, float* dlogits, void* stream);
 
 /* Training-step guard and schedule (src/training/one_epoch_train.py:98-108, :152-153;
  * src/training/warmup.py:38-52), one single-thread launch each, capturable, no host sync:

@@ -56,5 +56,13 @@ void bn_finalize_launch(const double* sums, int K, double n, const float* gamma,
 // [gamma*invstd, 0, 0] (eval);  dx = coef0 * (dz - coef1 - xhat*coef2).
 void bn_coeffs_launch(const float* S, int K, float n, const float* gamma, const float* invstd, float* dgamma,
                       float* dbeta, float* coef, int train, hipStream_t s);
+// The column reduction of R partial rows ([R][ld]: columns c and K + c) fused with the train-mode
+// finalize / the coefficients: one launch instead of colreduce (1-2 launches) + finalize / coeffs
+// (ogv_mbconv.hip; fixed-order, deterministic).
+void bn_reduce_finalize_launch(const double* part, long R, long ld, int K, double n, const float* gamma,
+                               const float* beta, float eps, float momentum, float* rm, float* rv, float* mean,
+                               float* invstd, float* sc, float* sh, hipStream_t s);
+void bn_reduce_coeffs_launch(const float* part, long R, long ld, int K, float n, const float* gamma,
+                             const float* invstd, float* dgamma, float* dbeta, float* coef, int train, hipStream_t s);
 
 }  // namespace ogv

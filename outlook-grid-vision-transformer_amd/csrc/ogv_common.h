@@ -48,6 +48,9 @@ void colreduce(const double* src, double* dst, long R, long n, long ld, double* 
 // single-pass colreduce4 kernel); otherwise identical to colreduce.
 void colreduce_param(const float* src, float* dst, long R, long n, long ld, float* tmp, hipStream_t s,
                      float* dst2 = nullptr, long n1 = 0);
+// Deferred tap-major -> channel-major reduction (the depthwise weight gradient: src columns tap*C + c,
+// dst[c*9 + tap]); returns false (nothing recorded) when deferral is off or the shape does not fit
+bool colreduce_param_tap(const float* src, float* dst, long R, long C, long ld);
 
 static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 static inline unsigned cdiv(long a, long b) { return (unsigned)((a + b - 1) / b); }

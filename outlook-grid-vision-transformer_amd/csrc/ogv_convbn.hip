@@ -318,6 +318,7 @@ struct CbWs {
   char* dy;       // conv-output gradient Mo x Cout
   float* dwt;     // tap-major dW
   char* gemm;     // wgrad slabs
+  char* stem;     // the stem weight gradient's partial rows + colreduce scratch (C_in <= 3)
   size_t bytes;
 };
 static CbWs cb_ws(const ogv_convbn_desc& d, ogv_dtype dt, void* base) {
@@ -339,6 +340,7 @@ static CbWs cb_ws(const ogv_convbn_desc& d, ogv_dtype dt, void* base) {
   w.dy = c.take<char>((size_t)g.Mo * d.Cout * esize(dt));
   w.dwt = c.take<float>((size_t)d.Cout * K9);
   w.gemm = c.take<char>(wgrad_ws_bytes((int)g.Mo, d.Cout, K9));
+  w.stem = c.take<char>(d.Cin <= 3 ? stem_wgrad_ws_bytes(g.Mo, d.Cout, d.Cin) : 16);
   w.bytes = c.off;
   return w;
 }
@@ -385,11 +387,17 @@ extern "C" int ogv_convbn_fwd(const void* x, void* out, void* saved, void* ws, c
     e.stat = w.dstat;
     e.stat_shift = p->bn_rm;
   }
-  conv_gemm_launch(dt, x, g.fwd, wt, y, (int)g.Mo, d->Cout, e, s);
+  // the stem (C_in <= 3): dedicated kernel (ogv_stem.hip); everything else: implicit-GEMM conv kernels
+  int srows = gemm_stat_rows((int)g.Mo);
+  if (!(dt == OGV_BF16 && stem_fwd_try(x, g.fwd, wt, y, (int)g.Mo, d->Cout, e, s, &srows)))
+    conv_gemm_launch(dt, x, g.fwd, wt, y, (int)g.Mo, d->Cout, e, s);
   if (d->has_bn) {
-    if (stats) colreduce(w.dstat, w.dsums, gemm_stat_rows((int)g.Mo), 2L * d->Cout, 2L * d->Cout, w.dtmp, s);
-    bn_finalize_launch(w.dsums, d->Cout, (double)g.Mo, p->bn_w, p->bn_b, d->bn_eps, d->bn_momentum, p->bn_rm, p->bn_rv,
-                       b.mean, b.invstd, b.sc, b.sh, d->train, s);
+    if (stats)   // partial rows -> batch statistics, running stats, apply coefficients: one launch
+      bn_reduce_finalize_launch(w.dstat, srows, 2L * d->Cout, d->Cout, (double)g.Mo, p->bn_w,
+                                p->bn_b, d->bn_eps, d->bn_momentum, p->bn_rm, p->bn_rv, b.mean, b.invstd, b.sc, b.sh, s);
+    else
+      bn_finalize_launch(w.dsums, d->Cout, (double)g.Mo, p->bn_w, p->bn_b, d->bn_eps, d->bn_momentum, p->bn_rm,
+                         p->bn_rv, b.mean, b.invstd, b.sc, b.sh, d->train, s);
   } else {
     bn_identity_kernel<<<cdiv(d->Cout, 256), 256, 0, s>>>(b.mean, b.invstd, b.sc, b.sh, nullptr, d->Cout);
   }
@@ -415,8 +423,8 @@ extern "C" int ogv_convbn_bwd(const void* dout, const void* x, const void* saved
     const RowSlices rs = row_slices(g.Mo);
     OGV_CB_DISPATCH(dt, V, bn_bwd_reduce_run, dout, y, b.sc, b.sh, d->act, b.mean, b.invstd, w.stat, g.Mo, d->Cout, rs,
                     s);
-    colreduce(w.stat, w.sums, rs.S, 2L * d->Cout, 2L * d->Cout, w.tmp, s);
-    bn_coeffs_launch(w.sums, d->Cout, (float)g.Mo, p->bn_w, b.invstd, dbn_w, dbn_b, w.coef, d->train, s);
+    bn_reduce_coeffs_launch(w.stat, rs.S, 2L * d->Cout, d->Cout, (float)g.Mo, p->bn_w, b.invstd, dbn_w, dbn_b, w.coef,
+                            d->train, s);
   } else {
     bn_identity_kernel<<<cdiv(d->Cout, 256), 256, 0, s>>>(nullptr, nullptr, nullptr, nullptr, w.coef, d->Cout);
   }
@@ -424,8 +432,10 @@ extern "C" int ogv_convbn_bwd(const void* dout, const void* x, const void* saved
                   s);
   // 2) weight (+bias) gradient: dW[n][tap*Cin+c] = sum_m dy[m,n] * gather(x)[m, tap*Cin+c]
   const int K9 = 9 * d->Cin;
-  gemm_wgrad_launch(dt, w.dy, d->Cout, x, 0, Pro(), nullptr, 1, d->w_layout ? dw : w.dwt, dbias, (int)g.Mo, d->Cout,
-                    K9, w.gemm, s, &g.fwd);
+  if (!(dt == OGV_BF16 && stem_wgrad_try(x, g.fwd, w.dy, d->w_layout ? dw : w.dwt, dbias, (int)g.Mo, d->Cout, w.stem,
+                                         s)))
+    gemm_wgrad_launch(dt, w.dy, d->Cout, x, 0, Pro(), nullptr, 1, d->w_layout ? dw : w.dwt, dbias, (int)g.Mo, d->Cout,
+                      K9, w.gemm, s, &g.fwd);
   const long nw = (long)d->Cout * d->Cin * 9;
   if (!d->w_layout) conv_dw_untranspose_kernel<<<cdiv(nw, 256), 256, 0, s>>>(w.dwt, dw, d->Cout, d->Cin);
   // 3) data gradient: transposed gather of dy against the (Cin x 9*Cout) weight matrix
@@ -474,9 +484,11 @@ extern "C" int ogv_bn_act_fwd(const void* x, void* out, float* saved, void* ws, 
   const int V = vec_width(C);
   if (train) {
     OGV_CB_DISPATCH(dt, V, bn_stats_run, x, rm, stat, (long)M, C, rs, s);
-    colreduce(stat, sums, rs.S, 2L * C, 2L * C, tmp, s);
+    bn_reduce_finalize_launch(stat, rs.S, 2L * C, C, (double)M, bn_w, bn_b, eps, momentum, rm, rv, b.mean, b.invstd,
+                              b.sc, b.sh, s);
+  } else {
+    bn_finalize_launch(sums, C, (double)M, bn_w, bn_b, eps, momentum, rm, rv, b.mean, b.invstd, b.sc, b.sh, train, s);
   }
-  bn_finalize_launch(sums, C, (double)M, bn_w, bn_b, eps, momentum, rm, rv, b.mean, b.invstd, b.sc, b.sh, train, s);
   OGV_CB_DISPATCH(dt, V, bn_apply_run, x, b.sc, b.sh, act, out, (long)M, C, s);
   return check_launch("ogv_bn_act_fwd");
 }
@@ -498,8 +510,7 @@ extern "C" int ogv_bn_act_bwd(const void* dout, const void* x, const float* save
   float* coef = cw.take<float>(3 * (size_t)C);
   const int V = vec_width(C);
   OGV_CB_DISPATCH(dt, V, bn_bwd_reduce_run, dout, x, b.sc, b.sh, act, b.mean, b.invstd, stat, (long)M, C, rs, s);
-  colreduce(stat, sums, rs.S, 2L * C, 2L * C, tmp, s);
-  bn_coeffs_launch(sums, C, (float)M, bn_w, b.invstd, dbn_w, dbn_b, coef, train, s);
+  bn_reduce_coeffs_launch(stat, rs.S, 2L * C, C, (float)M, bn_w, b.invstd, dbn_w, dbn_b, coef, train, s);
   OGV_CB_DISPATCH(dt, V, bn_bwd_apply_run, dout, x, b.sc, b.sh, act, b.mean, b.invstd, coef, dx, (long)M, C, s);
   return check_launch("ogv_bn_act_bwd");
 }

@@ -132,6 +132,7 @@ struct RedDesc {
   const float* src;
   float *dst, *dst2;
   long R, n, ld, n1;
+  long tapC;   // > 0: column tap*tapC + c stored at dst[c*9 + tap] (depthwise weight gradient)
 };
 constexpr int RED_BATCH = 48;   // descriptors per launch (kernel arguments < 4 KB)
 struct RedBatch {
@@ -179,6 +180,7 @@ __global__ __launch_bounds__(256) void colreduce_batch_kernel(RedBatch b) {
       const long c = col + q;
       if (c >= d.n) break;
       if (d.dst2 && c >= d.n1) d.dst2[c - d.n1] = o[q];
+      else if (d.tapC > 0) d.dst[(c % d.tapC) * 9 + c / d.tapC] = o[q];
       else d.dst[c] = o[q];
     }
   }
@@ -192,10 +194,19 @@ void colreduce_param(const float* src, float* dst, long R, long n, long ld, floa
   const bool fits = (n & 3) == 0 && (ld & 3) == 0 && (reinterpret_cast<uintptr_t>(src) & 15) == 0 && R > 0 &&
                     (n + 63) / 64 < (1L << 20);
   if (g_defer && fits) {
-    g_pending.push_back(RedDesc{src, dst, dst2, R, n, ld, dst2 ? n1 : n});
+    g_pending.push_back(RedDesc{src, dst, dst2, R, n, ld, dst2 ? n1 : n, 0});
     return;
   }
   colreduce(src, dst, R, n, ld, tmp, s, dst2, n1);
+}
+
+bool colreduce_param_tap(const float* src, float* dst, long R, long C, long ld) {
+  const long n = 9 * C;
+  const bool fits = (n & 3) == 0 && (ld & 3) == 0 && (reinterpret_cast<uintptr_t>(src) & 15) == 0 && R > 0 &&
+                    (n + 63) / 64 < (1L << 20);
+  if (!g_defer || !fits) return false;
+  g_pending.push_back(RedDesc{src, dst, nullptr, R, n, ld, n, C});
+  return true;
 }
 
 }  // namespace ogv

@@ -237,6 +237,15 @@ bool se_gemv_on();
 void set_se_gemv(int v);
 void set_dw_fuse(int v);
 void set_dw_bn2(int v);
+void set_dw_fwd_r(int v);
+void set_stem(int v);
+// the stem convolution (C_in <= 3, ogv_stem.hip): false = not taken (the caller runs the generic path)
+bool stem_fwd_try(const void* x, const ConvG& cv, const float* wt, void* out, int M, int N, const Epi& epi,
+                  hipStream_t s, int* stat_rows);
+int stem_fwd_stat_rows(long M);   // BN partial rows the stem forward writes (<= gemm_stat_rows(M))
+bool stem_wgrad_try(const void* x, const ConvG& cv, const void* dy, float* dw, float* dbias, int M, int N, void* ws,
+                    hipStream_t s);
+size_t stem_wgrad_ws_bytes(long M, int N, int Cin);
 void set_swg_min_m(int v);
 void set_pg_split(int v);
 int split_w();

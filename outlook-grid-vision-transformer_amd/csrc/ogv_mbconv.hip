@@ -134,28 +134,54 @@ __global__ __launch_bounds__(256) void bn_reduce_finalize_kernel(const double* _
   sh[c] = bt - mean * gm * is;
 }
 
+// BN2 (TERMS): the partial rows are not stored -- row b is formed from the SE reduce's per-image sums
+// R[5][B][K], the gate and dpool/HW.  dy2 = (dA3*gate + dpool/HW) * s', so
+//   sum dy2 = sum_b gate*R1 + dpool/HW*R2,  sum dy2*dh = sum_b gate*R3 + dpool/HW*R4
+struct Bn2Terms {
+  const float *R, *gate, *dpool;
+  int HW;
+};
+template <bool TERMS = false>
 __global__ __launch_bounds__(256) void bn_reduce_coeffs_kernel(const float* __restrict__ part, long R, long ld, int K,
                                                                float n, const float* __restrict__ gamma,
                                                                const float* __restrict__ invstd,
                                                                float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                                               float* __restrict__ coef, int train) {
+                                                               float* __restrict__ coef, int train, Bn2Terms bt = {}) {
   __shared__ float red[2][16][16];
   const int cl = threadIdx.x & 15, rg = threadIdx.x >> 4;
   const int c = blockIdx.x * 16 + cl;
   float s1 = 0.f, s2 = 0.f;
+  // row r's two partials: stored ([R][ld]), or the BN2 terms of image r
+  const long BK = R * K;
+  const float ihw = TERMS ? 1.f / (float)bt.HW : 0.f;
+  auto row = [&](long r, float& v1, float& v2) {
+    if constexpr (TERMS) {
+      const long i = r * K + c;
+      const float gg = bt.gate[i], dp = bt.dpool[i] * ihw;
+      v1 = gg * bt.R[1 * BK + i] + dp * bt.R[2 * BK + i];
+      v2 = gg * bt.R[3 * BK + i] + dp * bt.R[4 * BK + i];
+    } else {
+      v1 = part[r * ld + c];
+      v2 = part[r * ld + K + c];
+    }
+  };
   if (c < K) {   // four row groups' loads in flight per trip
     float a1[4] = {0.f, 0.f, 0.f, 0.f}, a2[4] = {0.f, 0.f, 0.f, 0.f};
     long r = rg;
     for (; r + 48 < R; r += 64) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        a1[u] += part[(r + 16 * u) * ld + c];
-        a2[u] += part[(r + 16 * u) * ld + K + c];
+        float v1, v2;
+        row(r + 16 * u, v1, v2);
+        a1[u] += v1;
+        a2[u] += v2;
       }
     }
     for (; r < R; r += 16) {
-      a1[0] += part[r * ld + c];
-      a2[0] += part[r * ld + K + c];
+      float v1, v2;
+      row(r, v1, v2);
+      a1[0] += v1;
+      a2[0] += v2;
     }
     s1 = (a1[0] + a1[1]) + (a1[2] + a1[3]);
     s2 = (a2[0] + a2[1]) + (a2[2] + a2[3]);
@@ -177,6 +203,16 @@ __global__ __launch_bounds__(256) void bn_reduce_coeffs_kernel(const float* __re
   coef[2 * K + c] = train ? sdyx / n : 0.f;
 }
 
+void bn_reduce_finalize_launch(const double* part, long R, long ld, int K, double n, const float* gamma,
+                               const float* beta, float eps, float momentum, float* rm, float* rv, float* mean,
+                               float* invstd, float* sc, float* sh, hipStream_t s) {
+  bn_reduce_finalize_kernel<<<cdiv(K, 16), 256, 0, s>>>(part, R, ld, K, n, gamma, beta, eps, momentum, rm, rv, mean,
+                                                        invstd, sc, sh);
+}
+void bn_reduce_coeffs_launch(const float* part, long R, long ld, int K, float n, const float* gamma,
+                             const float* invstd, float* dgamma, float* dbeta, float* coef, int train, hipStream_t s) {
+  bn_reduce_coeffs_kernel<<<cdiv(K, 16), 256, 0, s>>>(part, R, ld, K, n, gamma, invstd, dgamma, dbeta, coef, train);
+}
 void bn_finalize_launch(const double* sums, int K, double n, const float* gamma, const float* beta, float eps,
                         float momentum, float* rm, float* rv, float* mean, float* invstd, float* sc, float* sh, int train,
                         hipStream_t s) {
@@ -202,7 +238,12 @@ void bn_coeffs_launch(const float* S, int K, float n, const float* gamma, const 
 // one output row is ~256 (pixel, V-channel chunk) items: one per thread per row.  Statistics /
 // weight-gradient partials are reduced once per block into row rid = group*ncolt + colt of a
 // [rows][Q][C] slab.
-constexpr int DW_R = 4;
+constexpr int DW_R = 4;   // the data / weight-gradient kernels (two sources + per-pixel loads: VGPR-bound)
+// the forward kernel's rows per step, knob "dw_fwd_r" (4 or 8): 8 rows per step (one source, ~124 VGPRs:
+// room for the deeper row pipeline) measured 16.14-16.16 vs 16.08-16.13 ms/step at 4 (7M, paired,
+// profiles/r04_dw_fwd_r.log): the kernel is not bound by loads in flight, so 4 stays the default
+static int g_dw_fwd_r = 4;
+void set_dw_fwd_r(int v) { g_dw_fwd_r = v == 4 ? 4 : 8; }
 // tuning knob "dw_blocks": > 0 = target block count of the depthwise kernels; 0 (default) = images
 // per block chosen for ~32 output rows per block (many short blocks balance best over the CUs)
 static int g_dw_blocks = 0;
@@ -212,10 +253,10 @@ struct DwTile {
   __host__ __device__ long rows() const { return (long)ngroups * ncolt; }
   long rows_max() const { return (long)B * ncolt; }  // workspace sizing: any G
   __host__ __device__ long nblocks() const { return rows() * nct; }
-  size_t ring_bytes() const { return (size_t)(DW_R + 2) * (TW + 2) * PP * sizeof(float); }
-  size_t lds_bytes(int nq, int V, size_t asz) const {
+  size_t ring_bytes(int R = DW_R) const { return (size_t)(R + 2) * (TW + 2) * PP * sizeof(float); }
+  size_t lds_bytes(int nq, int V, size_t asz, int R = DW_R) const {
     const size_t red = (size_t)4 * chunks * nq * V * asz;
-    return ring_bytes() > red ? ring_bytes() : red;
+    return ring_bytes(R) > red ? ring_bytes(R) : red;
   }
 };
 static DwTile dw_tile_plan(int B, int H, int W, int C, int V) {
@@ -282,9 +323,11 @@ __device__ __forceinline__ VRow vadv(const DwTile& t, VRow p) {
   return p;
 }
 
-__device__ __forceinline__ int ring_slot(int r) { return (r + DW_R + 2) % (DW_R + 2); }
+template <int R = DW_R>
+__device__ __forceinline__ int ring_slot(int r) { return (r + R + 2) % (R + 2); }
+template <int R = DW_R>
 __device__ __forceinline__ const float* ring_px(const float* ring, const DwTile& t, int r, int px) {
-  return ring + ((size_t)ring_slot(r) * (t.TW + 2) + px) * t.PP;
+  return ring + ((size_t)ring_slot<R>(r) * (t.TW + 2) + px) * t.PP;
 }
 
 
@@ -293,10 +336,10 @@ __device__ __forceinline__ const float* ring_px(const float* ring, const DwTile&
 // transform (stage(v, v2, image): BatchNorm + activation forward, or the whole BN2 backward from
 // the two sources (dA3, d) when TWO) and the conversion to fp32 are applied as the rows enter the
 // LDS ring.
-template <typename T, int V, int LDQ, bool TWO = false>
+template <typename T, int V, int LDQ, bool TWO = false, int R = DW_R>
 struct RowPipe {
-  RawVec<T, V> raw[DW_R][LDQ];
-  RawVec<T, V> raw2[TWO ? DW_R : 1][TWO ? LDQ : 1];
+  RawVec<T, V> raw[R][LDQ];
+  RawVec<T, V> raw2[TWO ? R : 1][TWO ? LDQ : 1];
   template <int NR>
   __device__ __forceinline__ void load(const T* __restrict__ src, const T* __restrict__ src2, const DwTile& t,
                                        const TileIdx& ti, VRow p, int cc) {
@@ -320,11 +363,11 @@ struct RowPipe {
                                         bool cok, Stage&& stage) const {
     const int n = (ti.tw + 2) * t.chunks;
 #pragma unroll
-    for (int r = 0; r < DW_R; ++r, p = vnext(t, p)) {
+    for (int r = 0; r < R; ++r, p = vnext(t, p)) {
       if (r >= nr) break;
       const bool rok = cok && p.im >= 0 && p.im < ti.nimg && p.y < t.H;
       const int im = min(max(p.im, 0), ti.nimg - 1);
-      float* slot = ring + (size_t)ring_slot(p.u) * (t.TW + 2) * t.PP;
+      float* slot = ring + (size_t)ring_slot<R>(p.u) * (t.TW + 2) * t.PP;
 #pragma unroll
       for (int j = 0; j < LDQ; ++j) {
         const int i = threadIdx.x + j * 256;
@@ -391,28 +434,28 @@ __device__ __forceinline__ void dw_reduce_store(A (&q)[NQ][V], float* lds_raw, i
 // clamped row), then the output rows among u..u+R-1 (not seam rows) are computed through
 // body(r, u+r, image, y, px), one item (pixel, V channels) per thread and row.  Issue order = retire
 // order, so the body waits for its own loads only while the prefetch stays in flight.
-template <typename T, int V, int LDQ, bool TWO, typename Stage, typename Pre, typename Body>
+template <typename T, int V, int LDQ, bool TWO, int R, typename Stage, typename Pre, typename Body>
 __device__ __forceinline__ void dw_walk(float* ring, const T* __restrict__ src, const T* __restrict__ src2,
                                         const DwTile& t, const TileIdx& ti, int cc, int chunk, bool cok,
                                         Stage&& stage, Pre&& pre, Body&& body) {
-  RowPipe<T, V, LDQ, TWO> rp;
+  RowPipe<T, V, LDQ, TWO, R> rp;
   VRow p = {-1, -1, t.H};
   rp.template load<2>(src, src2, t, ti, p, cc);
   rp.store(ring, t, ti, p, 2, chunk, cok, stage);
-  rp.template load<DW_R>(src, src2, t, ti, vadv<2>(t, p), cc);
+  rp.template load<R>(src, src2, t, ti, vadv<2>(t, p), cc);
   const int nitems = ti.tw * t.chunks;  // <= 256 (dw_tile_plan)
   const bool item = cok && (int)threadIdx.x < nitems;
   const int px = min((int)threadIdx.x, nitems - 1) / t.chunks;
   const int nv = ti.nimg * (t.H + 1) - 1;  // virtual rows incl. the seams between images
-  for (p = vnext(t, p); p.u < nv; p = vadv<DW_R>(t, p)) {
-    rp.store(ring, t, ti, vnext(t, p), DW_R, chunk, cok, stage);
+  for (p = vnext(t, p); p.u < nv; p = vadv<R>(t, p)) {
+    rp.store(ring, t, ti, vnext(t, p), R, chunk, cok, stage);
     __syncthreads();
     pre(p, px);
-    rp.template load<DW_R>(src, src2, t, ti, vadv<DW_R + 1>(t, p), cc);
+    rp.template load<R>(src, src2, t, ti, vadv<R + 1>(t, p), cc);
     if (item) {
       VRow q = p;
 #pragma unroll
-      for (int r = 0; r < DW_R; ++r, q = vnext(t, q))
+      for (int r = 0; r < R; ++r, q = vnext(t, q))
         if (q.u < nv && q.y < t.H) body(r, q.u, ti.b0 + q.im, q.y, px);
     }
     __syncthreads();
@@ -428,7 +471,7 @@ __device__ __forceinline__ void dw_pixel_load(RawVec<T, V>& rv, const T* __restr
 }
 
 // d = dw3x3(act(e*sc1 + sh1)) (+ fp64 stats of the rounded output minus shift)
-template <typename T, int V, int LDQ, int ACT>
+template <typename T, int V, int LDQ, int ACT, int R>
 __global__ __launch_bounds__(256) void dw_fwd_tile_kernel(const T* __restrict__ e, const float* __restrict__ wdw,
                                                           const float* __restrict__ sc, const float* __restrict__ sh,
                                                           int act, T* __restrict__ out, double* __restrict__ stat,
@@ -457,7 +500,7 @@ __global__ __launch_bounds__(256) void dw_fwd_tile_kernel(const T* __restrict__ 
 #pragma unroll
     for (int k = 0; k < V; ++k) v[k] = act_fwd(ACT, fmaf(v[k], s[k], h[k]));
   };
-  dw_walk<T, V, LDQ, false>(ring, e, e, t, ti, cc, chunk, cok, stage, [&](VRow, int) {},
+  dw_walk<T, V, LDQ, false, R>(ring, e, e, t, ti, cc, chunk, cok, stage, [&](VRow, int) {},
                            [&](int, int u, long b, int y, int px) {
     float acc[V];
 #pragma unroll
@@ -466,7 +509,7 @@ __global__ __launch_bounds__(256) void dw_fwd_tile_kernel(const T* __restrict__ 
     for (int ki = 0; ki < 3; ++ki)
 #pragma unroll
       for (int kj = 0; kj < 3; ++kj) {
-        const float* src = ring_px(ring, t, u - 1 + ki, px + kj) + chunk * V;
+        const float* src = ring_px<R>(ring, t, u - 1 + ki, px + kj) + chunk * V;
 #pragma unroll
         for (int i = 0; i < V; i += 4) {
           const float4 a = *reinterpret_cast<const float4*>(src + i);
@@ -586,7 +629,7 @@ __global__ __launch_bounds__(256) void dw_dgrad_tile_kernel(const T* __restrict_
       }
     }
   };
-  dw_walk<T, V, LDQ, BN2>(ring, dd, b2.d, t, ti, cc, chunk, cok, stage, pre, [&](int r, int u, long b, int y, int px) {
+  dw_walk<T, V, LDQ, BN2, DW_R>(ring, dd, b2.d, t, ti, cc, chunk, cok, stage, pre, [&](int r, int u, long b, int y, int px) {
     const long off = ((b * t.H + y) * t.W + ti.x0 + px) * t.C + c;
     float ev[V];
     ce[r].unpack(ev);
@@ -662,7 +705,7 @@ __global__ __launch_bounds__(256) void dw_wgrad_tile_kernel(const T* __restrict_
 #pragma unroll
     for (int k = 0; k < V; ++k) v[k] = act_fwd(ACT, fmaf(v[k], s[k], h[k]));
   };
-  dw_walk<T, V, LDQ, false>(ring, e, e, t, ti, cc, chunk, cok, stage, pre, [&](int r, int u, long, int, int px) {
+  dw_walk<T, V, LDQ, false, DW_R>(ring, e, e, t, ti, cc, chunk, cok, stage, pre, [&](int r, int u, long, int, int px) {
     float g[V];
     cg[r].unpack(g);
 #pragma unroll
@@ -898,20 +941,6 @@ __global__ __launch_bounds__(256) void se_bwd_reduce_kernel(const T* __restrict_
     }
   }
   dw_reduce_store<5, V, float>(q, lds, chunks, R + b * K, (long)B * K, K, bx * chunks * V, gate + b * K, dz2 + b * K);
-}
-
-// BN2 reductions from the per-image sums: dy2 = (dA3*gate + dpool/HW) * s'
-//   sum dy2 = sum_b gate*R1 + dpool/HW*R2,  sum dy2*dh = sum_b gate*R3 + dpool/HW*R4
-// terms[b][0][c], terms[b][1][c] here; the sum over b is a column reduction (colreduce).
-__global__ void bn2_terms_kernel(const float* __restrict__ R, const float* __restrict__ gate,
-                                 const float* __restrict__ dpool, float* __restrict__ terms, int B, int HW, int K) {
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long BK = (long)B * K;
-  if (i >= BK) return;
-  const long b = i / K, c = i - b * K;
-  const float gg = gate[i], dp = dpool[i] * (1.f / (float)HW);
-  terms[b * 2 * K + c] = gg * R[1 * BK + i] + dp * R[2 * BK + i];
-  terms[b * 2 * K + K + c] = gg * R[3 * BK + i] + dp * R[4 * BK + i];
 }
 
 // ---- row-tiled elementwise kernels: thread = (channel chunk, row slot), EW_RPT rows per thread, so
@@ -1165,12 +1194,13 @@ static FwdWs fwd_ws_layout(void* base, const ogv_mbconv_desc& s, size_t* total) 
 
 struct BwdWs {
   void *dp, *bufA, *bufB;
-  float *stat, *S, *coef, *R, *dgate, *dz2, *dh, *dz1, *dpool, *part9, *tmp, *sums9, *terms;
+  float *stat, *S, *coef, *R, *dgate, *dz2, *dh, *dz1, *dpool, *part9, *tmp, *sums9;
   float *wtse, *split;  // transposed SE weight, split-K partials
   float* tmp2;          // colreduce scratch of the side stream
   char *gemm, *gemm2;   // GEMM workspaces: current stream, side stream
-  // slab partials of the four parameter weight gradients, one region each: their column reductions
-  // may be deferred to the end of the backward (colreduce_param), so no later phase may reuse them
+  // slab partials of the four parameter weight gradients, one region each, and the depthwise weight
+  // gradient's [rows][9][mid] partials: their column reductions may be deferred to the end of the
+  // backward (colreduce_param / colreduce_param_tap), so no later phase may reuse them
   char *wg_proj, *wg_expand, *wg_se2, *wg_se1;
 };
 static size_t max3(size_t a, size_t b, size_t c) { return a > b ? (a > c ? a : c) : (b > c ? b : c); }
@@ -1194,8 +1224,6 @@ static BwdWs bwd_ws_layout(void* base, const ogv_mbconv_desc& s, size_t esz, siz
   w.dh = b.take<float>((size_t)s.B * s.se);
   w.dz1 = b.take<float>((size_t)s.B * s.se);
   w.dpool = b.take<float>((size_t)s.B * s.mid);
-  w.part9 = b.take<float>(S2 * 9 * s.mid);
-  w.terms = b.take<float>((size_t)2 * s.B * s.mid);
   w.tmp = b.take<float>(max3(max3(colreduce_tmp_floats(Smax, 2 * K2), colreduce_tmp_floats(S2, 9L * s.mid), 16),
                              colreduce_tmp_floats(s.B, 2L * s.mid), 16));
   w.sums9 = b.take<float>(9 * (size_t)s.mid);
@@ -1209,6 +1237,7 @@ static BwdWs bwd_ws_layout(void* base, const ogv_mbconv_desc& s, size_t esz, siz
   w.tmp2 = b.take<float>(colreduce_tmp_floats(S2, 9L * s.mid) + 16);
   w.gemm2 = b.take<char>(g);
   w.wg_proj = w.wg_expand = w.wg_se2 = w.wg_se1 = nullptr;   // bwd_param_ws_layout
+  w.part9 = nullptr;
   if (total) *total = b.off + 256;
   return w;
 }
@@ -1221,11 +1250,13 @@ static void bwd_param_ws_layout(void* base, const ogv_mbconv_desc& s, BwdWs* w, 
   char* p1 = b.take<char>(wgrad_ws_bytes((int)M, s.mid, s.C));
   char* p2 = b.take<char>(wgrad_ws_bytes(s.B, s.mid, s.se));
   char* p3 = b.take<char>(wgrad_ws_bytes(s.B, s.se, s.mid));
+  float* p9 = b.take<float>(dw_tile_plan(s.B, s.H, s.W, s.mid, 4).rows_max() * 9 * s.mid);
   if (w) {
     w->wg_proj = p0;
     w->wg_expand = p1;
     w->wg_se2 = p2;
     w->wg_se1 = p3;
+    w->part9 = p9;
   }
   if (total) *total = b.off + 256;
 }
@@ -1299,13 +1330,17 @@ struct Ops {
                      const float* shift, const DwTile& t, hipStream_t st) {
     if (skip_mask() & 8) return;
     constexpr int V = 4;
-    const size_t lds = t.lds_bytes(2, V, sizeof(double));
-    OGV_DW_ACT(act, if (t.ldq <= 1) dw_fwd_tile_kernel<T, V, 1, A><<<dw_grid(t), 256, lds, st>>>(
-                        (const T*)e, w, sc, sh, act, (T*)out, stat, shift, t);
-               else if (t.ldq <= 2) dw_fwd_tile_kernel<T, V, 2, A><<<dw_grid(t), 256, lds, st>>>(
-                        (const T*)e, w, sc, sh, act, (T*)out, stat, shift, t);
-               else dw_fwd_tile_kernel<T, V, 3, A><<<dw_grid(t), 256, lds, st>>>(
+    const size_t lds = t.lds_bytes(2, V, sizeof(double), g_dw_fwd_r);
+#define OGV_DWF(R_)                                                                                  \
+    OGV_DW_ACT(act, if (t.ldq <= 1) dw_fwd_tile_kernel<T, V, 1, A, R_><<<dw_grid(t), 256, lds, st>>>( \
+                        (const T*)e, w, sc, sh, act, (T*)out, stat, shift, t);                        \
+               else if (t.ldq <= 2) dw_fwd_tile_kernel<T, V, 2, A, R_><<<dw_grid(t), 256, lds, st>>>( \
+                        (const T*)e, w, sc, sh, act, (T*)out, stat, shift, t);                        \
+               else dw_fwd_tile_kernel<T, V, 3, A, R_><<<dw_grid(t), 256, lds, st>>>(                  \
                         (const T*)e, w, sc, sh, act, (T*)out, stat, shift, t))
+    if (g_dw_fwd_r == 8) { OGV_DWF(8) }
+    else { OGV_DWF(4) }
+#undef OGV_DWF
   }
   // part != nullptr: the weight-gradient partials in the same pass (dw_dgrad_tile_kernel<.., WG>)
   // b2 != nullptr: dd is BN2-backward(dA3 = dd, b2->d), computed as the rows are staged
@@ -1568,9 +1603,10 @@ static void mbconv_bwd_impl(const void* dout, const void* x, const Saved& sv, vo
   // B5) BN2 backward: dd = ca*(dy2 - cb - dhat*cc)  -> bufB  (with dw_bn2: computed inside B6's staging)
   const bool bn2f = g_dw_fuse && g_dw_bn2;
   {
-    bn2_terms_kernel<<<cdiv((long)s.B * s.mid, 256), 256, 0, st>>>(w.R, sv.gate, w.dpool, w.terms, s.B, HW, s.mid);
-    bn_reduce_coeffs_kernel<<<cdiv(s.mid, 16), 256, 0, st>>>(w.terms, s.B, 2L * s.mid, s.mid, (float)M, P.bn2_w, sv.inv2,
-                                                            G.bn2_w, G.bn2_b, w.coef, s.train);
+    // BN2's column sums over the images, the per-image terms formed on the fly (no terms launch)
+    bn_reduce_coeffs_kernel<true><<<cdiv(s.mid, 16), 256, 0, st>>>(nullptr, s.B, 2L * s.mid, s.mid, (float)M, P.bn2_w,
+                                                                   sv.inv2, G.bn2_w, G.bn2_b, w.coef, s.train,
+                                                                   Bn2Terms{w.R, sv.gate, w.dpool, HW});
     if (!bn2f)
       OGV_V_DISPATCH(rp.V, O::template bn2_apply, w.bufA, sv.d, sv.sc2, sv.sh2, sv.mean2, sv.inv2, sv.gate, w.dpool,
                      w.coef, s.act, w.bufB, M, HW, s.mid, st);
@@ -1586,8 +1622,11 @@ static void mbconv_bwd_impl(const void* dout, const void* x, const Saved& sv, vo
       const Bn2In<T> b2 = {(const T*)sv.d, sv.sc2, sv.sh2, sv.mean2, sv.inv2, sv.gate, w.dpool, w.coef, HW};
       O::dw_dgrad(w.bufA, P.w_dw, sv.e, sv.sc1, sv.sh1, sv.mean1, sv.inv1, s.act, dy1, w.stat, t, st, w.part9, &b2);
       sd = fork_side(st);
-      colreduce(w.part9, w.sums9, t.rows(), 9L * s.mid, 9L * s.mid, w.tmp2, sd);
-      tapmajor_to_chan_kernel<<<cdiv(9 * s.mid, 256), 256, 0, sd>>>(w.sums9, G.w_dw, s.mid);
+      // dWdw: deferred into the batched flush (written channel-major there), or reduced here
+      if (!colreduce_param_tap(w.part9, G.w_dw, t.rows(), s.mid, 9L * s.mid)) {
+        colreduce(w.part9, w.sums9, t.rows(), 9L * s.mid, 9L * s.mid, w.tmp2, sd);
+        tapmajor_to_chan_kernel<<<cdiv(9 * s.mid, 256), 256, 0, sd>>>(w.sums9, G.w_dw, s.mid);
+      }
     } else if (g_dw_fuse) {   // one pass over (dd, e): data gradient + BN1 sums + dWdw partials
       O::dw_dgrad(w.bufB, P.w_dw, sv.e, sv.sc1, sv.sh1, sv.mean1, sv.inv1, s.act, w.bufA, w.stat, t, st, w.part9);
       sd = fork_side(st);  // the partials' reduction overlaps the BN1 backward

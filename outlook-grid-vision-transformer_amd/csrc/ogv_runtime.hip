@@ -180,6 +180,14 @@ extern "C" int ogv_set_option(const char* name, int value) {
     set_dw_fuse(value);
     return OGV_OK;
   }
+  if (!strcmp(name, "stem")) {
+    set_stem(value);
+    return OGV_OK;
+  }
+  if (!strcmp(name, "dw_fwd_r")) {
+    set_dw_fwd_r(value);
+    return OGV_OK;
+  }
   if (!strcmp(name, "dw_bn2")) {
     set_dw_bn2(value);
     return OGV_OK;

@@ -311,9 +311,9 @@ def op_cost(name: str, u: dict):
         w = 4 * (2 * m * C + 9 * m + 2 * m * se)                   # fp32 weights
         if name == "mbconv_fwd":     # expand (x -> e), dw (e -> d), SE pool (d), project (d -> p), BN3 + residual (p, x -> out)
             return s * M * (5 * C + 5 * m) + w, 2 * M * m * C * 2 + 18 * M * m
-        # BN3 reduce + apply, project dgrad + wgrad, SE reduce, BN2 apply, dw wgrad + dgrad, BN1 apply,
-        # expand wgrad + dgrad (+ the residual)
-        return s * M * (11 * C + 17 * m) + 2 * w, 2 * M * m * C * 4 + 36 * M * m
+        # BN3 reduce + apply, project dgrad + wgrad, SE reduce, dw wgrad + dgrad with the BN2 backward in its
+        # staging (reads dA3 and d: dd is never stored), BN1 apply, expand wgrad + dgrad (+ the residual)
+        return s * M * (11 * C + 15 * m) + 2 * w, 2 * M * m * C * 4 + 36 * M * m
     if name in ("convbn_fwd", "convbn_bwd"):
         Mi, Mo, Ci, Co = M, u["Mo"], u["Cin"], u["Cout"]
         f = 2 * Mo * Co * 9 * Ci
@@ -325,6 +325,10 @@ def op_cost(name: str, u: dict):
         return s * M * C * (3 if u.get("train") else 2), 4 * M * C
     if name == "bn_act_bwd":         # reduce (dout, x) + apply (dout, x -> dx)
         return s * M * C * 5, 8 * M * C
+    if name == "ce_fwd":             # read fp32 logits + int64 labels, write the per-row logsumexp
+        return 4 * u["B"] * u["K"] + 12 * u["B"], 4 * u["B"] * u["K"]
+    if name == "ce_bwd":             # read logits, labels, logsumexp; write dlogits
+        return 8 * u["B"] * u["K"] + 12 * u["B"], 4 * u["B"] * u["K"]
     raise KeyError(name)
 
 
@@ -607,6 +611,52 @@ def linear_rows_act(x2d, weight, bias, act):
     if w2d.shape[1] != x2d.shape[1]:
         raise ValueError(f"ogv.linear_act: weight in_features {w2d.shape[1]} != input features {x2d.shape[1]}")
     return _LinearAct.apply(x2d, w2d, f32(bias), act)
+
+
+# ------------------------------------------------------------------------------------------------
+# Training loss: cross-entropy with label smoothing (src/training/one_epoch_train.py:96)
+# ------------------------------------------------------------------------------------------------
+class _CrossEntropyLS(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, target, ls, found):
+        lib = _lib.load()
+        B, K = logits.shape
+        loss = torch.empty((), dtype=torch.float32, device=logits.device)
+        ws = torch.empty((lib.ogv_ce_ls_ws_bytes(B) // 4,), dtype=torch.float32, device=logits.device)
+        with _census("ce_fwd", dict(B=B, K=K, elem=4)):
+            check(lib.ogv_ce_ls_fwd(_ptr(logits), _ptr(target), B, K, float(ls), _ptr(loss), _ptr(ws),
+                                    _ptr(found) if found is not None else None, _stream()), "ogv_ce_ls_fwd")
+        ctx.save_for_backward(logits, target, ws)
+        ctx.ls = float(ls)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        lib = _lib.load()
+        logits, target, ws = ctx.saved_tensors
+        B, K = logits.shape
+        g = g.float().contiguous()
+        dz = torch.empty_like(logits)
+        with _census("ce_bwd", dict(B=B, K=K, elem=4)):
+            check(lib.ogv_ce_ls_bwd(_ptr(logits), _ptr(target), _ptr(ws), _ptr(g), B, K, ctx.ls, _ptr(dz), _stream()),
+                  "ogv_ce_ls_bwd")
+        return dz, None, None, None
+
+
+def cross_entropy_ls(logits, target, label_smoothing=0.0, found=None):
+    """F.cross_entropy(logits.float(), target, label_smoothing=ls) (mean, ignore_index -100) on the
+    native kernels: logits [B, K] (cast to contiguous fp32), target [B] int64 class indices.  found: an
+    optional fp32 [1] device tensor that receives !isfinite(loss) from the same launch (the training
+    step's found_inf guard).  A label outside [0, K) gives a NaN loss instead of torch's raise."""
+    require_device(logits, target, found, what="ogv.cross_entropy")
+    if logits.dim() != 2 or target.dim() != 1 or target.shape[0] != logits.shape[0]:
+        raise ValueError(f"ogv.cross_entropy: logits [B, K] and target [B] expected, got {tuple(logits.shape)} "
+                         f"and {tuple(target.shape)}")
+    if target.dtype != torch.int64:
+        raise ValueError("ogv.cross_entropy: class-index targets (int64) only")
+    if not 0.0 <= label_smoothing <= 1.0:
+        raise ValueError(f"ogv.cross_entropy: label_smoothing {label_smoothing} not in [0, 1]")
+    return _CrossEntropyLS.apply(logits.float().contiguous(), target.contiguous(), float(label_smoothing), found)
 
 
 # ------------------------------------------------------------------------------------------------

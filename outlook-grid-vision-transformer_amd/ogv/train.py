@@ -405,17 +405,24 @@ class Trainer:
 
     # -- pieces of one step -------------------------------------------------------------------
     def _loss(self, x, y):
+        """(loss, found_written): the reference's F.cross_entropy(logits.float(), y, label_smoothing)
+        (one_epoch_train.py:96) on the native kernel for class-index targets on the device, which also
+        writes the step's found_inf guard in the same launch."""
         with torch.autocast("cuda", dtype=self.amp_dtype or torch.float32, enabled=self.amp_dtype is not None,
                             cache_enabled=not self.graphs):
             logits = self.model(x)
         if y.is_floating_point():   # soft targets from MixUp/CutMix (one_epoch_train.py:89-92)
             from .mix import soft_target_cross_entropy
-            return soft_target_cross_entropy(logits.float(), y)
-        return F.cross_entropy(logits.float(), y, label_smoothing=self.ls)
+            return soft_target_cross_entropy(logits.float(), y), False
+        if logits.is_cuda and logits.dim() == 2 and y.dtype == torch.int64:
+            from .functional import cross_entropy_ls
+            found = self._found.view(1) if self.device_side else None
+            return cross_entropy_ls(logits, y, self.ls, found=found), found is not None
+        return F.cross_entropy(logits.float(), y, label_smoothing=self.ls), False
 
     def _fwd_bwd(self, x, y):
-        loss = self._loss(x, y)
-        if self.device_side:
+        loss, flagged = self._loss(x, y)
+        if self.device_side and not flagged:
             self._flag(loss.detach(), 0)
         if self.dp and self._overlap:
             self._launch_meta(loss)

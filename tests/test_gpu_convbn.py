@@ -53,6 +53,11 @@ ACTS = {"silu": nn.SiLU(), "gelu": nn.GELU(), "relu": nn.ReLU(), None: nn.Identi
     (2, 8, 40, 5, 6, 1, False, True, "relu"),        # use_bn=False: conv bias, no BN
     (2, 5, 12, 6, 6, 2, True, True, None),           # Cin % 8 != 0 on the strided path
     (3, 16, 24, 10, 6, 2, True, True, "gelu"),       # dgrad as 4 parity-class GEMMs, non-square
+    # the dedicated stem kernels (bf16, C_in <= 3, 16 | C_out <= 128; fp32 takes the generic path)
+    (3, 3, 32, 10, 7, 1, True, True, "silu"),        # ragged 128-row tiles, C_out 32
+    (2, 3, 128, 12, 12, 2, True, True, "silu"),      # stride 2, C_out 128
+    (2, 1, 48, 9, 9, 1, False, True, "relu"),        # C_in 1, conv bias: dbias from the ones column
+    (2, 2, 96, 8, 8, 1, True, False, "gelu"),        # C_in 2, eval BN
 ])
 @pytest.mark.parametrize("wcl", [False, True], ids=["w_oihw", "w_channels_last"])
 def test_conv_bn_act(case, dtype, wcl):
@@ -175,3 +180,35 @@ def test_convbn_full_size_stem_stats():
     want = 0.9 * rm0.double() + 0.1 * mean
     e = float((bn.running_mean.double() - want).abs().max())
     assert e <= 1e-4, e
+
+
+@pytest.mark.parametrize("B", [64, 512])
+def test_stem_kernels_match_generic_conv(B):
+    """Knob stem = 1 (dedicated stem kernels) against stem = 0 (the implicit-GEMM conv kernels) on the
+    Model-A stem at 32 x 32, bf16 train mode: output, weight gradient, BN affine gradients and running
+    statistics.  Both multiply by the split (hi + lo) weight with fp32 accumulation, so they differ only
+    by the order of the 27-term sums, the bf16 rounding of the output that follows and the order of the
+    row reductions (bounds: 1 bf16 ulp-scale on the output, 1e-3 relative on the reductions)."""
+    from ogv import functional as OF
+    from ogv._lib import load
+    lib = load()
+    conv, bn = _modules(3, 64, 1, True, "silu", seed=4)
+    x = torch.randn(B, 3, 32, 32, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    gy = torch.randn(B, 64, 32, 32, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    res = []
+    try:
+        for knob in (0, 1):
+            assert lib.ogv_set_option(b"stem", knob) == 0
+            c = copy.deepcopy(conv).cuda().to(memory_format=torch.channels_last)
+            b = copy.deepcopy(bn).cuda().train()
+            y = OF.conv3x3_bn_act(x, c, b, "silu")
+            y.backward(gy)
+            res.append(dict(y=y.float(), dw=c.weight.grad, dg=b.weight.grad, db=b.bias.grad, rm=b.running_mean,
+                            rv=b.running_var))
+    finally:
+        assert lib.ogv_set_option(b"stem", 1) == 0
+    for k in res[0]:
+        a, r = res[1][k], res[0][k]
+        scale = max(1.0, float(r.abs().max()))
+        tol = 1.6e-2 if k == "y" else 1e-3
+        assert float((a - r).abs().max()) <= tol * scale, (k, float((a - r).abs().max()), scale)

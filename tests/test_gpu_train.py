@@ -385,7 +385,7 @@ def test_deferred_param_reductions_match_immediate(cfg_name, B, dpr):
         t.opt.zero_grad(set_to_none=True)
         torch.manual_seed(99)                  # the same DropPath draws in both runs
         with OF.deferred_param_reductions(defer):
-            loss = t._loss(x, y)
+            loss, _ = t._loss(x, y)
             loss.backward()
             pending.append(load().ogv_reduce_defer(1 if defer else 0))
         torch.cuda.synchronize()

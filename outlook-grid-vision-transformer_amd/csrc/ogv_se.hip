@@ -24,17 +24,13 @@ bool se_gemv_on() { return g_se_gemv != 0; }
 void set_se_gemv(int v) { g_se_gemv = v; }
 constexpr int SE_NT = 256;   // threads per block
 
-// RM: NW waves split the reduction -- 16 for the backward products (B / SE_RB = 64 row blocks and
-// one to a few 64-column groups: the per-wave reduction chain, one L2 round trip per 8 k, is what
-// bounds them; with 4 waves it was 25 us per launch)
-template <bool RM, int NW = 4>
-__global__ __launch_bounds__(NW * 64) void se_gemv_kernel(const float* __restrict__ in, int ldi, int pro_act,
+template <bool RM>
+__global__ __launch_bounds__(SE_NT) void se_gemv_kernel(const float* __restrict__ in, int ldi, int pro_act,
                                                         const float* __restrict__ W, int ldw,
                                                         const float* __restrict__ bias, const float* __restrict__ Z,
                                                         int ldz, int zact, float* __restrict__ out, int ldo,
                                                         float* __restrict__ sig_out, int B, int N, int K) {
   extern __shared__ __attribute__((aligned(16))) float xs[];   // [SE_RB][Kp] (+ RM: [4][SE_RB][64])
-  constexpr int NT = NW * 64;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int b0 = blockIdx.x * SE_RB;
   const int Kp = (K + 3) / 4 * 4, K4 = Kp / 4, tot4 = SE_RB * K4;
@@ -42,11 +38,11 @@ __global__ __launch_bounds__(NW * 64) void se_gemv_kernel(const float* __restric
   // round trip per batch, not per element)
   constexpr int SU = 8;
   const bool av = (ldi & 3) == 0 && (reinterpret_cast<uintptr_t>(in) & 15) == 0;
-  for (int base = tid; base < tot4; base += NT * SU) {
+  for (int base = tid; base < tot4; base += SE_NT * SU) {
     float4 v[SU];
 #pragma unroll
     for (int u = 0; u < SU; ++u) {
-      const int idx = base + u * NT, r = idx / K4, k = (idx - r * K4) * 4;
+      const int idx = base + u * SE_NT, r = idx / K4, k = (idx - r * K4) * 4;
       v[u] = float4{0.f, 0.f, 0.f, 0.f};
       if (idx < tot4 && b0 + r < B) {
         const float* src = in + (long)(b0 + r) * ldi + k;
@@ -61,7 +57,7 @@ __global__ __launch_bounds__(NW * 64) void se_gemv_kernel(const float* __restric
     }
 #pragma unroll
     for (int u = 0; u < SU; ++u) {
-      const int idx = base + u * NT, r = idx / K4, k = (idx - r * K4) * 4;
+      const int idx = base + u * SE_NT, r = idx / K4, k = (idx - r * K4) * 4;
       if (idx >= tot4) continue;
       const bool live = b0 + r < B;
       float4 a;
@@ -119,11 +115,11 @@ __global__ __launch_bounds__(NW * 64) void se_gemv_kernel(const float* __restric
     }
   } else {
     // column n = blockIdx.y * 64 + lane; wave w reduces the contiguous k range [k0, k1) in steps of 4
-    // (four coalesced weight rows, one 16-B broadcast read of each staged input row), then the NW
+    // (four coalesced weight rows, one 16-B broadcast read of each staged input row), then the four
     // waves combine in a fixed order
-    float* red = xs + SE_RB * Kp;   // [NW][SE_RB][64]
+    float* red = xs + SE_RB * Kp;   // [4][SE_RB][64]
     const int n = blockIdx.y * 64 + lane;
-    const int kq = (Kp / 4 + NW - 1) / NW * 4;   // k per wave, a multiple of 4
+    const int kq = (Kp / 4 + 3) / 4 * 4;   // k per wave, a multiple of 4
     const int k0 = wave * kq, k1 = min(Kp, k0 + kq);
     float acc[SE_RB];
 #pragma unroll
@@ -144,14 +140,11 @@ __global__ __launch_bounds__(NW * 64) void se_gemv_kernel(const float* __restric
 #pragma unroll
     for (int r = 0; r < SE_RB; ++r) red[(wave * SE_RB + r) * 64 + lane] = acc[r];
     __syncthreads();
-    for (int i = tid; i < SE_RB * 64; i += NT) {
+    for (int i = tid; i < SE_RB * 64; i += SE_NT) {
       const int r = i / 64, c = i - r * 64, nn = blockIdx.y * 64 + c;
       if (nn >= N || b0 + r >= B) continue;
-      float v = 0.f;
-#pragma unroll
-      for (int w = 0; w < NW; w += 4)
-        v += (red[(w * SE_RB + r) * 64 + c] + red[((w + 1) * SE_RB + r) * 64 + c]) +
-             (red[((w + 2) * SE_RB + r) * 64 + c] + red[((w + 3) * SE_RB + r) * 64 + c]);
+      const float v = (red[(0 * SE_RB + r) * 64 + c] + red[(1 * SE_RB + r) * 64 + c]) +
+                      (red[(2 * SE_RB + r) * 64 + c] + red[(3 * SE_RB + r) * 64 + c]);
       finish(r, nn, v);
     }
   }
@@ -164,25 +157,17 @@ void se_gemv_launch(const float* in, int ldi, int pro_act, const float* W, int l
                     bool rm, hipStream_t s) {
   if (B <= 0 || N <= 0) return;
   const int Kp = (K + 3) / 4 * 4;
-  const bool deep = rm && K >= 64;   // 16 waves split the reduction
-  const int nw = deep ? 16 : 4;
-  const size_t lds = ((size_t)SE_RB * Kp + (rm ? (size_t)nw * SE_RB * 64 : 0)) * sizeof(float);
-  const int ai = !rm ? 0 : deep ? 2 : 1;
-  const void* fn = ai == 0 ? reinterpret_cast<const void*>(se_gemv_kernel<false>)
-                 : ai == 1 ? reinterpret_cast<const void*>(se_gemv_kernel<true>)
-                           : reinterpret_cast<const void*>(se_gemv_kernel<true, 16>);
+  const size_t lds = ((size_t)SE_RB * Kp + (rm ? 4 * SE_RB * 64 : 0)) * sizeof(float);
   if (lds > 64 * 1024) {
-    static bool attr[3] = {false, false, false};
-    if (!attr[ai]) {
-      (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      attr[ai] = true;
+    static bool attr[2] = {false, false};
+    if (!attr[rm]) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(rm ? se_gemv_kernel<true> : se_gemv_kernel<false>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      attr[rm] = true;
     }
   }
   dim3 grid((unsigned)cdiv(B, SE_RB), (unsigned)cdiv(N, rm ? 64 : 32));
-  if (deep)
-    se_gemv_kernel<true, 16><<<grid, 16 * 64, lds, s>>>(in, ldi, pro_act, W, ldw, bias, Z, ldz, zact, out, ldo,
-                                                        sig_out, B, N, K);
-  else if (rm)
+  if (rm)
     se_gemv_kernel<true><<<grid, SE_NT, lds, s>>>(in, ldi, pro_act, W, ldw, bias, Z, ldz, zact, out, ldo, sig_out, B,
                                                   N, K);
   else

@@ -88,11 +88,14 @@ __global__ __launch_bounds__(256) void stem_fwd_kernel(const bf16* __restrict__ 
       sft[j][r] = STATS ? bn_shift(shift[16 * j + 4 * fg + r]) : 0.f;
     }
   }
-  float s1[STATS ? NJ : 1][4], s2[STATS ? NJ : 1][4];
+  // fp64 per lane from the first term on: y - shift is exact in fp64 (a bf16 minus an fp32), so the
+  // statistics -- and through them the rounded output -- do not move with the running-mean shift
+  // (an fp32 per-lane partial did, by one bf16 ulp of the output: measured, tools/diag_stem.py)
+  double s1[STATS ? NJ : 1][4], s2[STATS ? NJ : 1][4];
 #pragma unroll
   for (int j = 0; j < (STATS ? NJ : 1); ++j)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) { s1[j][r] = 0.f; s2[j][r] = 0.f; }
+    for (int r = 0; r < 4; ++r) { s1[j][r] = 0.0; s2[j][r] = 0.0; }
   StemCols<CIN> cols;
   cols.load(x, g, t0 * ST_BM, M);
   for (int t = 0; t < tpb; ++t) {
@@ -135,9 +138,9 @@ __global__ __launch_bounds__(256) void stem_fwd_kernel(const bf16* __restrict__ 
         for (int r = 0; r < 4; ++r) {
           o[r] = (bf16)(acc[i][j][r] + bv[j][r]);
           if constexpr (STATS) {
-            const float dl = mok ? (float)o[r] - sft[j][r] : 0.f;
+            const double dl = mok ? (double)(float)o[r] - (double)sft[j][r] : 0.0;
             s1[j][r] += dl;
-            s2[j][r] = fmaf(dl, dl, s2[j][r]);
+            s2[j][r] = fma(dl, dl, s2[j][r]);
           }
         }
         if (mok) *reinterpret_cast<bf16x4*>(out + m * N + 16 * j + 4 * fg) = o;
@@ -145,7 +148,7 @@ __global__ __launch_bounds__(256) void stem_fwd_kernel(const bf16* __restrict__ 
     }
   }
   if constexpr (STATS) {
-    // per-lane fp32 partials (<= 2 tpb shifted terms each) -> fp64 across lanes, waves
+    // per-lane partials -> across the 16 lanes of a column group, then the 4 waves
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
 #pragma unroll
@@ -250,7 +253,9 @@ __global__ __launch_bounds__(256) void stem_wgrad_kernel(const bf16* __restrict_
 static int g_stem = 1;   // knob "stem": 1 (default) = the dedicated stem kernels where they apply
 void set_stem(int v) { g_stem = v; }
 
-static bool stem_ok(int Cin, int N) { return g_stem && Cin >= 1 && Cin <= 3 && N % 16 == 0 && N >= 32 && N <= 128; }
+// 32 or 64 output channels (the Model-A / B stems are 64 wide; wider stems take the generic conv
+// kernels: the fp64 statistics accumulators of NJ > 4 column blocks do not fit the register budget)
+static bool stem_ok(int Cin, int N) { return g_stem && Cin >= 1 && Cin <= 3 && (N == 32 || N == 64); }
 
 static StemG stem_geom(const ConvG& cv) {
   return StemG{0, cv.Hs, cv.Ws, cv.Hr, cv.Wr, cv.stride};
@@ -284,8 +289,6 @@ bool stem_fwd_try(const void* x, const ConvG& cv, const float* wt, void* out, in
   switch (N / 16) {                        \
     case 2: OGV_STEM_F(CIN, 2) break;      \
     case 4: OGV_STEM_F(CIN, 4) break;      \
-    case 6: OGV_STEM_F(CIN, 6) break;      \
-    case 8: OGV_STEM_F(CIN, 8) break;      \
     default: return false;                 \
   }
   switch (cv.Cs) {
@@ -326,8 +329,6 @@ bool stem_wgrad_try(const void* x, const ConvG& cv, const void* dy, float* dw, f
   switch (N / 16) {                        \
     case 2: OGV_STEM_W(CIN, 2) break;      \
     case 4: OGV_STEM_W(CIN, 4) break;      \
-    case 6: OGV_STEM_W(CIN, 6) break;      \
-    case 8: OGV_STEM_W(CIN, 8) break;      \
     default: return false;                 \
   }
   switch (cv.Cs) {

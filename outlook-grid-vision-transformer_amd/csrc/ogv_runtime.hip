@@ -180,6 +180,10 @@ extern "C" int ogv_set_option(const char* name, int value) {
     set_dw_fuse(value);
     return OGV_OK;
   }
+  if (!strcmp(name, "stem_wgs")) {
+    set_stem_wgs(value);
+    return OGV_OK;
+  }
   if (!strcmp(name, "stem")) {
     set_stem(value);
     return OGV_OK;

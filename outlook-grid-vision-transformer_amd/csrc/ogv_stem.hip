@@ -2,8 +2,10 @@
 // on dedicated kernels: with C_in = 3 the implicit GEMM has a 27-column reduction, so the generic
 // conv kernels (8 | C_in gathers, or the LDS-tiled kernel's per-element gather over 32-wide k
 // slabs) spend their time on addressing, not on the 67 MB output stream.  Here one 128-pixel tile
-// builds its whole im2col block [128][32] in LDS once (k = tap * C_in + c, zero padding; k = 27 is
-// a column of ones in the weight gradient, giving the bias gradient from the same MFMAs), and:
+// builds its whole im2col block [128][32] in LDS once -- gathered per pixel (forward, StemCols) or
+// from the input rows staged with 16-B loads (weight gradient, StemPatch) -- (k = tap * C_in + c,
+// zero padding; k = 27 is a column of ones in the weight gradient, giving the bias gradient from
+// the same MFMAs), and:
 //   forward:  y = im2col . W^T (+ bias) on v_mfma_f32_16x16x32_bf16 with the weight held in
 //             registers as bf16 hi + lo for the whole tile (the split-weight forward of the other
 //             projections), transposed product so a lane stores 4 consecutive channels; BatchNorm
@@ -25,8 +27,10 @@ struct StemG {
   int B, H, W, Ho, Wo, stride;
 };
 
-// The 16 im2col values of pixel p = tid >> 1, columns [16 h, 16 h + 16) (h = tid & 1), of the tile
-// starting at output row m0: loaded at clamped (always valid) addresses, zeros selected after.
+// Forward: the 16 im2col values of pixel p = tid >> 1, columns [16 h, 16 h + 16) (h = tid & 1), of the
+// tile starting at output row m0, gathered straight from HBM / L2 at clamped (always valid) addresses,
+// zeros selected after (measured faster for the forward than the LDS patch: 90.7 vs 99.9 us per
+// stem op, tools/bench_stem.py, profiles/r04_stem_bench.log; the weight gradient is faster with it)
 template <int CIN>
 struct StemCols {
   bf16 raw[16];
@@ -52,6 +56,64 @@ struct StemCols {
   __device__ __forceinline__ bf16 value(int j) const {
     const int k = 16 * (threadIdx.x & 1) + j;
     return ok_[j] ? raw[j] : (ONES && k == 9 * CIN ? (bf16)1.f : (bf16)0.f);
+  }
+};
+
+// The input a tile needs, staged in LDS: the contiguous range of source rows (flattened b * H + y,
+// NHWC rows are contiguous, so a tile spanning images is still one range) from the row above its
+// first output row to the row below its last, fetched with 16-B loads (SP_CH per thread, issued a
+// tile ahead into registers) -- instead of 27 two-byte gathers per output pixel, which made the
+// load-instruction rate the bound (60 us for the 7M stem forward).  The host checks that a tile's
+// range fits SP_CH * 256 chunks and that the tensor is a whole number of 16-B chunks.
+constexpr int SP_CH = 2;
+constexpr int SP_ELEMS = SP_CH * 256 * 8;
+template <int CIN>
+struct StemPatch {
+  uint4 raw[SP_CH];
+  long base = 0;   // first staged element (a multiple of 8)
+  int nchunk = 0;
+  __device__ __forceinline__ void load(const bf16* __restrict__ x, const StemG& g, long m0, long M) {
+    const long ml = m0 + ST_BM - 1 < M ? m0 + ST_BM - 1 : M - 1;
+    const int hw = g.Ho * g.Wo;
+    const long b0 = m0 / hw, b1 = ml / hw;
+    const int oy0 = (int)((m0 - b0 * hw) / g.Wo), oy1 = (int)((ml - b1 * hw) / g.Wo);
+    const long rlo = b0 * g.H + max(oy0 * g.stride - 1, 0), rhi = b1 * g.H + min(oy1 * g.stride + 1, g.H - 1);
+    base = (rlo * g.W * CIN) & ~7L;
+    nchunk = (int)(((rhi + 1) * g.W * CIN - base + 7) >> 3);
+#pragma unroll
+    for (int c = 0; c < SP_CH; ++c) {
+      const int idx = min((int)threadIdx.x + c * 256, nchunk - 1);
+      raw[c] = *reinterpret_cast<const uint4*>(x + base + (long)idx * 8);
+    }
+  }
+  __device__ __forceinline__ void store(bf16* P) const {
+#pragma unroll
+    for (int c = 0; c < SP_CH; ++c) {
+      const int idx = (int)threadIdx.x + c * 256;
+      if (idx < nchunk) *reinterpret_cast<uint4*>(P + idx * 8) = raw[c];
+    }
+  }
+  // im2col values of pixel p = tid >> 1 of the tile at m0, columns [16 h, 16 h + 16) (h = tid & 1),
+  // from the staged patch (zero padding; ONES: column K9 = 1 for the bias gradient, valid pixels)
+  template <bool ONES>
+  __device__ __forceinline__ void cols(const bf16* P, const StemG& g, long m0, long M, bf16 (&v)[16]) const {
+    constexpr int K9 = 9 * CIN;
+    const int p = threadIdx.x >> 1, h = threadIdx.x & 1;
+    const bool mok = m0 + p < M;
+    const long m = mok ? m0 + p : M - 1;
+    const int hw = g.Ho * g.Wo;
+    const long b = m / hw;
+    const int rem = (int)(m - b * hw), oy = rem / g.Wo, ox = rem - oy * g.Wo;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int k = 16 * h + j;
+      const int tap = k / CIN, c = k - tap * CIN, ky = tap / 3, kx = tap - 3 * ky;
+      const int sy = oy * g.stride - 1 + ky, sx = ox * g.stride - 1 + kx;
+      const bool ok = mok && k < K9 && sy >= 0 && sy < g.H && sx >= 0 && sx < g.W;
+      const long off = ok ? ((b * g.H + sy) * g.W + sx) * CIN + c - base : 0;
+      const bf16 e = P[off];
+      v[j] = ok ? e : (ONES && mok && k == K9 ? (bf16)1.f : (bf16)0.f);
+    }
   }
 };
 
@@ -188,10 +250,11 @@ __global__ __launch_bounds__(256) void stem_wgrad_kernel(const bf16* __restrict_
   f32x4 acc[TPW];
 #pragma unroll
   for (int t = 0; t < TPW; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  StemCols<CIN> cols;
+  __shared__ __attribute__((aligned(16))) bf16 P[SP_ELEMS];
+  StemPatch<CIN> patch;
   uint4 dr[DL];
   auto load = [&](long s0) {
-    cols.load(x, g, s0, M);
+    patch.load(x, g, s0, M);
 #pragma unroll
     for (int u = 0; u < DL; ++u) {
       const int idx = threadIdx.x + u * 256, p = idx / (N / 8), c8 = (idx - p * (N / 8)) * 8;
@@ -202,11 +265,15 @@ __global__ __launch_bounds__(256) void stem_wgrad_kernel(const bf16* __restrict_
   load(r0);
   for (long s0 = r0; s0 < r1; s0 += ST_BM) {
     // stage step s0 transposed (rows past the range / the tensor: zeros in both operands)
+    patch.store(P);
+    __syncthreads();
     {
       const int p = threadIdx.x >> 1, h = threadIdx.x & 1;
       const bool pok = s0 + p < r1;
+      bf16 v[16];
+      patch.template cols<true>(P, g, s0, M, v);
 #pragma unroll
-      for (int j = 0; j < 16; ++j) AT[(16 * h + j) * ST_TP + p] = pok ? cols.template value<true>(j) : (bf16)0.f;
+      for (int j = 0; j < 16; ++j) AT[(16 * h + j) * ST_TP + p] = pok ? v[j] : (bf16)0.f;
 #pragma unroll
       for (int u = 0; u < DL; ++u) {
         const int idx = threadIdx.x + u * 256, q = idx / (N / 8), c8 = (idx - q * (N / 8)) * 8;
@@ -257,14 +324,26 @@ void set_stem(int v) { g_stem = v; }
 // kernels: the fp64 statistics accumulators of NJ > 4 column blocks do not fit the register budget)
 static bool stem_ok(int Cin, int N) { return g_stem && Cin >= 1 && Cin <= 3 && (N == 32 || N == 64); }
 
+// the staged input range of any tile fits the LDS patch, and the tensor is whole 16-B chunks
+static bool stem_patch_ok(const void* x, const ConvG& cv, long M) {
+  const long B = M / ((long)cv.Hr * cv.Wr);
+  const long total = B * cv.Hs * cv.Ws * cv.Cs;
+  const long rows_out = (ST_BM + cv.Wr - 1) / cv.Wr + 1;
+  const long rows_in = rows_out * cv.stride + 3;
+  return (reinterpret_cast<uintptr_t>(x) & 15) == 0 && total % 8 == 0 &&
+         rows_in * cv.Ws * cv.Cs + 8 <= SP_ELEMS;
+}
+
 static StemG stem_geom(const ConvG& cv) {
   return StemG{0, cv.Hs, cv.Ws, cv.Hr, cv.Wr, cv.stride};
 }
 
-// tiles per forward workgroup: ~512 workgroups, at most 8 tiles each
+// tiles per forward workgroup: ~g_stem_wgs workgroups, at most 8 tiles each (knob "stem_wgs")
+static int g_stem_wgs = 512;
+void set_stem_wgs(int v) { g_stem_wgs = v > 0 ? v : 512; }
 static int stem_tpb(long M) {
   const long tiles = (M + ST_BM - 1) / ST_BM;
-  long t = tiles / 512;
+  long t = tiles / g_stem_wgs;
   return (int)(t < 1 ? 1 : (t > 8 ? 8 : t));
 }
 int stem_fwd_stat_rows(long M) {
@@ -314,7 +393,7 @@ size_t stem_wgrad_ws_bytes(long M, int N, int Cin) {
 
 bool stem_wgrad_try(const void* x, const ConvG& cv, const void* dy, float* dw, float* dbias, int M, int N, void* ws,
                     hipStream_t s) {
-  if (!stem_ok(cv.Cs, N) || cv.transposed) return false;
+  if (!stem_ok(cv.Cs, N) || cv.transposed || !stem_patch_ok(x, cv, M)) return false;
   const StemG g = stem_geom(cv);
   const int K9 = 9 * cv.Cs;
   const long S = stem_wg_blocks(M), ld = (long)N * K9 + N;

@@ -54,9 +54,10 @@ ACTS = {"silu": nn.SiLU(), "gelu": nn.GELU(), "relu": nn.ReLU(), None: nn.Identi
     (2, 5, 12, 6, 6, 2, True, True, None),           # Cin % 8 != 0 on the strided path
     (3, 16, 24, 10, 6, 2, True, True, "gelu"),       # dgrad as 4 parity-class GEMMs, non-square
     # the dedicated stem kernels (bf16, C_in <= 3, C_out 32 / 64; fp32 and wider stems: generic path)
-    (3, 3, 32, 10, 7, 1, True, True, "silu"),        # ragged 128-row tiles, C_out 32
+    (4, 3, 32, 10, 6, 1, True, True, "silu"),        # ragged 128-row tiles spanning images, C_out 32
     (2, 3, 64, 12, 12, 2, True, True, "silu"),       # stride 2
-    (2, 1, 64, 9, 9, 1, False, True, "relu"),        # C_in 1, conv bias: dbias from the ones column
+    (8, 1, 64, 9, 9, 1, False, True, "relu"),        # C_in 1, conv bias: dbias from the ones column
+    (3, 3, 64, 10, 7, 1, True, True, "silu"),        # input not whole 16-B chunks: generic path
     (2, 2, 32, 8, 8, 1, True, False, "gelu"),        # C_in 2, eval BN
     (2, 3, 96, 8, 8, 1, True, True, "silu"),         # C_out 96: generic path
 ])

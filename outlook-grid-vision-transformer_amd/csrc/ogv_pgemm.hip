@@ -572,6 +572,8 @@ static int g_pg_tn = 0;
 // on these shapes, beats 1-2 resident persistent workgroups: the hardware's dynamic dispatch
 // balances the tail better than the static tile walk)
 static int g_pg_per_cu = 8;
+static long g_pg_tn4_max_m = 262144;
+void set_pg_tn4_max_m(int v) { g_pg_tn4_max_m = v > 0 ? v : 262144; }
 void set_pgemm(int v) { g_pgemm = v; }
 static int g_pg_lds_kb = 80;  // knob "pg_lds_kb": LDS cap per workgroup the planner allows (80: two per CU)
 void set_pg_lds_kb(int v) { g_pg_lds_kb = v < 16 ? 16 : (v > 160 ? 160 : v); }
@@ -611,10 +613,14 @@ static bool al16p(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) 
 static PgPlan pg_plan(int M, int N, int K, bool stats, bool sw, bool bt, bool pa, bool gate) {
   PgPlan p;
   if (!g_pgemm || M <= 0 || (N & 7) || (K & 7)) return p;
-  // measured (tools/gpu_pgemm_sweep.sh, 7M census): at M <= 16384 64-column tiles win unless
-  // the output is >= 1024 wide
-  const bool narrow = M <= 16384 && N < 1024;
-  const int tns[3] = {narrow ? 4 : 8, 12, 4};
+  // 64-column tiles first at every shape: round 4 re-measured on the whole 7M step (paired 30-step
+  // runs on one box, profiles/r04_pgsweep.log): forcing them 15.49-15.52 vs 15.69-15.72 ms with the round-2 rule
+  // (64 columns only at M <= 16384 and N < 1024, tools/gpu_pgemm_sweep.sh census) -- the 128 / 192-
+  // column tiles need 220-256 VGPRs (two workgroups per CU), the 64-column ones 100-160
+  // (knob "pg_tn4_max_m": above it the 128-column tiles come first -- 22M@224's large-M data
+  // gradients: 343.6 ms forced 128 vs 347.0 with 64-column tiles)
+  const bool tn4 = M <= g_pg_tn4_max_m;
+  const int tns[3] = {tn4 ? 4 : 8, tn4 ? 8 : 12, tn4 ? 12 : 4};
   int best_tn = 0;
   for (int t : tns) {
     if (g_pg_tn && t != g_pg_tn) continue;

@@ -260,6 +260,10 @@ extern "C" int ogv_set_option(const char* name, int value) {
     set_pg_rs(value == 1 || value == 2 ? value : 0);
     return OGV_OK;
   }
+  if (!strcmp(name, "pg_tn4_max_m")) {
+    set_pg_tn4_max_m(value);
+    return OGV_OK;
+  }
   if (!strcmp(name, "pg_tn")) {
     set_pg_tn(value == 4 || value == 8 || value == 12 ? value : 0);
     return OGV_OK;

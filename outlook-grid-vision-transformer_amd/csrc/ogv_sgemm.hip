@@ -449,7 +449,10 @@ static int g_sg_prefetch = 3;
 void set_sg_prefetch(int v) { g_sg_prefetch = v & 3; }
 static int g_sg_wgs = 0;
 void set_sg_wgs(int v) { g_sg_wgs = v < 0 ? 0 : v; }
-static int g_sg_min_m = 65536;  // smallest M routed to the streaming kernels (tuning knob "sgemm_min_m")
+// smallest M routed to the streaming kernels (tuning knob "sgemm_min_m"): 262144 since round 4 -- with
+// the panel kernel's 64-column tiles, 7M stage 1 (M = 131072) runs faster there (paired 40-step runs:
+// 15.56-15.66 -> 15.48-15.53 ms; 14M 45.46 -> 45.30 ms, profiles/r04_sgemm_min_m.log)
+static int g_sg_min_m = 262144;
 void set_sgemm_min_m(int v) { g_sg_min_m = v; }
 int sgemm_min_m() { return g_sg_min_m; }
 

@@ -164,6 +164,8 @@ def test_gemm_routing_table():
     assert route(fwd, 524288, 48, 64, 0) == 1              # stage 0: streaming kernel
     assert route(fwd, 524288, 48, 192, 1) == 1             # fc2 with the GELU prologue, K <= 384
     assert route(fwd, 32768, 768, 192, 0) == 2             # stages 1-3: panel kernel
+    assert route(fwd, 131072, 384, 96, 0) == 2             # stage 1 (M = 131072): panel since round 4
+    assert route(fwd, 262144, 384, 96, 0) == 1             # sgemm_min_m = 262144
     assert route(fwd, 8192, 256, 1024, 1) == 2
     assert route(dgrad, 32768, 768, 192, 1) == 2
     assert route(dgrad, 524288, 256, 1024, 0) == 2         # long-reduction dgrad at large M

@@ -1263,8 +1263,11 @@ static void bwd_param_ws_layout(void* base, const ogv_mbconv_desc& s, BwdWs* w, 
 
 // Side stream for the weight-gradient work of the fused backward (independent of the data-gradient
 // chain): forked from / joined back into the caller's stream with events, which also works inside a
-// captured hipGraph (the side stream joins the capture).  Knob "mb_side" (default 1).
-static int g_mb_side = 1;
+// captured hipGraph (the side stream joins the capture).  Knob "mb_side": default 0 since round 4 --
+// with the round-4 kernels the concurrent weight gradients slowed the data-gradient chain more than
+// they overlapped it (7M, paired: 15.52-15.53 ms with it, 15.38-15.41 without; 15.13-15.14 with the
+// Linear fork off too, profiles/r04_side_streams.log)
+static int g_mb_side = 0;
 void set_mb_side(int v) { g_mb_side = v; }
 // knob "dw_fuse": 1 (default) = the depthwise data and weight gradients in one pass over (dd, e)
 static int g_dw_fuse = 1;

@@ -39,6 +39,12 @@ def _dt(t: torch.Tensor) -> int:
 
 
 _SIDE = {}
+# Linear backward: weight gradient forked onto a side stream ("1") or after the data gradient on the
+# current stream ("0", default since round 4).  Re-measured with the round-4 kernels (paired 40-step
+# 7M runs, profiles/r04_side_streams.log): both forks 15.52-15.53 ms, neither (this and the MBConv
+# library knob mb_side = 0) 15.13-15.14 ms -- concurrent kernels slow each other more than the
+# overlap wins, and every cross-stream edge costs ~10 us in the graph.
+_FORK = os.environ.get("OGV_FORK", "0") != "0"
 # smallest M*(N+K) of a Linear backward whose weight gradient is forked onto the side stream
 _FORK_MIN_WORK = int(os.environ.get("OGV_FORK_MIN_WORK", "0"))
 # fork policy for the Linears whose dgrad applies an activation derivative (the MLP fc2 inputs):
@@ -545,7 +551,7 @@ def _linear_bwd(dout, x2d, w2d, rs, rps, act, has_bias, want_dx, want_dw, x_act=
     # GEMMs overlap.
     # (below ~_FORK_MIN_WORK the fork/join latency (~10 us per cross-stream edge) outweighs the overlap)
     # (while a probe is armed everything stays on the current stream, where its events are)
-    fork = (want_dx and want_dw and M * (N + K) >= _FORK_MIN_WORK and not _serial()
+    fork = (_FORK and want_dx and want_dw and M * (N + K) >= _FORK_MIN_WORK and not _serial()
             and (_FORK_ACT or not act))
     with _fork(fork, dout, xw, rs, dw, db, ws_w if want_dw else None) as side:
         if want_dw:

@@ -546,7 +546,7 @@ struct Bn2In {
   const float *sc, *sh, *mean, *inv, *gate, *dpool, *coef;
   int HW;
 };
-template <typename T, int V, int LDQ, int ACT, bool WG = false, bool BN2 = false>
+template <typename T, int V, int LDQ, int ACT, bool WG = false, bool BN2 = false, int R = DW_R>
 __global__ __launch_bounds__(256) void dw_dgrad_tile_kernel(const T* __restrict__ dd, const float* __restrict__ wdw,
                                                             const T* __restrict__ e, const float* __restrict__ sc,
                                                             const float* __restrict__ sh,
@@ -604,10 +604,10 @@ __global__ __launch_bounds__(256) void dw_dgrad_tile_kernel(const T* __restrict_
 #pragma unroll
     for (int i = 0; i < V; ++i) q9[k][i] = 0.f;
   const int cc = cok ? c : 0;
-  RawVec<T, V> ce[DW_R];  // e at this thread's output pixel of the current rows
+  RawVec<T, V> ce[R];  // e at this thread's output pixel of the current rows
   auto pre = [&](VRow q, int px) {
 #pragma unroll
-    for (int r = 0; r < DW_R; ++r, q = vnext(t, q)) dw_pixel_load(ce[r], e, t, ti, q, px, cc);
+    for (int r = 0; r < R; ++r, q = vnext(t, q)) dw_pixel_load(ce[r], e, t, ti, q, px, cc);
   };
   auto stage = [&](float (&v)[V], const float (&dv)[V], int im) {
     if constexpr (BN2) {
@@ -629,7 +629,7 @@ __global__ __launch_bounds__(256) void dw_dgrad_tile_kernel(const T* __restrict_
       }
     }
   };
-  dw_walk<T, V, LDQ, BN2, DW_R>(ring, dd, b2.d, t, ti, cc, chunk, cok, stage, pre, [&](int r, int u, long b, int y, int px) {
+  dw_walk<T, V, LDQ, BN2, R>(ring, dd, b2.d, t, ti, cc, chunk, cok, stage, pre, [&](int r, int u, long b, int y, int px) {
     const long off = ((b * t.H + y) * t.W + ti.x0 + px) * t.C + c;
     float ev[V];
     ce[r].unpack(ev);
@@ -644,7 +644,7 @@ __global__ __launch_bounds__(256) void dw_dgrad_tile_kernel(const T* __restrict_
 #pragma unroll
       for (int kj = 0; kj < 3; ++kj) {
         // transposed conv: dd row y+1-ki, column x+1-kj  (ring pixel px + 2 - kj)
-        const float* src = ring_px(ring, t, u + 1 - ki, px + 2 - kj) + chunk * V;
+        const float* src = ring_px<R>(ring, t, u + 1 - ki, px + 2 - kj) + chunk * V;
 #pragma unroll
         for (int i = 0; i < V; i += 4) {
           const float4 a = *reinterpret_cast<const float4*>(src + i);
@@ -1276,6 +1276,8 @@ void set_dw_fuse(int v) { g_dw_fuse = v; }
 // written to HBM: one [M, mid] write + read and the bn2_apply launch saved); needs dw_fuse
 static int g_dw_bn2 = 1;
 void set_dw_bn2(int v) { g_dw_bn2 = v; }
+static int g_dw_bwd_r = 4;
+void set_dw_bwd_r(int v) { g_dw_bwd_r = v == 2 ? 2 : 4; }
 struct SideStream {
   hipStream_t s = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
@@ -1346,26 +1348,29 @@ struct Ops {
 #undef OGV_DWF
   }
   // part != nullptr: the weight-gradient partials in the same pass (dw_dgrad_tile_kernel<.., WG>)
-  // b2 != nullptr: dd is BN2-backward(dA3 = dd, b2->d), computed as the rows are staged
+  // b2 != nullptr: dd is BN2-backward(dA3 = dd, b2->d), computed as the rows are staged.  Rows per
+  // step: knob "dw_bwd_r" for the BN2-staged kernel (2 or 4)
   static void dw_dgrad(const void* dd, const float* w, const void* e, const float* sc, const float* sh,
                        const float* mean, const float* inv, int act, void* out, float* stat, const DwTile& t,
                        hipStream_t st, float* part = nullptr, const Bn2In<T>* b2 = nullptr) {
     if (skip_mask() & 8) return;
     constexpr int V = 4;
-    size_t lds = t.lds_bytes(part ? 9 : 2, V, sizeof(float));
+    const int R = b2 ? g_dw_bwd_r : DW_R;
+    size_t lds = t.lds_bytes(part ? 9 : 2, V, sizeof(float), R);
     const int tab_off = (int)(lds / sizeof(float));
     if (b2) lds += (size_t)t.G * 2 * t.CT * sizeof(float);
     const Bn2In<T> bi = b2 ? *b2 : Bn2In<T>{};
-#define OGV_DWD(WG_, B2_)                                                                                            \
-    OGV_DW_ACT(act, if (t.ldq <= 1) dw_dgrad_tile_kernel<T, V, 1, A, WG_, B2_><<<dw_grid(t), 256, lds, st>>>(        \
+#define OGV_DWD(WG_, B2_, R_)                                                                                        \
+    OGV_DW_ACT(act, if (t.ldq <= 1) dw_dgrad_tile_kernel<T, V, 1, A, WG_, B2_, R_><<<dw_grid(t), 256, lds, st>>>(    \
                         (const T*)dd, w, (const T*)e, sc, sh, mean, inv, act, (T*)out, stat, t, part, bi, tab_off);  \
-               else if (t.ldq <= 2) dw_dgrad_tile_kernel<T, V, 2, A, WG_, B2_><<<dw_grid(t), 256, lds, st>>>(        \
+               else if (t.ldq <= 2) dw_dgrad_tile_kernel<T, V, 2, A, WG_, B2_, R_><<<dw_grid(t), 256, lds, st>>>(    \
                         (const T*)dd, w, (const T*)e, sc, sh, mean, inv, act, (T*)out, stat, t, part, bi, tab_off);  \
-               else dw_dgrad_tile_kernel<T, V, 3, A, WG_, B2_><<<dw_grid(t), 256, lds, st>>>(                         \
+               else dw_dgrad_tile_kernel<T, V, 3, A, WG_, B2_, R_><<<dw_grid(t), 256, lds, st>>>(                     \
                         (const T*)dd, w, (const T*)e, sc, sh, mean, inv, act, (T*)out, stat, t, part, bi, tab_off))
-    if (part && b2) { OGV_DWD(true, true) }
-    else if (part) { OGV_DWD(true, false) }
-    else { OGV_DWD(false, false) }
+    if (part && b2 && R == 2) { OGV_DWD(true, true, 2) }
+    else if (part && b2) { OGV_DWD(true, true, DW_R) }
+    else if (part) { OGV_DWD(true, false, DW_R) }
+    else { OGV_DWD(false, false, DW_R) }
 #undef OGV_DWD
   }
   static void dw_wgrad(const void* dd, const void* e, const float* sc, const float* sh, int act, float* part,

@@ -188,6 +188,10 @@ extern "C" int ogv_set_option(const char* name, int value) {
     set_stem(value);
     return OGV_OK;
   }
+  if (!strcmp(name, "dw_bwd_r")) {
+    set_dw_bwd_r(value);
+    return OGV_OK;
+  }
   if (!strcmp(name, "dw_fwd_r")) {
     set_dw_fwd_r(value);
     return OGV_OK;

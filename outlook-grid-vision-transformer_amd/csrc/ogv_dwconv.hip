@@ -42,28 +42,33 @@ __global__ __launch_bounds__(256) void colreduce_kernel(const T* __restrict__ sr
   }
 }
 
-// Single-pass form for up to 2048 rows (one launch instead of two): block = 16 column quads
-// (64 columns, 16-B loads) x 16 row groups; each thread keeps 8 rows' loads in flight, then the 16
-// row-group sums are combined in a fixed order through LDS.  Needs n, ld % 4 == 0 and 16-B
-// alignment (fp32 only); split destination as in colreduce_kernel.
-__global__ __launch_bounds__(256) void colreduce4_kernel(const float* __restrict__ src, float* __restrict__ dst, long R,
-                                                         long n, long ld, float* __restrict__ dst2, long n1) {
-  __shared__ float4 red[16][16];
-  const int cq = threadIdx.x & 15, rg = threadIdx.x >> 4;
-  const long j = ((long)blockIdx.x * 16 + cq) * 4;
+// Single-pass form for up to 2048 rows (one launch instead of two): block = CR4_CQ column quads
+// (16-B loads) x CR4_RG row groups; each thread keeps 8 rows' loads in flight, then the row-group
+// sums are combined in a fixed order through LDS.  Needs n, ld % 4 == 0 and 16-B alignment (fp32
+// only); split destination as in colreduce_kernel.  Round 4: 64 quads x 4 row groups (1 KB of each
+// slab row per block, was 256 B: the partial slabs are rows ~100 KB-600 KB apart, and the wider
+// contiguous run per row keeps the HBM bursts full -- the batched parameter-gradient flush below
+// uses the same block body, so deferred and immediate reductions stay bit-identical).
+constexpr int CR4_CQ = 64, CR4_RG = 256 / CR4_CQ;
+__device__ __forceinline__ void colreduce4_block(const float* __restrict__ src, float* __restrict__ dst, long R,
+                                                 long n, long ld, float* __restrict__ dst2, long n1, long colblk,
+                                                 long tapC) {
+  __shared__ float4 red[CR4_RG][CR4_CQ];
+  const int cq = threadIdx.x % CR4_CQ, rg = threadIdx.x / CR4_CQ;
+  const long j = (colblk * CR4_CQ + cq) * 4;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   if (j < n) {
     long r = rg;
-    for (; r + 7 * 16 < R; r += 8 * 16) {
+    for (; r + 7 * CR4_RG < R; r += 8 * CR4_RG) {
       float4 v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(src + (r + u * 16) * ld + j);
+      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(src + (r + u * CR4_RG) * ld + j);
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w;
       }
     }
-    for (; r < R; r += 16) {
+    for (; r < R; r += CR4_RG) {
       const float4 v = *reinterpret_cast<const float4*>(src + r * ld + j);
       acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
     }
@@ -73,7 +78,7 @@ __global__ __launch_bounds__(256) void colreduce4_kernel(const float* __restrict
   if (rg == 0 && j < n) {
     float4 t = red[0][cq];
 #pragma unroll
-    for (int g = 1; g < 16; ++g) {
+    for (int g = 1; g < CR4_RG; ++g) {
       const float4 v = red[g][cq];
       t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
     }
@@ -83,10 +88,16 @@ __global__ __launch_bounds__(256) void colreduce4_kernel(const float* __restrict
       const long c = j + q;
       if (c >= n) break;
       if (dst2 && c >= n1) dst2[c - n1] = o[q];
+      else if (tapC > 0) dst[(c % tapC) * 9 + c / tapC] = o[q];
       else dst[c] = o[q];
     }
   }
 }
+__global__ __launch_bounds__(256) void colreduce4_kernel(const float* __restrict__ src, float* __restrict__ dst, long R,
+                                                         long n, long ld, float* __restrict__ dst2, long n1) {
+  colreduce4_block(src, dst, R, n, ld, dst2, n1, blockIdx.x, 0);
+}
+static inline unsigned colreduce4_blocks(long n) { return (unsigned)((n + 4 * CR4_CQ - 1) / (4 * CR4_CQ)); }
 
 // Sum R rows of a [R, ld] fp32 slab into dst[n].  Two passes when R is large; tmp needs
 // colreduce_tmp_floats(R, n) floats (may be null when that is 0).  Deterministic.
@@ -102,7 +113,7 @@ static void colreduce_t(const T* src, T* dst, long R, long n, long ld, T* tmp, h
   if (!dst2) n1 = n;
   if constexpr (sizeof(T) == 4) {
     if (R > 64 && R <= 2048 && (n & 3) == 0 && (ld & 3) == 0 && (reinterpret_cast<uintptr_t>(src) & 15) == 0) {
-      colreduce4_kernel<<<gx, 256, 0, s>>>(src, dst, R, n, ld, dst2, n1);
+      colreduce4_kernel<<<colreduce4_blocks(n), 256, 0, s>>>(src, dst, R, n, ld, dst2, n1);
       return;
     }
   }
@@ -142,48 +153,19 @@ struct RedBatch {
 };
 
 __global__ __launch_bounds__(256) void colreduce_batch_kernel(RedBatch b) {
-  __shared__ float4 red[16][16];
-  int j = 0;
-  while (j + 1 < b.count && b.start[j + 1] <= (int)blockIdx.x) ++j;
-  const RedDesc d = b.d[j];
-  const int cq = threadIdx.x & 15, rg = threadIdx.x >> 4;
-  const long col = ((long)(blockIdx.x - b.start[j]) * 16 + cq) * 4;
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (col < d.n) {
-    long r = rg;
-    for (; r + 7 * 16 < d.R; r += 8 * 16) {
-      float4 v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(d.src + (r + u * 16) * d.ld + col);
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w;
-      }
-    }
-    for (; r < d.R; r += 16) {
-      const float4 v = *reinterpret_cast<const float4*>(d.src + r * d.ld + col);
-      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
-    }
+  // descriptor of this block: the number of start offsets <= blockIdx.x, counted with one ballot
+  // (a dynamically indexed walk over the kernel-argument table made every step a dependent load)
+  __shared__ int jd;
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    const bool le = lane >= 1 && lane < b.count && b.start[lane] <= (int)blockIdx.x;
+    const unsigned long long m = __ballot(le);
+    if (lane == 0) jd = __popcll(m);
   }
-  red[rg][cq] = acc;
   __syncthreads();
-  if (rg == 0 && col < d.n) {
-    float4 t = red[0][cq];
-#pragma unroll
-    for (int g = 1; g < 16; ++g) {
-      const float4 v = red[g][cq];
-      t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
-    }
-    const float o[4] = {t.x, t.y, t.z, t.w};
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const long c = col + q;
-      if (c >= d.n) break;
-      if (d.dst2 && c >= d.n1) d.dst2[c - d.n1] = o[q];
-      else if (d.tapC > 0) d.dst[(c % d.tapC) * 9 + c / d.tapC] = o[q];
-      else d.dst[c] = o[q];
-    }
-  }
+  const int j = __builtin_amdgcn_readfirstlane(jd);
+  const RedDesc d = b.d[j];
+  colreduce4_block(d.src, d.dst, d.R, d.n, d.ld, d.dst2, d.n1, (long)blockIdx.x - b.start[j], d.tapC);
 }
 
 static bool g_defer = false;
@@ -228,7 +210,7 @@ extern "C" int ogv_reduce_flush(void* stream) {
       const RedDesc& d = g_pending[i];
       b.d[b.count] = d;
       b.start[b.count] = blocks;
-      blocks += (int)((d.n + 63) / 64);
+      blocks += (int)colreduce4_blocks(d.n);
       ++b.count;
     }
     b.start[b.count] = blocks;

@@ -241,6 +241,7 @@ void set_dw_fwd_r(int v);
 void set_dw_bwd_r(int v);
 void set_stem(int v);
 void set_pg_tn4_max_m(int v);
+void set_pg_pa_wide(int v);
 void set_stem_wgs(int v);
 // the stem convolution (C_in <= 3, ogv_stem.hip): false = not taken (the caller runs the generic path)
 bool stem_fwd_try(const void* x, const ConvG& cv, const float* wt, void* out, int M, int N, const Epi& epi,

@@ -573,6 +573,8 @@ static int g_pg_tn = 0;
 // balances the tail better than the static tile walk)
 static int g_pg_per_cu = 8;
 static long g_pg_tn4_max_m = 262144;
+static int g_pg_pa_wide = 0;
+void set_pg_pa_wide(int v) { g_pg_pa_wide = v ? 1 : 0; }
 void set_pg_tn4_max_m(int v) { g_pg_tn4_max_m = v > 0 ? v : 262144; }
 void set_pgemm(int v) { g_pgemm = v; }
 static int g_pg_lds_kb = 80;  // knob "pg_lds_kb": LDS cap per workgroup the planner allows (80: two per CU)
@@ -619,7 +621,9 @@ static PgPlan pg_plan(int M, int N, int K, bool stats, bool sw, bool bt, bool pa
   // column tiles need 220-256 VGPRs (two workgroups per CU), the 64-column ones 100-160
   // (knob "pg_tn4_max_m": above it the 128-column tiles come first -- 22M@224's large-M data
   // gradients: 343.6 ms forced 128 vs 347.0 with 64-column tiles)
-  const bool tn4 = M <= g_pg_tn4_max_m;
+  // an A prologue (MBConv BN + SiLU + SE gate, GELU) is recomputed for every column tile, so with
+  // one there the 128-column tiles come first (knob "pg_pa_wide")
+  const bool tn4 = M <= g_pg_tn4_max_m && !(pa && g_pg_pa_wide);
   const int tns[3] = {tn4 ? 4 : 8, tn4 ? 8 : 12, tn4 ? 12 : 4};
   int best_tn = 0;
   for (int t : tns) {

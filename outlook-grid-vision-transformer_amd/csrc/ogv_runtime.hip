@@ -264,6 +264,10 @@ extern "C" int ogv_set_option(const char* name, int value) {
     set_pg_rs(value == 1 || value == 2 ? value : 0);
     return OGV_OK;
   }
+  if (!strcmp(name, "pg_pa_wide")) {
+    set_pg_pa_wide(value);
+    return OGV_OK;
+  }
   if (!strcmp(name, "pg_tn4_max_m")) {
     set_pg_tn4_max_m(value);
     return OGV_OK;

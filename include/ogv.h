@@ -375,11 +375,13 @@ int ogv_clip_adamw(const ogv_adamw_tensor* tensors, int n, const ogv_adamw_group
  * ogv_ce_ls_fwd: *loss = (1-ls) * mean nll + (ls/K) * mean(-sum_k log_softmax); ws (ogv_ce_ls_ws_bytes)
  *   receives the per-row logsumexp and the count of non-ignored rows for the backward; found != NULL:
  *   *found = !isfinite(loss) (ogv_step_flag mode 0, fused).  A label outside [0, K) other than -100
- *   (torch raises; a raise needs a device sync) makes the loss NaN, so the guarded step is skipped.
+ *   (torch raises; a raise needs a device sync) makes the loss NaN, so the guarded step is skipped, and
+ *   bad_labels != NULL: *bad_labels += the number of such rows (a device counter the host reads to raise
+ *   as torch does: a bad label is a data error, not a non-finite step).
  * ogv_ce_ls_bwd: dlogits = (*grad_loss / n) * (softmax - (1-ls) onehot - ls/K), 0 on ignored rows. */
 size_t ogv_ce_ls_ws_bytes(int B);
 int ogv_ce_ls_fwd(const float* logits, const int64_t* target, int B, int K, float label_smoothing, float* loss,
-                  float* ws, float* found, void* stream);
+                  float* ws, float* found, float* bad_labels, void* stream);
 int ogv_ce_ls_bwd(const float* logits, const int64_t* target, const float* ws, const float* grad_loss, int B, int K,
                   float label_smoothing, float* dlogits, void* stream);
 

@@ -391,18 +391,21 @@ def lr_at(t: int, base: float, warmup_steps: int, total_steps: int, min_lr: floa
 
 
 def train_steps(batches, p, stages, lr=5e-4, weight_decay=0.05, clip=1.0, label_smoothing=0.1, total_steps=8,
-                warmup_steps=2, min_lr=0.0, on_step=None):
+                warmup_steps=2, min_lr=0.0, on_step=None, autocast=False):
     """The reference's training loop over ``batches`` (src/training/one_epoch_train.py:85-153 with the
     optimizer / schedule of train_full_model.py:56-66 and warmup.py:29-59): zero_grad, forward, CE with
     label smoothing; a non-finite loss skips the step (no update, no scheduler.step -- :98-108); else
     backward, clip_grad_norm_, AdamW.step, scheduler.step.  The first step runs at the base lr (the
-    schedule only writes the lr after a step).  on_step(t, loss, lr_used, skipped, step_num) per batch."""
+    schedule only writes the lr after a step).  on_step(t, loss, lr_used, skipped, step_num) per batch.
+    autocast=True runs the forward under CPU bf16 autocast as use_amp=True does (one_epoch_train.py:88-90,
+    autocast.py:71-78); the loss stays fp32 on logits.float() (:92-96)."""
     opt = make_optimizer(p, lr, weight_decay)
     step_num = 0
     for t, (x, y) in enumerate(batches):
         lr_used = [float(g["lr"]) for g in opt.param_groups]
         opt.zero_grad(set_to_none=True)
-        logits = model_a(x, p, stages, train=True)
+        with torch.autocast("cpu", dtype=torch.bfloat16, enabled=autocast):
+            logits = model_a(x, p, stages, train=True)
         loss = F.cross_entropy(logits.float(), y, label_smoothing=label_smoothing)
         skipped = not bool(torch.isfinite(loss))
         if not skipped:

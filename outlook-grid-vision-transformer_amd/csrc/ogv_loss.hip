@@ -8,8 +8,10 @@
 //   nll_i = lse_i - z[i, y_i],   smooth_i = -sum_k logp_ik = K * lse_i - sum_k z[i, k]
 //   dz[i, k] = g / n * (softmax_ik - (1 - ls) [k == y_i] - ls / K)   (0 for ignored rows)
 // A label outside [0, K) (torch raises, which needs a device sync) makes the loss NaN, so the step's
-// found_inf guard skips the update.  The forward also writes that guard (found = !isfinite(loss))
-// when asked, so the step needs no separate flag launch.
+// found_inf guard skips the update; the forward ALSO adds the number of such rows to a separate
+// device counter (bad_labels, when given), which the Trainer reads to raise as torch would -- a
+// bad label is a data error, not a non-finite step.  The forward also writes that guard
+// (found = !isfinite(loss)) when asked, so the step needs no separate flag launch.
 #include "ogv_common.h"
 
 #include <cmath>
@@ -18,7 +20,7 @@ namespace ogv {
 
 // Forward in two launches: ce_rows_kernel (a wave per row, B / 4 workgroups) writes each row's
 // logsumexp and its two loss terms; ce_final_kernel (one workgroup) sums them in a fixed order.
-// ws = [lse (B) | nll (B) | smooth (B) | valid (B) | n_valid]
+// ws = [lse (B) | nll (B) | smooth (B) | valid (B) | n_valid | bad (B)]
 __device__ __forceinline__ float wave_max_f(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
@@ -52,27 +54,32 @@ __global__ __launch_bounds__(256) void ce_rows_kernel(const float* __restrict__ 
     ws[B + i] = valid ? nll : 0.f;
     ws[2 * B + i] = valid ? (float)K * lse - sz : 0.f;
     ws[3 * B + i] = valid ? 1.f : 0.f;
+    ws[4 * B + 1 + i] = (valid && (t < 0 || t >= K)) ? 1.f : 0.f;
   }
 }
 
 __global__ __launch_bounds__(256) void ce_final_kernel(float* __restrict__ ws, int B, int K, float ls,
-                                                       float* __restrict__ loss, float* __restrict__ found) {
-  __shared__ double part[3][256];
-  double a = 0.0, b = 0.0, n = 0.0;
+                                                       float* __restrict__ loss, float* __restrict__ found,
+                                                       float* __restrict__ bad_labels) {
+  __shared__ double part[4][256];
+  double a = 0.0, b = 0.0, n = 0.0, nb = 0.0;
   for (int i = threadIdx.x; i < B; i += 256) {
     a += (double)ws[B + i];
     b += (double)ws[2 * B + i];
     n += (double)ws[3 * B + i];
+    nb += (double)ws[4 * B + 1 + i];
   }
   part[0][threadIdx.x] = a;
   part[1][threadIdx.x] = b;
   part[2][threadIdx.x] = n;
+  part[3][threadIdx.x] = nb;
   __syncthreads();
   for (int h = 128; h > 0; h >>= 1) {
     if ((int)threadIdx.x < h) {
       part[0][threadIdx.x] += part[0][threadIdx.x + h];
       part[1][threadIdx.x] += part[1][threadIdx.x + h];
       part[2][threadIdx.x] += part[2][threadIdx.x + h];
+      part[3][threadIdx.x] += part[3][threadIdx.x + h];
     }
     __syncthreads();
   }
@@ -82,6 +89,7 @@ __global__ __launch_bounds__(256) void ce_final_kernel(float* __restrict__ ws, i
     *loss = l;
     ws[4 * B] = (float)nv;
     if (found) *found = __builtin_isfinite(l) ? 0.f : 1.f;
+    if (bad_labels) *bad_labels += (float)part[3][0];    // accumulates over steps until the host reads it
   }
 }
 
@@ -115,16 +123,16 @@ __global__ __launch_bounds__(256) void ce_ls_bwd_kernel(const float* __restrict_
 
 using namespace ogv;
 
-extern "C" size_t ogv_ce_ls_ws_bytes(int B) { return (size_t)(B > 0 ? 4 * B + 1 : 1) * sizeof(float); }
+extern "C" size_t ogv_ce_ls_ws_bytes(int B) { return (size_t)(B > 0 ? 5 * B + 1 : 1) * sizeof(float); }
 
 extern "C" int ogv_ce_ls_fwd(const float* logits, const int64_t* target, int B, int K, float label_smoothing,
-                             float* loss, float* ws, float* found, void* stream) {
+                             float* loss, float* ws, float* found, float* bad_labels, void* stream) {
   OGV_REQUIRE(logits && target && loss && ws, "ogv_ce_ls_fwd: null pointer");
   OGV_REQUIRE(B > 0 && K > 0, "ogv_ce_ls_fwd: bad shape B=%d K=%d", B, K);
   OGV_REQUIRE(label_smoothing >= 0.f && label_smoothing <= 1.f, "ogv_ce_ls_fwd: label_smoothing %g not in [0, 1]",
               (double)label_smoothing);
   ce_rows_kernel<<<cdiv(B, 4), 256, 0, as_stream(stream)>>>(logits, target, B, K, ws);
-  ce_final_kernel<<<1, 256, 0, as_stream(stream)>>>(ws, B, K, label_smoothing, loss, found);
+  ce_final_kernel<<<1, 256, 0, as_stream(stream)>>>(ws, B, K, label_smoothing, loss, found, bad_labels);
   return check_launch("ogv_ce_ls_fwd");
 }
 

@@ -1911,6 +1911,248 @@ static void vbig_run(const bf16* x, int ldx, const float* Wc, int wrows, const f
   kern<<<grid, VB_NW * 64, lds, s>>>(x, ldx, Wc, wrows, bias, cat, ldc, y, H, W, C, heads, t, g_vp_dbg);
 }
 
+// ------------------------------------------------------------------------------------------------
+// The fused Outlooker forward for WIDE stages on SMALL images (7M stages 2-3: 8 x 8 / 4 x 4 pixels,
+// C = 192 / 256; 14M stage 3, 22M stage 3), decomposed by HEAD instead of by pixel tile:
+//   * a panel is IPP WHOLE images (RI = H*W rounded up to 16 rows each, R = IPP * RI <= 128 rows), so
+//     every 3 x 3 neighbour of a panel pixel is in the panel or outside its image (zero padding):
+//     no halo, no recomputed projection;
+//   * a workgroup owns ONE head and a strided set of panels: its weight slice -- the head's hd rows of
+//     W_v and 9 rows of W_attn (+ bias), 16 (hd + 16) x C as bf16 hi + lo -- is staged in LDS once,
+//     so the weight is read from L2 once per workgroup instead of once per tile (the streaming kernel
+//     above re-reads all of [W_v; W_attn] per 8 x 8 tile, which is what made it lose);
+//   * per panel: the wave's x rows go straight from HBM into MFMA operand registers (16-B loads,
+//     the NEXT panel's issued right after this panel's MFMAs), [v_h | logits_h] = x . W_h^T + b on
+//     v_mfma_f32_16x16x32_bf16 (transposed product, weight = A operand), rounded to bf16 into an LDS
+//     result tile exactly where the unfused GEMM rounds its output; the head's columns of cat (the
+//     backward's input, training) are written from it, softmax over the 9 logits per pixel, and the
+//     3 x 3 gather y[:, head] from LDS.
+// grid = RG row groups x heads, block b -> head (b / 8) % heads, row group (b % 8) + 8 (b / 8 heads):
+// all heads of a row group run on ONE XCD (b % 8), so a panel's x rows are fetched from HBM once
+// into that XCD's L2 and its cat rows (whose columns the heads write piecewise) are assembled there.
+// ------------------------------------------------------------------------------------------------
+struct VHead {
+  int RI, IPP, R, npanels, RG;
+  int WP, RP;
+  FDiv fRI, fW;
+};
+
+template <int NJV, int NK>
+static size_t vhead_lds(const VHead& t, bool sw) {
+  constexpr int NCOL = (NJV + 1) * 16;
+  return (size_t)(sw ? 2 : 1) * NCOL * t.WP * 2 + (size_t)NCOL * 4 + ((size_t)t.R * t.RP * 2 + 15) / 16 * 16 +
+         (size_t)t.R * 9 * 4;
+}
+
+template <int NJV, int NK, int NF, bool SW>
+__global__ __launch_bounds__(256, 2) void outlook_vproj_head_fwd_kernel(
+    const bf16* __restrict__ x, int ldx, const float* __restrict__ Wc, const float* __restrict__ bias,
+    bf16* __restrict__ cat, int ldc, bf16* __restrict__ y, int B, int H, int W, int C, int heads, VHead t) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NJ = NJV + 1, NCOL = NJ * 16, KP = NK * 32, HD = NJV * 16, HD8 = HD / 8;
+  const int WP = t.WP, RP = t.RP, R = t.R, HW = H * W;
+  bf16* ws = reinterpret_cast<bf16*>(smem);                                  // [hi | lo][NCOL][WP]
+  float* bs = reinterpret_cast<float*>(ws + (size_t)(SW ? 2 : 1) * NCOL * WP);   // [NCOL]
+  bf16* rs = reinterpret_cast<bf16*>(bs + NCOL);                             // [R][RP]: [v_h | logits_h | 0]
+  float* P = reinterpret_cast<float*>(reinterpret_cast<char*>(rs) + ((size_t)R * RP * 2 + 15) / 16 * 16);  // [R][9]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int head = (blockIdx.x >> 3) % heads;
+  const int rg = (blockIdx.x & 7) + 8 * (int)(blockIdx.x / (8 * heads));
+  // weight slice of this head: slab row n < HD <- Wc[head*HD + n] (v), HD <= n < HD + 9 <-
+  // Wc[C + 9 head + n - HD] (logits), zero rows above; columns >= C zero
+  for (int idx = tid; idx < NCOL * (KP / 4); idx += 256) {
+    const int n = idx / (KP / 4), k = (idx - n * (KP / 4)) * 4;
+    const int row = n < HD ? head * HD + n : (n < HD + 9 ? C + 9 * head + n - HD : -1);
+    float4 w4 = float4{0.f, 0.f, 0.f, 0.f};
+    if (row >= 0 && k < C) w4 = *reinterpret_cast<const float4*>(Wc + (long)row * C + k);
+    const bf16x4 h = {(bf16)w4.x, (bf16)w4.y, (bf16)w4.z, (bf16)w4.w};
+    *reinterpret_cast<bf16x4*>(ws + n * WP + k) = h;
+    if constexpr (SW) {
+      const bf16x4 l = {(bf16)(w4.x - (float)h[0]), (bf16)(w4.y - (float)h[1]), (bf16)(w4.z - (float)h[2]),
+                        (bf16)(w4.w - (float)h[3])};
+      *reinterpret_cast<bf16x4*>(ws + (NCOL + n) * WP + k) = l;
+    }
+  }
+  for (int n = tid; n < NCOL; n += 256) {
+    const int row = n < HD ? head * HD + n : (n < HD + 9 ? C + 9 * head + n - HD : -1);
+    bs[n] = (bias && row >= 0) ? bias[row] : 0.f;
+  }
+  // panel-local row r -> global row (or -1: a pad row of an image, or an image past B)
+  auto grow_of = [&](int p, int r) -> long {
+    const int i = fdiv(r, t.fRI), pix = r - i * t.RI;
+    const long img = (long)p * t.IPP + i;
+    return (pix < HW && img < B) ? img * HW + pix : -1L;
+  };
+  const int NFR = R / 16;   // row fragments per panel; wave w owns fragments w, w + 4, ...
+  bf16x8 xf[NF][NK];
+  auto load_x = [&](int p) {
+#pragma unroll
+    for (int q = 0; q < NF; ++q) {
+      const int f = wave + 4 * q;
+      const long g = f < NFR ? grow_of(p, f * 16 + fr) : -1L;
+      const bf16* src = x + (g < 0 ? 0L : g) * ldx + fg * 8;   // clamped: always a valid address
+#pragma unroll
+      for (int kt = 0; kt < NK; ++kt) {
+        const bf16x8 v = (kt * 32 + fg * 8 < C) ? *reinterpret_cast<const bf16x8*>(src + kt * 32) : bf16x8{};
+        xf[q][kt] = g < 0 ? bf16x8{} : v;
+      }
+    }
+  };
+  if (rg < t.npanels) load_x(rg);
+  for (int p = rg; p < t.npanels; p += t.RG) {
+    // 1. [v_h | logits_h] of the panel's rows on MFMA
+    f32x4 acc[NF][NJ];
+#pragma unroll
+    for (int q = 0; q < NF; ++q)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[q][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    __syncthreads();   // weights staged (first panel) / the previous panel's gather is done with rs and P
+#pragma unroll
+    for (int kt = 0; kt < NK; ++kt)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const bf16x8 wh = *reinterpret_cast<const bf16x8*>(ws + (j * 16 + fr) * WP + kt * 32 + fg * 8);
+#pragma unroll
+        for (int q = 0; q < NF; ++q) acc[q][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, xf[q][kt], acc[q][j], 0, 0, 0);
+        if constexpr (SW) {
+          const bf16x8 wl = *reinterpret_cast<const bf16x8*>(ws + (NCOL + j * 16 + fr) * WP + kt * 32 + fg * 8);
+#pragma unroll
+          for (int q = 0; q < NF; ++q) acc[q][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl, xf[q][kt], acc[q][j], 0, 0, 0);
+        }
+      }
+    if (p + t.RG < t.npanels) load_x(p + t.RG);   // in flight during the epilogue, softmax and gather
+    // lane: row f * 16 + fr, columns 16 j + 4 fg .. + 3 (+ bias, rounded to bf16 as the GEMM output)
+#pragma unroll
+    for (int q = 0; q < NF; ++q) {
+      const int f = wave + 4 * q;
+      if (f >= NFR) continue;
+      const int m = f * 16 + fr;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int n = j * 16 + 4 * fg;
+        const float4 b4 = *reinterpret_cast<const float4*>(bs + n);
+        const bf16x4 o = {(bf16)(acc[q][j][0] + b4.x), (bf16)(acc[q][j][1] + b4.y), (bf16)(acc[q][j][2] + b4.z),
+                          (bf16)(acc[q][j][3] + b4.w)};
+        *reinterpret_cast<bf16x4*>(rs + m * RP + n) = o;
+      }
+    }
+    __syncthreads();
+    // 2a. the head's columns of cat (training): v_h as 16-B rows, the 9 logits as bf16 elements
+    if (cat) {
+      for (int idx = tid; idx < R * HD8; idx += 256) {
+        const int r = idx / HD8, c8 = idx - r * HD8;
+        const long g = grow_of(p, r);
+        if (g >= 0)
+          *reinterpret_cast<uint4*>(cat + g * ldc + head * HD + c8 * 8) = *reinterpret_cast<const uint4*>(rs + r * RP + c8 * 8);
+      }
+      for (int idx = tid; idx < R * 9; idx += 256) {
+        const int r = idx / 9, jj = idx - r * 9;
+        const long g = grow_of(p, r);
+        if (g >= 0) cat[g * ldc + C + 9 * head + jj] = rs[r * RP + HD + jj];
+      }
+      const int pad = ldc - C - 9 * heads;   // the zero columns of [v | logits | 0] (the last head's)
+      if (head == heads - 1)
+        for (int idx = tid; idx < R * pad; idx += 256) {
+          const int r = idx / pad, jj = idx - r * pad;
+          const long g = grow_of(p, r);
+          if (g >= 0) cat[g * ldc + C + 9 * heads + jj] = (bf16)0.f;
+        }
+    }
+    // 2b. softmax over the 9 (bf16-rounded) logits of every panel pixel
+    for (int r = tid; r < R; r += 256) {
+      const bf16* l = rs + r * RP + HD;
+      float a[9], mx = -INFINITY;
+#pragma unroll
+      for (int jj = 0; jj < 9; ++jj) {
+        a[jj] = (float)l[jj];
+        mx = fmaxf(mx, a[jj]);
+      }
+      float sm = 0.f;
+#pragma unroll
+      for (int jj = 0; jj < 9; ++jj) {
+        a[jj] = __expf(a[jj] - mx);
+        sm += a[jj];
+      }
+      const float inv = 1.0f / sm;
+#pragma unroll
+      for (int jj = 0; jj < 9; ++jj) P[r * 9 + jj] = a[jj] * inv;
+    }
+    __syncthreads();
+    // 3. y[:, head] = 3 x 3 gather of v_h weighted by the softmax (out-of-image neighbours: v = 0)
+    for (int idx = tid; idx < R * HD8; idx += 256) {
+      const int r = idx / HD8, cc = idx - r * HD8;
+      const long g = grow_of(p, r);
+      if (g < 0) continue;
+      const int i = fdiv(r, t.fRI), pix = r - i * t.RI;
+      const int yy = fdiv(pix, t.fW), xx = pix - yy * W;
+      float accy[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) accy[e] = 0.f;
+#pragma unroll
+      for (int ki = 0; ki < 3; ++ki)
+#pragma unroll
+        for (int kj = 0; kj < 3; ++kj) {
+          const int ny = yy + ki - 1, nx = xx + kj - 1;
+          if (ny < 0 || ny >= H || nx < 0 || nx >= W) continue;
+          const float w = P[r * 9 + ki * 3 + kj];
+          const uint4 raw = *reinterpret_cast<const uint4*>(rs + (i * t.RI + ny * W + nx) * RP + cc * 8);
+          const bf16* e8 = reinterpret_cast<const bf16*>(&raw);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) accy[e] = fmaf(w, (float)e8[e], accy[e]);
+        }
+      store_vec<bf16, 8>(y + g * C + head * HD + cc * 8, accy);
+    }
+  }
+}
+
+// knob "vp_head" (default 1): the per-head whole-image kernel above for the wide stages it plans;
+// "vph_rows": target rows per panel (64 default; a panel is whole images, <= 128 rows)
+static int g_vp_head = 1;
+void set_vp_head(int v) { g_vp_head = v ? 1 : 0; }
+static int g_vph_rows = 64;
+void set_vph_rows(int v) { g_vph_rows = v < 16 ? 16 : (v > 128 ? 128 : v); }
+
+static bool vhead_plan(int B, int H, int W, int C, int heads, int k, int ldc, ogv_dtype dt, VHead& t) {
+  if (!g_outlook_vproj || !g_vp_head) return false;
+  if (dt != OGV_BF16 || k != 3 || B <= 0 || H <= 0 || W <= 0 || heads <= 0) return false;
+  if (C % 32 != 0 || !vbig_cj(C / 32) || C % heads != 0) return false;   // C in {128, 192, 256, 384}
+  const int hd = C / heads;
+  if (hd != 32 && hd != 64) return false;
+  if (ldc != (C + heads * 9 + 7) / 8 * 8) return false;
+  const int HW = H * W;
+  t = VHead{};
+  t.RI = (HW + 15) / 16 * 16;
+  if (t.RI > 128) return false;
+  t.IPP = g_vph_rows / t.RI < 1 ? 1 : g_vph_rows / t.RI;
+  t.R = t.IPP * t.RI;
+  t.npanels = (B + t.IPP - 1) / t.IPP;
+  const int NCOL = hd + 16, KP = C;
+  t.WP = KP + 8;      // (KP + 8) / 2 dwords per row: 16 fragment rows on distinct bank quads
+  t.RP = NCOL + 8;
+  const size_t lds = (hd == 32 ? vhead_lds<2, 4> : vhead_lds<4, 4>)(t, true);
+  const int per_cu = lds <= 80 * 1024 ? 2 : 1;
+  if (lds > 160 * 1024) return false;
+  int rg = (256 * per_cu / heads) / 8 * 8;
+  const int np8 = (t.npanels + 7) / 8 * 8;
+  t.RG = rg < 8 ? 8 : (rg > np8 ? np8 : rg);
+  if ((long)t.RG * heads >= (1L << 24)) return false;
+  t.fRI = fdiv_make(t.RI);
+  t.fW = fdiv_make(W);
+  return true;
+}
+
+template <int NJV, int NK, int NF>
+static void vhead_run(const bf16* x, int ldx, const float* Wc, const float* bias, bf16* cat, int ldc, bf16* y, int B,
+                      int H, int W, int C, int heads, const VHead& t, bool sw, hipStream_t s) {
+  const size_t lds = vhead_lds<NJV, NK>(t, sw);
+  auto kern = sw ? outlook_vproj_head_fwd_kernel<NJV, NK, NF, true> : outlook_vproj_head_fwd_kernel<NJV, NK, NF, false>;
+  if (lds > 64 * 1024)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+  kern<<<(unsigned)(t.RG * heads), 256, lds, s>>>(x, ldx, Wc, bias, cat, ldc, y, B, H, W, C, heads, t);
+}
+
 static bool vproj_bwd_plan(int B, int H, int W, int C, int heads, int k, int ldc, ogv_dtype dt, VTile& t, int& nw) {
   return vtile_plan(B, H, W, C, heads, k, ldc, dt, true, t, nw);
 }
@@ -1942,6 +2184,8 @@ extern "C" int ogv_outlook_vproj_supported(int B, int H, int W, int C, int heads
   VTile t;
   if (g_outlook_vproj < (train ? 2 : 1)) return 0;
   int nw = 0;
+  VHead th;
+  if (vhead_plan(B, H, W, C, heads, k, ldc, dt, th)) return 1;   // wide stages, small images: per-head kernel
   if (vbig_plan(B, H, W, C, heads, k, ldc, dt, t)) return 1;   // wide stages: forward with cat, tiled backward
   if (!vproj_plan(B, H, W, C, heads, k, ldc, dt, t, nw)) return 0;
   if (!train || g_outlook_vproj < 3) return 1;
@@ -1997,6 +2241,26 @@ extern "C" int ogv_outlook_vproj_fwd(const void* x, int ldx, const float* w, con
   if (rc) return rc;
   VTile t;
   int nw = 0;
+  VHead th;
+  if (vhead_plan(B, H, W, C, heads, k, ldc, dt, th)) {
+    OGV_REQUIRE(ldx >= C && ldx % 8 == 0 && al16p(x) && al16p(y) && (!cat || al16p(cat)) && al16p(w),
+                "ogv_outlook_vproj_fwd: rows must be 16-B aligned (ldx %d)", ldx);
+    const bool sw = (split_w() & 1) != 0;
+    hipStream_t s = as_stream(stream);
+    const bf16* xb = (const bf16*)x;
+    bf16 *cb = (bf16*)cat, *yb = (bf16*)y;
+    const int nf = th.R > 64 ? 2 : 1;
+#define OGV_VHEAD(njv, nk)                                                                                  \
+  if (C / heads == njv * 16 && C / 32 == nk) {                                                              \
+    if (nf == 1) vhead_run<njv, nk, 1>(xb, ldx, w, bias, cb, ldc, yb, B, H, W, C, heads, th, sw, s);        \
+    else vhead_run<njv, nk, 2>(xb, ldx, w, bias, cb, ldc, yb, B, H, W, C, heads, th, sw, s);                \
+    return check_launch("ogv_outlook_vproj_fwd");                                                          \
+  }
+    OGV_VHEAD(2, 4) OGV_VHEAD(2, 6) OGV_VHEAD(2, 8) OGV_VHEAD(2, 12)
+    OGV_VHEAD(4, 4) OGV_VHEAD(4, 6) OGV_VHEAD(4, 8) OGV_VHEAD(4, 12)
+#undef OGV_VHEAD
+    OGV_REQUIRE(false, "ogv_outlook_vproj_fwd: no per-head instantiation for C %d / %d heads", C, heads);
+  }
   const bool big = vbig_plan(B, H, W, C, heads, k, ldc, dt, t);
   OGV_REQUIRE(big || vproj_plan(B, H, W, C, heads, k, ldc, dt, t, nw),
               "ogv_outlook_vproj_fwd: unsupported shape (needs bf16, k=3, 8 | head_dim, 16 | C <= 96 or "

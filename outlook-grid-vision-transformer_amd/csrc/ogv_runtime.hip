@@ -220,6 +220,14 @@ extern "C" int ogv_set_option(const char* name, int value) {
     set_vp_big(value);
     return OGV_OK;
   }
+  if (!strcmp(name, "vp_head")) {
+    set_vp_head(value);
+    return OGV_OK;
+  }
+  if (!strcmp(name, "vph_rows")) {
+    set_vph_rows(value);
+    return OGV_OK;
+  }
   if (!strcmp(name, "vp_tile")) {
     set_vp_tile(value);
     return OGV_OK;

@@ -117,7 +117,7 @@ SIGNATURES = {
     "ogv_cast": (_i, [_p, _i, _p, _i, _sz, _p]),
     "ogv_step_flag": (_i, [_p, _i, _p, _p]),
     "ogv_ce_ls_ws_bytes": (_sz, [_i]),
-    "ogv_ce_ls_fwd": (_i, [_p, _p, _i, _i, _f, _p, _p, _p, _p]),
+    "ogv_ce_ls_fwd": (_i, [_p, _p, _i, _i, _f, _p, _p, _p, _p, _p]),
     "ogv_ce_ls_bwd": (_i, [_p, _p, _p, _p, _i, _i, _f, _p, _p]),
     "ogv_clip_adamw_ws_bytes": (_sz, [ctypes.POINTER(AdamWTensor), _i]),
     "ogv_clip_adamw": (_i, [ctypes.POINTER(AdamWTensor), _i, ctypes.POINTER(AdamWGroup), _i, _p, _f, _p, _p]),

@@ -624,14 +624,15 @@ def linear_rows_act(x2d, weight, bias, act):
 # ------------------------------------------------------------------------------------------------
 class _CrossEntropyLS(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, logits, target, ls, found):
+    def forward(ctx, logits, target, ls, found, bad):
         lib = _lib.load()
         B, K = logits.shape
         loss = torch.empty((), dtype=torch.float32, device=logits.device)
         ws = torch.empty((lib.ogv_ce_ls_ws_bytes(B) // 4,), dtype=torch.float32, device=logits.device)
         with _census("ce_fwd", dict(B=B, K=K, elem=4)):
             check(lib.ogv_ce_ls_fwd(_ptr(logits), _ptr(target), B, K, float(ls), _ptr(loss), _ptr(ws),
-                                    _ptr(found) if found is not None else None, _stream()), "ogv_ce_ls_fwd")
+                                    _ptr(found) if found is not None else None, _ptr(bad) if bad is not None else None,
+                                    _stream()), "ogv_ce_ls_fwd")
         ctx.save_for_backward(logits, target, ws)
         ctx.ls = float(ls)
         return loss
@@ -646,15 +647,17 @@ class _CrossEntropyLS(torch.autograd.Function):
         with _census("ce_bwd", dict(B=B, K=K, elem=4)):
             check(lib.ogv_ce_ls_bwd(_ptr(logits), _ptr(target), _ptr(ws), _ptr(g), B, K, ctx.ls, _ptr(dz), _stream()),
                   "ogv_ce_ls_bwd")
-        return dz, None, None, None
+        return dz, None, None, None, None
 
 
-def cross_entropy_ls(logits, target, label_smoothing=0.0, found=None):
+def cross_entropy_ls(logits, target, label_smoothing=0.0, found=None, bad_labels=None):
     """F.cross_entropy(logits.float(), target, label_smoothing=ls) (mean, ignore_index -100) on the
     native kernels: logits [B, K] (cast to contiguous fp32), target [B] int64 class indices.  found: an
     optional fp32 [1] device tensor that receives !isfinite(loss) from the same launch (the training
-    step's found_inf guard).  A label outside [0, K) gives a NaN loss instead of torch's raise."""
-    require_device(logits, target, found, what="ogv.cross_entropy")
+    step's found_inf guard).  A label outside [0, K) gives a NaN loss instead of torch's raise (a raise
+    needs a device sync); bad_labels: an optional fp32 [1] device counter the same launch adds the number
+    of such rows to, so the caller can raise when it next syncs (Trainer does)."""
+    require_device(logits, target, found, bad_labels, what="ogv.cross_entropy")
     if logits.dim() != 2 or target.dim() != 1 or target.shape[0] != logits.shape[0]:
         raise ValueError(f"ogv.cross_entropy: logits [B, K] and target [B] expected, got {tuple(logits.shape)} "
                          f"and {tuple(target.shape)}")
@@ -662,7 +665,8 @@ def cross_entropy_ls(logits, target, label_smoothing=0.0, found=None):
         raise ValueError("ogv.cross_entropy: class-index targets (int64) only")
     if not 0.0 <= label_smoothing <= 1.0:
         raise ValueError(f"ogv.cross_entropy: label_smoothing {label_smoothing} not in [0, 1]")
-    return _CrossEntropyLS.apply(logits.float().contiguous(), target.contiguous(), float(label_smoothing), found)
+    return _CrossEntropyLS.apply(logits.float().contiguous(), target.contiguous(), float(label_smoothing), found,
+                                 bad_labels)
 
 
 # ------------------------------------------------------------------------------------------------

@@ -305,7 +305,7 @@ class Trainer:
                  total_steps=10_000, warmup_ratio=0.05, min_lr=1e-6, amp_dtype: Optional[torch.dtype] = torch.bfloat16,
                  graphs: bool = False, capture_warmup: int = 3, capture_hook=None, bucket_mb: float = 8.0,
                  broadcast_buffers: bool = True, defer_reductions: bool = True, native_optimizer: bool = True,
-                 force_dp: bool = False, dp_capture_collective: bool = False):
+                 force_dp: bool = False, dp_capture_collective: bool = False, label_check_every: int = 100):
         self.model = model
         core = model.module if hasattr(model, "module") else model
         self.core = core
@@ -338,10 +338,17 @@ class Trainer:
         self.eager_fallbacks = 0
         self._g = None
         self._nonfinite_host = 0
+        self.label_check_every = int(label_check_every)
+        self._steps_taken = 0
         if self.device_side:
             self._found = torch.zeros((), dtype=torch.float32, device=dev)
             self.opt.found_inf = self._found       # read by the fused AdamW kernel (1 = skip)
             self._nonfinite = torch.zeros((), dtype=torch.float32, device=dev)
+            # rows whose class index is outside [0, K) (and not -100): the native loss counts them here;
+            # read (one sync) after the first step, every label_check_every steps and with nonfinite_steps,
+            # raising ValueError as torch's cross_entropy would (a bad label is a data error,
+            # not a silently skipped step)
+            self._bad_labels = torch.zeros((), dtype=torch.float32, device=dev)
             self.sched.bind_device(torch.zeros((), dtype=torch.float32, device=dev))
         self.world = 1 if self.ddp else _dist_world()
         # the data-parallel path (broadcast at start, gradient / buffer exchange every step); force_dp
@@ -417,7 +424,8 @@ class Trainer:
         if logits.is_cuda and logits.dim() == 2 and y.dtype == torch.int64:
             from .functional import cross_entropy_ls
             found = self._found.view(1) if self.device_side else None
-            return cross_entropy_ls(logits, y, self.ls, found=found), found is not None
+            bad = self._bad_labels.view(1) if self.device_side else None
+            return cross_entropy_ls(logits, y, self.ls, found=found, bad_labels=bad), found is not None
         return F.cross_entropy(logits.float(), y, label_smoothing=self.ls), False
 
     def _fwd_bwd(self, x, y):
@@ -677,6 +685,26 @@ class Trainer:
                 and y.shape == self._y.shape and y.dtype == self._y.dtype and y.device == self._y.device)
 
     def step(self, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+        loss = self._step(x, y)
+        self._steps_taken += 1
+        if self.device_side and (self._steps_taken == 1 or (self.label_check_every > 0
+                                                            and self._steps_taken % self.label_check_every == 0)):
+            self.check_labels()
+        return loss
+
+    def check_labels(self):
+        """Raise ValueError if any step so far had a class index outside [0, num_classes) other than -100
+        (the native loss counts them on the device; torch's cross_entropy raises on the first such batch).
+        One host sync; Trainer.step calls it after the first step and every ``label_check_every`` steps."""
+        if self.device_side:
+            n = int(self._bad_labels.item())
+            if n:
+                self._bad_labels.zero_()
+                raise ValueError(f"Trainer: {n} target label(s) outside [0, num_classes) (and not -100) since the "
+                                 f"last check; those steps were skipped (loss NaN) -- torch's cross_entropy raises "
+                                 f"on such targets")
+
+    def _step(self, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
         if not self.graphs or (self._g is None and self._eager_steps < self.capture_warmup):
             self._eager_steps += 1
             return self._eager(x, y)
@@ -695,6 +723,7 @@ class Trainer:
 
     @property
     def nonfinite_steps(self) -> int:
+        self.check_labels()
         return int(self._nonfinite.item()) if self.device_side else self._nonfinite_host
 
     # -- checkpoint / resume (src/training/chekpoints.py dict keys) -----------------------------

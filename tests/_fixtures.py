@@ -175,7 +175,7 @@ def train_stable_masks(meta, arr, params):
     return out
 
 
-def train_step_errors(meta, arr, t, params, p0, masks=None):
+def train_step_errors(meta, arr, t, params, p0, masks=None, prefix=""):
     """Deviation of parameters ``params`` (name -> tensor, any device) after fixture step t from the
     reference's, with p0 (name -> tensor) the common start.  Returns a dict of maxima over parameters:
       upd    max|sketch(ours) - sketch(ref)| / max(|update_ref|_F, 1e-12) on the stable elements -- the
@@ -184,24 +184,32 @@ def train_step_errors(meta, arr, t, params, p0, masks=None):
       norm   max| |p|_F ours - ref | / max(1, |p|_F ref)
       full   (steps recorded in full) max|p - p_ref| / max(1, max|p_ref|) over the stable elements of every
              small parameter
-    and 'worst' = the parameter name behind the largest 'upd'."""
+    'worst' = the parameter name behind the largest 'upd', and per parameter (numpy arrays in param_names
+    order): 'upd_all', 'pn_abs' = | |p|_F ours - ref |, 'pns_abs' (with a 'pns{t}' array: the same on the
+    stable elements).  ``prefix`` selects the fixture arrays' prefix ('amp_' for the bf16 fixture's)."""
     names = meta["param_names"]
     if masks is None:
         masks = train_stable_masks(meta, arr, params)
     dsk, dn, pn = arr[f"dsk{t}"], arr[f"dn{t}"], arr[f"pn{t}"]
     upd = dnerr = norm = 0.0
     worst = None
+    upd_all, pn_abs, pns_abs = np.zeros(len(names)), np.zeros(len(names)), np.zeros(len(names))
     for i, k in enumerate(names):
         p = params[k].detach().double().cpu()
         d = (p - p0[k].detach().double().cpu()) * masks[k]
         scale = max(float(dn[i]), 1e-12)
         e = (update_sketch(k, d) - torch.from_numpy(dsk[i])).abs().max().item() / scale
+        if float(dn[i]) > 0:
+            upd_all[i] = e
         if float(dn[i]) > 0 and e > upd:
             upd, worst = e, k
         if float(dn[i]) > 0:
             dnerr = max(dnerr, abs(d.norm().item() - float(dn[i])) / scale)
-        norm = max(norm, abs(p.norm().item() - float(pn[i])) / max(1.0, float(pn[i])))
-    out = dict(upd=upd, dn=dnerr, norm=norm, worst=worst)
+        pn_abs[i] = abs(p.norm().item() - float(pn[i]))
+        norm = max(norm, pn_abs[i] / max(1.0, float(pn[i])))
+        if f"pns{t}" in arr:
+            pns_abs[i] = abs((p * masks[k]).norm().item() - float(arr[f"pns{t}"][i]))
+    out = dict(upd=upd, dn=dnerr, norm=norm, worst=worst, upd_all=upd_all, pn_abs=pn_abs, pns_abs=pns_abs)
     if f"p{t}" in arr:
         flat, off, full = arr[f"p{t}"], 0, 0.0
         for k in names:
@@ -212,6 +220,39 @@ def train_step_errors(meta, arr, t, params, p0, masks=None):
             off += p.numel()
             full = max(full, ((p.contiguous() - ref) * masks[k]).abs().max().item() / max(1.0, ref.abs().max().item()))
         assert off == flat.size
+        out["full"] = full
+    return out
+
+
+def amp_reference_errors(meta, arr, amp, t, params, masks):
+    """The REFERENCE'S OWN bf16-autocast step's deviation from its fp32 step after step t (fixtures
+    train_steps_7m_b16 = ``arr`` and train_steps_7m_b16_amp = ``amp``, make_golden.py r5: the same sketches,
+    the same noise mask), in train_step_errors' terms: 'upd_all' / 'upd' (relative update-sketch error per
+    parameter / max), 'dn', 'norm', 'full' (steps recorded in full, stable elements of every small
+    parameter), 'loss' (|loss_bf16 - loss_fp32|).  ``params`` / ``masks`` give the parameter sizes and the
+    stable-element masks (train_stable_masks)."""
+    names = meta["param_names"]
+    dn = arr[f"dn{t}"]
+    scale = np.maximum(dn, 1e-12)
+    upd_all = np.abs(amp[f"amp_dsk{t}"] - arr[f"dsk{t}"]).reshape(len(names), -1).max(1) / scale
+    upd_all[dn == 0] = 0.0
+    dn_err = np.abs(amp[f"amp_dn{t}"] - dn) / scale
+    dn_err[dn == 0] = 0.0
+    pn = arr[f"pn{t}"]
+    out = dict(upd_all=upd_all, upd=float(upd_all.max()), dn=float(dn_err.max()),
+               norm=float((np.abs(amp[f"amp_pn{t}"] - pn) / np.maximum(1.0, pn)).max()),
+               loss=abs(float(amp["amp_loss"][t]) - float(arr["loss"][t])))
+    if f"p{t}" in arr:
+        a, b, off, full = arr[f"p{t}"].astype(np.float64), amp[f"amp_p{t}"].astype(np.float64), 0, 0.0
+        for k in names:
+            n = params[k].numel()
+            if n > meta["full_max"]:
+                continue
+            m = masks[k].contiguous().reshape(-1).numpy() if masks[k].dim() else masks[k].reshape(-1).numpy()
+            ref = a[off:off + n]
+            full = max(full, float((np.abs(b[off:off + n] - ref) * m).max() / max(1.0, np.abs(ref).max())))
+            off += n
+        assert off == a.size
         out["full"] = full
     return out
 

@@ -197,9 +197,17 @@ def test_outlook_vproj_plan_and_knob():
         assert sup(512, 32, 32, 48, 2, False) == 1          # 7M stage 0
         assert sup(512, 16, 16, 96, 3, False) == 1          # 7M stage 1
         assert sup(128, 224, 224, 64, 2, False) == 1        # 22M stage 0
-        # wide stages (C > 96): the weight-streaming variant (opt-in, knob vp_big), forward with cat; no
-        # recompute backward
-        assert sup(512, 8, 8, 192, 6, False) == 0           # default: unfused GEMM + aggregation
+        # wide stages (C > 96) on images of <= 128 pixels: the per-head whole-image kernel (knob vp_head,
+        # default on), forward with cat; larger wide-stage images keep the unfused GEMM + aggregation
+        for shape in ((512, 8, 8, 192, 6), (512, 4, 4, 256, 8), (256, 8, 8, 384, 6), (3, 5, 11, 128, 4)):
+            assert sup(*shape, False) == 1 and sup(*shape, True) == 1, shape
+        assert sup(256, 32, 32, 128, 4, False) == 0         # 14M stage 1: 1024-pixel images
+        assert sup(256, 16, 16, 256, 8, False) == 0         # 14M stage 2: 256-pixel images
+        assert sup(512, 8, 8, 160, 5, False) == 0           # C = 160: no instantiation (C / 32 = 5)
+        assert sup(512, 8, 8, 288, 6, False) == 0           # head_dim 48: the per-head kernel takes 32 / 64
+        assert lib.ogv_set_option(b"vp_head", 0) == 0
+        assert sup(512, 8, 8, 192, 6, False) == 0           # vp_head off: unfused GEMM + aggregation
+        # the weight-streaming variant (opt-in, knob vp_big), forward with cat; no recompute backward
         assert lib.ogv_set_option(b"vp_big", 1) == 0
         for shape in ((512, 8, 8, 192, 6), (512, 4, 4, 256, 8), (256, 32, 32, 128, 4), (128, 14, 14, 384, 6)):
             assert sup(*shape, False) == 1 and sup(*shape, True) == 1, shape
@@ -232,6 +240,7 @@ def test_outlook_vproj_plan_and_knob():
         assert lib.ogv_set_option(b"outlook_vproj", 2) == 0
         assert lib.ogv_set_option(b"vp_tile", 0) == 0
         assert lib.ogv_set_option(b"vp_big", 0) == 0
+        assert lib.ogv_set_option(b"vp_head", 1) == 0
     x = ctypes.c_void_p(16)
     rc = lib.ogv_outlook_vproj_fwd(x, 192, x, None, None, 200, x, 2, 8, 8, 192, 6, 3, L.OGV_BF16, None)
     assert rc != 0 and b"unsupported" in lib.ogv_last_error()

@@ -50,9 +50,43 @@ def test_cross_entropy_ls_ignore_index_and_bad_label():
     # a label outside [0, K): torch raises; the native loss is NaN and the step guard is set
     y2 = y.clone()
     y2[0] = K
+    y2[7] = -5
     found = torch.zeros(1, device=DEV)
-    bad = cross_entropy_ls(z.to(DEV), y2.to(DEV), 0.1, found=found)
-    assert torch.isnan(bad).item() and found.item() == 1.0
+    nbad = torch.full((1,), 2.0, device=DEV)       # the counter accumulates
+    bad = cross_entropy_ls(z.to(DEV), y2.to(DEV), 0.1, found=found, bad_labels=nbad)
+    assert torch.isnan(bad).item() and found.item() == 1.0 and nbad.item() == 4.0
+    # ignored rows are not bad labels, and a NaN logit alone sets found but counts no bad label
+    z3 = z.clone()
+    z3[4, 9] = float("nan")
+    found.zero_()
+    nbad.zero_()
+    l3 = cross_entropy_ls(z3.to(DEV), y.to(DEV), 0.1, found=found, bad_labels=nbad)
+    assert torch.isnan(l3).item() and found.item() == 1.0 and nbad.item() == 0.0
+
+
+@pytest.mark.parametrize("graphs", [False, True], ids=["eager", "graph"])
+def test_trainer_raises_on_bad_labels(graphs):
+    """a label outside [0, K) must not be skipped silently -- the Trainer raises ValueError (as
+    torch's cross_entropy does) at its next label check: after the first step, every label_check_every
+    steps, and when nonfinite_steps is read."""
+    from ogv.train import Trainer
+    from src.Model_A_OutGridNet import MaxOutNet
+    from src.stage_config import StageCfg
+    torch.manual_seed(0)
+    m = MaxOutNet(10, [StageCfg(dim=48, depth=1, num_heads=2, grid_size=4, outlook_heads=2)], 3, 32, 0.0)
+    m = m.to(DEV).to(memory_format=torch.channels_last).train()
+    t = Trainer(m, graphs=graphs, capture_warmup=1, label_check_every=3)
+    x = torch.randn(4, 3, 16, 16, device=DEV).contiguous(memory_format=torch.channels_last)
+    y = torch.tensor([1, 2, 3, 4], device=DEV)
+    t.step(x, y)                                    # the first-step check passes
+    t.step(x, y)
+    ybad = torch.tensor([1, 10, 3, 4], device=DEV)  # 10 classes: label 10 is out of range
+    with pytest.raises(ValueError, match="outside"):
+        t.step(x, ybad)                             # step 3: the periodic check
+    assert t.nonfinite_steps == 1                   # the skipped step; the counter was reset by the raise
+    t.step(x, ybad)
+    with pytest.raises(ValueError, match="outside"):
+        t.nonfinite_steps
 
 
 def test_cross_entropy_ls_rejects_host_tensors_and_soft_targets():

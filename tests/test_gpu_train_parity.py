@@ -10,8 +10,12 @@ and the parameters -- the update p_t - p_0 of every parameter through the fixtur
 (relative error of the update <= 2e-3: measured 4.8e-4 - 9.2e-4 on MI355X, profiles/r04_parity.jsonl; two CPU
 fp32 implementations, the reference and the oracle, differ by <= 2.2e-4, tests/test_oracle_golden.py::
 test_train_steps_oracle), every small parameter in full at the recorded steps (1e-4 * max(1, |p|); measured
-<= 2.9e-6), the parameters' norms (1e-4 * max(1, |p|): they include the noise elements below), and the
-BatchNorm running buffers before the NaN step.  Elements whose
+<= 2.9e-6), the parameters' norms, and the BatchNorm running buffers before the NaN step.  The norm bars are
+derived, per parameter, from recorded numbers (fixture train_steps_7m_b16_amp, make_golden.py r5): a norm can move
+by at most the norm of the update's error (triangle inequality), so on the stable elements
+| |p s|_F - ref | <= 1e-6 |p s|_F (fp32 storage) + UPD_TOL * |update_ref s|_F, and on the whole parameter the
+noise elements' own update (both realisations, 2 * 'noise{t}') is added.  (Round 4 used a flat 1e-4 * max(1, |p|)
+here after measuring 1.2e-5 on proj_in.bias; the noise budget behind it is now recorded.)  Elements whose
 gradient is rounding noise (the key slice of qkv.bias, the last block's fc2.bias before the head's
 train-mode BatchNorm, ~0.6% of all) take a +-lr Adam step of random sign in any fp32 implementation and
 are excluded by the fixture's mask (make_golden.py main_r4)."""
@@ -24,7 +28,8 @@ import gen_params as gp
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-UPD_TOL, FULL_TOL, LOSS_TOL, NORM_TOL = 2e-3, 1e-4, 1e-4, 1e-4
+UPD_TOL, FULL_TOL, LOSS_TOL = 2e-3, 1e-4, 1e-4
+AMP_FACTOR = 1.5     # bf16 step: ours vs the reference's own bf16 deviation (two realisations of rounding noise)
 
 
 @pytest.fixture(autouse=True, scope="module")
@@ -50,12 +55,14 @@ def test_train_steps_match_reference(graphs, native):
     assert list(params) == meta["param_names"]
     p0 = {k: p.detach().clone() for k, p in params.items()}
     masks = fx.train_stable_masks(meta, arr, params)
+    _, amp = fx.load("train_steps_7m_b16_amp")
+    arr = dict(arr, **{k: v for k, v in amp.items() if k.startswith("pns")})     # stable-element norms (r5)
     t = Trainer(m, lr=meta["lr"], weight_decay=meta["weight_decay"], clip=meta["clip"],
                 label_smoothing=meta["label_smoothing"], total_steps=meta["total_steps"],
                 warmup_ratio=meta["warmup_ratio"], min_lr=meta["min_lr"], amp_dtype=None, graphs=graphs,
                 capture_warmup=1, native_optimizer=native)
     assert [len(g["params"]) for g in t.opt.param_groups] == meta["group_sizes"]
-    worst = dict(upd=0.0, full=0.0, loss=0.0)
+    worst = dict(upd=0.0, full=0.0, loss=0.0, pn_ratio=0.0, pns_ratio=0.0)
     for step, (x, y) in enumerate(fx.train_batches(meta)):
         lr_used = [float(g["lr"]) for g in t.opt.param_groups]
         loss = float(t.step(x.to(DEV).contiguous(memory_format=torch.channels_last), y.to(DEV)))
@@ -72,9 +79,17 @@ def test_train_steps_match_reference(graphs, native):
         e = fx.train_step_errors(meta, arr, step, params, p0, masks)
         print(f"step {step}: loss {loss:.6f} ref {float(arr['loss'][step]):.6f} lr {lr_used[0]:.6g} -> {lr_after[0]:.6g} {e}")
         assert e["upd"] <= UPD_TOL and e["dn"] <= UPD_TOL, (step, e)
-        assert e["norm"] <= NORM_TOL and e.get("full", 0.0) <= FULL_TOL, (step, e)
+        assert e.get("full", 0.0) <= FULL_TOL, (step, e)
+        dn = arr[f"dn{step}"]
+        pns_bar = 1e-6 * amp[f"pns{step}"] + UPD_TOL * dn
+        pn_bar = 1e-6 * arr[f"pn{step}"] + UPD_TOL * dn + 2.0 * amp[f"noise{step}"]
+        assert (e["pns_abs"] <= pns_bar).all(), (step, meta["param_names"][int(np.argmax(e["pns_abs"] / pns_bar))])
+        assert (e["pn_abs"] <= pn_bar).all(), (step, meta["param_names"][int(np.argmax(e["pn_abs"] / pn_bar))])
+        worst["pn_ratio"] = max(worst["pn_ratio"], float((e["pn_abs"] / pn_bar).max()))
+        worst["pns_ratio"] = max(worst["pns_ratio"], float((e["pns_abs"] / pns_bar).max()))
         worst["upd"] = max(worst["upd"], e["upd"])
         worst["full"] = max(worst["full"], e.get("full", 0.0))
+        worst["norm"] = max(worst.get("norm", 0.0), e["norm"])
         if f"buf{step}" in arr:
             bufs = [b for k, b in m.named_buffers() if k.endswith(("running_mean", "running_var"))]
             got = torch.cat([b.detach().float().reshape(-1).cpu() for b in bufs])
@@ -88,4 +103,68 @@ def test_train_steps_match_reference(graphs, native):
         assert t.native_optimizer_fallbacks == 0
     fx.record("train_steps", fixture="train_steps_7m_b16", graphs=graphs, native_optimizer=native,
               loss_max_abs=worst["loss"], loss_tol=LOSS_TOL, update_rel_max=worst["upd"], update_tol=UPD_TOL,
-              param_full_max=worst["full"], param_tol=FULL_TOL)
+              param_full_max=worst["full"], param_tol=FULL_TOL, norm_rel_max=worst.get("norm", None),
+              norm_over_bar_max=worst["pn_ratio"], stable_norm_over_bar_max=worst["pns_ratio"])
+
+
+@pytest.mark.parametrize("graphs", [True, False], ids=["graph", "eager"])
+def test_train_steps_bf16_vs_reference_own_bf16(graphs):
+    """The BENCHMARKED precision: Trainer(amp_dtype=bf16) -- the bench's step, hipGraph replay and eager -- on
+    the fixture's five batches, against the reference's fp32 step (train_steps_7m_b16), with the bar = the
+    REFERENCE'S OWN bf16-autocast step's deviation from that fp32 step (train_steps_7m_b16_amp: its
+    train_one_epoch with use_amp=True, make_golden.py r5) on the same measure, x AMP_FACTOR (1.5: two
+    independent realisations of bf16 rounding noise).  Per applied step:
+      loss      |ours - fp32| <= max(1e-2 * max(1, |loss|) (north star bf16), 1.5 x the reference's own)
+      updates   median and RMS over parameters of the relative update-sketch error <= 1.5 x the reference's
+                (Adam's first steps are ~lr * sign(g): every sign that bf16 noise flips moves an element by
+                2 lr, so per-parameter errors of O(1) are what ANY bf16 step shows -- the reference's own
+                median is 0.59-0.91)
+      dn, norm, full   the max over parameters <= 1.5 x the reference's
+    and the skip / lr / schedule counter exactly."""
+    from ogv.train import Trainer
+    from src.Model_A_OutGridNet import MaxOutNet
+    from src.stage_config import StageCfg
+    meta, arr = fx.load("train_steps_7m_b16")
+    _, amp = fx.load("train_steps_7m_b16_amp")
+    m = MaxOutNet(meta["num_classes"], [StageCfg(**s) for s in meta["stages"]], 3, meta["stem_dim"], meta["dpr_max"])
+    gp.fill_module(m, meta["seed"])
+    m = m.to(DEV).to(memory_format=torch.channels_last).train()
+    params = dict(m.named_parameters())
+    p0 = {k: p.detach().clone() for k, p in params.items()}
+    masks = fx.train_stable_masks(meta, arr, params)
+    t = Trainer(m, lr=meta["lr"], weight_decay=meta["weight_decay"], clip=meta["clip"],
+                label_smoothing=meta["label_smoothing"], total_steps=meta["total_steps"],
+                warmup_ratio=meta["warmup_ratio"], min_lr=meta["min_lr"], amp_dtype=torch.bfloat16, graphs=graphs,
+                capture_warmup=1)
+    rms = lambda a: float(np.sqrt(np.mean(np.square(a))))
+    rows = []
+    for step, (x, y) in enumerate(fx.train_batches(meta)):
+        loss = float(t.step(x.to(DEV).contiguous(memory_format=torch.channels_last), y.to(DEV)))
+        torch.cuda.synchronize()
+        assert t.sched.step_num == int(arr["sched_step"][step])
+        skipped = bool(arr["skipped"][step])
+        assert bool(amp["amp_skipped"][step]) == skipped
+        assert (not np.isfinite(loss)) == skipped, (step, loss)
+        if skipped:
+            continue
+        e = fx.train_step_errors(meta, arr, step, params, p0, masks)
+        r = fx.amp_reference_errors(meta, arr, amp, step, params, masks)
+        live = arr[f"dn{step}"] > 0
+        row = dict(step=step, loss=abs(loss - float(arr["loss"][step])), loss_ref=r["loss"],
+                   upd_median=float(np.median(e["upd_all"][live])), upd_median_ref=float(np.median(r["upd_all"][live])),
+                   upd_rms=rms(e["upd_all"][live]), upd_rms_ref=rms(r["upd_all"][live]),
+                   dn=e["dn"], dn_ref=r["dn"], norm=e["norm"], norm_ref=r["norm"],
+                   full=e.get("full"), full_ref=r.get("full"))
+        print(row)
+        rows.append(row)
+        assert row["loss"] <= max(1e-2 * max(1.0, abs(float(arr["loss"][step]))), AMP_FACTOR * r["loss"]), row
+        for key in ("upd_median", "upd_rms"):
+            assert row[key] <= AMP_FACTOR * row[key + "_ref"], (key, row)
+        for key in ("dn", "norm", "full"):
+            if row[key] is not None:
+                assert row[key] <= AMP_FACTOR * row[key + "_ref"], (key, row)
+    assert t.nonfinite_steps == int(arr["skipped"].sum())
+    if graphs:
+        assert t._g is not None and t.eager_fallbacks == 0
+    fx.record("train_steps_bf16", fixture="train_steps_7m_b16 + train_steps_7m_b16_amp", graphs=graphs,
+              factor=AMP_FACTOR, steps=rows)

@@ -145,6 +145,8 @@ def test_train_steps_oracle():
     """The oracle's training loop (optimizer, warmup-cosine schedule, clip, non-finite skip) against
     the reference's own train_one_epoch run (fixture train_steps_7m_b16, make_golden.py r4)."""
     meta, arr = fx.load("train_steps_7m_b16")
+    _, amp = fx.load("train_steps_7m_b16_amp")
+    arr = dict(arr, **{k: v for k, v in amp.items() if k.startswith("pns")})
     shapes = orc.model_a_shapes(meta["stages"], meta["num_classes"], 3, meta["stem_dim"])
     p = orc.make_params(shapes, lambda k, s: gp.param_value(k, s, meta["seed"]))
     assert [k for k, t in p.items() if t.requires_grad] == meta["param_names"]
@@ -167,3 +169,48 @@ def test_train_steps_oracle():
         if not skipped:
             assert abs(loss - arr["loss"][t]) <= 1e-5, (t, loss)
         assert e["upd"] <= 1e-3 and e["dn"] <= 1e-3 and e["norm"] <= 1e-5 and e.get("full", 0.0) <= 1e-6, (t, e)
+        # the derived norm bars of tests/test_gpu_train_parity.py hold for two CPU fp32 implementations too
+        dn = arr[f"dn{t}"]
+        assert (e["pns_abs"] <= 1e-6 * amp[f"pns{t}"] + 2e-3 * dn).all(), t
+        assert (e["pn_abs"] <= 1e-6 * arr[f"pn{t}"] + 2e-3 * dn + 2.0 * amp[f"noise{t}"]).all(), t
+
+
+def test_train_steps_amp_fixture():
+    """The bf16 step fixture (make_golden.py r5: the reference's train_one_epoch with use_amp=True) against the
+    oracle's training loop under the same CPU bf16 autocast: the same skip / schedule, the first loss to 1e-5
+    (same weights, same autocast ops; measured equal), later losses within the bf16 bar 1e-2 * max(1, |loss|)
+    (two bf16 runs drift apart after the first Adam step: measured 1.1e-3 and 5.3e-3), and
+    the oracle's own bf16-vs-fp32 update deviation of the same size as the reference's (it restates the same
+    ops, so both are the one autocast run up to summation order) -- the fixture the GPU bf16 step test
+    (tests/test_gpu_train_parity.py) takes its bars from is pinned by a second implementation."""
+    meta, arr = fx.load("train_steps_7m_b16")
+    mamp, amp = fx.load("train_steps_7m_b16_amp")
+    assert mamp["base"] == "train_steps_7m_b16" and mamp["param_names"] == meta["param_names"]
+    shapes = orc.model_a_shapes(meta["stages"], meta["num_classes"], 3, meta["stem_dim"])
+    p = orc.make_params(shapes, lambda k, s: gp.param_value(k, s, meta["seed"]))
+    params = {k: p[k] for k in meta["param_names"]}
+    p0 = {k: t.detach().clone() for k, t in params.items()}
+    masks = fx.train_stable_masks(meta, arr, params)
+    rec = []
+
+    def on_step(t, loss, lr_used, skipped, step_num):
+        if skipped:
+            rec.append((t, float(loss), skipped, step_num, None, None))
+            return
+        e = fx.train_step_errors(meta, arr, t, params, p0, masks)
+        r = fx.amp_reference_errors(meta, arr, amp, t, params, masks)
+        rec.append((t, float(loss), skipped, step_num, e, r))
+
+    orc.train_steps(fx.train_batches(meta), p, meta["stages"], lr=meta["lr"], weight_decay=meta["weight_decay"],
+                    clip=meta["clip"], label_smoothing=meta["label_smoothing"], total_steps=meta["total_steps"],
+                    warmup_steps=int(meta["total_steps"] * meta["warmup_ratio"]), min_lr=meta["min_lr"],
+                    on_step=on_step, autocast=True)
+    for t, loss, skipped, step_num, e, r in rec:
+        assert skipped == bool(amp["amp_skipped"][t]) and step_num == amp["amp_sched_step"][t]
+        if skipped:
+            continue
+        live = arr[f"dn{t}"] > 0
+        med, med_ref = np.median(e["upd_all"][live]), np.median(r["upd_all"][live])
+        print(t, loss, float(amp["amp_loss"][t]), med, med_ref, e["dn"], r["dn"])
+        assert abs(loss - float(amp["amp_loss"][t])) <= (1e-5 if t == 0 else 1e-2 * max(1.0, abs(loss))), (t, loss)
+        assert 0.5 * med_ref <= med <= 1.5 * med_ref, (t, med, med_ref)

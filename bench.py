@@ -58,7 +58,10 @@ def parse():
                     help="take the data-parallel path (process group, broadcast, per-step gradient all_reduce) at "
                          "N=1 too: a world-size-1 RCCL ('nccl') group on one GPU")
     ap.add_argument("--dp-capture", action="store_true",
-                    help="graph mode with DP: capture the RCCL all_reduce inside the step's graph")
+                    help="graph mode with DP: capture ONE flat RCCL all_reduce at the end of the step's graph")
+    ap.add_argument("--dp-flat", action="store_true",
+                    help="graph mode with DP: graph A -> one flat all_reduce -> graph B instead of the default "
+                         "bucketed all_reduces captured on a side stream during backward")
     ap.add_argument("--step-roofline", type=int, default=1,
                     help="1: time every C-ABI op of one eager step (after the timed region) for roofline.step")
     return ap.parse_args()
@@ -291,7 +294,7 @@ def main():
     model = model.to(device).to(memory_format=torch.channels_last)
     trainer = Trainer(model, total_steps=max(100, args.steps + args.warmup + 1), graphs=not args.eager,
                       capture_warmup=max(0, args.warmup - 1), force_dp=args.force_dp,
-                      dp_capture_collective=args.dp_capture)
+                      dp_capture_collective=args.dp_capture, dp_overlap=not args.dp_flat)
 
     B, S = args.batch, cfg["img"]
     g = torch.Generator(device=device).manual_seed(7 + rank)
@@ -390,7 +393,11 @@ def main():
                        "per_gpu_batch": B, "global_batch": B * world, "parallelism": f"dp{world}",
                        "execution": "hipGraph replay" if trainer.graphs else "eager launches",
                        "backend": trainer.backend or "none (single process, no collective)",
-                       "dp_collective": (None if not trainer.dp else "all_reduce captured in the step graph"
+                       "dp_collective": (None if not trainer.dp else
+                                         f"{len(trainer._gbuckets)} bucketed all_reduces captured in the step graph on a "
+                                         "side stream, each launched as backward completes its bucket"
+                                         if getattr(trainer, "dp_overlap", False) and hasattr(trainer, "_gbuckets") else
+                                         "all_reduce captured in the step graph"
                                          if trainer.dp_capture_collective else
                                          "one flat all_reduce between graph A and graph B" if trainer.graphs else
                                          "bucketed async all_reduce during backward")},

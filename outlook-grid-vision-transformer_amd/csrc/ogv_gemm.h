@@ -231,6 +231,8 @@ void set_vp_tile(int v);
 void set_vp_big(int v);
 void set_vp_head(int v);
 void set_vph_rows(int v);
+void set_vph_wgs(int v);
+void set_vph_dbg(int v);
 // Squeeze-Excite GEMVs (ogv_se.hip); knob "se_gemv" (1 default, 0 = the split-K tiled GEMM + reduce)
 void se_gemv_launch(const float* in, int ldi, int pro_act, const float* W, int ldw, const float* bias,
                     const float* Z, int ldz, int zact, float* out, int ldo, float* sig_out, int B, int N, int K,

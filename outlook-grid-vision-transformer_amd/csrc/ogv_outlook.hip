@@ -1947,7 +1947,7 @@ static size_t vhead_lds(const VHead& t, bool sw) {
 template <int NJV, int NK, int NF, bool SW>
 __global__ __launch_bounds__(256, 2) void outlook_vproj_head_fwd_kernel(
     const bf16* __restrict__ x, int ldx, const float* __restrict__ Wc, const float* __restrict__ bias,
-    bf16* __restrict__ cat, int ldc, bf16* __restrict__ y, int B, int H, int W, int C, int heads, VHead t) {
+    bf16* __restrict__ cat, int ldc, bf16* __restrict__ y, int B, int H, int W, int C, int heads, VHead t, int dbg) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NJ = NJV + 1, NCOL = NJ * 16, KP = NK * 32, HD = NJV * 16, HD8 = HD / 8;
   const int WP = t.WP, RP = t.RP, R = t.R, HW = H * W;
@@ -1959,25 +1959,6 @@ __global__ __launch_bounds__(256, 2) void outlook_vproj_head_fwd_kernel(
   const int fr = lane & 15, fg = lane >> 4;
   const int head = (blockIdx.x >> 3) % heads;
   const int rg = (blockIdx.x & 7) + 8 * (int)(blockIdx.x / (8 * heads));
-  // weight slice of this head: slab row n < HD <- Wc[head*HD + n] (v), HD <= n < HD + 9 <-
-  // Wc[C + 9 head + n - HD] (logits), zero rows above; columns >= C zero
-  for (int idx = tid; idx < NCOL * (KP / 4); idx += 256) {
-    const int n = idx / (KP / 4), k = (idx - n * (KP / 4)) * 4;
-    const int row = n < HD ? head * HD + n : (n < HD + 9 ? C + 9 * head + n - HD : -1);
-    float4 w4 = float4{0.f, 0.f, 0.f, 0.f};
-    if (row >= 0 && k < C) w4 = *reinterpret_cast<const float4*>(Wc + (long)row * C + k);
-    const bf16x4 h = {(bf16)w4.x, (bf16)w4.y, (bf16)w4.z, (bf16)w4.w};
-    *reinterpret_cast<bf16x4*>(ws + n * WP + k) = h;
-    if constexpr (SW) {
-      const bf16x4 l = {(bf16)(w4.x - (float)h[0]), (bf16)(w4.y - (float)h[1]), (bf16)(w4.z - (float)h[2]),
-                        (bf16)(w4.w - (float)h[3])};
-      *reinterpret_cast<bf16x4*>(ws + (NCOL + n) * WP + k) = l;
-    }
-  }
-  for (int n = tid; n < NCOL; n += 256) {
-    const int row = n < HD ? head * HD + n : (n < HD + 9 ? C + 9 * head + n - HD : -1);
-    bs[n] = (bias && row >= 0) ? bias[row] : 0.f;
-  }
   // panel-local row r -> global row (or -1: a pad row of an image, or an image past B)
   auto grow_of = [&](int p, int r) -> long {
     const int i = fdiv(r, t.fRI), pix = r - i * t.RI;
@@ -1987,6 +1968,7 @@ __global__ __launch_bounds__(256, 2) void outlook_vproj_head_fwd_kernel(
   const int NFR = R / 16;   // row fragments per panel; wave w owns fragments w, w + 4, ...
   bf16x8 xf[NF][NK];
   auto load_x = [&](int p) {
+    if (dbg & 16) return;
 #pragma unroll
     for (int q = 0; q < NF; ++q) {
       const int f = wave + 4 * q;
@@ -1999,7 +1981,39 @@ __global__ __launch_bounds__(256, 2) void outlook_vproj_head_fwd_kernel(
       }
     }
   };
-  if (rg < t.npanels) load_x(rg);
+  if (rg < t.npanels) load_x(rg);   // the first panel's x in flight while the weights are staged
+  // weight slice of this head: slab row n < HD <- Wc[head*HD + n] (v), HD <= n < HD + 9 <-
+  // Wc[C + 9 head + n - HD] (logits), zero rows above; columns >= C zero
+  // (every load of the slice issued before the first conversion: one memory round trip)
+  constexpr int WPT = (NCOL * (KP / 4) + 255) / 256;
+  float4 wv[WPT];
+#pragma unroll
+  for (int u = 0; u < WPT; ++u) {
+    const int idx = tid + u * 256;
+    const int n = idx / (KP / 4), k = (idx - n * (KP / 4)) * 4;
+    const int row = n < HD ? head * HD + n : (n < HD + 9 ? C + 9 * head + n - HD : -1);
+    const bool ok = idx < NCOL * (KP / 4) && row >= 0 && k < C;
+    const float4 w4 = *reinterpret_cast<const float4*>(Wc + (ok ? (long)row * C + k : 0L));   // clamped address
+    wv[u] = ok ? w4 : float4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int u = 0; u < WPT; ++u) {
+    const int idx = tid + u * 256;
+    if (idx >= NCOL * (KP / 4)) break;
+    const int n = idx / (KP / 4), k = (idx - n * (KP / 4)) * 4;
+    const float4 w4 = wv[u];
+    const bf16x4 h = {(bf16)w4.x, (bf16)w4.y, (bf16)w4.z, (bf16)w4.w};
+    *reinterpret_cast<bf16x4*>(ws + n * WP + k) = h;
+    if constexpr (SW) {
+      const bf16x4 l = {(bf16)(w4.x - (float)h[0]), (bf16)(w4.y - (float)h[1]), (bf16)(w4.z - (float)h[2]),
+                        (bf16)(w4.w - (float)h[3])};
+      *reinterpret_cast<bf16x4*>(ws + (NCOL + n) * WP + k) = l;
+    }
+  }
+  for (int n = tid; n < NCOL; n += 256) {
+    const int row = n < HD ? head * HD + n : (n < HD + 9 ? C + 9 * head + n - HD : -1);
+    bs[n] = (bias && row >= 0) ? bias[row] : 0.f;
+  }
   for (int p = rg; p < t.npanels; p += t.RG) {
     // 1. [v_h | logits_h] of the panel's rows on MFMA
     f32x4 acc[NF][NJ];
@@ -2009,7 +2023,7 @@ __global__ __launch_bounds__(256, 2) void outlook_vproj_head_fwd_kernel(
       for (int j = 0; j < NJ; ++j) acc[q][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     __syncthreads();   // weights staged (first panel) / the previous panel's gather is done with rs and P
 #pragma unroll
-    for (int kt = 0; kt < NK; ++kt)
+    for (int kt = 0; kt < ((dbg & 8) ? 0 : NK); ++kt)
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const bf16x8 wh = *reinterpret_cast<const bf16x8*>(ws + (j * 16 + fr) * WP + kt * 32 + fg * 8);
@@ -2040,13 +2054,13 @@ __global__ __launch_bounds__(256, 2) void outlook_vproj_head_fwd_kernel(
     __syncthreads();
     // 2a. the head's columns of cat (training): v_h as 16-B rows, the 9 logits as bf16 elements
     if (cat) {
-      for (int idx = tid; idx < R * HD8; idx += 256) {
+      for (int idx = tid; idx < ((dbg & 2) ? 0 : R * HD8); idx += 256) {
         const int r = idx / HD8, c8 = idx - r * HD8;
         const long g = grow_of(p, r);
         if (g >= 0)
           *reinterpret_cast<uint4*>(cat + g * ldc + head * HD + c8 * 8) = *reinterpret_cast<const uint4*>(rs + r * RP + c8 * 8);
       }
-      for (int idx = tid; idx < R * 9; idx += 256) {
+      for (int idx = tid; idx < ((dbg & 1) ? 0 : R * 9); idx += 256) {
         const int r = idx / 9, jj = idx - r * 9;
         const long g = grow_of(p, r);
         if (g >= 0) cat[g * ldc + C + 9 * head + jj] = rs[r * RP + HD + jj];
@@ -2080,7 +2094,7 @@ __global__ __launch_bounds__(256, 2) void outlook_vproj_head_fwd_kernel(
     }
     __syncthreads();
     // 3. y[:, head] = 3 x 3 gather of v_h weighted by the softmax (out-of-image neighbours: v = 0)
-    for (int idx = tid; idx < R * HD8; idx += 256) {
+    for (int idx = tid; idx < ((dbg & 4) ? 0 : R * HD8); idx += 256) {
       const int r = idx / HD8, cc = idx - r * HD8;
       const long g = grow_of(p, r);
       if (g < 0) continue;
@@ -2107,32 +2121,44 @@ __global__ __launch_bounds__(256, 2) void outlook_vproj_head_fwd_kernel(
 }
 
 // knob "vp_head" (default 1): the per-head whole-image kernel above for the wide stages it plans;
-// "vph_rows": target rows per panel (64 default; a panel is whole images, <= 128 rows)
+// "vph_rows": target rows per panel (a panel is whole images, <= 128 rows)
+// (2: also head_dim 64 -- 14M / 22M stage 3 -- whose 125 KB weight slice leaves one workgroup per CU:
+// measured slower than the unfused pair there, 86 vs 48 us at 14M stage 3, profiles/r05b_vph.log)
 static int g_vp_head = 1;
-void set_vp_head(int v) { g_vp_head = v ? 1 : 0; }
-static int g_vph_rows = 64;
-void set_vph_rows(int v) { g_vph_rows = v < 16 ? 16 : (v > 128 ? 128 : v); }
+void set_vp_head(int v) { g_vp_head = v < 0 ? 0 : (v > 2 ? 2 : v); }
+// (0 = auto: 128 for images of <= 32 pixels, 64 otherwise -- measured, tools/bench_vproj.py cold L2,
+// profiles/r05c_vph.log: 7M stage 3 (4 x 4) 21.2 -> 19.4 us at 128 rows, stage 2 (8 x 8) 34.6 vs 41.9 us at 64)
+static int g_vph_rows = 0;
+void set_vph_rows(int v) { g_vph_rows = v <= 0 ? 0 : (v < 16 ? 16 : (v > 128 ? 128 : v)); }
+// "vph_wgs": workgroups per CU the grid is sized for (default 3, as many as the LDS allows below that); "vph_dbg" (timing only, wrong results):
+// skip 1 the cat logit stores, 2 the cat v stores, 4 the gather, 8 the MFMAs, 16 the x loads
+static int g_vph_wgs = 3;
+void set_vph_wgs(int v) { g_vph_wgs = v < 1 ? 1 : (v > 8 ? 8 : v); }
+static int g_vph_dbg = 0;
+void set_vph_dbg(int v) { g_vph_dbg = v; }
 
 static bool vhead_plan(int B, int H, int W, int C, int heads, int k, int ldc, ogv_dtype dt, VHead& t) {
   if (!g_outlook_vproj || !g_vp_head) return false;
   if (dt != OGV_BF16 || k != 3 || B <= 0 || H <= 0 || W <= 0 || heads <= 0) return false;
   if (C % 32 != 0 || !vbig_cj(C / 32) || C % heads != 0) return false;   // C in {128, 192, 256, 384}
   const int hd = C / heads;
-  if (hd != 32 && hd != 64) return false;
+  if (hd != 32 && !(hd == 64 && g_vp_head == 2)) return false;
   if (ldc != (C + heads * 9 + 7) / 8 * 8) return false;
   const int HW = H * W;
   t = VHead{};
   t.RI = (HW + 15) / 16 * 16;
   if (t.RI > 128) return false;
-  t.IPP = g_vph_rows / t.RI < 1 ? 1 : g_vph_rows / t.RI;
+  const int rows = g_vph_rows ? g_vph_rows : (t.RI <= 32 ? 128 : 64);
+  t.IPP = rows / t.RI < 1 ? 1 : rows / t.RI;
   t.R = t.IPP * t.RI;
   t.npanels = (B + t.IPP - 1) / t.IPP;
   const int NCOL = hd + 16, KP = C;
   t.WP = KP + 8;      // (KP + 8) / 2 dwords per row: 16 fragment rows on distinct bank quads
   t.RP = NCOL + 8;
   const size_t lds = (hd == 32 ? vhead_lds<2, 4> : vhead_lds<4, 4>)(t, true);
-  const int per_cu = lds <= 80 * 1024 ? 2 : 1;
   if (lds > 160 * 1024) return false;
+  const int fit = (int)((160 * 1024) / lds);
+  const int per_cu = g_vph_wgs < fit ? g_vph_wgs : fit;
   int rg = (256 * per_cu / heads) / 8 * 8;
   const int np8 = (t.npanels + 7) / 8 * 8;
   t.RG = rg < 8 ? 8 : (rg > np8 ? np8 : rg);
@@ -2150,7 +2176,7 @@ static void vhead_run(const bf16* x, int ldx, const float* Wc, const float* bias
   if (lds > 64 * 1024)
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
-  kern<<<(unsigned)(t.RG * heads), 256, lds, s>>>(x, ldx, Wc, bias, cat, ldc, y, B, H, W, C, heads, t);
+  kern<<<(unsigned)(t.RG * heads), 256, lds, s>>>(x, ldx, Wc, bias, cat, ldc, y, B, H, W, C, heads, t, g_vph_dbg);
 }
 
 static bool vproj_bwd_plan(int B, int H, int W, int C, int heads, int k, int ldc, ogv_dtype dt, VTile& t, int& nw) {

@@ -224,6 +224,14 @@ extern "C" int ogv_set_option(const char* name, int value) {
     set_vp_head(value);
     return OGV_OK;
   }
+  if (!strcmp(name, "vph_wgs")) {
+    set_vph_wgs(value);
+    return OGV_OK;
+  }
+  if (!strcmp(name, "vph_dbg")) {
+    set_vph_dbg(value);
+    return OGV_OK;
+  }
   if (!strcmp(name, "vph_rows")) {
     set_vph_rows(value);
     return OGV_OK;

@@ -137,6 +137,14 @@ class deferred_param_reductions:
         return False
 
 
+def flush_deferred_reductions():
+    """Run the parameter-gradient reductions recorded so far (deferral stays on for the rest of the
+    backward): the gradients of every parameter whose AccumulateGrad already ran are final after this.
+    The graph-mode DP buckets call it when a bucket's last gradient is in (Trainer(dp_overlap))."""
+    if _DEFER["on"]:
+        check(_lib.load().ogv_reduce_flush(_stream()), "ogv_reduce_flush")
+
+
 _warned_fp16 = False
 
 # ------------------------------------------------------------------------------------------------

@@ -305,7 +305,8 @@ class Trainer:
                  total_steps=10_000, warmup_ratio=0.05, min_lr=1e-6, amp_dtype: Optional[torch.dtype] = torch.bfloat16,
                  graphs: bool = False, capture_warmup: int = 3, capture_hook=None, bucket_mb: float = 8.0,
                  broadcast_buffers: bool = True, defer_reductions: bool = True, native_optimizer: bool = True,
-                 force_dp: bool = False, dp_capture_collective: bool = False, label_check_every: int = 100):
+                 force_dp: bool = False, dp_capture_collective: bool = False, label_check_every: int = 100,
+                 dp_overlap: Optional[bool] = None):
         self.model = model
         core = model.module if hasattr(model, "module") else model
         self.core = core
@@ -361,6 +362,15 @@ class Trainer:
         # graph mode: the all_reduce captured INSIDE the step's one graph (RCCL collectives are
         # capturable; gloo's are host work and never are) instead of graph A -> all_reduce -> graph B
         self.dp_capture_collective = bool(dp_capture_collective) and self.dp and self.backend == "nccl"
+        # graph mode on RCCL (default): the gradients are all-reduced in ~bucket_mb buckets INSIDE the step's
+        # one graph, each on a side stream as soon as backward has produced its last gradient, overlapping
+        # the rest of the backward; the optimizer reads the reduced gradients where the collectives left
+        # them (no unflatten).  Needs the Linear weight-gradient fork off (OGV_FORK=0, the default): the
+        # bucket's deferred reductions are flushed on the main stream when it completes.
+        from .functional import _FORK
+        self.dp_overlap = (self.dp and self.graphs and self.backend == "nccl" and not self.dp_capture_collective
+                           and not _FORK and (dp_overlap is None or bool(dp_overlap)))
+        self._bucket_mb = float(bucket_mb) if bucket_mb and bucket_mb > 0 else 8.0
         self._warned_fallback = False
         if self.dp:
             with torch.no_grad():   # identical start on every rank (what DDP's constructor does)
@@ -482,7 +492,9 @@ class Trainer:
         device: batched native copies of every dense fp32 tensor straight from its storage (a dense
         tensor's bytes are its elements in memory order, channels_last included: the unflatten writes
         them back the same way), torch.cat otherwise."""
-        if self.device_side and all(self._dense_fp32(p.grad) or p.grad is None for p in self.params) \
+        # (native copies only when every gradient is laid out like its parameter: the unflatten -- or a rank
+        # whose gradient is None, unflattened into empty_like(p) -- then reads the bytes back in the same order)
+        if self.device_side and all(p.grad is None or _dense_like(p.grad, p) for p in self.params) \
                 and all(self._dense_fp32(b) for b in self._bufs):
             base, esz = self.flat.data_ptr(), 4
             offs = self._flat_offsets()
@@ -511,7 +523,7 @@ class Trainer:
         for p in self.params:
             if p.grad is None:
                 p.grad = torch.empty_like(p)
-        if self.device_side and all(self._dense_fp32(p.grad) for p in self.params) \
+        if self.device_side and all(_dense_like(p.grad, p) for p in self.params) \
                 and all(self._dense_fp32(b) for b in self._bufs):
             base, esz = self.flat.data_ptr(), 4
             offs = self._flat_offsets()
@@ -622,6 +634,122 @@ class Trainer:
     def _allreduce(self):
         torch.distributed.all_reduce(self.flat)
 
+    # -- graph mode on RCCL: bucketed collectives captured on a side stream, overlapping backward ------
+    def _overlap_setup(self, dev):
+        """Buckets of ~bucket_mb in reverse registration order (~ the order backward finishes them) laid
+        out back to back in self.gflat, then [rank 0's buffers | non-finite flag]; per parameter a view of
+        its slot with the parameter's strides (what the optimizer reads after the collectives)."""
+        cap = int(self._bucket_mb * 2 ** 20) // 4
+        order = list(range(len(self.params)))[::-1]
+        self._gbuckets, cur, n = [], [], 0
+        for i in order:
+            if cur and n + self._sizes[i] > cap:
+                self._gbuckets.append(cur)
+                cur, n = [], 0
+            cur.append(i)
+            n += self._sizes[i]
+        if cur:
+            self._gbuckets.append(cur)
+        # every slot starts on a 256-B boundary, as the allocator's own gradient tensors do (the native
+        # optimizer takes its float4 path on 16-B aligned tensors: the same arithmetic as without DP)
+        al = lambda v: (v + 63) // 64 * 64  # noqa: E731
+        self._goff, self._gbrange, o = [0] * len(self.params), [], 0
+        self._gbucket_of = {}
+        for bi, b in enumerate(self._gbuckets):
+            o0 = o
+            for i in b:
+                self._goff[i] = o
+                self._gbucket_of[i] = bi
+                o = al(o + self._sizes[i])
+            self._gbrange.append((o0, o))
+        self._gng = o                        # gradient part incl. alignment padding (zeros)
+        self.gflat = torch.zeros(self._gng + self._nb + 1, device=dev, dtype=torch.float32)
+        self._gviews = [torch.as_strided(self.gflat, p.shape, p.stride(), self._goff[i])
+                        for i, p in enumerate(self.params)]
+        self._gside = torch.cuda.Stream(device=dev)
+
+    def _overlap_launch(self, segs, lo, hi, scale):
+        """On the side stream (joined into the capture): pack segs into gflat[lo:hi] (x scale), then
+        all_reduce that slice."""
+        cur = torch.cuda.current_stream()
+        self._gside.wait_stream(cur)
+        with torch.cuda.stream(self._gside):
+            self._copy_segments(segs, scale)
+            torch.distributed.all_reduce(self.gflat[lo:hi])
+
+    def _overlap_bucket(self, bi):
+        base = self.gflat.data_ptr()
+        segs = [(self.params[i].grad.data_ptr() if self.params[i].grad is not None else None, base + 4 * self._goff[i],
+                 self._sizes[i]) for i in self._gbuckets[bi]]
+        for i in self._gbuckets[bi]:
+            g = self.params[i].grad
+            if g is not None:
+                if not _dense_like(g, self.params[i]):
+                    raise RuntimeError(f"Trainer(dp_overlap): gradient of parameter {i} is not laid out like the "
+                                       f"parameter (strides {tuple(g.stride())} vs {tuple(self.params[i].stride())})")
+                self._glocal.append(g)          # the graph keeps reading it: hold it past the capture
+        self._gdone[bi] = True
+        lo, hi = self._gbrange[bi]
+        self._overlap_launch(segs, lo, hi, 1.0 / self.world)
+
+    def _overlap_ready(self, p):
+        i = self._pidx[p]
+        bi = self._gbucket_of[i]
+        self._gseen[bi].add(i)                  # (a set: a parameter used twice fires twice)
+        if len(self._gseen[bi]) == len(self._gbuckets[bi]) and not self._gdone[bi]:
+            from .functional import flush_deferred_reductions
+            flush_deferred_reductions()         # this bucket's parameter gradients are final from here on
+            self._overlap_bucket(bi)
+
+    def _fwd_bwd_overlap(self, x, y):
+        """_fwd_bwd with the gradient buckets all-reduced as backward completes them (graph capture only)."""
+        dev = self._found.device
+        if getattr(self, "gflat", None) is None:
+            self._overlap_setup(dev)
+        self._pidx = {p: i for i, p in enumerate(self.params)}
+        self._gseen = [set() for _ in self._gbuckets]
+        self._gdone = [False] * len(self._gbuckets)
+        self._glocal = []
+        loss, flagged = self._loss(x, y)
+        if not flagged:
+            self._flag(loss.detach(), 0)
+        # [rank 0's BatchNorm buffers (final after the forward) | non-finite flag]: launched right away
+        base = self.gflat.data_ptr() + 4 * self._gng
+        boffs = [0]
+        for n in self._bsizes:
+            boffs.append(boffs[-1] + n)
+        msegs = [(b.data_ptr() if self.rank == 0 else None, base + 4 * o, n)
+                 for b, o, n in zip(self._bufs, boffs, self._bsizes)]
+        msegs.append((self._found.data_ptr(), base + 4 * self._nb, 1))
+        self._overlap_launch(msegs, self._gng, self._gng + self._nb + 1, 1.0)
+        hooks = [p.register_post_accumulate_grad_hook(self._overlap_ready) for p in self.params]
+        from .functional import deferred_param_reductions
+        try:
+            with deferred_param_reductions(self.defer_reductions):
+                loss.backward()
+        finally:
+            for h in hooks:
+                h.remove()
+        for bi in range(len(self._gbuckets)):      # parameters that got no gradient: their slots are zeroed
+            if not self._gdone[bi]:
+                self._overlap_bucket(bi)
+        torch.cuda.current_stream().wait_stream(self._gside)
+        return loss.detach()
+
+    def _overlap_finish(self):
+        """After the collectives: every parameter's .grad is its view of the reduced buffer (the optimizer,
+        clip and the caller read the all-reduced gradients there), rank 0's buffers copied back; returns the
+        all-reduced non-finite count."""
+        for p, v in zip(self.params, self._gviews):
+            p.grad = v
+        base = self.gflat.data_ptr() + 4 * self._gng
+        segs, o = [], 0
+        for b, n in zip(self._bufs, self._bsizes):
+            segs.append((base + 4 * o, b.data_ptr(), n))
+            o += n
+        self._copy_segments(segs)
+        return self.gflat[self._gng + self._nb:]
+
     def _eager(self, x, y):
         self.opt.zero_grad(set_to_none=True)
         if self.dp and self._buckets:
@@ -664,6 +792,12 @@ class Trainer:
         # thread captures; under the default "global" capture mode that poll is a capture-unsupported
         # call from another thread (hipErrorStreamCaptureUnsupported -> abort), so capture thread-locally
         mode = "thread_local" if self.backend == "nccl" else "global"
+        if self.dp_overlap:
+            with torch.cuda.graph(self._g, pool=pool, capture_error_mode=mode):
+                self._loss_static = self._fwd_bwd_overlap(self._x, self._y)
+                self._update(self._overlap_finish())
+            self.graph_grads = [p.grad for p in self.params]   # views of the reduced-gradient buffer
+            return loss
         with torch.cuda.graph(self._g, pool=pool, capture_error_mode=mode):
             self._loss_static = self._fwd_bwd(self._x, self._y)
             if self.dp:
@@ -716,7 +850,7 @@ class Trainer:
         self._x.copy_(x)
         self._y.copy_(y)
         self._g.replay()
-        if self.dp and not self.dp_capture_collective:
+        if self.dp and not self.dp_capture_collective and not self.dp_overlap:
             self._allreduce()
             self._g2.replay()
         return self._loss_static.clone()

@@ -32,20 +32,24 @@ def main():
         batches.append((torch.randn(16, 3, 32, 32, device="cuda", generator=g).contiguous(memory_format=torch.channels_last),
                         torch.randint(0, 100, (16,), device="cuda", generator=g)))
     runs = {}
-    for mode in ("plain", "dp_graph", "dp_capture", "plain_eager", "dp_eager"):
+    for mode in ("plain", "dp_graph", "dp_graph_flat", "dp_capture", "plain_eager", "dp_eager"):
         torch.backends.cudnn.benchmark = False
         torch.manual_seed(31)
         m = build_model(dict(type="model_a", num_classes=100, stem_dim=64, dpr_max=0.0, stages=cfg["stages"]))
         m = m.cuda().to(memory_format=torch.channels_last)
         dp = mode.startswith("dp")
         t = Trainer(m, total_steps=50, warmup_ratio=0.1, graphs=not mode.endswith("eager"), capture_warmup=1,
-                    force_dp=dp, dp_capture_collective=mode == "dp_capture")
+                    force_dp=dp, dp_capture_collective=mode == "dp_capture", dp_overlap=mode != "dp_graph_flat")
         assert t.dp == dp and t.dp_capture_collective == (mode == "dp_capture")
+        assert t.dp_overlap == (mode == "dp_graph"), (mode, t.dp_overlap)
         losses = [t.step(*b).float().item() for b in batches]     # eager, capture, replay, replay
         torch.cuda.synchronize()
         state = [p.detach().clone() for p in m.parameters()] + [b.detach().clone() for b in m.buffers()]
         runs[mode] = (losses, state)
-        out = {"mode": mode, "backend": t.backend, "losses": losses, "graphs": t.graphs}
+        out = {"mode": mode, "backend": t.backend, "losses": losses, "graphs": t.graphs, "dp_overlap": t.dp_overlap}
+        if t.dp_overlap:     # the reduced gradients the optimizer read are the parameters' .grad
+            out["buckets"] = len(t._gbuckets)
+            out["grad_is_view"] = all(p.grad.data_ptr() == v.data_ptr() for p, v in zip(t.params, t._gviews))
         for ref in ("plain", "plain_eager"):
             if ref in runs and ref != mode:
                 out["max_param_diff_vs_" + ref] = max(float((a.double() - b.double()).abs().max())

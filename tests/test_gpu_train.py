@@ -503,8 +503,9 @@ def _free_port():
 def test_rccl_world1_dp_path_matches_single_process():
     """The RCCL branch executed: a world-size-1 "nccl" (= RCCL) process group, the Trainer's data-parallel
     path forced on (force_dp: rank-0 broadcast, gradient + buffer + non-finite-flag bucket, all_reduce), in
-    graph mode (graph A -> RCCL all_reduce -> graph B), with the all_reduce captured inside the step's graph
-    (dp_capture_collective), and eagerly with the bucketed asynchronous all_reduces during backward: every
+    graph mode with the bucketed all_reduces captured on a side stream as backward completes each bucket
+    (dp_overlap, the RCCL default), with the flat path (graph A -> RCCL all_reduce -> graph B), with the
+    all_reduce captured at the end of the step's graph (dp_capture_collective), and eagerly with the bucketed asynchronous all_reduces during backward: every
     loss and parameter equals the single-process Trainer's (the all_reduce of one rank is the identity; the
     eager bucket path runs its parameter-gradient reductions immediately instead of deferred, so it is held
     to one lr step per element, Adam's sign flips of near-zero gradients).  Runs tests/_rccl_world1.py as a
@@ -518,10 +519,12 @@ def test_rccl_world1_dp_path_matches_single_process():
     print(r.stdout[-4000:], r.stderr[-4000:])
     lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
     res = {d["mode"]: d for d in lines if "mode" in d}
-    assert set(res) >= {"plain", "dp_graph", "dp_capture", "plain_eager", "dp_eager"}, (r.returncode, list(res))
-    for mode in ("dp_graph", "dp_capture", "dp_eager"):
+    assert set(res) >= {"plain", "dp_graph", "dp_graph_flat", "dp_capture", "plain_eager", "dp_eager"}, \
+        (r.returncode, list(res))
+    for mode in ("dp_graph", "dp_graph_flat", "dp_capture", "dp_eager"):
         assert res[mode]["backend"] == "nccl", res[mode]
-    for mode, ref in (("dp_graph", "plain"), ("dp_capture", "plain")):
+    assert res["dp_graph"]["dp_overlap"] and res["dp_graph"]["buckets"] >= 2 and res["dp_graph"]["grad_is_view"]
+    for mode, ref in (("dp_graph", "plain"), ("dp_graph_flat", "plain"), ("dp_capture", "plain")):
         assert res[mode]["losses"] == res[ref]["losses"], (mode, res[mode]["losses"], res[ref]["losses"])
         assert res[mode]["max_param_diff_vs_" + ref] == 0.0, res[mode]
     la, lb = res["dp_eager"]["losses"], res["plain_eager"]["losses"]

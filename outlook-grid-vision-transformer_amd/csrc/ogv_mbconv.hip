@@ -248,6 +248,10 @@ void set_dw_fwd_r(int v) { g_dw_fwd_r = v == 4 ? 4 : 8; }
 // per block chosen for ~32 output rows per block (many short blocks balance best over the CUs)
 static int g_dw_blocks = 0;
 void set_dw_blocks(int v) { g_dw_blocks = v > 0 ? v : 0; }
+// knob "dw_tw": the column strip width (pixels, 8 / 16 / 32; default 32): a narrower strip widens the
+// channel tile (~256 (pixel, 4-channel) items per row), i.e. more contiguous bytes per pixel per load
+static int g_dw_tw = 32;
+void set_dw_tw(int v) { g_dw_tw = v <= 8 ? 8 : (v <= 16 ? 16 : 32); }
 struct DwTile {
   int B, H, W, C, TW, ncolt, chunks, CT, nct, PP, ldq, G, ngroups;
   __host__ __device__ long rows() const { return (long)ngroups * ncolt; }
@@ -262,7 +266,7 @@ struct DwTile {
 static DwTile dw_tile_plan(int B, int H, int W, int C, int V) {
   DwTile t;
   t.B = B; t.H = H; t.W = W; t.C = C;
-  t.TW = W < 32 ? W : 32;
+  t.TW = W < g_dw_tw ? W : g_dw_tw;
   t.ncolt = (W + t.TW - 1) / t.TW;
   int ch = 1;
   while (ch * 2 * t.TW <= 256 && ch < 64) ch *= 2;            // ~256 items per output row

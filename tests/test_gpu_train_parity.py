@@ -85,8 +85,9 @@ def test_train_steps_match_reference(graphs, native):
         pn_bar = 1e-6 * arr[f"pn{step}"] + UPD_TOL * dn + 2.0 * amp[f"noise{step}"]
         assert (e["pns_abs"] <= pns_bar).all(), (step, meta["param_names"][int(np.argmax(e["pns_abs"] / pns_bar))])
         assert (e["pn_abs"] <= pn_bar).all(), (step, meta["param_names"][int(np.argmax(e["pn_abs"] / pn_bar))])
-        worst["pn_ratio"] = max(worst["pn_ratio"], float((e["pn_abs"] / pn_bar).max()))
-        worst["pns_ratio"] = max(worst["pns_ratio"], float((e["pns_abs"] / pns_bar).max()))
+        ratio = lambda a, b: float(np.max(np.where(b > 0, a / np.where(b > 0, b, 1.0), 0.0)))  # noqa: E731
+        worst["pn_ratio"] = max(worst["pn_ratio"], ratio(e["pn_abs"], pn_bar))
+        worst["pns_ratio"] = max(worst["pns_ratio"], ratio(e["pns_abs"], pns_bar))
         worst["upd"] = max(worst["upd"], e["upd"])
         worst["full"] = max(worst["full"], e.get("full", 0.0))
         worst["norm"] = max(worst.get("norm", 0.0), e["norm"])

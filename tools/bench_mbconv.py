@@ -18,11 +18,15 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--batch", type=int, default=512)
     ap.add_argument("--dw-blocks", type=int, default=0, help="dw_blocks option (0: library default)")
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE")
     a = ap.parse_args()
     import ogv
     from ogv._lib import load
     ogv.load()
     assert load().ogv_set_option(b"dw_blocks", a.dw_blocks) == 0
+    for o in a.opt:
+        k, v = o.split("=")
+        assert load().ogv_set_option(k.encode(), int(v)) == 0, o
     from src.model.mbc_conv import MBConv, MBConvConfig
     for C, H in ((48, 32), (96, 16), (192, 8), (256, 4)):
         m = MBConv(C, C, 1, MBConvConfig()).cuda().to(memory_format=torch.channels_last).train()

@@ -49,7 +49,9 @@ def main():
         dur[family(r["Kernel_Name"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-3)
     cnt = collections.defaultdict(lambda: collections.defaultdict(float))
     launches = collections.Counter()
-    for sub in ("fetch", "write", "mfma"):
+    for sub in ("fetch", "write", "mfma", "stall"):
+        if sub == "stall" and not os.path.isdir(os.path.join(a.dir, sub)):
+            continue
         seen = set()
         for r in rows_of(os.path.join(a.dir, sub), "*counter_collection.csv"):
             f = family(r["Kernel_Name"])
@@ -70,16 +72,25 @@ def main():
             row["hbm_bytes_per_launch"] = int(b)
             row["hbm_GBs"] = round(b / (avg_us * 1e3), 1)
             row["hbm_frac"] = round(b / (avg_us * 1e3) / HBM, 4)
+        wc = c.get("SQ_WAVE_CYCLES", 0.0)
+        if wc > 0:   # where the waves' cycles went (disjoint: parked on s_waitcnt / barrier, issue-stalled, issuing)
+            row["wait_frac"] = round(c.get("SQ_WAIT_ANY", 0.0) / wc, 3)
+            row["issue_stall_frac"] = round(c.get("SQ_WAIT_INST_ANY", 0.0) / wc, 3)
+            row["active_frac"] = round(c.get("SQ_ACTIVE_INST_ANY", 0.0) / wc, 3)
+        if c.get("SQ_LDS_IDX_ACTIVE", 0.0) > 0:
+            row["lds_conflict_frac"] = round(c.get("SQ_LDS_BANK_CONFLICT", 0.0) / c["SQ_LDS_IDX_ACTIVE"], 3)
         gui = c.get("GRBM_GUI_ACTIVE", 0.0)
         if gui > 0:
             row["mfma_util"] = round(c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / (gui / 8 * 1024), 4)
         table.append(row)
     table.sort(key=lambda r: -r["total_ms"])
-    print(f"{'family':52s} {'n':>5s} {'avg us':>8s} {'total ms':>9s} {'MB/launch':>10s} {'GB/s':>7s} {'frac':>6s} {'MFMA':>6s}")
+    print(f"{'family':52s} {'n':>5s} {'avg us':>8s} {'total ms':>9s} {'MB/launch':>10s} {'GB/s':>7s} {'frac':>6s} {'MFMA':>6s}"
+          f" {'wait':>5s} {'stall':>5s} {'issue':>5s} {'ldsCF':>5s}")
     for r in table[: a.top]:
         print(f"{r['family']:52s} {r['launches']:5d} {r['avg_us']:8.1f} {r['total_ms']:9.3f} "
               f"{r.get('hbm_bytes_per_launch', 0) / 1e6:10.2f} {r.get('hbm_GBs', 0):7.0f} {r.get('hbm_frac', 0):6.3f} "
-              f"{r.get('mfma_util', 0):6.3f}")
+              f"{r.get('mfma_util', 0):6.3f} {r.get('wait_frac', 0):5.2f} {r.get('issue_stall_frac', 0):5.2f} "
+              f"{r.get('active_frac', 0):5.2f} {r.get('lds_conflict_frac', 0):5.2f}")
     if a.out:
         with open(a.out, "w") as fo:
             json.dump(table, fo, indent=1)

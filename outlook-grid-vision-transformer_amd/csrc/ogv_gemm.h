@@ -230,6 +230,7 @@ void set_vp_dbg(int v);
 void set_vp_tile(int v);
 void set_vp_big(int v);
 void set_dw_tw(int v);
+void set_ln_rpi(int v);
 void set_vp_head(int v);
 void set_vph_rows(int v);
 void set_vph_wgs(int v);

@@ -7,7 +7,7 @@
 
 namespace ogv {
 
-template <typename T, int G, int NV, int VEC>
+template <typename T, int G, int NV, int VEC, int RPI = 2>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, const float* __restrict__ gamma,
                                                      const float* __restrict__ beta, T* __restrict__ y,
                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
@@ -28,8 +28,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, co
     }
   }
   const float invC = 1.f / (float)C;
-  // two rows per iteration, both loads issued before any use
-  constexpr int RPI = 2;
+  // RPI rows per iteration, every load issued before any use (RPI independent reduction chains)
   const long stride = (long)gridDim.x * rows_per_block;
   for (long row0 = blockIdx.x * rows_per_block + threadIdx.x / G; row0 < M; row0 += RPI * stride) {
     float xv[RPI][E];
@@ -79,7 +78,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, co
 
 // dx = rstd * (g - mean(g) - xhat * mean(g * xhat)),  g = dy * gamma
 // per-block partial dgamma = sum dy*xhat, dbeta = sum dy  -> part[block][2][C]
-template <typename T, int G, int NV, int VEC>
+template <typename T, int G, int NV, int VEC, int RPI = 2>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                      const float* __restrict__ gamma, const float* __restrict__ mean,
                                                      const float* __restrict__ rstd, const T* __restrict__ dres,
@@ -101,8 +100,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
     }
   }
   const float invC = 1.f / (float)C;
-  // two rows per iteration, every load of both (x, dy, dres, mean, rstd) issued before any use
-  constexpr int RPI = 2;
+  // RPI rows per iteration, every load of all of them (x, dy, dres, mean, rstd) issued before any use
   const long stride = (long)gridDim.x * rows_per_block;
   for (long row0 = blockIdx.x * rows_per_block + threadIdx.x / G; row0 < M; row0 += RPI * stride) {
     float xv[RPI][E], dv[RPI][E], rv[RPI][E], mu[RPI], rs[RPI];
@@ -174,24 +172,31 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
       }
     }
   }
-  // reduce the per-lane partials of the (256/G) row slots of this block through LDS
-  __shared__ float red[256];
+  // reduce the per-lane partials of the (256/G) row slots of this block: across a wave's 64/G slots with
+  // xor shuffles (every value at once), then the 4 waves through LDS, ONE barrier (was 2 x 2E barriers and
+  // a serial 256/G-long LDS walk per value)
   float* out = part + (long)blockIdx.x * 2 * C;
+#pragma unroll
+  for (int e = 0; e < E; ++e)
+    for (int o = G; o < 64; o <<= 1) {
+      dgam[e] += __shfl_xor(dgam[e], o, 64);
+      dbet[e] += __shfl_xor(dbet[e], o, 64);
+    }
+  __shared__ float red[4][E * G];   // <= 32 KB (E * G <= 2048)
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
   for (int which = 0; which < 2; ++which) {
+    if (which) __syncthreads();   // the first pass's readers are done
+    if (lane < G) {
 #pragma unroll
-    for (int v = 0; v < NV; ++v) {
-#pragma unroll
-      for (int i = 0; i < VEC; ++i) {
-        red[threadIdx.x] = which == 0 ? dgam[v * VEC + i] : dbet[v * VEC + i];
-        __syncthreads();
-        if (threadIdx.x < G) {
-          float acc = 0.f;
-          for (int r = threadIdx.x; r < (int)blockDim.x; r += G) acc += red[r];
-          const int c = (v * G + threadIdx.x) * VEC + i;
-          if (c < C) out[which * C + c] = acc;
-        }
-        __syncthreads();
-      }
+      for (int e = 0; e < E; ++e) red[wave][e * G + lane] = which ? dbet[e] : dgam[e];
+    }
+    __syncthreads();
+    for (int r = threadIdx.x; r < E * G; r += blockDim.x) {
+      const float acc = ((red[0][r] + red[1][r]) + red[2][r]) + red[3][r];
+      const int e = r / G, lg = r - e * G, v = e / VEC, i = e - v * VEC;
+      const int c = (v * G + lg) * VEC + i;
+      if (c < C) out[which * C + c] = acc;
     }
   }
 }
@@ -246,18 +251,31 @@ static long ln_blocks(long M, int G) {
     }                                                                          \
   } while (0)
 
+// knob "ln_rpi": rows per iteration of the LayerNorm kernels (2 or 4, default 2): 4 measured slower on the
+// 7M step (backward 0.60 -> 0.66 ms: 168 VGPRs, 3 waves per SIMD; forward unchanged), profiles/r05j_ln.log
+static int g_ln_rpi = 2;
+void set_ln_rpi(int v) { g_ln_rpi = v >= 4 ? 4 : 2; }
+
 template <typename T, int G, int NV, int VEC>
 static void ln_fwd_launch(const void* x, const float* gamma, const float* beta, void* y, float* mean, float* rstd,
                           long M, int C, float eps, hipStream_t s) {
-  ln_fwd_kernel<T, G, NV, VEC><<<(unsigned)ln_blocks(M, G), 256, 0, s>>>((const T*)x, gamma, beta, (T*)y, mean, rstd,
-                                                                         M, C, eps);
+  if (g_ln_rpi == 4 && NV <= 2)
+    ln_fwd_kernel<T, G, NV, VEC, 4><<<(unsigned)ln_blocks(M, G), 256, 0, s>>>((const T*)x, gamma, beta, (T*)y, mean,
+                                                                              rstd, M, C, eps);
+  else
+    ln_fwd_kernel<T, G, NV, VEC, 2><<<(unsigned)ln_blocks(M, G), 256, 0, s>>>((const T*)x, gamma, beta, (T*)y, mean,
+                                                                              rstd, M, C, eps);
 }
 
 template <typename T, int G, int NV, int VEC>
 static void ln_bwd_launch(const void* dy, const void* x, const float* gamma, const float* mean, const float* rstd,
                           const void* dres, void* dx, float* part, long nb, long M, int C, hipStream_t s) {
-  ln_bwd_kernel<T, G, NV, VEC><<<(unsigned)nb, 256, 0, s>>>((const T*)dy, (const T*)x, gamma, mean, rstd,
-                                                            (const T*)dres, (T*)dx, part, M, C);
+  if (g_ln_rpi == 4 && NV <= 2)
+    ln_bwd_kernel<T, G, NV, VEC, 4><<<(unsigned)nb, 256, 0, s>>>((const T*)dy, (const T*)x, gamma, mean, rstd,
+                                                                 (const T*)dres, (T*)dx, part, M, C);
+  else
+    ln_bwd_kernel<T, G, NV, VEC, 2><<<(unsigned)nb, 256, 0, s>>>((const T*)dy, (const T*)x, gamma, mean, rstd,
+                                                                 (const T*)dres, (T*)dx, part, M, C);
 }
 
 }  // namespace ogv

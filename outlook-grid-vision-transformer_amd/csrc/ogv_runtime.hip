@@ -120,6 +120,10 @@ extern "C" int ogv_set_option(const char* name, int value) {
     set_mb_side(value ? 1 : 0);
     return OGV_OK;
   }
+  if (!strcmp(name, "ln_rpi")) {
+    set_ln_rpi(value);
+    return OGV_OK;
+  }
   if (!strcmp(name, "dw_tw")) {
     set_dw_tw(value);
     return OGV_OK;

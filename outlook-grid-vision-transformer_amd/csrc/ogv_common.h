@@ -26,6 +26,16 @@ __device__ __forceinline__ float bn_shift(float v) { return __builtin_isfinite(v
 // ---------------------------------------------------------------- host-side error plumbing
 void set_error(const char* fmt, ...);
 int check_launch(const char* what);
+// Dynamic LDS above the 64 KB default needs the kernel's grant raised (to 160 KB) once per kernel and
+// DEVICE; returns false when the runtime refuses it (or bytes > 160 KB), so callers can plan around it.
+bool lds_grant(const void* kern, size_t bytes);
+// The current device lets one workgroup opt in to 160 KB of LDS (cached per device).  The *_supported
+// queries of the kernels that need more than 64 KB answer 0 without it, so callers take the unfused path.
+// With no device at all it answers true: the queries stay pure shape questions (nothing can launch).
+bool lds_160k();
+// lds_grant for a launch site with no fallback: on refusal the caller skips the launch and the next
+// check_launch reports OGV_ERR_LAUNCH naming kname (never a silent skipped kernel).
+bool lds_ok(const void* kern, size_t bytes, const char* kname);
 
 #define OGV_REQUIRE(cond, ...)                 \
   do {                                         \

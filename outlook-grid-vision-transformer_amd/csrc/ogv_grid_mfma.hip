@@ -1301,14 +1301,9 @@ static bool grid_big_fwd_try(const GridGeomM& G, const void* qkv, void* out, flo
   const int Np = (G.N + 15) / 16 * 16;
   const size_t lds = 2 * (size_t)Np * gm_pitch<HDP>() * sizeof(bf16);
   if (!g_grid_big || lds > GB_LDS_MAX) return false;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(grid_big_fwd_kernel<HDP>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)GB_LDS_MAX);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(grid_big_fwd2_kernel<HDP>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)GB_LDS_MAX);
-    attr = true;
-  }
+  if (!lds_grant(reinterpret_cast<const void*>(grid_big_fwd_kernel<HDP>), GB_LDS_MAX) ||
+      !lds_grant(reinterpret_cast<const void*>(grid_big_fwd2_kernel<HDP>), GB_LDS_MAX))
+    return false;   // the caller takes the unfused path
   const long pairs = (long)G.B * G.g * G.g * G.heads;
   if (g_grid_big == 2)
     grid_big_fwd2_kernel<HDP><<<(unsigned)pairs, GB_NW * 64, lds, s>>>((const bf16*)qkv, (bf16*)out, lse, G, scale, Np);
@@ -1323,18 +1318,11 @@ static bool grid_big_bwd_try(const GridGeomM& G, const void* dout, const void* q
   const int Np = (G.N + 15) / 16 * 16;
   const size_t l1 = 2 * (size_t)Np * gm_pitch<HDP>() * sizeof(bf16), l2 = l1 + 2 * (size_t)Np * sizeof(float);
   if (!g_grid_big || l2 > GB_LDS_MAX) return false;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(grid_big_dq_kernel<HDP>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)GB_LDS_MAX);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(grid_big_dkv_kernel<HDP>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)GB_LDS_MAX);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(grid_big_dq2_kernel<HDP>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)GB_LDS_MAX);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(grid_big_dkv2_kernel<HDP>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)GB_LDS_MAX);
-    attr = true;
-  }
+  for (const void* k : {reinterpret_cast<const void*>(grid_big_dq_kernel<HDP>),
+                        reinterpret_cast<const void*>(grid_big_dkv_kernel<HDP>),
+                        reinterpret_cast<const void*>(grid_big_dq2_kernel<HDP>),
+                        reinterpret_cast<const void*>(grid_big_dkv2_kernel<HDP>)})
+    if (!lds_grant(k, GB_LDS_MAX)) return false;
   const long pairs = (long)G.B * G.g * G.g * G.heads;
   if (g_grid_big == 2) {
     grid_big_dq2_kernel<HDP><<<(unsigned)pairs, GB_NW * 64, l1, s>>>((const bf16*)dout, (const bf16*)qkv, lse, delta,

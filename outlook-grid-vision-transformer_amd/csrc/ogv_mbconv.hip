@@ -1282,6 +1282,13 @@ static int g_dw_bn2 = 1;
 void set_dw_bn2(int v) { g_dw_bn2 = v; }
 static int g_dw_bwd_r = 4;
 void set_dw_bwd_r(int v) { g_dw_bwd_r = v == 2 ? 2 : 4; }
+// dynamic LDS of dw_dgrad_tile_kernel: the staged tile (+ the 9-tap partials with part) and, BN2-staged
+// (b2), the per-image gate / dpool table
+static size_t dw_dgrad_lds(const DwTile& t, bool part, bool b2) {
+  size_t lds = t.lds_bytes(part ? 9 : 2, 4, sizeof(float), b2 ? g_dw_bwd_r : DW_R);
+  if (b2) lds += (size_t)t.G * 2 * t.CT * sizeof(float);
+  return lds;
+}
 struct SideStream {
   hipStream_t s = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
@@ -1360,9 +1367,8 @@ struct Ops {
     if (skip_mask() & 8) return;
     constexpr int V = 4;
     const int R = b2 ? g_dw_bwd_r : DW_R;
-    size_t lds = t.lds_bytes(part ? 9 : 2, V, sizeof(float), R);
-    const int tab_off = (int)(lds / sizeof(float));
-    if (b2) lds += (size_t)t.G * 2 * t.CT * sizeof(float);
+    const size_t lds = dw_dgrad_lds(t, part != nullptr, b2 != nullptr);
+    const int tab_off = (int)(t.lds_bytes(part ? 9 : 2, V, sizeof(float), R) / sizeof(float));
     const Bn2In<T> bi = b2 ? *b2 : Bn2In<T>{};
 #define OGV_DWD(WG_, B2_, R_)                                                                                        \
     OGV_DW_ACT(act, if (t.ldq <= 1) dw_dgrad_tile_kernel<T, V, 1, A, WG_, B2_, R_><<<dw_grid(t), 256, lds, st>>>(    \
@@ -1613,7 +1619,10 @@ static void mbconv_bwd_impl(const void* dout, const void* x, const Saved& sv, vo
     }
   }
   // B5) BN2 backward: dd = ca*(dy2 - cb - dhat*cc)  -> bufB  (with dw_bn2: computed inside B6's staging)
-  const bool bn2f = g_dw_fuse && g_dw_bn2;
+  // The BN2-staged kernel adds a per-image (gate, dpool) table of G x 2 x CT floats to the tile's LDS; a
+  // plan whose total would pass the 64 KB default grant takes the unfused bn2_apply path instead.
+  const DwTile t6 = dw_tile_plan(s.B, s.H, s.W, s.mid, 4);
+  const bool bn2f = g_dw_fuse && g_dw_bn2 && dw_dgrad_lds(t6, true, true) <= 64 * 1024;
   {
     // BN2's column sums over the images, the per-image terms formed on the fly (no terms launch)
     bn_reduce_coeffs_kernel<true><<<cdiv(s.mid, 16), 256, 0, st>>>(nullptr, s.B, 2L * s.mid, s.mid, (float)M, P.bn2_w,
@@ -1628,7 +1637,7 @@ static void mbconv_bwd_impl(const void* dout, const void* x, const Saved& sv, vo
   void* dy1 = bn2f ? w.bufB : w.bufA;
   void* de = bn2f ? w.bufA : w.bufB;
   {
-    const DwTile t = dw_tile_plan(s.B, s.H, s.W, s.mid, 4);
+    const DwTile& t = t6;
     join_side(st, sd);
     if (bn2f) {  // one pass over (dA3, d, e): BN2 backward + data gradient + BN1 sums + dWdw partials
       const Bn2In<T> b2 = {(const T*)sv.d, sv.sc2, sv.sh2, sv.mean2, sv.inv2, sv.gate, w.dpool, w.coef, HW};

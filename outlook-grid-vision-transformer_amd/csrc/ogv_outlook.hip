@@ -1833,21 +1833,20 @@ static bool vproj_plan(int B, int H, int W, int C, int heads, int k, int ldc, og
 }
 
 template <int NJ, int NK, int NW>
-static void vproj_run(const bf16* x, int ldx, const float* Wc, int wrows, const float* bias, bf16* cat, int ldc, bf16* y,
+static int vproj_run(const bf16* x, int ldx, const float* Wc, int wrows, const float* bias, bf16* cat, int ldc, bf16* y,
                       int H, int W, int C, int heads, const VTile& t, bool sw, hipStream_t s) {
   const size_t lds = vtile_lds(t, heads, sw);
   const long per_cu = NW == 4 ? 2 : 1;
   const long nb = std::min<long>(t.ntiles, 256 * per_cu);
   const unsigned grid = (unsigned)((nb + 7) / 8 * 8);
   auto kern = sw ? outlook_vproj_fwd_kernel<NJ, NK, true, NW> : outlook_vproj_fwd_kernel<NJ, NK, false, NW>;
-  static bool attr[2] = {false, false};
-  if (!attr[sw]) {   // dynamic LDS above the default grant
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    attr[sw] = true;
+  if (!lds_grant(reinterpret_cast<const void*>(kern), lds)) {
+    set_error("%s: dynamic LDS grant of %zu bytes refused", "ogv_outlook_vproj_fwd", lds);
+    return OGV_ERR_LAUNCH;
   }
   kern<<<grid, NW * 64, lds, s>>>(x, ldx, Wc, wrows, bias, cat, ldc, y, H, W, C, heads, t,
                                     (int)vtile_x_bytes(t, heads), g_vp_dbg);
+  return OGV_OK;
 }
 
 // wide stages (C > 96): the weight-streaming kernel, 8 x 8 tiles, CJ 16-column blocks per weight chunk
@@ -1895,20 +1894,19 @@ static bool vbig_plan(int B, int H, int W, int C, int heads, int k, int ldc, ogv
 }
 
 template <int NK>
-static void vbig_run(const bf16* x, int ldx, const float* Wc, int wrows, const float* bias, bf16* cat, int ldc, bf16* y,
+static int vbig_run(const bf16* x, int ldx, const float* Wc, int wrows, const float* bias, bf16* cat, int ldc, bf16* y,
                      int H, int W, int C, int heads, const VTile& t, bool sw, hipStream_t s) {
   constexpr int CJ = NK == 4 ? 6 : NK == 6 ? 3 : NK == 8 ? 2 : 1;
   const size_t lds = vbig_lds(t, C, heads, CJ, sw);
   const long nb = std::min<long>(t.ntiles, 256);
   const unsigned grid = (unsigned)((nb + 7) / 8 * 8);
   auto kern = sw ? outlook_vproj_big_fwd_kernel<NK, CJ, true> : outlook_vproj_big_fwd_kernel<NK, CJ, false>;
-  static bool attr[2] = {false, false};
-  if (!attr[sw]) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    attr[sw] = true;
+  if (!lds_grant(reinterpret_cast<const void*>(kern), lds)) {
+    set_error("%s: dynamic LDS grant of %zu bytes refused", "ogv_outlook_vproj_fwd", lds);
+    return OGV_ERR_LAUNCH;
   }
   kern<<<grid, VB_NW * 64, lds, s>>>(x, ldx, Wc, wrows, bias, cat, ldc, y, H, W, C, heads, t, g_vp_dbg);
+  return OGV_OK;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2169,14 +2167,16 @@ static bool vhead_plan(int B, int H, int W, int C, int heads, int k, int ldc, og
 }
 
 template <int NJV, int NK, int NF>
-static void vhead_run(const bf16* x, int ldx, const float* Wc, const float* bias, bf16* cat, int ldc, bf16* y, int B,
+static int vhead_run(const bf16* x, int ldx, const float* Wc, const float* bias, bf16* cat, int ldc, bf16* y, int B,
                       int H, int W, int C, int heads, const VHead& t, bool sw, hipStream_t s) {
   const size_t lds = vhead_lds<NJV, NK>(t, sw);
   auto kern = sw ? outlook_vproj_head_fwd_kernel<NJV, NK, NF, true> : outlook_vproj_head_fwd_kernel<NJV, NK, NF, false>;
-  if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
+  if (!lds_grant(reinterpret_cast<const void*>(kern), lds)) {
+    set_error("%s: dynamic LDS grant of %zu bytes refused", "ogv_outlook_vproj_fwd", lds);
+    return OGV_ERR_LAUNCH;
+  }
   kern<<<(unsigned)(t.RG * heads), 256, lds, s>>>(x, ldx, Wc, bias, cat, ldc, y, B, H, W, C, heads, t, g_vph_dbg);
+  return OGV_OK;
 }
 
 static bool vproj_bwd_plan(int B, int H, int W, int C, int heads, int k, int ldc, ogv_dtype dt, VTile& t, int& nw) {
@@ -2184,21 +2184,20 @@ static bool vproj_bwd_plan(int B, int H, int W, int C, int heads, int k, int ldc
 }
 
 template <int NJ, int NK, int NW>
-static void vproj_bwd_run(const bf16* x, int ldx, const float* Wc, int wrows, const float* bias, const bf16* dy,
+static int vproj_bwd_run(const bf16* x, int ldx, const float* Wc, int wrows, const float* bias, const bf16* dy,
                           bf16* dcat, int ldc, int H, int W, int C, int heads, const VTile& t, bool sw, hipStream_t s) {
   const size_t lds = vtile_bwd_lds(t, C, heads, sw);
   const long per_cu = NW == 4 ? 2 : 1;
   const long nb = std::min<long>(t.ntiles, 256 * per_cu);
   const unsigned grid = (unsigned)((nb + 7) / 8 * 8);
   auto kern = sw ? outlook_vproj_bwd_kernel<NJ, NK, true, NW> : outlook_vproj_bwd_kernel<NJ, NK, false, NW>;
-  static bool attr[2] = {false, false};
-  if (!attr[sw]) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    attr[sw] = true;
+  if (!lds_grant(reinterpret_cast<const void*>(kern), lds)) {
+    set_error("%s: dynamic LDS grant of %zu bytes refused", "ogv_outlook_vproj_bwd", lds);
+    return OGV_ERR_LAUNCH;
   }
   kern<<<grid, NW * 64, lds, s>>>(x, ldx, Wc, wrows, bias, dy, C, dcat, ldc, H, W, C, heads, t,
                                     (int)vtile_bwd_x_bytes(t, heads), g_vp_dbg);
+  return OGV_OK;
 }
 
 }  // namespace ogv
@@ -2208,7 +2207,7 @@ using namespace ogv;
 extern "C" int ogv_outlook_vproj_supported(int B, int H, int W, int C, int heads, int k, int ldc, int train,
                                            ogv_dtype dt) {
   VTile t;
-  if (g_outlook_vproj < (train ? 2 : 1)) return 0;
+  if (g_outlook_vproj < (train ? 2 : 1) || !lds_160k()) return 0;   // every fused variant may need > 64 KB
   int nw = 0;
   VHead th;
   if (vhead_plan(B, H, W, C, heads, k, ldc, dt, th)) return 1;   // wide stages, small images: per-head kernel
@@ -2221,7 +2220,7 @@ extern "C" int ogv_outlook_vproj_supported(int B, int H, int W, int C, int heads
 extern "C" int ogv_outlook_vproj_bwd_supported(int B, int H, int W, int C, int heads, int k, int ldc, ogv_dtype dt) {
   VTile t;
   int nw = 0;
-  return vproj_bwd_plan(B, H, W, C, heads, k, ldc, dt, t, nw) ? 1 : 0;
+  return lds_160k() && vproj_bwd_plan(B, H, W, C, heads, k, ldc, dt, t, nw) ? 1 : 0;
 }
 
 extern "C" int ogv_outlook_vproj_bwd(const void* x, int ldx, const float* w, const float* bias, const void* dy,
@@ -2246,9 +2245,9 @@ extern "C" int ogv_outlook_vproj_bwd(const void* x, int ldx, const float* w, con
   bf16* db = (bf16*)dcat;
 #define OGV_VPROJ_BWD(nj, nk)                                                                          \
   if (NJ == nj && NK == nk) {                                                                          \
-    if (nw == 4) vproj_bwd_run<nj, nk, 4>(xb, ldx, w, ldc, bias, gb, db, ldc, H, W, C, heads, t, sw, s); \
-    else vproj_bwd_run<nj, nk, 8>(xb, ldx, w, ldc, bias, gb, db, ldc, H, W, C, heads, t, sw, s);         \
-    return check_launch("ogv_outlook_vproj_bwd");                                                      \
+    const int e = nw == 4 ? vproj_bwd_run<nj, nk, 4>(xb, ldx, w, ldc, bias, gb, db, ldc, H, W, C, heads, t, sw, s) \
+                          : vproj_bwd_run<nj, nk, 8>(xb, ldx, w, ldc, bias, gb, db, ldc, H, W, C, heads, t, sw, s); \
+    return e ? e : check_launch("ogv_outlook_vproj_bwd");                                              \
   }
   // (NJ, NK) pairs the plan admits: 16 | C <= 96, 8 | head_dim, ncol = C + 9 heads rounded to 16 <= 128
   OGV_VPROJ_BWD(2, 1) OGV_VPROJ_BWD(3, 1) OGV_VPROJ_BWD(4, 1) OGV_VPROJ_BWD(5, 1)
@@ -2278,9 +2277,9 @@ extern "C" int ogv_outlook_vproj_fwd(const void* x, int ldx, const float* w, con
     const int nf = th.R > 64 ? 2 : 1;
 #define OGV_VHEAD(njv, nk)                                                                                  \
   if (C / heads == njv * 16 && C / 32 == nk) {                                                              \
-    if (nf == 1) vhead_run<njv, nk, 1>(xb, ldx, w, bias, cb, ldc, yb, B, H, W, C, heads, th, sw, s);        \
-    else vhead_run<njv, nk, 2>(xb, ldx, w, bias, cb, ldc, yb, B, H, W, C, heads, th, sw, s);                \
-    return check_launch("ogv_outlook_vproj_fwd");                                                          \
+    const int e = nf == 1 ? vhead_run<njv, nk, 1>(xb, ldx, w, bias, cb, ldc, yb, B, H, W, C, heads, th, sw, s) \
+                          : vhead_run<njv, nk, 2>(xb, ldx, w, bias, cb, ldc, yb, B, H, W, C, heads, th, sw, s); \
+    return e ? e : check_launch("ogv_outlook_vproj_fwd");                                                  \
   }
     OGV_VHEAD(2, 4) OGV_VHEAD(2, 6) OGV_VHEAD(2, 8) OGV_VHEAD(2, 12)
     OGV_VHEAD(4, 4) OGV_VHEAD(4, 6) OGV_VHEAD(4, 8) OGV_VHEAD(4, 12)
@@ -2299,13 +2298,14 @@ extern "C" int ogv_outlook_vproj_fwd(const void* x, int ldx, const float* w, con
     hipStream_t s = as_stream(stream);
     const bf16* xb = (const bf16*)x;
     bf16 *cb = (bf16*)cat, *yb = (bf16*)y;
+    int e;
     switch (C / 32) {
-      case 4: vbig_run<4>(xb, ldx, w, ldc, bias, cb, ldc, yb, H, W, C, heads, t, sw, s); break;
-      case 6: vbig_run<6>(xb, ldx, w, ldc, bias, cb, ldc, yb, H, W, C, heads, t, sw, s); break;
-      case 8: vbig_run<8>(xb, ldx, w, ldc, bias, cb, ldc, yb, H, W, C, heads, t, sw, s); break;
-      default: vbig_run<12>(xb, ldx, w, ldc, bias, cb, ldc, yb, H, W, C, heads, t, sw, s); break;
+      case 4: e = vbig_run<4>(xb, ldx, w, ldc, bias, cb, ldc, yb, H, W, C, heads, t, sw, s); break;
+      case 6: e = vbig_run<6>(xb, ldx, w, ldc, bias, cb, ldc, yb, H, W, C, heads, t, sw, s); break;
+      case 8: e = vbig_run<8>(xb, ldx, w, ldc, bias, cb, ldc, yb, H, W, C, heads, t, sw, s); break;
+      default: e = vbig_run<12>(xb, ldx, w, ldc, bias, cb, ldc, yb, H, W, C, heads, t, sw, s); break;
     }
-    return check_launch("ogv_outlook_vproj_fwd");
+    return e ? e : check_launch("ogv_outlook_vproj_fwd");
   }
   const int NJ = t.ncol / 16, NK = (C + 31) / 32;
   const bool sw = (split_w() & 1) != 0;
@@ -2314,9 +2314,9 @@ extern "C" int ogv_outlook_vproj_fwd(const void* x, int ldx, const float* w, con
   bf16 *cb = (bf16*)cat, *yb = (bf16*)y;
 #define OGV_VPROJ(nj, nk)                                                                      \
   if (NJ == nj && NK == nk) {                                                                  \
-    if (nw == 4) vproj_run<nj, nk, 4>(xb, ldx, w, ldc, bias, cb, ldc, yb, H, W, C, heads, t, sw, s); \
-    else vproj_run<nj, nk, 8>(xb, ldx, w, ldc, bias, cb, ldc, yb, H, W, C, heads, t, sw, s);         \
-    return check_launch("ogv_outlook_vproj_fwd");                                              \
+    const int e = nw == 4 ? vproj_run<nj, nk, 4>(xb, ldx, w, ldc, bias, cb, ldc, yb, H, W, C, heads, t, sw, s) \
+                          : vproj_run<nj, nk, 8>(xb, ldx, w, ldc, bias, cb, ldc, yb, H, W, C, heads, t, sw, s); \
+    return e ? e : check_launch("ogv_outlook_vproj_fwd");                                      \
   }
   // (NJ, NK) pairs the plan admits: 16 | C <= 96, 8 | head_dim, ncol = C + 9 heads rounded to 16 <= 128
   OGV_VPROJ(2, 1) OGV_VPROJ(3, 1) OGV_VPROJ(4, 1) OGV_VPROJ(5, 1)

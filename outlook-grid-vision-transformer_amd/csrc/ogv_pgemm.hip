@@ -658,12 +658,7 @@ static void pg_launch(const PgPlan& p, const bf16* A, int lda, const Pro& pro, c
                       const Epi& epi, bf16* out, int ldo, int M, int N, int K, const ConvG& cv, hipStream_t s) {
   if (skip_mask() & 1) return;
   auto kern = pgemm_bf16_kernel<RS, TN, PA, GT, ZA, STATS, BT, SW, CV>;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    attr = true;
-  }
+  if (!lds_ok(reinterpret_cast<const void*>(kern), p.lds, "pgemm_bf16_kernel")) return;
   // persistent: at most pg_per_cu workgroups per CU, a multiple of 8 (keeps each one's XCD)
   const long vb = (long)((p.nMt + 7) / 8) * 8 * p.nNt;
   const unsigned grid = (unsigned)std::min<long>(vb, (long)pg_cus() * g_pg_per_cu / 8 * 8);

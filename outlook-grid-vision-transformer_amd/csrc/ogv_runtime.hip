@@ -3,6 +3,8 @@
 #include "ogv_gemm.h"
 
 #include <cstring>
+#include <mutex>
+#include <vector>
 
 namespace ogv {
 
@@ -15,13 +17,63 @@ void set_error(const char* fmt, ...) {
   va_end(ap);
 }
 
+static thread_local const char* g_refused = nullptr;   // a launch skipped because its LDS grant was refused
+
 int check_launch(const char* what) {
+  if (g_refused) {
+    set_error("%s: %s not launched: dynamic LDS grant refused", what, g_refused);
+    g_refused = nullptr;
+    return OGV_ERR_LAUNCH;
+  }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     set_error("%s: launch failed: %s", what, hipGetErrorString(e));
     return OGV_ERR_LAUNCH;
   }
   return OGV_OK;
+}
+
+bool lds_160k() {
+  int dev = 0, n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {   // no device: a pure shape query (nothing can launch)
+    (void)hipGetLastError();
+    return true;
+  }
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  static std::mutex mu;
+  static std::vector<std::pair<int, bool>> seen;
+  std::lock_guard<std::mutex> lock(mu);
+  for (const auto& d : seen)
+    if (d.first == dev) return d.second;
+  int optin = 0;
+  const bool ok = hipDeviceGetAttribute(&optin, hipDeviceAttributeSharedMemPerBlockOptin, dev) == hipSuccess &&
+                  optin >= 160 * 1024;
+  if (!ok) (void)hipGetLastError();
+  seen.emplace_back(dev, ok);
+  return ok;
+}
+
+bool lds_grant(const void* kern, size_t bytes) {
+  if (bytes <= 64 * 1024) return true;   // the default grant
+  if (bytes > 160 * 1024 || !lds_160k()) return false;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  struct Grant { const void* kern; int dev; bool ok; };
+  static std::mutex mu;
+  static std::vector<Grant> done;
+  std::lock_guard<std::mutex> lock(mu);
+  for (const Grant& g : done)
+    if (g.kern == kern && g.dev == dev) return g.ok;
+  const bool ok = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+  if (!ok) (void)hipGetLastError();
+  done.push_back(Grant{kern, dev, ok});
+  return ok;
+}
+
+bool lds_ok(const void* kern, size_t bytes, const char* kname) {
+  if (lds_grant(kern, bytes)) return true;
+  g_refused = kname;
+  return false;
 }
 
 template <typename S, typename D>

@@ -158,14 +158,8 @@ void se_gemv_launch(const float* in, int ldi, int pro_act, const float* W, int l
   if (B <= 0 || N <= 0) return;
   const int Kp = (K + 3) / 4 * 4;
   const size_t lds = ((size_t)SE_RB * Kp + (rm ? 4 * SE_RB * 64 : 0)) * sizeof(float);
-  if (lds > 64 * 1024) {
-    static bool attr[2] = {false, false};
-    if (!attr[rm]) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(rm ? se_gemv_kernel<true> : se_gemv_kernel<false>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      attr[rm] = true;
-    }
-  }
+  if (!lds_ok(reinterpret_cast<const void*>(rm ? se_gemv_kernel<true> : se_gemv_kernel<false>), lds, "se_gemv_kernel"))
+    return;
   dim3 grid((unsigned)cdiv(B, SE_RB), (unsigned)cdiv(N, rm ? 64 : 32));
   if (rm)
     se_gemv_kernel<true><<<grid, SE_NT, lds, s>>>(in, ldi, pro_act, W, ldw, bias, Z, ldz, zact, out, ldo, sig_out, B,

@@ -543,12 +543,7 @@ static int sg_launch(const SgPlan& p, const bf16* A, int lda, const Pro& pro, co
   if (skip_mask() & 2) return p.grid;
   const int sw = p.sw;
   auto kern = sw ? sgemm_bf16_kernel<KT, RS, PA, ZA, STATS, BT, true> : sgemm_bf16_kernel<KT, RS, PA, ZA, STATS, BT, false>;
-  static bool attr[2] = {false, false};
-  if (!attr[sw]) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)SG_LDS_CAP);
-    attr[sw] = true;
-  }
+  if (!lds_ok(reinterpret_cast<const void*>(kern), p.lds, "sgemm_bf16_kernel")) return p.grid;
   int gx = p.grid;
   if (g_sg_per_cu > 2) {
     int occ = 0;

@@ -55,13 +55,22 @@ def classifier_head(x, classifier: nn.Linear):
     features are averaged in fp32 and the classifier keeps its fp32 weights, so the logits carry no
     bf16 rounding of their own.  The Linear runs on the native fp32 GEMM (ogv_gemm_fwd: the
     thread-group kernel for [B, K] outputs, its dgrad / weight gradient on the exact-f32 MFMA kernels)
-    -- the module is called directly only when it carries forward hooks, which must see the call."""
+    -- the module itself is called instead whenever the call must be observable or is not a plain
+    Linear on the GPU: a subclass or wrapper (its own forward), module or global forward (pre-)hooks,
+    or CPU features (the native kernels take device pointers only)."""
     pooled = x.mean(dim=(2, 3), dtype=torch.float32)
-    if classifier._forward_hooks or classifier._forward_pre_hooks:
-        with torch.autocast("cuda", enabled=False):
+    if not _native_classifier_ok(classifier, pooled):
+        with torch.autocast(pooled.device.type, enabled=False):
             return classifier(pooled)
     from ogv import functional as OF
     return OF.linear_rows(pooled, classifier.weight, classifier.bias)
+
+
+def _native_classifier_ok(classifier, pooled) -> bool:
+    from torch.nn.modules import module as _m
+    return (type(classifier) is nn.Linear and pooled.is_cuda
+            and not (classifier._forward_hooks or classifier._forward_pre_hooks
+                     or _m._global_forward_hooks or _m._global_forward_pre_hooks))
 
 
 def train_prologue(model: nn.Module, x):

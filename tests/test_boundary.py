@@ -154,6 +154,38 @@ def test_build_model_dispatch_matches_reference_aliases():
         build_model(dict(type="model_b", stages=[]))
 
 
+def test_classifier_head_native_path_only_for_plain_gpu_linear():
+    """Model_A_OutGridNet.py:65-67 head: the native fp32 GEMM replaces nn.Linear.forward only when
+    nothing can observe the difference -- on CPU features, a Linear subclass, or with module / global
+    forward hooks the module itself is called (and the CPU result equals the reference's formula)."""
+    from torch import nn
+    from src.Model_A_OutGridNet import _native_classifier_ok, classifier_head
+    lin = nn.Linear(8, 5)
+    x = torch.randn(3, 8, 2, 2)
+    pooled = x.mean(dim=(2, 3))
+    assert not _native_classifier_ok(lin, pooled)                       # CPU tensor
+    torch.testing.assert_close(classifier_head(x, lin), lin(pooled))   # runs the module on CPU
+
+    class MyLinear(nn.Linear):
+        pass
+
+    fake_cuda = type("T", (), {"is_cuda": True})()
+    assert _native_classifier_ok(lin, fake_cuda)
+    assert not _native_classifier_ok(MyLinear(8, 5), fake_cuda)
+    seen = []
+    h = torch.nn.modules.module.register_module_forward_hook(lambda m, i, o: seen.append(type(m)))
+    try:
+        assert not _native_classifier_ok(lin, fake_cuda)
+        classifier_head(x, lin)
+        assert nn.Linear in seen                                        # the global hook saw the call
+    finally:
+        h.remove()
+    h = lin.register_forward_pre_hook(lambda m, i: None)
+    assert not _native_classifier_ok(lin, fake_cuda)
+    h.remove()
+    assert _native_classifier_ok(lin, fake_cuda)
+
+
 def test_gemm_routing_table():
     """Host-side planner (no GPU): which kernel a bf16 projection runs on (ogv_gemm_stream_route:
     1 streaming, 2 panel, 0 LDS-tiled), on the Model-A-7M shapes and the edges of each route."""
@@ -199,8 +231,14 @@ def test_outlook_vproj_plan_and_knob():
         assert sup(128, 224, 224, 64, 2, False) == 1        # 22M stage 0
         # wide stages (C > 96) on images of <= 128 pixels: the per-head whole-image kernel (knob vp_head,
         # default on), forward with cat; larger wide-stage images keep the unfused GEMM + aggregation
-        for shape in ((512, 8, 8, 192, 6), (512, 4, 4, 256, 8), (256, 8, 8, 384, 6), (3, 5, 11, 128, 4)):
+        for shape in ((512, 8, 8, 192, 6), (512, 4, 4, 256, 8), (3, 5, 11, 128, 4), (256, 8, 8, 384, 12)):
             assert sup(*shape, False) == 1 and sup(*shape, True) == 1, shape
+        # head_dim 64 (14M / 22M stage 3): a 125 KB weight slice, one workgroup per CU -- measured slower
+        # than the unfused pair, so planned only with vp_head = 2
+        assert sup(256, 8, 8, 384, 6, False) == 0 and sup(256, 4, 4, 256, 4, False) == 0
+        assert lib.ogv_set_option(b"vp_head", 2) == 0
+        assert sup(256, 8, 8, 384, 6, False) == 1 and sup(256, 4, 4, 256, 4, True) == 1
+        assert lib.ogv_set_option(b"vp_head", 1) == 0
         assert sup(256, 32, 32, 128, 4, False) == 0         # 14M stage 1: 1024-pixel images
         assert sup(256, 16, 16, 256, 8, False) == 0         # 14M stage 2: 256-pixel images
         assert sup(512, 8, 8, 160, 5, False) == 0           # C = 160: no instantiation (C / 32 = 5)

@@ -796,11 +796,24 @@ class Trainer:
         # call from another thread (hipErrorStreamCaptureUnsupported -> abort), so capture thread-locally
         mode = "thread_local" if self.backend == "nccl" else "global"
         if self.dp_overlap:
-            with torch.cuda.graph(self._g, pool=pool, capture_error_mode=mode):
-                self._loss_static = self._fwd_bwd_overlap(self._x, self._y)
-                self._update(self._overlap_finish())
-            self.graph_grads = [p.grad for p in self.params]   # views of the reduced-gradient buffer
-            return loss
+            try:
+                with torch.cuda.graph(self._g, pool=pool, capture_error_mode=mode):
+                    self._loss_static = self._fwd_bwd_overlap(self._x, self._y)
+                    self._update(self._overlap_finish())
+                self.graph_grads = [p.grad for p in self.params]   # views of the reduced-gradient buffer
+                return loss
+            except RuntimeError as e:
+                # a runtime that cannot record collectives into a graph raises during the capture (before any
+                # of them ran: every rank fails alike): record the flat form instead -- one all_reduce between
+                # two graphs, outside any capture -- rather than end the job
+                import warnings
+                warnings.warn(f"Trainer: capturing the bucketed all-reduces failed ({e}); using the flat all-reduce "
+                              f"between two graphs instead", RuntimeWarning, stacklevel=3)
+                torch.cuda.synchronize()
+                self.dp_overlap = False
+                self._gworks, self._glocal = [], []
+                self.opt.zero_grad(set_to_none=True)
+                self._g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self._g, pool=pool, capture_error_mode=mode):
             self._loss_static = self._fwd_bwd(self._x, self._y)
             if self.dp:

@@ -32,7 +32,7 @@ def main():
         batches.append((torch.randn(16, 3, 32, 32, device="cuda", generator=g).contiguous(memory_format=torch.channels_last),
                         torch.randint(0, 100, (16,), device="cuda", generator=g)))
     runs = {}
-    for mode in ("plain", "dp_graph", "dp_graph_flat", "dp_capture", "plain_eager", "dp_eager"):
+    for mode in ("plain", "dp_graph", "dp_graph_flat", "dp_capture", "plain_eager", "dp_eager", "dp_graph_fallback"):
         torch.backends.cudnn.benchmark = False
         torch.manual_seed(31)
         m = build_model(dict(type="model_a", num_classes=100, stem_dim=64, dpr_max=0.0, stages=cfg["stages"]))
@@ -41,12 +41,22 @@ def main():
         t = Trainer(m, total_steps=50, warmup_ratio=0.1, graphs=not mode.endswith("eager"), capture_warmup=1,
                     force_dp=dp, dp_capture_collective=mode == "dp_capture", dp_overlap=mode != "dp_graph_flat")
         assert t.dp == dp and t.dp_capture_collective == (mode == "dp_capture")
-        assert t.dp_overlap == (mode == "dp_graph"), (mode, t.dp_overlap)
-        losses = [t.step(*b).float().item() for b in batches]     # eager, capture, replay, replay
+        assert t.dp_overlap == (mode in ("dp_graph", "dp_graph_fallback")), (mode, t.dp_overlap)
+        if mode == "dp_graph_fallback":   # a runtime that refuses to record the collectives: the capture raises
+            def refuse(*a, **k):
+                raise RuntimeError("simulated: collective not capturable")
+            t._fwd_bwd_overlap = refuse
+        warned = []
+        import warnings
+        with warnings.catch_warnings(record=True) as wl:
+            warnings.simplefilter("always")
+            losses = [t.step(*b).float().item() for b in batches]     # eager, capture, replay, replay
+            warned = [str(w.message) for w in wl if "bucketed all-reduces failed" in str(w.message)]
         torch.cuda.synchronize()
         state = [p.detach().clone() for p in m.parameters()] + [b.detach().clone() for b in m.buffers()]
         runs[mode] = (losses, state)
-        out = {"mode": mode, "backend": t.backend, "losses": losses, "graphs": t.graphs, "dp_overlap": t.dp_overlap}
+        out = {"mode": mode, "backend": t.backend, "losses": losses, "graphs": t.graphs, "dp_overlap": t.dp_overlap,
+               "fallback_warned": len(warned)}
         if t.dp_overlap:     # the reduced gradients the optimizer read are the parameters' .grad
             out["buckets"] = len(t._gbuckets)
             out["grad_is_view"] = all(p.grad.data_ptr() == v.data_ptr() for p, v in zip(t.params, t._gviews))

@@ -509,7 +509,9 @@ def test_rccl_world1_dp_path_matches_single_process():
     loss and parameter equals the single-process Trainer's (the all_reduce of one rank is the identity; the
     eager bucket path runs its parameter-gradient reductions immediately instead of deferred, so it is held
     to one lr step per element, Adam's sign flips of near-zero gradients).  Runs tests/_rccl_world1.py as a
-    child process (its own process group and HIP context; an RCCL abort cannot take the test runner down)."""
+    child process (its own process group and HIP context; an RCCL abort cannot take the test runner down).
+    dp_graph_fallback: the overlapped capture made to raise (a runtime that refuses to record collectives)
+    -- the Trainer warns once and records the flat two-graph form instead, with the same result."""
     import json
     import pathlib
     import subprocess
@@ -519,12 +521,17 @@ def test_rccl_world1_dp_path_matches_single_process():
     print(r.stdout[-4000:], r.stderr[-4000:])
     lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
     res = {d["mode"]: d for d in lines if "mode" in d}
-    assert set(res) >= {"plain", "dp_graph", "dp_graph_flat", "dp_capture", "plain_eager", "dp_eager"}, \
+    assert set(res) >= {"plain", "dp_graph", "dp_graph_flat", "dp_capture", "plain_eager", "dp_eager",
+                        "dp_graph_fallback"}, \
         (r.returncode, list(res))
     for mode in ("dp_graph", "dp_graph_flat", "dp_capture", "dp_eager"):
         assert res[mode]["backend"] == "nccl", res[mode]
     assert res["dp_graph"]["dp_overlap"] and res["dp_graph"]["buckets"] >= 2 and res["dp_graph"]["grad_is_view"]
-    for mode, ref in (("dp_graph", "plain"), ("dp_graph_flat", "plain"), ("dp_capture", "plain")):
+    # the overlapped capture refused (simulated): one warning, the flat two-graph form, same result
+    assert not res["dp_graph_fallback"]["dp_overlap"] and res["dp_graph_fallback"]["fallback_warned"] == 1
+    assert res["dp_graph"]["fallback_warned"] == 0
+    for mode, ref in (("dp_graph", "plain"), ("dp_graph_flat", "plain"), ("dp_capture", "plain"),
+                      ("dp_graph_fallback", "plain")):
         assert res[mode]["losses"] == res[ref]["losses"], (mode, res[mode]["losses"], res[ref]["losses"])
         assert res[mode]["max_param_diff_vs_" + ref] == 0.0, res[mode]
     la, lb = res["dp_eager"]["losses"], res["plain_eager"]["losses"]

@@ -191,10 +191,15 @@ static int vec_width(int C) { return (C % 8 == 0) ? 8 : (C % 4 == 0) ? 4 : 1; }
 struct RowSlices {
   long S, per;
 };
+// knob "bn_slices": the cap on row slices (blocks per channel group) of the BatchNorm statistics / backward
+// reductions (default 1024; each slice >= 1024 rows): 7M step, 30 steps, 256 -> 14.79 / 14.82 ms, 512 -> 14.78,
+// 1024 -> 14.76 / 14.77, 2048 -> 14.80 (profiles/r05r_bn_slices.log)
+static long g_bn_slices = 1024;
+void set_bn_slices(int v) { g_bn_slices = v < 16 ? 16 : (v > 4096 ? 4096 : v); }
 static RowSlices row_slices(long M) {
   RowSlices r;
   r.S = (M + 1023) / 1024;
-  if (r.S > 256) r.S = 256;
+  if (r.S > g_bn_slices) r.S = g_bn_slices;
   if (r.S < 1) r.S = 1;
   r.per = (M + r.S - 1) / r.S;
   r.S = (M + r.per - 1) / r.per;

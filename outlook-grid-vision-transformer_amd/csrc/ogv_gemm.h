@@ -244,6 +244,7 @@ void set_se_gemv(int v);
 void set_dw_fuse(int v);
 void set_dw_bn2(int v);
 void set_dw_fwd_r(int v);
+void set_bn_slices(int v);
 void set_dw_bwd_r(int v);
 void set_stem(int v);
 void set_pg_tn4_max_m(int v);

@@ -79,31 +79,37 @@ __global__ void bn_coeffs_kernel(const float* __restrict__ S, int K, float n, co
   coef[2 * K + c] = train ? sdyx / n : 0.f;
 }
 
-// Fused column reduction + finalize / coefficients: a block owns 16 channels, its 16 row groups walk
+// Fused column reduction + finalize / coefficients: a block owns 16 channels, its RG row groups walk
 // the [R][ld] partial rows (columns c and K + c) in a fixed order, combined in a fixed order in LDS;
-// one launch instead of colreduce + bn_finalize / bn_coeffs.
-__global__ __launch_bounds__(256) void bn_reduce_finalize_kernel(const double* __restrict__ part, long R, long ld, int K,
+// one launch instead of colreduce + bn_finalize / bn_coeffs.  The walk is latency-bound (a few dozen
+// blocks, thousands of partial rows): knob "bn_red_rg" (16 or 64, default 64) sets the row groups, i.e.
+// the loads in flight per channel (16 x RG threads per block): 7M step, 30 steps x 2, 16 -> 14.743 / 14.757 ms,
+// 64 -> 14.733 / 14.714 (profiles/r05s_bn_red_rg.log)
+static int g_bn_red_rg = 64;
+void set_bn_red_rg(int v) { g_bn_red_rg = v >= 64 ? 64 : 16; }
+template <int RG>
+__global__ __launch_bounds__(16 * RG) void bn_reduce_finalize_kernel(const double* __restrict__ part, long R, long ld, int K,
                                                                  double n, const float* __restrict__ gamma,
                                                                  const float* __restrict__ beta, float eps,
                                                                  float momentum, float* rm, float* rv,
                                                                  float* __restrict__ mean_out,
                                                                  float* __restrict__ invstd_out, float* __restrict__ sc,
                                                                  float* __restrict__ sh) {
-  __shared__ double red[2][16][16];
+  __shared__ double red[2][RG][16];
   const int cl = threadIdx.x & 15, rg = threadIdx.x >> 4;
   const int c = blockIdx.x * 16 + cl;
   double s1 = 0.0, s2 = 0.0;
   if (c < K) {   // four row groups' loads in flight per trip (the loop is latency-bound otherwise)
     double a1[4] = {0.0, 0.0, 0.0, 0.0}, a2[4] = {0.0, 0.0, 0.0, 0.0};
     long r = rg;
-    for (; r + 48 < R; r += 64) {
+    for (; r + 3 * RG < R; r += 4 * RG) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        a1[u] += part[(r + 16 * u) * ld + c];
-        a2[u] += part[(r + 16 * u) * ld + K + c];
+        a1[u] += part[(r + RG * u) * ld + c];
+        a2[u] += part[(r + RG * u) * ld + K + c];
       }
     }
-    for (; r < R; r += 16) {
+    for (; r < R; r += RG) {
       a1[0] += part[r * ld + c];
       a2[0] += part[r * ld + K + c];
     }
@@ -115,8 +121,8 @@ __global__ __launch_bounds__(256) void bn_reduce_finalize_kernel(const double* _
   __syncthreads();
   if (rg != 0 || c >= K) return;
   double t1 = 0.0, t2 = 0.0;
-#pragma unroll
-  for (int g = 0; g < 16; ++g) {
+#pragma unroll 16
+  for (int g = 0; g < RG; ++g) {
     t1 += red[0][g][cl];
     t2 += red[1][g][cl];
   }
@@ -141,13 +147,13 @@ struct Bn2Terms {
   const float *R, *gate, *dpool;
   int HW;
 };
-template <bool TERMS = false>
-__global__ __launch_bounds__(256) void bn_reduce_coeffs_kernel(const float* __restrict__ part, long R, long ld, int K,
+template <bool TERMS, int RG>
+__global__ __launch_bounds__(16 * RG) void bn_reduce_coeffs_kernel(const float* __restrict__ part, long R, long ld, int K,
                                                                float n, const float* __restrict__ gamma,
                                                                const float* __restrict__ invstd,
                                                                float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                                float* __restrict__ coef, int train, Bn2Terms bt = {}) {
-  __shared__ float red[2][16][16];
+  __shared__ float red[2][RG][16];
   const int cl = threadIdx.x & 15, rg = threadIdx.x >> 4;
   const int c = blockIdx.x * 16 + cl;
   float s1 = 0.f, s2 = 0.f;
@@ -168,16 +174,16 @@ __global__ __launch_bounds__(256) void bn_reduce_coeffs_kernel(const float* __re
   if (c < K) {   // four row groups' loads in flight per trip
     float a1[4] = {0.f, 0.f, 0.f, 0.f}, a2[4] = {0.f, 0.f, 0.f, 0.f};
     long r = rg;
-    for (; r + 48 < R; r += 64) {
+    for (; r + 3 * RG < R; r += 4 * RG) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         float v1, v2;
-        row(r + 16 * u, v1, v2);
+        row(r + RG * u, v1, v2);
         a1[u] += v1;
         a2[u] += v2;
       }
     }
-    for (; r < R; r += 16) {
+    for (; r < R; r += RG) {
       float v1, v2;
       row(r, v1, v2);
       a1[0] += v1;
@@ -191,8 +197,8 @@ __global__ __launch_bounds__(256) void bn_reduce_coeffs_kernel(const float* __re
   __syncthreads();
   if (rg != 0 || c >= K) return;
   float sdy = 0.f, sdyx = 0.f;
-#pragma unroll
-  for (int g = 0; g < 16; ++g) {
+#pragma unroll 16
+  for (int g = 0; g < RG; ++g) {
     sdy += red[0][g][cl];
     sdyx += red[1][g][cl];
   }
@@ -206,12 +212,26 @@ __global__ __launch_bounds__(256) void bn_reduce_coeffs_kernel(const float* __re
 void bn_reduce_finalize_launch(const double* part, long R, long ld, int K, double n, const float* gamma,
                                const float* beta, float eps, float momentum, float* rm, float* rv, float* mean,
                                float* invstd, float* sc, float* sh, hipStream_t s) {
-  bn_reduce_finalize_kernel<<<cdiv(K, 16), 256, 0, s>>>(part, R, ld, K, n, gamma, beta, eps, momentum, rm, rv, mean,
-                                                        invstd, sc, sh);
+  if (g_bn_red_rg == 64)
+    bn_reduce_finalize_kernel<64><<<cdiv(K, 16), 16 * 64, 0, s>>>(part, R, ld, K, n, gamma, beta, eps, momentum, rm, rv,
+                                                                   mean, invstd, sc, sh);
+  else
+    bn_reduce_finalize_kernel<16><<<cdiv(K, 16), 16 * 16, 0, s>>>(part, R, ld, K, n, gamma, beta, eps, momentum, rm, rv,
+                                                                   mean, invstd, sc, sh);
+}
+template <bool TERMS = false>
+void bn_reduce_coeffs_run(const float* part, long R, long ld, int K, float n, const float* gamma, const float* invstd,
+                          float* dgamma, float* dbeta, float* coef, int train, hipStream_t s, Bn2Terms bt = {}) {
+  if (g_bn_red_rg == 64)
+    bn_reduce_coeffs_kernel<TERMS, 64><<<cdiv(K, 16), 16 * 64, 0, s>>>(part, R, ld, K, n, gamma, invstd, dgamma, dbeta,
+                                                                       coef, train, bt);
+  else
+    bn_reduce_coeffs_kernel<TERMS, 16><<<cdiv(K, 16), 16 * 16, 0, s>>>(part, R, ld, K, n, gamma, invstd, dgamma, dbeta,
+                                                                       coef, train, bt);
 }
 void bn_reduce_coeffs_launch(const float* part, long R, long ld, int K, float n, const float* gamma,
                              const float* invstd, float* dgamma, float* dbeta, float* coef, int train, hipStream_t s) {
-  bn_reduce_coeffs_kernel<<<cdiv(K, 16), 256, 0, s>>>(part, R, ld, K, n, gamma, invstd, dgamma, dbeta, coef, train);
+  bn_reduce_coeffs_run(part, R, ld, K, n, gamma, invstd, dgamma, dbeta, coef, train, s);
 }
 void bn_finalize_launch(const double* sums, int K, double n, const float* gamma, const float* beta, float eps,
                         float momentum, float* rm, float* rv, float* mean, float* invstd, float* sc, float* sh, int train,
@@ -1492,8 +1512,8 @@ static void mbconv_fwd_impl(const void* x, void* out, const Saved& sv, const Fwd
     if (tr) { e.stat = w.stat1; e.stat_shift = P.bn1_rm; }
     const int R = gemm_fwd_launch(dt, x, s.C, Pro(), P.w_expand, s.C, sv.e, s.mid, (int)M, s.mid, s.C, s.C, s.C, e, st);
     if (tr)
-      bn_reduce_finalize_kernel<<<cdiv(s.mid, 16), 256, 0, st>>>(w.stat1, R, 2L * s.mid, s.mid, (double)M, P.bn1_w, P.bn1_b,
-                                                        s.bn_eps, s.bn_momentum, P.bn1_rm, P.bn1_rv, sv.mean1, sv.inv1, sv.sc1, sv.sh1);
+      bn_reduce_finalize_launch(w.stat1, R, 2L * s.mid, s.mid, (double)M, P.bn1_w, P.bn1_b,
+                                                        s.bn_eps, s.bn_momentum, P.bn1_rm, P.bn1_rv, sv.mean1, sv.inv1, sv.sc1, sv.sh1, st);
     else
       bn_finalize_kernel<<<cdiv(s.mid, 256), 256, 0, st>>>(w.sums, s.mid, (double)M, P.bn1_w, P.bn1_b, s.bn_eps, s.bn_momentum,
                                                          P.bn1_rm, P.bn1_rv, sv.mean1, sv.inv1, sv.sc1, sv.sh1, 0);
@@ -1504,8 +1524,8 @@ static void mbconv_fwd_impl(const void* x, void* out, const Saved& sv, const Fwd
     O::dw_fwd(sv.e, P.w_dw, sv.sc1, sv.sh1, s.act, sv.d, tr ? w.stat2 : nullptr,
                      tr ? P.bn2_rm : nullptr, t, st);
     if (tr)
-      bn_reduce_finalize_kernel<<<cdiv(s.mid, 16), 256, 0, st>>>(w.stat2, t.rows(), 2L * s.mid, s.mid, (double)M, P.bn2_w, P.bn2_b,
-                                                        s.bn_eps, s.bn_momentum, P.bn2_rm, P.bn2_rv, sv.mean2, sv.inv2, sv.sc2, sv.sh2);
+      bn_reduce_finalize_launch(w.stat2, t.rows(), 2L * s.mid, s.mid, (double)M, P.bn2_w, P.bn2_b,
+                                                        s.bn_eps, s.bn_momentum, P.bn2_rm, P.bn2_rv, sv.mean2, sv.inv2, sv.sc2, sv.sh2, st);
     else
       bn_finalize_kernel<<<cdiv(s.mid, 256), 256, 0, st>>>(w.sums, s.mid, (double)M, P.bn2_w, P.bn2_b, s.bn_eps, s.bn_momentum,
                                                          P.bn2_rm, P.bn2_rv, sv.mean2, sv.inv2, sv.sc2, sv.sh2, 0);
@@ -1544,8 +1564,8 @@ static void mbconv_fwd_impl(const void* x, void* out, const Saved& sv, const Fwd
     if (tr) { e.stat = w.stat3; e.stat_shift = P.bn3_rm; }
     const int R = gemm_fwd_launch(dt, sv.d, s.mid, pr, P.w_proj, s.mid, sv.p, s.C, (int)M, s.C, s.mid, s.mid, s.mid, e, st);
     if (tr)
-      bn_reduce_finalize_kernel<<<cdiv(s.C, 16), 256, 0, st>>>(w.stat3, R, 2L * s.C, s.C, (double)M, P.bn3_w, P.bn3_b,
-                                                        s.bn_eps, s.bn_momentum, P.bn3_rm, P.bn3_rv, sv.mean3, sv.inv3, sv.sc3, sv.sh3);
+      bn_reduce_finalize_launch(w.stat3, R, 2L * s.C, s.C, (double)M, P.bn3_w, P.bn3_b,
+                                                        s.bn_eps, s.bn_momentum, P.bn3_rm, P.bn3_rv, sv.mean3, sv.inv3, sv.sc3, sv.sh3, st);
     else
       bn_finalize_kernel<<<cdiv(s.C, 256), 256, 0, st>>>(w.sums, s.C, (double)M, P.bn3_w, P.bn3_b, s.bn_eps, s.bn_momentum,
                                                          P.bn3_rm, P.bn3_rv, sv.mean3, sv.inv3, sv.sc3, sv.sh3, 0);
@@ -1565,8 +1585,7 @@ static void mbconv_bwd_impl(const void* dout, const void* x, const Saved& sv, vo
   {
     const long S = dw_slices(M, rc), per = (M + S - 1) / S;
     OGV_V_DISPATCH(rc.V, O::template bn_reduce, dout, sv.p, sv.mean3, sv.inv3, w.stat, M, s.C, rc, S, per, st);
-    bn_reduce_coeffs_kernel<<<cdiv(s.C, 16), 256, 0, st>>>(w.stat, S, 2L * s.C, s.C, (float)M, P.bn3_w, sv.inv3, G.bn3_w,
-                                                          G.bn3_b, w.coef, s.train);
+    bn_reduce_coeffs_run(w.stat, S, 2L * s.C, s.C, (float)M, P.bn3_w, sv.inv3, G.bn3_w, G.bn3_b, w.coef, s.train, st);
     OGV_V_DISPATCH(rc.V, O::template bn_apply, dout, sv.p, sv.mean3, sv.inv3, w.coef, w.dp, M, s.C, st);
   }
   // B2) project: dA3 = dp . Wp ; dWp = dp^T . (act(BN2(d)) * gate)   (dWp on the side stream)
@@ -1625,9 +1644,8 @@ static void mbconv_bwd_impl(const void* dout, const void* x, const Saved& sv, vo
   const bool bn2f = g_dw_fuse && g_dw_bn2 && dw_dgrad_lds(t6, true, true) <= 64 * 1024;
   {
     // BN2's column sums over the images, the per-image terms formed on the fly (no terms launch)
-    bn_reduce_coeffs_kernel<true><<<cdiv(s.mid, 16), 256, 0, st>>>(nullptr, s.B, 2L * s.mid, s.mid, (float)M, P.bn2_w,
-                                                                   sv.inv2, G.bn2_w, G.bn2_b, w.coef, s.train,
-                                                                   Bn2Terms{w.R, sv.gate, w.dpool, HW});
+    bn_reduce_coeffs_run<true>(nullptr, s.B, 2L * s.mid, s.mid, (float)M, P.bn2_w, sv.inv2, G.bn2_w, G.bn2_b, w.coef,
+                               s.train, st, Bn2Terms{w.R, sv.gate, w.dpool, HW});
     if (!bn2f)
       OGV_V_DISPATCH(rp.V, O::template bn2_apply, w.bufA, sv.d, sv.sc2, sv.sh2, sv.mean2, sv.inv2, sv.gate, w.dpool,
                      w.coef, s.act, w.bufB, M, HW, s.mid, st);
@@ -1666,8 +1684,8 @@ static void mbconv_bwd_impl(const void* dout, const void* x, const Saved& sv, vo
   // B7) BN1 backward: de = ca*(dy1 - cb - ehat*cc)
   {
     const long R1 = dw_tile_plan(s.B, s.H, s.W, s.mid, 4).rows();
-    bn_reduce_coeffs_kernel<<<cdiv(s.mid, 16), 256, 0, st>>>(w.stat, R1, 2L * s.mid, s.mid, (float)M, P.bn1_w, sv.inv1,
-                                                            G.bn1_w, G.bn1_b, w.coef, s.train);
+    bn_reduce_coeffs_run(w.stat, R1, 2L * s.mid, s.mid, (float)M, P.bn1_w, sv.inv1, G.bn1_w, G.bn1_b, w.coef, s.train,
+                         st);
   }
   OGV_V_DISPATCH(rp.V, O::template bn_apply, dy1, sv.e, sv.mean1, sv.inv1, w.coef, de, M, s.mid, st);
   // B8) expand: dx = de . We + dout (residual) ; dWe = de^T . x

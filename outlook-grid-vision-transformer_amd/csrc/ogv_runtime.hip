@@ -8,6 +8,8 @@
 
 namespace ogv {
 
+void set_bn_red_rg(int v);   // ogv_mbconv.hip
+
 static thread_local char g_err[512] = "";
 
 void set_error(const char* fmt, ...) {
@@ -250,6 +252,14 @@ extern "C" int ogv_set_option(const char* name, int value) {
   }
   if (!strcmp(name, "dw_bwd_r")) {
     set_dw_bwd_r(value);
+    return OGV_OK;
+  }
+  if (!strcmp(name, "bn_red_rg")) {
+    set_bn_red_rg(value);
+    return OGV_OK;
+  }
+  if (!strcmp(name, "bn_slices")) {
+    set_bn_slices(value);
     return OGV_OK;
   }
   if (!strcmp(name, "dw_fwd_r")) {

@@ -329,7 +329,7 @@ struct CbWs {
 static CbWs cb_ws(const ogv_convbn_desc& d, ogv_dtype dt, void* base) {
   const CbGeom g = cb_geom(d);
   const int K9 = 9 * d.Cin;
-  const long nMt = gemm_stat_rows((int)g.Mo);
+  const long nMt = conv_stat_rows((int)g.Mo);
   const RowSlices rs = row_slices(g.Mo);
   const long srows = nMt > rs.S ? nMt : rs.S;
   Carve c(base);
@@ -395,7 +395,7 @@ extern "C" int ogv_convbn_fwd(const void* x, void* out, void* saved, void* ws, c
   // the stem (C_in <= 3): dedicated kernel (ogv_stem.hip); everything else: implicit-GEMM conv kernels
   int srows = gemm_stat_rows((int)g.Mo);
   if (!(dt == OGV_BF16 && stem_fwd_try(x, g.fwd, wt, y, (int)g.Mo, d->Cout, e, s, &srows)))
-    conv_gemm_launch(dt, x, g.fwd, wt, y, (int)g.Mo, d->Cout, e, s);
+    srows = conv_gemm_launch(dt, x, g.fwd, wt, y, (int)g.Mo, d->Cout, e, s);
   if (d->has_bn) {
     if (stats)   // partial rows -> batch statistics, running stats, apply coefficients: one launch
       bn_reduce_finalize_launch(w.dstat, srows, 2L * d->Cout, d->Cout, (double)g.Mo, p->bn_w,

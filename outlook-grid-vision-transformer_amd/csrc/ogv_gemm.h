@@ -133,6 +133,8 @@ __device__ __forceinline__ long conv_src(const ConvG& g, const ConvRow& r, int t
 
 constexpr int GEMM_BM = 128;
 inline int gemm_stat_rows(int M) { return (M + GEMM_BM - 1) / GEMM_BM; }
+// BatchNorm partial rows an implicit-conv forward may write (conv_gemm_launch: 64-row panels on small M)
+inline int conv_stat_rows(int M) { return (M + 63) / 64; }
 
 // out[M,N] = epi( pro(A)[M,K] . W[N,K]^T );  Ka / Kb = valid reduction columns of A / W.
 // Returns the number of BatchNorm partial rows written to epi.stat (<= gemm_stat_rows(M)); the
@@ -164,7 +166,7 @@ void transpose_f32_launch(const float* W, float* WT, int N, int K, int ldt, hipS
 // Implicit-GEMM 3x3 conv:  out[M, N] = epi( gather(A)[M, 9*Cs] . Wt[N, 9*Cs]^T ),  M = B*Hr*Wr.
 // Wt is tap-major ([N][tap][Cs]).  Used for the conv forward (cv.transposed = 0) and its data
 // gradient (cv.transposed = 1, Wt = the tap-major transposed weights).
-void conv_gemm_launch(ogv_dtype dt, const void* A, const ConvG& cv, const float* Wt, void* out, int M, int N,
+int conv_gemm_launch(ogv_dtype dt, const void* A, const ConvG& cv, const float* Wt, void* out, int M, int N,
                       const Epi& epi, hipStream_t s);
 
 // Persistent streaming GEMM (ogv_sgemm.hip) for tall-skinny bf16 shapes; 0 / false = not handled.
@@ -245,6 +247,7 @@ void set_dw_fuse(int v);
 void set_dw_bn2(int v);
 void set_dw_fwd_r(int v);
 void set_bn_slices(int v);
+void set_pg_conv_rs1(int v);
 void set_dw_bwd_r(int v);
 void set_stem(int v);
 void set_pg_tn4_max_m(int v);

@@ -1199,17 +1199,20 @@ static void launch_conv_mm(const void* A, const ConvG& cv, const float* Wt, void
   }
 }
 
-void conv_gemm_launch(ogv_dtype dt, const void* A, const ConvG& cv, const float* Wt, void* out, int M, int N,
-                      const Epi& epi, hipStream_t s) {
-  if (M <= 0) return;
+int conv_gemm_launch(ogv_dtype dt, const void* A, const ConvG& cv, const float* Wt, void* out, int M, int N,
+                     const Epi& epi, hipStream_t s) {
+  if (M <= 0) return 1;
   const int K = 9 * cv.Cs;
   const bool st = epi.stat != nullptr;
-  // the pipelined panel kernel with implicit-conv A fragments (8 | Cs), BN partial rows per 128-row
-  // panel exactly like the tiled kernel's (gemm_stat_rows)
-  if (dt == OGV_BF16 && pgemm_conv_try(A, cv, Wt, out, M, N, epi, s)) return;
+  // the pipelined panel kernel with implicit-conv A fragments (8 | Cs): BN partial rows per 128-row panel
+  // (or per 64-row panel on small M, knob pg_conv_rs1: at most conv_stat_rows(M)), the count returned
+  if (dt == OGV_BF16) {
+    const int rows = pgemm_conv_try(A, cv, Wt, out, M, N, epi, s);
+    if (rows) return rows;
+  }
   if (dt == OGV_BF16 && !epi.stat && !epi.res && !epi.zact && !epi.bias && !epi.rs &&
       pgemm_tconv_try(A, cv, Wt, out, M, N, s))
-    return;
+    return 1;
   if (dt == OGV_BF16) {
     if (st) launch_conv_mm<bf16, true>(A, cv, Wt, out, M, N, K, epi, s);
     else launch_conv_mm<bf16, false>(A, cv, Wt, out, M, N, K, epi, s);
@@ -1217,6 +1220,7 @@ void conv_gemm_launch(ogv_dtype dt, const void* A, const ConvG& cv, const float*
     if (st) launch_conv_mm<float, true>(A, cv, Wt, out, M, N, K, epi, s);
     else launch_conv_mm<float, false>(A, cv, Wt, out, M, N, K, epi, s);
   }
+  return gemm_stat_rows(M);
 }
 
 // ------------------------------------------------------------------ small-M fp32 GEMMs (SE MLP)

@@ -7,7 +7,7 @@
 //
 // The tensor table travels in kernel arguments (64 tensors per launch, AdamWBatch below), so a
 // hipGraph captured over a step bakes the parameter / gradient / moment pointers into its nodes
-// and no host->device table copy is needed.  Work unit = one chunk of up to OPT_CHUNK elements of
+// and no host->device table copy is needed.  Work unit = one chunk of up to opt_chunk elements of
 // one tensor (one workgroup).
 //   pass 1 (adamw_norm_kernel): per-chunk sum of grad^2 -> norm_ws[chunk]; the first workgroup of
 //          each launch advances its tensors' step counters unless found_inf is set;
@@ -23,8 +23,14 @@
 
 namespace ogv {
 
-constexpr int OPT_CHUNK = 8192;
 constexpr int OPT_MAXT = 64;
+// knob "opt_chunk": elements per workgroup (a power of two, 1024-16384; default 2048: more workgroups per launch)
+static int g_opt_chunk = 2048;   // 7M step, 30 steps: 8192 14.831 / 14.825, 4096 14.814, 2048 14.810 / 14.815, 1024 14.831 ms (profiles/r05t_opt_chunk.log)
+void set_opt_chunk(int v) {
+  int c = 1024;
+  while (c < v && c < 16384) c <<= 1;
+  g_opt_chunk = c;
+}
 
 struct AdamWBatch {
   float* p[OPT_MAXT];
@@ -37,6 +43,7 @@ struct AdamWBatch {
   unsigned char group[OPT_MAXT];
   int n;                         // tensors in this launch
   int chunk_base;                // global index of this launch's first chunk in norm_ws
+  int csz;                       // elements per chunk
 };
 
 struct AdamWGroups {
@@ -72,8 +79,8 @@ __global__ __launch_bounds__(256) void adamw_norm_kernel(AdamWBatch b, const flo
   const int chunk = blockIdx.x;
   const int t = opt_find(b, chunk);
   const int c0 = t ? b.chunk_end[t - 1] : 0;
-  const long e0 = (long)(chunk - c0) * OPT_CHUNK;
-  const int n = min((long)OPT_CHUNK, (long)b.numel[t] - e0);
+  const long e0 = (long)(chunk - c0) * b.csz;
+  const int n = min((long)b.csz, (long)b.numel[t] - e0);
   const float* __restrict__ g = b.g[t] + e0;
   float s = 0.f;
   if ((reinterpret_cast<uintptr_t>(g) & 15) == 0) {
@@ -108,8 +115,8 @@ __global__ __launch_bounds__(256) void adamw_update_kernel(AdamWBatch b, AdamWGr
   const int chunk = blockIdx.x;
   const int t = opt_find(b, chunk);
   const int c0 = t ? b.chunk_end[t - 1] : 0;
-  const long e0 = (long)(chunk - c0) * OPT_CHUNK;
-  const int n = min((long)OPT_CHUNK, (long)b.numel[t] - e0);
+  const long e0 = (long)(chunk - c0) * b.csz;
+  const int n = min((long)b.csz, (long)b.numel[t] - e0);
   const int gi = b.group[t];
   const float lr = *G.lr[gi], wd = G.wd[gi], b1 = G.beta1[gi], b2 = G.beta2[gi], eps = G.eps[gi];
   const float omb1 = G.omb1[gi], omb2 = G.omb2[gi];
@@ -157,7 +164,7 @@ __global__ __launch_bounds__(256) void adamw_update_kernel(AdamWBatch b, AdamWGr
   }
 }
 
-static int opt_chunks(long long numel) { return (int)((numel + OPT_CHUNK - 1) / OPT_CHUNK); }
+static int opt_chunks(long long numel) { return (int)((numel + g_opt_chunk - 1) / g_opt_chunk); }
 
 }  // namespace ogv
 
@@ -197,6 +204,7 @@ extern "C" int ogv_clip_adamw(const ogv_adamw_tensor* tensors, int n, const ogv_
       batches.emplace_back();
       std::memset(&batches.back(), 0, sizeof(AdamWBatch));
       batches.back().chunk_base = total;
+      batches.back().csz = g_opt_chunk;
     }
     AdamWBatch& b = batches.back();
     const int k = b.n++;

@@ -612,7 +612,13 @@ static bool al16p(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) 
 // than 1/16 (then 192, then 64),
 // then enough workgroups (>= 2 per CU) by halving the rows; BatchNorm statistics need the 128-row
 // panel (one partial row per gemm_stat_rows panel).
-static PgPlan pg_plan(int M, int N, int K, bool stats, bool sw, bool bt, bool pa, bool gate) {
+// knob "pg_conv_rs1": 1 (default) lets the implicit-conv forward WITH BatchNorm statistics take 64-row panels
+// when 128-row ones would leave fewer than 512 tiles (the caller sizes the partial rows for M / 64): the 7M
+// stage-3 downsample (M = 8192, K = 1728) gets two workgroups per CU; 7M 14.751 / 14.769 -> 14.722 / 14.747 ms,
+// 14M unchanged (profiles/r05u_pg_conv_rs1.log)
+static int g_pg_conv_rs1 = 1;
+void set_pg_conv_rs1(int v) { g_pg_conv_rs1 = v ? 1 : 0; }
+static PgPlan pg_plan(int M, int N, int K, bool stats, bool sw, bool bt, bool pa, bool gate, bool stats_rs1 = false) {
   PgPlan p;
   if (!g_pgemm || M <= 0 || (N & 7) || (K & 7)) return p;
   // 64-column tiles first at every shape: round 4 re-measured on the whole 7M step (paired 30-step
@@ -642,7 +648,7 @@ static PgPlan pg_plan(int M, int N, int K, bool stats, bool sw, bool bt, bool pa
   p.nNt = (N + 16 * p.TN - 1) / (16 * p.TN);
   p.RS = 2;
   if (p.TN == 12) p.RS = 1;
-  else if (!stats && !g_pg_rs) {
+  else if ((!stats || stats_rs1) && !g_pg_rs) {
     const long wg2 = (long)((M + 127) / 128) * p.nNt;
     if (wg2 < 512) p.RS = 1;
   }
@@ -678,6 +684,9 @@ static void pg_tiles(const PgPlan& p, const bf16* A, int lda, const Pro& pro, co
       if (p.TN == 12) {
         if constexpr (!GT) OGV_PG(1, 12);
       } else if (p.TN == 8) OGV_PG(1, 8);
+      else OGV_PG(1, 4);
+    } else if constexpr (CV) {   // 64-row panels with statistics: the implicit-conv forward only
+      if (p.TN == 8) OGV_PG(1, 8);
       else OGV_PG(1, 4);
     }
   }
@@ -791,7 +800,7 @@ int pgemm_conv_try(const void* A, const ConvG& cv, const float* Wt, void* out, i
     return 0;
   const bool st = epi.stat != nullptr;
   const bool sw = (split_w() & (cv.transposed ? 2 : 1)) != 0 && (g_pg_split & 2);
-  const PgPlan p = pg_plan(M, N, K, st, sw, false, false, false);
+  const PgPlan p = pg_plan(M, N, K, st, sw, false, false, false, g_pg_conv_rs1 != 0);
   if (!p.ok) return 0;
   const bf16* a = static_cast<const bf16*>(A);
   bf16* o = static_cast<bf16*>(out);

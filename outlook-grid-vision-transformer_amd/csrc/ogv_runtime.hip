@@ -9,6 +9,7 @@
 namespace ogv {
 
 void set_bn_red_rg(int v);   // ogv_mbconv.hip
+void set_opt_chunk(int v);   // ogv_optim.hip
 
 static thread_local char g_err[512] = "";
 
@@ -254,8 +255,16 @@ extern "C" int ogv_set_option(const char* name, int value) {
     set_dw_bwd_r(value);
     return OGV_OK;
   }
+  if (!strcmp(name, "opt_chunk")) {
+    set_opt_chunk(value);
+    return OGV_OK;
+  }
   if (!strcmp(name, "bn_red_rg")) {
     set_bn_red_rg(value);
+    return OGV_OK;
+  }
+  if (!strcmp(name, "pg_conv_rs1")) {
+    set_pg_conv_rs1(value);
     return OGV_OK;
   }
   if (!strcmp(name, "bn_slices")) {

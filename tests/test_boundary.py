@@ -284,3 +284,33 @@ def test_outlook_vproj_plan_and_knob():
     assert rc != 0 and b"unsupported" in lib.ogv_last_error()
     rc = lib.ogv_outlook_vproj_fwd(None, 48, x, None, None, 72, x, 2, 8, 8, 48, 2, 3, L.OGV_BF16, None)
     assert rc != 0 and b"null" in lib.ogv_last_error()
+
+
+def test_workspace_sizes_follow_their_knobs():
+    """Host-side workspace queries (no GPU): the cap on BatchNorm reduction slices (knob bn_slices,
+    default 1024) and the AdamW work unit (knob opt_chunk, default 2048 elements) size the workspaces
+    the launches then use -- the query and the launch read the same knob."""
+    import ctypes
+    import ogv._lib as L
+    lib = L.load()
+    M, C = 524288, 64
+    try:
+        assert lib.ogv_set_option(b"bn_slices", 256) == 0
+        small = lib.ogv_bn_act_ws_bytes(M, C)
+        assert lib.ogv_set_option(b"bn_slices", 1024) == 0
+        big = lib.ogv_bn_act_ws_bytes(M, C)
+        assert big > small > 0
+    finally:
+        assert lib.ogv_set_option(b"bn_slices", 1024) == 0
+    t = (L.AdamWTensor * 2)()
+    t[0].numel, t[1].numel = 10000, 1
+    try:
+        assert lib.ogv_set_option(b"opt_chunk", 8192) == 0
+        assert lib.ogv_clip_adamw_ws_bytes(t, 2) == 4 * (2 + 1)
+        assert lib.ogv_set_option(b"opt_chunk", 2048) == 0
+        assert lib.ogv_clip_adamw_ws_bytes(t, 2) == 4 * (5 + 1)
+        assert lib.ogv_set_option(b"opt_chunk", 3000) == 0          # rounded up to a power of two: 4096
+        assert lib.ogv_clip_adamw_ws_bytes(t, 2) == 4 * (3 + 1)
+    finally:
+        assert lib.ogv_set_option(b"opt_chunk", 2048) == 0
+    assert lib.ogv_set_option(b"bn_red_rg", 64) == 0 and lib.ogv_set_option(b"pg_conv_rs1", 1) == 0

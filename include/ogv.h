@@ -58,7 +58,11 @@ const char* ogv_last_error(void);
  *   column-reduce launch (measured slower); "grid_big" 0/1/2 (default 2): one-(group, head)-pair-per-block
  *   LDS-resident grid attention for groups too large for the multi-pair kernels off / first generation /
  *   second generation (exp2 + lazy rescale + paired 16x16x32 MFMAs); "vp_dbg", "pg_dbg": phase-skipping timing experiments
- *   (wrong results).
+ *   (wrong results); "bn_slices" (default 1024): cap on the row slices of the conv+BN statistics / backward
+ *   reductions; "bn_red_rg" 16 / 64 (default): row groups per block of the fused BatchNorm finalize /
+ *   coefficient reductions; "opt_chunk" (default 2048): elements per workgroup of ogv_clip_adamw (also
+ *   sizes ogv_clip_adamw_ws_bytes); "pg_conv_rs1" 0 / 1 (default): 64-row statistics panels for small
+ *   implicit-conv forwards.
  * Options pick kernel plans, and every *_ws_bytes query sizes the workspace for the plans in force
  * when it is called: set options first, then size workspaces (a workspace sized under other option
  * values can be too small -- e.g. wg_blocks / wg_tile / swg_min_m change the split-M partial count).

@@ -394,8 +394,8 @@ def main():
                        "execution": "hipGraph replay" if trainer.graphs else "eager launches",
                        "backend": trainer.backend or "none (single process, no collective)",
                        "dp_collective": (None if not trainer.dp else
-                                         f"{len(trainer._gbuckets)} bucketed all_reduces captured in the step graph on a "
-                                         "side stream, each launched as backward completes its bucket"
+                                         f"{len(trainer._gbuckets)} bucketed all_reduces captured in the step graph (on "
+                                         "RCCL's stream), each launched as backward completes its bucket"
                                          if getattr(trainer, "dp_overlap", False) and hasattr(trainer, "_gbuckets") else
                                          "all_reduce captured in the step graph"
                                          if trainer.dp_capture_collective else

@@ -998,6 +998,39 @@ __device__ __forceinline__ bool ew_idx(const EwPlan& p, int V, int& c0, long& m0
   return true;
 }
 
+// A3 = act(d*sc2 + sh2) * gate, rounded to T once: the project GEMM's input with exactly the arithmetic
+// of the GEMM kernels' A prologue (knob mb_a3), so the GEMM and its weight gradient run prologue-free
+template <typename T, int V, int ACT>
+__global__ __launch_bounds__(256) void a3_kernel(const T* __restrict__ d, const float* __restrict__ sc,
+                                                 const float* __restrict__ sh, const float* __restrict__ gate,
+                                                 T* __restrict__ out, long M, int HW, int K, EwPlan ep) {
+  int c0;
+  long m0;
+  if (!ew_idx(ep, V, c0, m0)) return;
+  float s[V], h[V];
+  load_vec<float, V>(sc + c0, s);
+  load_vec<float, V>(sh + c0, h);
+  float dv[EW_RPT][V];
+#pragma unroll
+  for (int j = 0; j < EW_RPT; ++j) {
+    const long m = min(m0 + (long)j * ep.RB, M - 1);
+    load_vec<T, V>(d + m * K + c0, dv[j]);
+  }
+#pragma unroll
+  for (int j = 0; j < EW_RPT; ++j) {
+    const long m = m0 + (long)j * ep.RB;
+    if (m >= M) break;
+    float gt[V], o[V];
+    load_vec<float, V>(gate + (m / HW) * K + c0, gt);
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      o[i] = act_fwd(ACT, fmaf(dv[j][i], s[i], h[i]));
+      o[i] *= gt[i];
+    }
+    store_vec<T, V>(out + m * K + c0, o);
+  }
+}
+
 // dd = ca*(dy2 - cb - dh*cc), dy2 = (dA3*gate + dpool/HW) * act'(d*sc2+sh2)
 template <typename T, int V, int ACT>
 __global__ __launch_bounds__(256) void bn2_apply_kernel(const T* __restrict__ dA3, const T* __restrict__ d,
@@ -1159,8 +1192,24 @@ struct Buf {
 };
 
 // Saved-for-backward layout (lives in the caller's `saved` buffer).
+// knob "mb_a3": once the SE gate is known, one elementwise pass writes the project GEMM's input
+// A3 = act(BN2(d)) * gate (the GEMM prologue's arithmetic), and the project GEMM runs without an A prologue
+// (recomputed per element -- and per column tile -- the SiLU's exp / rcp made it 0.42-0.47 ms of the 7M step,
+// profiles/r05x_mb_a3_rejected.txt).  1 (default): A3 lives in the forward workspace (no extra memory: the
+// backward's workspace is larger), the weight gradient keeps its prologue; 2: A3 is saved for the backward
+// too (+1 [M, 4C] activation per MBConv -- Model-A-22M at 224^2, bs 128 then no longer fits 288 GB), the
+// weight gradient prologue-free as well; 0: the prologue form everywhere; 3 (default): 2 for an MBConv whose A3
+// takes at most 512 MB, else 1 (7M, 30 steps: 0 -> 14.76-14.79 ms, 1 -> 14.69-14.70, 2 -> 14.60-14.63;
+// 22M 339.5 -> 338.9 ms with 1; profiles/r05ac_mb_a3.log)
+static int g_mb_a3 = 3;
+void set_mb_a3(int v) { g_mb_a3 = v < 0 ? 0 : (v > 3 ? 3 : v); }
+static int a3_mode(const ogv_mbconv_desc& s, size_t esz) {
+  if (g_mb_a3 != 3) return g_mb_a3;
+  return (size_t)s.B * s.H * s.W * s.mid * esz <= (512u << 20) ? 2 : 1;
+}
 struct Saved {
   void *e, *d, *p;                             // [M,mid], [M,mid], [M,C] activation dtype
+  void* a3;                                    // [M,mid] act(BN2(d)) * gate (knob mb_a3 = 2 only)
   float *mean1, *inv1, *sc1, *sh1;             // [mid]
   float *mean2, *inv2, *sc2, *sh2;             // [mid]
   float *mean3, *inv3, *sc3, *sh3;             // [C]
@@ -1173,6 +1222,7 @@ static Saved saved_layout(void* base, const ogv_mbconv_desc& s, size_t esz, size
   v.e = b.take<char>(M * s.mid * esz);
   v.d = b.take<char>(M * s.mid * esz);
   v.p = b.take<char>(M * s.C * esz);
+  v.a3 = a3_mode(s, esz) == 2 ? b.take<char>(M * s.mid * esz) : nullptr;
   v.mean1 = b.take<float>(s.mid); v.inv1 = b.take<float>(s.mid); v.sc1 = b.take<float>(s.mid); v.sh1 = b.take<float>(s.mid);
   v.mean2 = b.take<float>(s.mid); v.inv2 = b.take<float>(s.mid); v.sc2 = b.take<float>(s.mid); v.sh2 = b.take<float>(s.mid);
   v.mean3 = b.take<float>(s.C); v.inv3 = b.take<float>(s.C); v.sc3 = b.take<float>(s.C); v.sh3 = b.take<float>(s.C);
@@ -1196,8 +1246,9 @@ struct FwdWs {
   double *stat1, *stat2, *stat3, *sums, *tmp;  // fp64 BatchNorm batch statistics
   float* split;                                // SE split-K partials
   char* gemm;
+  void* a3;                                    // mb_a3 = 1: [M,mid] A3 (within the backward's workspace size)
 };
-static FwdWs fwd_ws_layout(void* base, const ogv_mbconv_desc& s, size_t* total) {
+static FwdWs fwd_ws_layout(void* base, const ogv_mbconv_desc& s, size_t esz, size_t* total) {
   Buf b(base);
   const long M = (long)s.B * s.H * s.W;
   RowPlan rp = row_plan(s.mid);
@@ -1212,6 +1263,7 @@ static FwdWs fwd_ws_layout(void* base, const ogv_mbconv_desc& s, size_t* total) 
   w.tmp = b.take<double>(colreduce_tmp_floats(Rmax, 2L * (s.mid > s.C ? s.mid : s.C)) + 16);
   w.split = b.take<float>(std::max(splitk_ws_bytes(s.B, s.se, s.mid), splitk_ws_bytes(s.B, s.mid, s.se)) / 4 + 64);
   w.gemm = b.take<char>(64);
+  w.a3 = a3_mode(s, esz) == 1 ? b.take<char>(M * s.mid * esz) : nullptr;
   if (total) *total = b.off + 256;
   return w;
 }
@@ -1479,6 +1531,19 @@ struct Ops {
 #undef OGV_BN2
   }
   template <int V>
+  static void a3(const void* d, const float* sc, const float* sh, const float* gate, int act, void* out, long M, int HW,
+                 int K, hipStream_t st) {
+    const EwPlan ep = ew_plan(M, K, V);
+#define OGV_A3(A) a3_kernel<T, V, A><<<ep.grid(), 256, 0, st>>>((const T*)d, sc, sh, gate, (T*)out, M, HW, K, ep)
+    switch (act) {
+      case OGV_ACT_SILU: OGV_A3(OGV_ACT_SILU); break;
+      case OGV_ACT_GELU: OGV_A3(OGV_ACT_GELU); break;
+      case OGV_ACT_RELU: OGV_A3(OGV_ACT_RELU); break;
+      default: OGV_A3(OGV_ACT_NONE);
+    }
+#undef OGV_A3
+  }
+  template <int V>
   static void bn_reduce(const void* dy, const void* x, const float* mean, const float* inv, float* stat, long M, int K,
                         const RowPlan& rp, long S, long per, hipStream_t st) {
     bn_bwd_reduce_kernel<T, V><<<xcd_grid((long)cdiv(K, 4 * V) * S), 256, 0, st>>>((const T*)dy, (const T*)x, mean, inv, stat, M,
@@ -1560,9 +1625,17 @@ static void mbconv_fwd_impl(const void* x, void* out, const Saved& sv, const Fwd
     pr.gate = sv.gate;
     pr.rps = HW;
     pr.gld = s.mid;
+    const void* a = sv.d;
+    const int am = a3_mode(s, sizeof(T));
+    if (am) {   // A3 materialised (kept for the backward in mode 2): a prologue-free GEMM
+      void* a3 = am == 2 ? sv.a3 : w.a3;
+      OGV_V_DISPATCH(rp.V, O::template a3, sv.d, sv.sc2, sv.sh2, sv.gate, s.act, a3, M, HW, s.mid, st);
+      pr = Pro();
+      a = a3;
+    }
     Epi e;
     if (tr) { e.stat = w.stat3; e.stat_shift = P.bn3_rm; }
-    const int R = gemm_fwd_launch(dt, sv.d, s.mid, pr, P.w_proj, s.mid, sv.p, s.C, (int)M, s.C, s.mid, s.mid, s.mid, e, st);
+    const int R = gemm_fwd_launch(dt, a, s.mid, pr, P.w_proj, s.mid, sv.p, s.C, (int)M, s.C, s.mid, s.mid, s.mid, e, st);
     if (tr)
       bn_reduce_finalize_launch(w.stat3, R, 2L * s.C, s.C, (double)M, P.bn3_w, P.bn3_b,
                                                         s.bn_eps, s.bn_momentum, P.bn3_rm, P.bn3_rv, sv.mean3, sv.inv3, sv.sc3, sv.sh3, st);
@@ -1600,8 +1673,10 @@ static void mbconv_bwd_impl(const void* dout, const void* x, const Saved& sv, vo
     pr.gate = sv.gate;
     pr.rps = HW;
     pr.gld = s.mid;
-    gemm_wgrad_launch(dt, w.dp, s.C, sv.d, s.mid, pr, nullptr, 1, G.w_proj, nullptr, (int)M, s.C, s.mid, w.wg_proj, sd,
-                      nullptr, true);
+    const bool a3 = a3_mode(s, sizeof(T)) == 2 && sv.a3;   // the forward's A3 (the prologue's values)
+    if (a3) pr = Pro();
+    gemm_wgrad_launch(dt, w.dp, s.C, a3 ? sv.a3 : sv.d, s.mid, pr, nullptr, 1, G.w_proj, nullptr, (int)M, s.C, s.mid,
+                      w.wg_proj, sd, nullptr, true);
   }
   // B3) one pass over (dA3, d): SE gate grads + BN2 partial sums per image
   // (+ dz2 = dgate * g * (1 - g), the gate's sigmoid backward, written by the same reduce)
@@ -1721,7 +1796,7 @@ extern "C" size_t ogv_mbconv_saved_bytes(const ogv_mbconv_desc* s, ogv_dtype dt)
 extern "C" size_t ogv_mbconv_ws_bytes(const ogv_mbconv_desc* s, ogv_dtype dt) {
   if (!s) return 0;
   size_t a = 0, b = 0;
-  fwd_ws_layout(nullptr, *s, &a);
+  fwd_ws_layout(nullptr, *s, dt == OGV_BF16 ? 2 : 4, &a);
   bwd_ws_layout(nullptr, *s, dt == OGV_BF16 ? 2 : 4, &b);
   return a > b ? a : b;
 }
@@ -1736,7 +1811,7 @@ extern "C" int ogv_mbconv_fwd(const void* x, void* out, void* saved, void* ws, c
   OGV_REQUIRE(P->bn1_rm && P->bn1_rv && P->bn2_rm && P->bn2_rv && P->bn3_rm && P->bn3_rv,
               "ogv_mbconv_fwd: missing BatchNorm running statistics");
   Saved sv = saved_layout(saved, *s, dt == OGV_BF16 ? 2 : 4, nullptr);
-  FwdWs w = fwd_ws_layout(ws, *s, nullptr);
+  FwdWs w = fwd_ws_layout(ws, *s, dt == OGV_BF16 ? 2 : 4, nullptr);
   if (dt == OGV_BF16) mbconv_fwd_impl<bf16>(x, out, sv, w, *s, *P, dt, as_stream(stream));
   else mbconv_fwd_impl<float>(x, out, sv, w, *s, *P, dt, as_stream(stream));
   return check_launch("ogv_mbconv_fwd");

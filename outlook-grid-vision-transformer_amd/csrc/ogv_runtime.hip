@@ -10,6 +10,7 @@ namespace ogv {
 
 void set_bn_red_rg(int v);   // ogv_mbconv.hip
 void set_opt_chunk(int v);   // ogv_optim.hip
+void set_mb_a3(int v);       // ogv_mbconv.hip
 
 static thread_local char g_err[512] = "";
 
@@ -261,6 +262,10 @@ extern "C" int ogv_set_option(const char* name, int value) {
   }
   if (!strcmp(name, "bn_red_rg")) {
     set_bn_red_rg(value);
+    return OGV_OK;
+  }
+  if (!strcmp(name, "mb_a3")) {
+    set_mb_a3(value);
     return OGV_OK;
   }
   if (!strcmp(name, "pg_conv_rs1")) {

@@ -1115,3 +1115,42 @@ def test_outlook_vproj_wide_train_grads_full_size_match_unfused(shape, vp_big):
         assert fx.maxabs(a, r) <= (3 if i >= 2 else 1) * 1e-2 * max(1.0, r.abs().max().item()), (shape, i)
     with pytest.raises(ValueError):
         OF.outlook_vproj(x.clone().requires_grad_(), w, b, C, B, H, W, h, 3, save_cat=False)
+
+
+@pytest.mark.parametrize("C,H,B", [(48, 32, 4), (96, 16, 3), (192, 8, 2), (256, 4, 5), (20, 6, 2)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("mode", [1, 2, 3])
+def test_mbconv_materialised_a3_matches_prologue(C, H, B, dtype, mode):
+    """mb_a3 = 1 / 2 (one elementwise pass writes A3 = act(BN2(d)) * gate once the SE gate is known; the
+    project GEMM -- with 2 also its weight gradient, A3 then saved -- runs prologue-free on it) against
+    mb_a3 = 0 (both recompute it in their A prologue).  The pass uses the prologue's own arithmetic (fmaf,
+    act, * gate, one rounding to the storage type), so bf16 is bit-identical wherever the GEMMs run on the
+    panel / streaming / split-M kernels; the fp32 GEMMs' generic prologue multiplies then adds (two
+    roundings), hence 1e-5."""
+    from ogv._lib import load
+    from src.model.mbc_conv import MBConv, MBConvConfig
+    lib = load()
+    torch.manual_seed(C + H + B)
+    m = MBConv(C, C, 1, MBConvConfig()).to(DEV)
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    x = torch.randn(B, C, H, H, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+    dy = torch.randn_like(x)
+    res = []
+    try:
+        for knob in (0, mode):
+            assert lib.ogv_set_option(b"mb_a3", knob) == 0
+            m.load_state_dict(sd)
+            m.zero_grad(set_to_none=True)
+            xx = x.clone().requires_grad_()
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=dtype == torch.bfloat16):
+                y = m.train()(xx)
+            y.backward(dy)
+            res.append([y.detach().float(), xx.grad.float()] + [p.grad.clone() for p in m.parameters()]
+                       + [b.float().clone() for b in m.buffers() if b.is_floating_point()])
+    finally:
+        assert lib.ogv_set_option(b"mb_a3", 3) == 0
+    for k, (a, b) in enumerate(zip(*res)):
+        if dtype == torch.bfloat16:
+            assert torch.equal(a, b), (k, fx.maxabs(b, a))
+        else:
+            assert fx.maxabs(b, a) <= 1e-5 * max(1.0, a.abs().max().item()), (k, fx.maxabs(b, a))

@@ -8,7 +8,10 @@ A step = one full training iteration on a synthetic batch already resident in HB
 autocast(bf16) forward through the HIP OutGridBlock kernels, CE(label smoothing 0.1), backward,
 clip_grad_norm(1.0), fused AdamW, WarmupCosine — bs=512 per GPU (weak scaling).  The step runs
 as a replayed hipGraph (ogv.train.Trainer, graphs=True; --eager for plain launches); for N>1 the
-gradients are averaged by one RCCL all_reduce of a flat bucket between two graphs.
+gradients are averaged by ~8 MB bucketed RCCL all_reduces recorded INSIDE the step's one graph, each
+launched as soon as backward has produced its bucket (overlapping the rest of the backward;
+--dp-flat: one flat all_reduce between two graphs, --dp-capture: one flat all_reduce captured at
+the end of the graph).
 Prints ONE JSON line on rank 0 with `roofline` (dominant kernel: HIP events around every launch
 of it in one step — in graph mode an eager step right after the timed replays, since ROCm graphs
 cannot hold timing events) and `cpu_baseline`
@@ -324,6 +327,21 @@ def main():
         elapsed = t.item()
     whatif = any(o.split("=")[0] in ("skip", "pg_dbg", "vp_dbg") and o.split("=")[1] != "0" for o in args.opt)
     assert whatif or torch.isfinite(loss).item(), "non-finite loss"   # (what-if timing runs leave outputs unwritten)
+    # device memory of the benchmarked run (the reference logs the same two peaks every epoch,
+    # src/training/train_full_model.py:19-20,184-185): warm-up + capture + the timed steps
+    gib = float(2 ** 30)
+    free_b, total_b = torch.cuda.mem_get_info(device)
+    memory = {"peak_alloc_gib": round(torch.cuda.max_memory_allocated(device) / gib, 3),
+              "peak_reserved_gib": round(torch.cuda.max_memory_reserved(device) / gib, 3),
+              "device_total_gib": round(total_b / gib, 3),
+              "device_used_gib_after_timing": round((total_b - free_b) / gib, 3)}
+    memory["headroom_frac"] = round(1.0 - memory["peak_reserved_gib"] / memory["device_total_gib"], 4)
+    if trainer.graphs:
+        # the diagnostics below run eager steps: drop the recorded graph and return its private pool first,
+        # so they never allocate beside it (22M at 224^2 came within 1.1 GB of the device that way, round 5)
+        trainer.release_graphs()
+        torch.cuda.empty_cache()
+    torch.cuda.reset_peak_memory_stats(device)
     if trainer.graphs:
         # ROCm graphs cannot carry timing events (torch: "External events are disallowed in rocm"), so
         # the probed kernel's launches are timed with HIP events in one eager step right after the
@@ -342,6 +360,7 @@ def main():
         trainer._eager(x, y)
         OF.census_disarm()
         census = OF.census_results(HBM_PEAK_GBS, MFMA_PEAK_TFLOPS)
+    memory["diagnostic_eager_peak_alloc_gib"] = round(torch.cuda.max_memory_allocated(device) / gib, 3)
 
     if rank == 0:
         value = world * B * args.steps / elapsed
@@ -402,6 +421,8 @@ def main():
                                          "one flat all_reduce between graph A and graph B" if trainer.graphs else
                                          "bucketed async all_reduce during backward")},
             "roofline": roof,
+            "peak_alloc_gib": memory["peak_alloc_gib"], "peak_reserved_gib": memory["peak_reserved_gib"],
+            "memory": memory,
         }
         if world == 1 and not args.no_parity:
             out["fwd_max_abs_diff"] = fwd_parity(device)

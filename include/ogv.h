@@ -62,7 +62,15 @@ const char* ogv_last_error(void);
  *   reductions; "bn_red_rg" 16 / 64 (default): row groups per block of the fused BatchNorm finalize /
  *   coefficient reductions; "opt_chunk" (default 2048): elements per workgroup of ogv_clip_adamw (also
  *   sizes ogv_clip_adamw_ws_bytes); "pg_conv_rs1" 0 / 1 (default): 64-row statistics panels for small
- *   implicit-conv forwards.
+ *   implicit-conv forwards; "mb_a3" 0 / 1 / 2 / 3 (default): how the fused MBConv keeps the project GEMM's input
+ *   A3 = act(BN2(d)) * gate -- 0 recomputed in the GEMM prologues, 1 materialised in the forward workspace,
+ *   2 materialised AND saved for the backward (ogv_mbconv_saved_bytes grows by [M, mid]), 3 = 2 where A3 is
+ *   at most 512 MB else 1 (resolved per shape by ogv_mbconv_a3_mode; a desc with a3 >= 0 ignores the knob);
+ *   "vp_head" 0 / 1 (default) / 2: the per-head fused Outlooker forward for the wide stages off / on / also
+ *   head_dim 64; "vph_rows" (0 = auto): target rows per panel of that kernel; "vph_wgs" (default 3):
+ *   workgroups per CU its grid is sized for; "vph_dbg": phase-skipping timing experiments (wrong results);
+ *   "dw_tw" 8 / 16 / 32 (default): column strip width of the depthwise kernels; "ln_rpi" 2 (default) / 4:
+ *   rows per iteration of the LayerNorm kernels.
  * Options pick kernel plans, and every *_ws_bytes query sizes the workspace for the plans in force
  * when it is called: set options first, then size workspaces (a workspace sized under other option
  * values can be too small -- e.g. wg_blocks / wg_tile / swg_min_m change the split-M partial count).
@@ -233,6 +241,11 @@ typedef struct {
   int train;        /* 1: BatchNorm batch statistics; 0: running statistics */
   float bn_eps, bn_momentum;
   int act;          /* ogv_act of MBConvConfig.act (silu in all reference configs) */
+  int a3;           /* the saved-data variant: how the project GEMM's input A3 = act(BN2(d)) * gate is kept
+                       (0 prologue, 1 forward workspace, 2 saved for the backward -- ogv_mbconv_saved_bytes
+                       grows by [M, mid]); -1 = resolve knob "mb_a3" at each call.  Pin it with
+                       ogv_mbconv_a3_mode() before the forward and pass the SAME desc to the backward: the
+                       saved buffer's contents depend on it. */
 } ogv_mbconv_desc;
 
 typedef struct {
@@ -250,6 +263,8 @@ typedef struct {
   float *w_expand, *bn1_w, *bn1_b, *w_dw, *bn2_w, *bn2_b, *se_w1, *se_b1, *se_w2, *se_b2, *w_proj, *bn3_w, *bn3_b;
 } ogv_mbconv_grads;
 
+/* the A3 mode knob "mb_a3" selects for this shape now (0, 1 or 2; -1 for a NULL desc) */
+int ogv_mbconv_a3_mode(const ogv_mbconv_desc* desc, ogv_dtype dt);
 size_t ogv_mbconv_saved_bytes(const ogv_mbconv_desc* desc, ogv_dtype dt);
 size_t ogv_mbconv_ws_bytes(const ogv_mbconv_desc* desc, ogv_dtype dt);
 size_t ogv_mbconv_param_ws_bytes(const ogv_mbconv_desc* desc);

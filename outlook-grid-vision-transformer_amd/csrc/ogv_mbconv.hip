@@ -1195,21 +1195,25 @@ struct Buf {
 // knob "mb_a3": once the SE gate is known, one elementwise pass writes the project GEMM's input
 // A3 = act(BN2(d)) * gate (the GEMM prologue's arithmetic), and the project GEMM runs without an A prologue
 // (recomputed per element -- and per column tile -- the SiLU's exp / rcp made it 0.42-0.47 ms of the 7M step,
-// profiles/r05x_mb_a3_rejected.txt).  1 (default): A3 lives in the forward workspace (no extra memory: the
-// backward's workspace is larger), the weight gradient keeps its prologue; 2: A3 is saved for the backward
-// too (+1 [M, 4C] activation per MBConv -- Model-A-22M at 224^2, bs 128 then no longer fits 288 GB), the
-// weight gradient prologue-free as well; 0: the prologue form everywhere; 3 (default): 2 for an MBConv whose A3
-// takes at most 512 MB, else 1 (7M, 30 steps: 0 -> 14.76-14.79 ms, 1 -> 14.69-14.70, 2 -> 14.60-14.63;
-// 22M 339.5 -> 338.9 ms with 1; profiles/r05ac_mb_a3.log)
+// profiles/r05x_mb_a3_rejected.txt).  Modes: 0: the prologue form everywhere; 1: A3 lives in the forward
+// workspace (no extra memory: the backward's workspace is larger), the weight gradient keeps its prologue;
+// 2: A3 is saved for the backward too (+1 [M, 4C] activation per MBConv -- Model-A-22M at 224^2, bs 128 then
+// no longer fits 288 GB), the weight gradient prologue-free as well; 3 (the knob's default): 2 for an MBConv
+// whose A3 takes at most 512 MB, else 1 (7M, 30 steps: 0 -> 14.76-14.79 ms, 1 -> 14.69-14.70,
+// 2 -> 14.60-14.63; 22M 339.5 -> 338.9 ms with 1; profiles/r05ac_mb_a3.log).
+// The mode is part of the saved data's contract: desc.a3 pins it (ogv_mbconv_a3_mode resolves the knob once,
+// the caller keeps the desc for the backward), and the optional A3 slab sits AFTER every fixed field, so a
+// knob change between a forward and its backward can neither shift the statistics nor read past the buffer.
 static int g_mb_a3 = 3;
 void set_mb_a3(int v) { g_mb_a3 = v < 0 ? 0 : (v > 3 ? 3 : v); }
-static int a3_mode(const ogv_mbconv_desc& s, size_t esz) {
+static int a3_resolve(const ogv_mbconv_desc& s, size_t esz) {
   if (g_mb_a3 != 3) return g_mb_a3;
   return (size_t)s.B * s.H * s.W * s.mid * esz <= (512u << 20) ? 2 : 1;
 }
+static int a3_mode(const ogv_mbconv_desc& s, size_t esz) { return s.a3 >= 0 ? s.a3 : a3_resolve(s, esz); }
 struct Saved {
   void *e, *d, *p;                             // [M,mid], [M,mid], [M,C] activation dtype
-  void* a3;                                    // [M,mid] act(BN2(d)) * gate (knob mb_a3 = 2 only)
+  void* a3;                                    // [M,mid] act(BN2(d)) * gate (A3 mode 2 only; stored last)
   float *mean1, *inv1, *sc1, *sh1;             // [mid]
   float *mean2, *inv2, *sc2, *sh2;             // [mid]
   float *mean3, *inv3, *sc3, *sh3;             // [C]
@@ -1222,7 +1226,6 @@ static Saved saved_layout(void* base, const ogv_mbconv_desc& s, size_t esz, size
   v.e = b.take<char>(M * s.mid * esz);
   v.d = b.take<char>(M * s.mid * esz);
   v.p = b.take<char>(M * s.C * esz);
-  v.a3 = a3_mode(s, esz) == 2 ? b.take<char>(M * s.mid * esz) : nullptr;
   v.mean1 = b.take<float>(s.mid); v.inv1 = b.take<float>(s.mid); v.sc1 = b.take<float>(s.mid); v.sh1 = b.take<float>(s.mid);
   v.mean2 = b.take<float>(s.mid); v.inv2 = b.take<float>(s.mid); v.sc2 = b.take<float>(s.mid); v.sh2 = b.take<float>(s.mid);
   v.mean3 = b.take<float>(s.C); v.inv3 = b.take<float>(s.C); v.sc3 = b.take<float>(s.C); v.sh3 = b.take<float>(s.C);
@@ -1230,6 +1233,7 @@ static Saved saved_layout(void* base, const ogv_mbconv_desc& s, size_t esz, size
   v.z1 = b.take<float>((size_t)s.B * s.se);
   v.z2 = b.take<float>((size_t)s.B * s.mid);
   v.gate = b.take<float>((size_t)s.B * s.mid);
+  v.a3 = a3_mode(s, esz) == 2 ? b.take<char>(M * s.mid * esz) : nullptr;   // last: the fixed fields never move
   if (total) *total = b.off + 256;
   return v;
 }
@@ -1779,6 +1783,7 @@ static int mb_check(const ogv_mbconv_desc* s, ogv_dtype dt, const char* who) {
               s->mid);
   OGV_REQUIRE(dt == OGV_F32 || dt == OGV_BF16, "%s: bad dtype", who);
   OGV_REQUIRE(s->act >= OGV_ACT_NONE && s->act <= OGV_ACT_RELU, "%s: bad activation", who);
+  OGV_REQUIRE(s->a3 >= -1 && s->a3 <= 2, "%s: bad A3 mode %d (-1, 0, 1 or 2)", who, s->a3);
   return OGV_OK;
 }
 
@@ -1791,6 +1796,11 @@ extern "C" size_t ogv_mbconv_saved_bytes(const ogv_mbconv_desc* s, ogv_dtype dt)
   size_t t = 0;
   saved_layout(nullptr, *s, dt == OGV_BF16 ? 2 : 4, &t);
   return t;
+}
+
+extern "C" int ogv_mbconv_a3_mode(const ogv_mbconv_desc* s, ogv_dtype dt) {
+  if (!s) return -1;
+  return a3_resolve(*s, dt == OGV_BF16 ? 2 : 4);
 }
 
 extern "C" size_t ogv_mbconv_ws_bytes(const ogv_mbconv_desc* s, ogv_dtype dt) {

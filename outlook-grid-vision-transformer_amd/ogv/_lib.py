@@ -22,7 +22,7 @@ _sz = ctypes.c_size_t
 
 class MBConvDesc(ctypes.Structure):
     _fields_ = [("B", _i), ("H", _i), ("W", _i), ("C", _i), ("mid", _i), ("se", _i), ("train", _i),
-                ("bn_eps", _f), ("bn_momentum", _f), ("act", _i)]
+                ("bn_eps", _f), ("bn_momentum", _f), ("act", _i), ("a3", _i)]
 
 
 MBCONV_PARAM_FIELDS = ["w_expand", "bn1_w", "bn1_b", "bn1_rm", "bn1_rv", "w_dw", "bn2_w", "bn2_b", "bn2_rm", "bn2_rv",
@@ -99,6 +99,7 @@ SIGNATURES = {
     "ogv_dwconv3x3_fwd": (_i, [_p, _p, _p, _p, _i, _i, _i, _i, _i, _p, _i, _p]),
     "ogv_dwconv_bwd_ws_bytes": (_sz, [_i, _i, _i, _i, _i]),
     "ogv_dwconv3x3_bwd": (_i, [_p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p, _i, _p]),
+    "ogv_mbconv_a3_mode": (_i, [_PD, _i]),
     "ogv_mbconv_saved_bytes": (_sz, [_PD, _i]),
     "ogv_mbconv_ws_bytes": (_sz, [_PD, _i]),
     "ogv_mbconv_fwd": (_i, [_p, _p, _p, _p, _PD, _PP, _i, _p]),

@@ -1051,11 +1051,13 @@ class _MBConv(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x2d, geom, buffers, *params):
         lib = _lib.load()
-        desc = _lib.MBConvDesc(*geom)
+        dt = _dt(x2d)
+        desc = _lib.MBConvDesc(*geom, -1)
+        # pin the saved-data variant (knob mb_a3) now: the backward reads `saved` with this same desc
+        desc.a3 = lib.ogv_mbconv_a3_mode(ctypes.byref(desc), dt)
         w = dict(zip(_lib.MBCONV_GRAD_FIELDS, params))
         w.update(buffers)
         P = _lib.MBConvParams(*[_vp(w[n].data_ptr()) for n in _lib.MBCONV_PARAM_FIELDS])
-        dt = _dt(x2d)
         saved = torch.empty(lib.ogv_mbconv_saved_bytes(ctypes.byref(desc), dt), dtype=torch.uint8, device=x2d.device)
         ws = _ws(lib.ogv_mbconv_ws_bytes(ctypes.byref(desc), dt), x2d.device)
         out = torch.empty_like(x2d)
@@ -1063,7 +1065,7 @@ class _MBConv(torch.autograd.Function):
             check(lib.ogv_mbconv_fwd(_ptr(x2d), _ptr(out), _ptr(saved), _ptr(ws), ctypes.byref(desc), ctypes.byref(P),
                                      dt, _stream()), "ogv_mbconv_fwd")
         ctx.save_for_backward(x2d, saved, *params)
-        ctx.geom, ctx.buffers = geom, buffers
+        ctx.geom, ctx.buffers = geom + (int(desc.a3),), buffers
         return out
 
     @staticmethod

@@ -16,12 +16,15 @@ so ~1200 kernel launches per step cost one graph launch instead of ~1200 Python/
 The learning rate lives in a device tensor the schedule updates before each replay.
 
 Data parallelism (the reference has none): one process per GPU, torch.distributed with the
-"nccl" backend (= RCCL on ROCm) over xGMI.  The step is split at the one exchange the path has:
-graph A = fwd + bwd + flatten of the fp32 gradients into ONE bucket (7.5 M params = 30 MB for
-Model-A-7M, pre-divided by world size); one all_reduce of that bucket (a single large ring
-collective: xGMI links are point-to-point, so one 30 MB message beats many small DDP buckets);
-graph B = unflatten + clip_grad_norm + AdamW.  Parameters and buffers are broadcast from rank 0
-once at start; the BatchNorm running buffers then ride in the same all_reduce every step (rank 0's
+"nccl" backend (= RCCL on ROCm) over xGMI.  Graph mode on RCCL (the default, Trainer(dp_overlap)):
+ONE graph per step, the fp32 gradients all-reduced (pre-divided by world size) in ~bucket_mb buckets
+recorded inside it, each launched as soon as backward has produced its last gradient so it overlaps
+the rest of the backward, the optimizer reading the reduced gradients in place.  Alternatives:
+graph A (fwd + bwd + flatten into one bucket) -> one all_reduce -> graph B (unflatten + clip +
+AdamW) -- the form gloo groups (whose collectives cannot be recorded) and dp_overlap=False use, and
+the fallback when a runtime refuses to record collectives -- or that flat all_reduce recorded at
+the end of the one graph (dp_capture_collective).  Parameters and buffers are broadcast from rank 0
+once at start; the BatchNorm running buffers then ride in the collectives every step (rank 0's
 values, the others contribute zeros: DDP's broadcast_buffers), and each rank normalises with its
 own batch statistics.  Eager mode all-reduces 8 MB buckets asynchronously as backward
 produces them.
@@ -277,6 +280,24 @@ class _Bucket:
         self.work = None
 
 
+def _capture_unsupported(e: BaseException) -> bool:
+    """True for the error a runtime raises when an operation (here: a collective) cannot be recorded into a
+    graph; False for everything else (out of memory, a kernel error, a layout error): those are re-raised."""
+    msg = str(e).lower()
+    if "out of memory" in msg:
+        return False
+    return any(k in msg for k in ("capture", "not permitted when stream is capturing", "not supported"))
+
+
+def agree_status(status: int, device) -> int:
+    """max(status) over the ranks of the default process group (status itself without one)."""
+    if not (torch.distributed.is_available() and torch.distributed.is_initialized()):
+        return int(status)
+    t = torch.tensor([float(status)], device=device)
+    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    return int(t.item())
+
+
 class Trainer:
     """Holds model/optimizer/schedule; ``step(x, y)`` is one full training iteration
     (src/training/one_epoch_train.py:85-153 without its host syncs).
@@ -297,9 +318,11 @@ class Trainer:
     rank 0 at start; every step all-reduces the gradients (pre-divided by world size), the float
     buffers (BatchNorm running statistics: rank 0 contributes them, the others zeros, so the sum IS
     rank 0's values -- DDP's ``broadcast_buffers`` riding in the same collective) and the
-    non-finite flag (so every rank takes the same skip decision).  Graph mode: graph A (fwd + bwd +
-    flatten into one bucket) -> one all_reduce -> graph B (unflatten + clip + AdamW); eager mode:
-    ``bucket_mb`` buckets all-reduced asynchronously as backward produces them."""
+    non-finite flag (so every rank takes the same skip decision).  Graph mode on RCCL: ``bucket_mb``
+    buckets all-reduced inside the step's one graph as backward completes them (``dp_overlap``, default);
+    gloo / ``dp_overlap=False``: graph A (fwd + bwd + flatten into one bucket) -> one all_reduce -> graph B
+    (unflatten + clip + AdamW); eager mode: ``bucket_mb`` buckets all-reduced asynchronously as backward
+    produces them."""
 
     def __init__(self, model: nn.Module, lr=5e-4, weight_decay=0.05, clip=1.0, label_smoothing=0.1,
                  total_steps=10_000, warmup_ratio=0.05, min_lr=1e-6, amp_dtype: Optional[torch.dtype] = torch.bfloat16,
@@ -346,9 +369,9 @@ class Trainer:
             self.opt.found_inf = self._found       # read by the fused AdamW kernel (1 = skip)
             self._nonfinite = torch.zeros((), dtype=torch.float32, device=dev)
             # rows whose class index is outside [0, K) (and not -100): the native loss counts them here;
-            # read (one sync) after the first step, every label_check_every steps and with nonfinite_steps,
-            # raising ValueError as torch's cross_entropy would (a bad label is a data error,
-            # not a silently skipped step)
+            # read (one sync, summed over the ranks) after the first step, every label_check_every steps and by
+            # check_labels(), raising ValueError as torch's cross_entropy would (a bad label is a data
+            # error, not a silently skipped step)
             self._bad_labels = torch.zeros((), dtype=torch.float32, device=dev)
             self.sched.bind_device(torch.zeros((), dtype=torch.float32, device=dev))
         self.world = 1 if self.ddp else _dist_world()
@@ -634,6 +657,11 @@ class Trainer:
     def _allreduce(self):
         torch.distributed.all_reduce(self.flat)
 
+    def _agree(self, status: int) -> int:
+        """The largest status over the ranks (0 ok, 1 capture unsupported, 2 any other failure): one small
+        all_reduce outside any capture, so every rank takes the same capture decision."""
+        return agree_status(status, self._found.device if self.backend == "nccl" else torch.device("cpu"))
+
     # -- graph mode on RCCL: bucketed collectives captured on a side stream, overlapping backward ------
     def _overlap_setup(self, dev):
         """Buckets of ~bucket_mb in reverse registration order (~ the order backward finishes them) laid
@@ -784,6 +812,7 @@ class Trainer:
             loss = self._eager(x, y)
         torch.cuda.current_stream().wait_stream(side)
         loss = loss.clone()
+        warm_grads = [p.grad for p in self.params]
         self.opt.zero_grad(set_to_none=True)
         self._x = x.detach().clone(memory_format=torch.preserve_format)
         self._y = y.detach().clone()
@@ -796,24 +825,40 @@ class Trainer:
         # call from another thread (hipErrorStreamCaptureUnsupported -> abort), so capture thread-locally
         mode = "thread_local" if self.backend == "nccl" else "global"
         if self.dp_overlap:
+            # every gradient must be laid out like its parameter for the in-place reduced views: checked on the
+            # warm-up step's gradients before recording (a layout error raised mid-capture would leave earlier
+            # buckets' collectives recorded on this rank only)
+            for i, (p, g) in enumerate(zip(self.params, warm_grads)):
+                if g is not None and not _dense_like(g, p):
+                    raise RuntimeError(f"Trainer(dp_overlap): gradient of parameter {i} is not laid out like the "
+                                       f"parameter (strides {tuple(g.stride())} vs {tuple(p.stride())})")
+            status, err = 0, None
             try:
                 with torch.cuda.graph(self._g, pool=pool, capture_error_mode=mode):
                     self._loss_static = self._fwd_bwd_overlap(self._x, self._y)
                     self._update(self._overlap_finish())
+            except RuntimeError as e:
+                status, err = (1 if _capture_unsupported(e) else 2), e
+            # one decision for every rank: a rank that recorded the bucketed graph must not replay it
+            # while another records the flat form -- their collective sequences would no longer match
+            agreed = self._agree(status)
+            if agreed == 0:
                 self.graph_grads = [p.grad for p in self.params]   # views of the reduced-gradient buffer
                 return loss
-            except RuntimeError as e:
-                # a runtime that cannot record collectives into a graph raises during the capture (before any
-                # of them ran: every rank fails alike): record the flat form instead -- one all_reduce between
-                # two graphs, outside any capture -- rather than end the job
-                import warnings
-                warnings.warn(f"Trainer: capturing the bucketed all-reduces failed ({e}); using the flat all-reduce "
-                              f"between two graphs instead", RuntimeWarning, stacklevel=3)
-                torch.cuda.synchronize()
-                self.dp_overlap = False
-                self._gworks, self._glocal = [], []
-                self.opt.zero_grad(set_to_none=True)
-                self._g = torch.cuda.CUDAGraph()
+            if agreed == 2:
+                if err is not None and status == 2:
+                    raise err
+                raise RuntimeError("Trainer: graph capture of the step failed on another rank")
+            # a runtime that cannot record collectives into a graph: record the flat form instead -- one
+            # all_reduce between two graphs, outside any capture -- rather than end the job
+            import warnings
+            warnings.warn(f"Trainer: capturing the bucketed all-reduces failed ({err if err is not None else 'on another rank'}); "
+                          f"using the flat all-reduce between two graphs instead", RuntimeWarning, stacklevel=3)
+            torch.cuda.synchronize()
+            self.dp_overlap = False
+            self._gworks, self._glocal = [], []
+            self.opt.zero_grad(set_to_none=True)
+            self._g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self._g, pool=pool, capture_error_mode=mode):
             self._loss_static = self._fwd_bwd(self._x, self._y)
             if self.dp:
@@ -829,6 +874,23 @@ class Trainer:
             with torch.cuda.graph(self._g2, pool=pool, capture_error_mode=mode):
                 self._update(self._unflatten())
         return loss
+
+    def release_graphs(self):
+        """Drop the recorded step graph(s) and the tensors only they hold (their private memory pool can
+        then be returned with torch.cuda.empty_cache()); the trainer state -- parameters, moments, schedule
+        -- is untouched and the next step() records the graph again."""
+        for name in ("_g", "_g2"):
+            g = getattr(self, name, None)
+            if g is not None:
+                g.reset()
+            setattr(self, name, None)
+        self._loss_static = None
+        self.graph_grads = None
+        self._gworks, self._glocal = [], []
+        if getattr(self, "gflat", None) is not None:    # allocated inside the capture: re-made by the next one
+            self.gflat, self._gviews = None, None
+        self.opt.zero_grad(set_to_none=True)
+        self._eager_steps = max(self._eager_steps, self.capture_warmup)
 
     def _replayable(self, x, y) -> bool:
         return (x.shape == self._x.shape and x.dtype == self._x.dtype and x.device == self._x.device
@@ -847,7 +909,13 @@ class Trainer:
         (the native loss counts them on the device; torch's cross_entropy raises on the first such batch).
         One host sync; Trainer.step calls it after the first step and every ``label_check_every`` steps."""
         if self.device_side:
-            n = int(self._bad_labels.item())
+            bad = self._bad_labels
+            if self.dp:   # every rank raises at the same check (a lone rank raising would leave the others
+                bad = bad.detach().clone().reshape(1)          # blocked in the next step's collectives)
+                if self.backend != "nccl":
+                    bad = bad.cpu()
+                torch.distributed.all_reduce(bad)
+            n = int(bad.sum().item())
             if n:
                 self._bad_labels.zero_()
                 raise ValueError(f"Trainer: {n} target label(s) outside [0, num_classes) (and not -100) since the "
@@ -873,8 +941,14 @@ class Trainer:
 
     @property
     def nonfinite_steps(self) -> int:
-        self.check_labels()
+        """Steps skipped by the non-finite guard so far (one host sync; no side effects)."""
         return int(self._nonfinite.item()) if self.device_side else self._nonfinite_host
+
+    @property
+    def bad_label_count(self) -> int:
+        """This rank's rows with a class index outside [0, K) (and not -100) since the last check_labels()
+        (one host sync; no side effects -- check_labels() raises and resets)."""
+        return int(self._bad_labels.item()) if self.device_side else 0
 
     # -- checkpoint / resume (src/training/chekpoints.py dict keys) -----------------------------
     def state_dict(self):

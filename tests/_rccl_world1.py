@@ -32,7 +32,8 @@ def main():
         batches.append((torch.randn(16, 3, 32, 32, device="cuda", generator=g).contiguous(memory_format=torch.channels_last),
                         torch.randint(0, 100, (16,), device="cuda", generator=g)))
     runs = {}
-    for mode in ("plain", "dp_graph", "dp_graph_flat", "dp_capture", "plain_eager", "dp_eager", "dp_graph_fallback"):
+    for mode in ("plain", "dp_graph", "dp_graph_flat", "dp_capture", "plain_eager", "dp_eager", "dp_graph_fallback",
+                 "dp_graph_other_error"):
         torch.backends.cudnn.benchmark = False
         torch.manual_seed(31)
         m = build_model(dict(type="model_a", num_classes=100, stem_dim=64, dpr_max=0.0, stages=cfg["stages"]))
@@ -41,11 +42,25 @@ def main():
         t = Trainer(m, total_steps=50, warmup_ratio=0.1, graphs=not mode.endswith("eager"), capture_warmup=1,
                     force_dp=dp, dp_capture_collective=mode == "dp_capture", dp_overlap=mode != "dp_graph_flat")
         assert t.dp == dp and t.dp_capture_collective == (mode == "dp_capture")
-        assert t.dp_overlap == (mode in ("dp_graph", "dp_graph_fallback")), (mode, t.dp_overlap)
+        assert t.dp_overlap == (mode in ("dp_graph", "dp_graph_fallback", "dp_graph_other_error")), (mode, t.dp_overlap)
         if mode == "dp_graph_fallback":   # a runtime that refuses to record the collectives: the capture raises
             def refuse(*a, **k):
-                raise RuntimeError("simulated: collective not capturable")
+                raise RuntimeError("simulated: operation not permitted when stream is capturing")
             t._fwd_bwd_overlap = refuse
+        if mode == "dp_graph_other_error":   # any other failure (here: OOM) is re-raised on every rank, no fallback
+            def oom(*a, **k):
+                raise RuntimeError("simulated: HIP out of memory")
+            t._fwd_bwd_overlap = oom
+            try:
+                for b in batches:
+                    t.step(*b)
+                raised = ""
+            except RuntimeError as e:
+                raised = str(e)
+            print(json.dumps({"mode": mode, "backend": t.backend, "raised": raised, "dp_overlap": t.dp_overlap}),
+                  flush=True)
+            del t
+            continue
         warned = []
         import warnings
         with warnings.catch_warnings(record=True) as wl:

@@ -260,3 +260,30 @@ def test_load_optimizer_state_keeps_device_lr_and_tensors():
     for p, q in zip(m2.parameters(), m.parameters()):
         assert opt2.state[p]["exp_avg"] is old[id(p)]
         torch.testing.assert_close(opt2.state[p]["exp_avg"], opt.state[q]["exp_avg"], rtol=0, atol=0)
+
+
+def _agree_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from ogv.train import agree_status
+        # only rank 1 fails its capture: every rank must see the failure
+        got = [agree_status(s, torch.device("cpu")) for s in ((0, 1, 0) if rank == 0 else (1, 2, 0))]
+        torch.save(got, os.path.join(out_dir, f"a{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_capture_decision_agreed_over_ranks(tmp_path):
+    """Trainer._capture's fallback decision is the MAX of the per-rank capture statuses (0 ok, 1 capture
+    unsupported -> flat form, 2 other error -> raise), one all_reduce, so no rank replays the bucketed
+    graph while another records the flat one; the error classifier sends only capture refusals to the
+    fallback."""
+    from ogv.train import _capture_unsupported
+    mp.spawn(_agree_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    for r in range(2):
+        assert torch.load(tmp_path / f"a{r}.pt") == [1, 2, 0]
+    assert _capture_unsupported(RuntimeError("operation not permitted when stream is capturing"))
+    assert _capture_unsupported(RuntimeError("hipErrorStreamCaptureUnsupported"))
+    assert not _capture_unsupported(RuntimeError("HIP out of memory. Tried to allocate 2.00 GiB"))
+    assert not _capture_unsupported(RuntimeError("ogv_gemm_fwd: bad shape"))

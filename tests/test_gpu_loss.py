@@ -68,7 +68,8 @@ def test_cross_entropy_ls_ignore_index_and_bad_label():
 def test_trainer_raises_on_bad_labels(graphs):
     """a label outside [0, K) must not be skipped silently -- the Trainer raises ValueError (as
     torch's cross_entropy does) at its next label check: after the first step, every label_check_every
-    steps, and when nonfinite_steps is read."""
+    steps, and whenever check_labels() is called; reading nonfinite_steps / bad_label_count has no side
+    effects."""
     from ogv.train import Trainer
     from src.Model_A_OutGridNet import MaxOutNet
     from src.stage_config import StageCfg
@@ -84,9 +85,13 @@ def test_trainer_raises_on_bad_labels(graphs):
     with pytest.raises(ValueError, match="outside"):
         t.step(x, ybad)                             # step 3: the periodic check
     assert t.nonfinite_steps == 1                   # the skipped step; the counter was reset by the raise
+    assert t.bad_label_count == 0
     t.step(x, ybad)
+    assert t.nonfinite_steps == 2 and t.bad_label_count == 1   # metrics: no raise, no reset
+    assert t.bad_label_count == 1
     with pytest.raises(ValueError, match="outside"):
-        t.nonfinite_steps
+        t.check_labels()
+    assert t.bad_label_count == 0
 
 
 def test_cross_entropy_ls_rejects_host_tensors_and_soft_targets():

@@ -1154,3 +1154,36 @@ def test_mbconv_materialised_a3_matches_prologue(C, H, B, dtype, mode):
             assert torch.equal(a, b), (k, fx.maxabs(b, a))
         else:
             assert fx.maxabs(b, a) <= 1e-5 * max(1.0, a.abs().max().item()), (k, fx.maxabs(b, a))
+
+
+@pytest.mark.parametrize("first,then", [(1, 2), (2, 1), (2, 0), (0, 2)])
+def test_mbconv_a3_knob_change_between_fwd_and_bwd(first, then):
+    """the A3 mode is part of the saved data -- the forward pins it in the desc it keeps for the
+    backward, and the optional A3 slab sits after the fixed fields -- so changing knob mb_a3 between a
+    forward and its backward leaves every gradient bit-identical to a backward run under the same knob."""
+    from ogv._lib import load
+    from src.model.mbc_conv import MBConv, MBConvConfig
+    lib = load()
+    torch.manual_seed(11)
+    m = MBConv(96, 96, 1, MBConvConfig()).to(DEV)
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    x = torch.randn(8, 96, 16, 16, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    dy = torch.randn_like(x)
+    res = []
+    try:
+        for switch in (False, True):
+            assert lib.ogv_set_option(b"mb_a3", first) == 0
+            m.load_state_dict(sd)
+            m.zero_grad(set_to_none=True)
+            xx = x.clone().requires_grad_()
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                y = m.train()(xx)
+            if switch:
+                assert lib.ogv_set_option(b"mb_a3", then) == 0
+            y.backward(dy)
+            torch.cuda.synchronize()
+            res.append([xx.grad.float()] + [p.grad.clone() for p in m.parameters()])
+    finally:
+        assert lib.ogv_set_option(b"mb_a3", 3) == 0
+    for k, (a, b) in enumerate(zip(*res)):
+        assert torch.equal(a, b), (k, fx.maxabs(b, a))

@@ -141,6 +141,39 @@ def test_graph_ragged_batch_runs_eager():
     assert t.eager_fallbacks == 1
 
 
+def test_release_graphs_then_recapture_continues_bit_identically():
+    """Trainer.release_graphs() (bench.py drops the recorded graph before its eager diagnostic steps so they
+    never allocate beside the graph's pool): the next step records the graph again and the run continues
+    as one that never released it (losses, parameters) -- and the pool's memory is returned to the device by
+    empty_cache."""
+    from ogv.train import Trainer
+    runs = []
+    for release in (False, True):
+        m = _model(12)
+        t = Trainer(m, total_steps=50, warmup_ratio=0.1, graphs=True, capture_warmup=1)
+        losses = [t.step(*_batch(8, 40 + i)).item() for i in range(3)]      # eager, capture, replay
+        if release:
+            torch.cuda.synchronize()
+            before = torch.cuda.memory_reserved()
+            t.release_graphs()
+            torch.cuda.empty_cache()
+            assert t._g is None and torch.cuda.memory_reserved() < before
+        losses += [t.step(*_batch(8, 43 + i)).item() for i in range(3)]     # (re-)capture, replay, replay
+        assert t._g is not None
+        torch.cuda.synchronize()
+        runs.append((losses, [p.detach().clone() for p in m.parameters()],
+                     [v.detach().clone() for p in t.params for v in t.opt.state[p].values()]))
+        del t
+    # steps 1-3 identical; the released run takes step 4 as the capture step's eager update, which equals a
+    # replay to the tolerances of test_graph_replay_matches_eager_step (Adam sign flips: <= 2 lr per step)
+    assert runs[0][0][:3] == runs[1][0][:3]
+    for a, b in zip(runs[0][0][3:], runs[1][0][3:]):
+        assert abs(a - b) <= 1e-4 * max(1.0, abs(a)), (runs[0][0], runs[1][0])
+    lr = 5e-4
+    for a, b in zip(runs[0][1], runs[1][1]):
+        assert float((a - b).abs().max()) <= 3 * 2 * lr + 1e-6
+
+
 @pytest.mark.parametrize("graphs", [True, False])
 def test_nonfinite_loss_skips_update_without_sync(graphs):
     """one_epoch_train.py:98-108 on the device: a NaN batch leaves parameters, BN-free optimizer
@@ -522,13 +555,14 @@ def test_rccl_world1_dp_path_matches_single_process():
     lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
     res = {d["mode"]: d for d in lines if "mode" in d}
     assert set(res) >= {"plain", "dp_graph", "dp_graph_flat", "dp_capture", "plain_eager", "dp_eager",
-                        "dp_graph_fallback"}, \
+                        "dp_graph_fallback", "dp_graph_other_error"}, \
         (r.returncode, list(res))
     for mode in ("dp_graph", "dp_graph_flat", "dp_capture", "dp_eager"):
         assert res[mode]["backend"] == "nccl", res[mode]
     assert res["dp_graph"]["dp_overlap"] and res["dp_graph"]["buckets"] >= 2 and res["dp_graph"]["grad_is_view"]
     # the overlapped capture refused (simulated): one warning, the flat two-graph form, same result
     assert not res["dp_graph_fallback"]["dp_overlap"] and res["dp_graph_fallback"]["fallback_warned"] == 1
+    assert "out of memory" in res["dp_graph_other_error"]["raised"], res["dp_graph_other_error"]
     assert res["dp_graph"]["fallback_warned"] == 0
     for mode, ref in (("dp_graph", "plain"), ("dp_graph_flat", "plain"), ("dp_capture", "plain"),
                       ("dp_graph_fallback", "plain")):

@@ -67,7 +67,9 @@ const char* ogv_last_error(void);
  *   2 materialised AND saved for the backward (ogv_mbconv_saved_bytes grows by [M, mid]), 3 = 2 where A3 is
  *   at most 512 MB else 1 (resolved per shape by ogv_mbconv_a3_mode; a desc with a3 >= 0 ignores the knob);
  *   "vp_head" 0 / 1 (default) / 2: the per-head fused Outlooker forward for the wide stages off / on / also
- *   head_dim 64; "vph_rows" (0 = auto): target rows per panel of that kernel; "vph_wgs" (default 3):
+ *   head_dim 64 (two 32-column units per head); "vph_halo" 0 (default) / 1 / 2 / 3: its halo-tile form for images of
+ *   more than 128 pixels off / where <= 4 units share a pixel (C = 128) / every wide shape / with 8-wave workgroups; "vph_tile" (TH * 100 + TW, 0 = auto): force its tile; "vp_l32" 1 (default) / 0: the fused Outlooker's fp32-logits form
+ *   (ogv_outlook_vproj_l32_supported answers 0 with 0); "vph_rows" (0 = auto): target rows per panel of that kernel; "vph_wgs" (default 3):
  *   workgroups per CU its grid is sized for; "vph_dbg": phase-skipping timing experiments (wrong results);
  *   "dw_tw" 8 / 16 / 32 (default): column strip width of the depthwise kernels; "ln_rpi" 2 (default) / 4:
  *   rows per iteration of the LayerNorm kernels.
@@ -138,6 +140,24 @@ int ogv_outlook_vproj_supported(int B, int H, int W, int C, int heads, int k, in
                                 ogv_dtype dt);
 int ogv_outlook_vproj_fwd(const void* x, int ldx, const float* w, const float* bias, void* cat, int ldc,
                           void* y, int B, int H, int W, int C, int heads, int k, ogv_dtype dt, void* stream);
+/* The fp32-logits form of the fused Outlooker (training and inference; no reference counterpart -- a
+ * precision choice): the same projections, softmax and gather as ogv_outlook_vproj_fwd, but the logits stay
+ * fp32 -- the softmax reads them unrounded and training writes them to `logits` ([M, ld_logits] fp32,
+ * ld_logits >= 9*heads rounded up to 4, 16-B rows) while `v` ([M, ld_v] bf16, ld_v >= C, 8 | ld_v) receives
+ * only the v columns; both NULL = inference.  w is [C + 9*heads rounded up to 8, C] as above.  The
+ * reference's own bf16 path rounds the attn conv's output (the logits) to bf16 (autocast); keeping them fp32
+ * moves the bf16 gradients closer to the fp32 reference.
+ * ogv_outlook_vproj_l32_supported: 1 when this form takes the shape (the per-head kernel where it plans,
+ * else the tile kernel; not the weight-streaming kernel), knob "vp_l32" on.
+ * ogv_outlook_agg_bwd_l32: ogv_outlook_agg_bwd reading those fp32 logits (the LDS-tiled backward only:
+ * bf16, k = 3, 8 | head_dim <= 64). */
+int ogv_outlook_vproj_l32_supported(int B, int H, int W, int C, int heads, int k, int train, ogv_dtype dt);
+int ogv_outlook_vproj_fwd_l32(const void* x, int ldx, const float* w, const float* bias, void* v, int ld_v,
+                              float* logits, int ld_logits, void* y, int B, int H, int W, int C, int heads, int k,
+                              ogv_dtype dt, void* stream);
+int ogv_outlook_agg_bwd_l32(const void* dy, const void* v, const float* logits, void* dv, void* dlogits,
+                            int B, int H, int W, int C, int heads, int k, int ld_logits, int ld_v, int ld_dv,
+                            int ld_dlogits, int dl_cols, ogv_dtype dt, void* stream);
 int ogv_outlook_vproj_bwd(const void* x, int ldx, const float* w, const float* bias, const void* dy,
                           void* dcat, int ldc, int B, int H, int W, int C, int heads, int k, ogv_dtype dt,
                           void* stream);

@@ -236,6 +236,9 @@ void set_ln_rpi(int v);
 void set_vp_head(int v);
 void set_vph_rows(int v);
 void set_vph_wgs(int v);
+void set_vph_halo(int v);
+void set_vp_l32(int v);
+void set_vph_tile(int v);
 void set_vph_dbg(int v);
 // Squeeze-Excite GEMVs (ogv_se.hip); knob "se_gemv" (1 default, 0 = the split-K tiled GEMM + reduce)
 void se_gemv_launch(const float* in, int ldi, int pro_act, const float* W, int ldw, const float* bias,

@@ -474,7 +474,8 @@ __device__ __forceinline__ void otile_stage2(const bf16* __restrict__ s1, int ld
 
 // Softmax item idx of otile_probs split in two: the logits loads (into registers, so they can be
 // issued ahead of the staging loads) and the softmax + LDS store.
-__device__ __forceinline__ void otile_logits_load(const bf16* __restrict__ lg, int ldl, int col, const OTile& t,
+template <typename LT>
+__device__ __forceinline__ void otile_logits_load(const LT* __restrict__ lg, int ldl, int col, const OTile& t,
                                                   long tile0, int H, int W, bool halo, int idx, float (&a)[9],
                                                   int& dst, bool& ok) {
   const int HW2 = t.TW + 2, HP = (t.TH + 2) * HW2, PT = t.TH * t.TW;
@@ -498,7 +499,7 @@ __device__ __forceinline__ void otile_logits_load(const bf16* __restrict__ lg, i
     const int yy = y0 - 1 + hy, xx = x0 - 1 + hp - hy * HW2;
     if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
       ok = true;
-      const bf16* l = lg + ((long)(b * H + yy) * W + xx) * ldl + col + hb * 9;
+      const LT* l = lg + ((long)(b * H + yy) * W + xx) * ldl + col + hb * 9;
 #pragma unroll
       for (int j = 0; j < 9; ++j) a[j] = (float)l[j];
     }
@@ -614,10 +615,10 @@ __global__ __launch_bounds__(256) void outlook_fwd_tile_kernel(const bf16* __res
   }
 }
 
-template <int HD>
+template <int HD, typename LT = bf16>   // LT: the logits' storage type (float: the fp32-logits forward's lg)
 __global__ __launch_bounds__(256) void outlook_bwd_tile_kernel(const bf16* __restrict__ dy, int lddy,
                                                                const bf16* __restrict__ v, int ldv,
-                                                               const bf16* __restrict__ lg, int ldl,
+                                                               const LT* __restrict__ lg, int ldl,
                                                                bf16* __restrict__ dv, int lddv, bf16* __restrict__ dl,
                                                                int lddl, int dl_cols, int H, int W, int heads,
                                                                OTile t) {
@@ -786,13 +787,13 @@ static void otile_fwd_run(const bf16* v, int ldv, const bf16* lg, int ldl, bf16*
   outlook_fwd_tile_kernel<HD><<<xcd_grid(nb), 256, otile_lds(t, HD, false), s>>>(v, ldv, lg, ldl, y, ldy, H, W, heads, t);
 }
 
-template <int HD>
-static void otile_bwd_run(const bf16* dy, int lddy, const bf16* v, int ldv, const bf16* lg, int ldl, bf16* dv,
+template <int HD, typename LT>
+static void otile_bwd_run(const bf16* dy, int lddy, const bf16* v, int ldv, const LT* lg, int ldl, bf16* dv,
                           int lddv, bf16* dl, int lddl, int dl_cols, int H, int W, int heads, const OTile& t,
                           hipStream_t s) {
   const long nb = (t.ntiles + t.G - 1) / t.G * (heads / t.HB);
-  outlook_bwd_tile_kernel<HD><<<xcd_grid(nb), 256, otile_lds(t, HD, true), s>>>(dy, lddy, v, ldv, lg, ldl, dv, lddv,
-                                                                                dl, lddl, dl_cols, H, W, heads, t);
+  outlook_bwd_tile_kernel<HD, LT><<<xcd_grid(nb), 256, otile_lds(t, HD, true), s>>>(dy, lddy, v, ldv, lg, ldl, dv, lddv,
+                                                                                    dl, lddl, dl_cols, H, W, heads, t);
 }
 
 #define OGV_OTILE_HD(FN, hd, ...)                  \
@@ -917,8 +918,11 @@ struct VTile {
   int HP, HPr;         // halo pixels, rounded up to 16
   int XP, RP, WP;      // LDS pitches (elements): x tile, result tile, weight slab
   int ncol;            // computed output columns (16 * NJ >= C + heads * 9)
+  int l32;             // the logits kept in fp32 (result-tile slots C + 2 (n - C)): the fp32-logits forward
   FDiv per_img, fntx, fHW2, fTW, fHB, fCH, fQ;
 };
+// bf16 slots of a result-tile row whose logit columns are fp32: C + 2 * (9 heads rounded up to 4)
+static inline int vtile_l32_slots(int C, int heads) { return C + 2 * ((heads * 9 + 3) / 4 * 4); }
 
 // waves per workgroup: 4 with two workgroups per CU (16 | C <= 64), 8 with one (C > 64: the split
 // weight slab alone is 47-53 KB); 16-B x chunks per thread and tile, prefetched into registers
@@ -938,11 +942,15 @@ static size_t vtile_lds(const VTile& t, int heads, bool sw) {
          (size_t)t.ncol * 4;
 }
 
-template <int NJ, int NK, bool SW, int NW>
+// L32 (the fp32-logits form): the logit columns stay fp32 in the result tile (slots C + 2 (n - C)), the softmax
+// reads them unrounded, and training writes v to `cat` ([M, ldc] bf16 rows, v only) and the logits to
+// lg ([M, ldl] fp32) -- the bf16 rounding of the logits (O(1-10) values whose rounding moves the softmax)
+// is gone from both the forward and the backward (which recomputes the softmax from lg)
+template <int NJ, int NK, bool SW, int NW, bool L32>
 __global__ __launch_bounds__(NW * 64, 8 / NW) void outlook_vproj_fwd_kernel(
     const bf16* __restrict__ x, int ldx, const float* __restrict__ Wc, int wrows, const float* __restrict__ bias,
     bf16* __restrict__ cat, int ldc, bf16* __restrict__ y, int H, int W, int C, int heads, VTile t, int xbytes,
-    int dbg) {
+    int dbg, float* __restrict__ lg, int ldl) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int KP = NK * 32, NCOL = NJ * 16, NT = NW * 64, VP_PF = vp_pf<NW>();
   const int XP = t.XP, RP = t.RP, WP = t.WP, HW2 = t.TW + 2, HP = t.HP;
@@ -1062,6 +1070,13 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void outlook_vproj_fwd_kernel(
         for (int j = 0; j < NJ; ++j) {
           const int n = j * 16 + 4 * fg;
           const float4 b4 = *reinterpret_cast<const float4*>(bs + n);
+          if (L32 && n >= C) {   // logit columns: fp32 at slots C + 2 (n - C) (pad-only groups dropped)
+            if (n < C + (heads * 9 + 3) / 4 * 4)
+              *reinterpret_cast<float4*>(rs + m * RP + C + 2 * (n - C)) =
+                  float4{inb ? acc[r][j][0] + b4.x : 0.f, inb ? acc[r][j][1] + b4.y : 0.f,
+                         inb ? acc[r][j][2] + b4.z : 0.f, inb ? acc[r][j][3] + b4.w : 0.f};
+            continue;
+          }
           bf16x4 o;
           o[0] = (bf16)(inb ? acc[r][j][0] + b4.x : 0.f);
           o[1] = (bf16)(inb ? acc[r][j][1] + b4.y : 0.f);
@@ -1072,8 +1087,22 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void outlook_vproj_fwd_kernel(
       }
     }
     __syncthreads();   // the result tile is complete; xs is free (P aliases it)
-    // 3a. interior rows of [v | logits | 0] -> cat (the backward's input)
-    if (cat && !(dbg & 8)) {
+    // 3a. interior rows of [v | logits | 0] -> cat (the backward's input); L32: v -> cat, fp32 logits -> lg
+    if (L32 && cat && !(dbg & 8)) {
+      const int VC = C / 8, LQ = (heads * 9 + 3) / 4, NQ = VC + LQ;
+      for (int idx = tid; idx < PT * NQ; idx += NT) {
+        const int pt = idx / NQ, q = idx - pt * NQ;
+        const int ty = fdiv(pt, t.fTW), tx = pt - ty * t.TW;
+        if (y0 + ty >= H || x0 + tx >= W) continue;
+        const int s = (ty + 1) * HW2 + tx + 1;
+        const long g = (long)(b * H + y0 + ty) * W + x0 + tx;
+        if (q < VC)
+          *reinterpret_cast<uint4*>(cat + g * ldc + q * 8) = *reinterpret_cast<const uint4*>(rs + s * RP + q * 8);
+        else
+          *reinterpret_cast<uint4*>(lg + g * ldl + (q - VC) * 4) =
+              *reinterpret_cast<const uint4*>(rs + s * RP + C + (q - VC) * 8);
+      }
+    } else if (cat && !(dbg & 8)) {
       const int LC = ldc / 8;
       for (int idx = tid; idx < PT * LC; idx += NT) {
         const int pt = idx / LC, c8 = idx - pt * LC;
@@ -1089,10 +1118,11 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void outlook_vproj_fwd_kernel(
       const int pt = fdiv(idx, t.fHB), hb = idx - pt * heads;
       const int ty = fdiv(pt, t.fTW), tx = pt - ty * t.TW;
       const bf16* l = rs + ((ty + 1) * HW2 + tx + 1) * RP + C + hb * 9;
+      const float* l32 = reinterpret_cast<const float*>(rs + ((ty + 1) * HW2 + tx + 1) * RP + C) + hb * 9;
       float a[9], mx = -INFINITY;
 #pragma unroll
       for (int jj = 0; jj < 9; ++jj) {
-        a[jj] = (float)l[jj];
+        a[jj] = L32 ? l32[jj] : (float)l[jj];
         mx = fmaxf(mx, a[jj]);
       }
       float sm = 0.f;
@@ -1739,19 +1769,21 @@ static long vtile_rs_cycles(const VTile& t, int C, int heads, int ldc, int RP) {
 // the least-conflicted result-tile pitch (the model above), memoised per tile geometry: the search
 // costs ~1 ms of host time, so it must not run on every launch
 static int vtile_best_rp(const VTile& t, int C, int heads, int ldc) {
-  struct Entry { int C, heads, ldc, TH, TW, rp; };
+  struct Entry { int C, heads, ldc, TH, TW, l32, rp; };
   static Entry cache[64];
   static int n = 0;
   for (int i = 0; i < n; ++i)
-    if (cache[i].C == C && cache[i].heads == heads && cache[i].ldc == ldc && cache[i].TH == t.TH && cache[i].TW == t.TW)
+    if (cache[i].C == C && cache[i].heads == heads && cache[i].ldc == ldc && cache[i].TH == t.TH && cache[i].TW == t.TW &&
+        cache[i].l32 == t.l32)
       return cache[i].rp;
-  int rp_best = t.ncol;
+  const int rp0 = t.l32 ? std::max(t.ncol, (vtile_l32_slots(C, heads) + 7) / 8 * 8) : t.ncol;
+  int rp_best = rp0;
   long best = -1;
-  for (int rp = t.ncol; rp <= t.ncol + 72; rp += 8) {
+  for (int rp = rp0; rp <= rp0 + 72; rp += 8) {
     const long c = vtile_rs_cycles(t, C, heads, ldc, rp);
     if (best < 0 || c < best) { best = c; rp_best = rp; }
   }
-  if (n < 64) cache[n++] = Entry{C, heads, ldc, t.TH, t.TW, rp_best};
+  if (n < 64) cache[n++] = Entry{C, heads, ldc, t.TH, t.TW, t.l32, rp_best};
   return rp_best;
 }
 
@@ -1782,7 +1814,7 @@ static int g_vp_tile = 0;
 void set_vp_tile(int v) { g_vp_tile = v < 0 ? 0 : (v > 4 ? 4 : v); }
 
 static bool vtile_plan(int B, int H, int W, int C, int heads, int k, int ldc, ogv_dtype dt, bool bwd, VTile& t,
-                       int& nw) {
+                       int& nw, bool l32 = false) {
   if (dt != OGV_BF16 || k != 3 || B <= 0 || H <= 0 || W <= 0 || heads <= 0) return false;
   if (C % 16 != 0 || C > 96 || C % heads != 0 || (C / heads) % 8 != 0) return false;
   const int NL = heads * 9;
@@ -1795,6 +1827,7 @@ static bool vtile_plan(int B, int H, int W, int C, int heads, int k, int ldc, og
   for (int i = 0; i < (g_vp_tile ? 1 : 4) && !ok; ++i) {
     const int pass = g_vp_tile ? g_vp_tile - 1 : order[i];
     t = VTile{};
+    t.l32 = l32 && !bwd;
     t.TH = H < 8 ? H : 8;
     t.TW = W < tws[pass] ? W : tws[pass];
     t.ntx = (W + t.TW - 1) / t.TW;
@@ -1810,7 +1843,8 @@ static bool vtile_plan(int B, int H, int W, int C, int heads, int k, int ldc, og
     for (int pad = 16; pad >= 8 && !ok; pad -= 8) {
       t.XP = KP + pad;
       t.WP = KP + pad;
-      t.RP = pad == 16 ? vtile_best_rp(t, C, heads, ldc) : t.ncol;
+      t.RP = pad == 16 ? vtile_best_rp(t, C, heads, ldc)
+                       : (t.l32 ? std::max(t.ncol, (vtile_l32_slots(C, heads) + 7) / 8 * 8) : t.ncol);
       nw = pass < 2 ? 4 : 8;
       const size_t lds = bwd ? vtile_bwd_lds(t, C, heads, true) : vtile_lds(t, heads, true);
       const int pf = bwd ? (nw == 8 ? vp_bwd_pf<8>() : vp_bwd_pf<4>()) : (nw == 8 ? vp_pf<8>() : vp_pf<4>());
@@ -1828,24 +1862,27 @@ static bool vtile_plan(int B, int H, int W, int C, int heads, int k, int ldc, og
   return true;
 }
 
-static bool vproj_plan(int B, int H, int W, int C, int heads, int k, int ldc, ogv_dtype dt, VTile& t, int& nw) {
-  return g_outlook_vproj && vtile_plan(B, H, W, C, heads, k, ldc, dt, false, t, nw);
+static bool vproj_plan(int B, int H, int W, int C, int heads, int k, int ldc, ogv_dtype dt, VTile& t, int& nw,
+                       bool l32 = false) {
+  return g_outlook_vproj && vtile_plan(B, H, W, C, heads, k, ldc, dt, false, t, nw, l32);
 }
 
 template <int NJ, int NK, int NW>
 static int vproj_run(const bf16* x, int ldx, const float* Wc, int wrows, const float* bias, bf16* cat, int ldc, bf16* y,
-                      int H, int W, int C, int heads, const VTile& t, bool sw, hipStream_t s) {
+                      int H, int W, int C, int heads, const VTile& t, bool sw, hipStream_t s, float* lg = nullptr,
+                      int ldl = 0) {
   const size_t lds = vtile_lds(t, heads, sw);
   const long per_cu = NW == 4 ? 2 : 1;
   const long nb = std::min<long>(t.ntiles, 256 * per_cu);
   const unsigned grid = (unsigned)((nb + 7) / 8 * 8);
-  auto kern = sw ? outlook_vproj_fwd_kernel<NJ, NK, true, NW> : outlook_vproj_fwd_kernel<NJ, NK, false, NW>;
+  auto kern = t.l32 ? (sw ? outlook_vproj_fwd_kernel<NJ, NK, true, NW, true> : outlook_vproj_fwd_kernel<NJ, NK, false, NW, true>)
+                    : (sw ? outlook_vproj_fwd_kernel<NJ, NK, true, NW, false> : outlook_vproj_fwd_kernel<NJ, NK, false, NW, false>);
   if (!lds_grant(reinterpret_cast<const void*>(kern), lds)) {
     set_error("%s: dynamic LDS grant of %zu bytes refused", "ogv_outlook_vproj_fwd", lds);
     return OGV_ERR_LAUNCH;
   }
   kern<<<grid, NW * 64, lds, s>>>(x, ldx, Wc, wrows, bias, cat, ldc, y, H, W, C, heads, t,
-                                    (int)vtile_x_bytes(t, heads), g_vp_dbg);
+                                    (int)vtile_x_bytes(t, heads), g_vp_dbg, lg, ldl);
   return OGV_OK;
 }
 
@@ -1933,73 +1970,107 @@ struct VHead {
   int RI, IPP, R, npanels, RG;
   int WP, RP;
   FDiv fRI, fW;
+  int S, units;                      // units per head (head_dim / 32) and heads * S: a unit = 32 v columns of a head
+  int halo, TH, TW, HWD, TX, TPI, NOUT;   // halo mode: TH x TW output tiles, (TH + 2) x HWD halo rows, HWD = TW + 2
+  FDiv fHWD, fTX, fTPI, fTW;
 };
 
-template <int NJV, int NK>
+// rows of the panel's LDS result tile, its softmax table and the weight slab (bf16 hi [+ lo]) + bias
 static size_t vhead_lds(const VHead& t, bool sw) {
-  constexpr int NCOL = (NJV + 1) * 16;
+  constexpr int NCOL = 48;
   return (size_t)(sw ? 2 : 1) * NCOL * t.WP * 2 + (size_t)NCOL * 4 + ((size_t)t.R * t.RP * 2 + 15) / 16 * 16 +
-         (size_t)t.R * 9 * 4;
+         (size_t)(t.halo ? t.NOUT : t.R) * 9 * 4;
 }
 
-template <int NJV, int NK, int NF, bool SW>
-__global__ __launch_bounds__(256, 2) void outlook_vproj_head_fwd_kernel(
+// A unit of work = 32 v columns of one head plus that head's 9 logit columns: NCOL = 48 slab rows
+// (head_dim 64 -- 14M / 22M stage 3 -- is two units that both compute the head's logits, so the weight
+// slice stays 48 x C and two workgroups fit a CU).  Two panel forms:
+//   HALO = false: a panel is IPP whole images (<= 128 rows), no halo;
+//   HALO = true (images of > 128 pixels: 14M stages 1-2, 22M stages 1-3): a panel is a TH x TW pixel tile
+//     of one image plus its 1-pixel halo, (TH + 2) x (TW + 2) rows whose projection is computed (the halo
+//     rows' again by the neighbouring tiles: ~1.3-1.5x the MFMA work, x re-read from L2) so the gather never
+//     leaves the LDS tile; out-of-image halo rows are skipped by the gather (the reference's zero padding).
+// L32: the fp32-logits form (as outlook_vproj_fwd_kernel's): the 9 logits stay fp32 in result-tile slots
+// 32 .. 49, the softmax reads them unrounded, training writes v_u to cat ([M, ldc] bf16, v only) and the head's
+// logits to lg ([M, ldl] fp32)
+template <int NK, int NF, bool SW, bool HALO, int NW, bool L32>
+__global__ __launch_bounds__(NW * 64, 8 / NW) void outlook_vproj_head_fwd_kernel(
     const bf16* __restrict__ x, int ldx, const float* __restrict__ Wc, const float* __restrict__ bias,
-    bf16* __restrict__ cat, int ldc, bf16* __restrict__ y, int B, int H, int W, int C, int heads, VHead t, int dbg) {
+    bf16* __restrict__ cat, int ldc, bf16* __restrict__ y, int B, int H, int W, int C, int heads, VHead t, int dbg,
+    float* __restrict__ lg, int ldl) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int NJ = NJV + 1, NCOL = NJ * 16, KP = NK * 32, HD = NJV * 16, HD8 = HD / 8;
+  constexpr int NJ = 3, NCOL = 48, KP = NK * 32, UD = 32, UD8 = 4, NT = NW * 64;
   const int WP = t.WP, RP = t.RP, R = t.R, HW = H * W;
   bf16* ws = reinterpret_cast<bf16*>(smem);                                  // [hi | lo][NCOL][WP]
   float* bs = reinterpret_cast<float*>(ws + (size_t)(SW ? 2 : 1) * NCOL * WP);   // [NCOL]
-  bf16* rs = reinterpret_cast<bf16*>(bs + NCOL);                             // [R][RP]: [v_h | logits_h | 0]
-  float* P = reinterpret_cast<float*>(reinterpret_cast<char*>(rs) + ((size_t)R * RP * 2 + 15) / 16 * 16);  // [R][9]
+  bf16* rs = reinterpret_cast<bf16*>(bs + NCOL);                             // [R][RP]: [v_u | logits_h | 0]
+  float* P = reinterpret_cast<float*>(reinterpret_cast<char*>(rs) + ((size_t)R * RP * 2 + 15) / 16 * 16);  // [.][9]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fg = lane >> 4;
-  const int head = (blockIdx.x >> 3) % heads;
-  const int rg = (blockIdx.x & 7) + 8 * (int)(blockIdx.x / (8 * heads));
-  // panel-local row r -> global row (or -1: a pad row of an image, or an image past B)
-  auto grow_of = [&](int p, int r) -> long {
-    const int i = fdiv(r, t.fRI), pix = r - i * t.RI;
-    const long img = (long)p * t.IPP + i;
-    return (pix < HW && img < B) ? img * HW + pix : -1L;
+  const int u = (blockIdx.x >> 3) % t.units;
+  const int rg = (blockIdx.x & 7) + 8 * (int)(blockIdx.x / (8 * t.units));
+  const int head = t.S == 1 ? u : (u >> 1), sub = u - head * t.S;
+  const int vc0 = head * (C / heads) + sub * UD;   // this unit's first v column (W_v row, cat / y column)
+  // panel p -> (image, top-left pixel of its halo tile); panel-local row r -> global row (or -1)
+  struct Pos { long img; int y0, x0; };
+  auto pos_of = [&](int p) -> Pos {
+    if constexpr (HALO) {
+      const int img = fdiv(p, t.fTPI), tt = p - img * t.TPI;
+      const int ty = fdiv(tt, t.fTX), tx = tt - ty * t.TX;
+      return Pos{img, ty * t.TH - 1, tx * t.TW - 1};
+    } else {
+      return Pos{(long)p * t.IPP, 0, 0};
+    }
   };
-  const int NFR = R / 16;   // row fragments per panel; wave w owns fragments w, w + 4, ...
+  auto grow_of = [&](const Pos& q, int r) -> long {
+    if constexpr (HALO) {
+      const int ly = fdiv(r, t.fHWD), lx = r - ly * t.HWD;
+      const int gy = q.y0 + ly, gx = q.x0 + lx;
+      return (ly < t.TH + 2 && gy >= 0 && gy < H && gx >= 0 && gx < W) ? q.img * HW + gy * W + gx : -1L;
+    } else {
+      const int i = fdiv(r, t.fRI), pix = r - i * t.RI;
+      const long img = q.img + i;
+      return (pix < HW && img < B) ? img * HW + pix : -1L;
+    }
+  };
+  const int NFR = R / 16;   // row fragments per panel; wave w owns fragments w, w + NW, ...
   bf16x8 xf[NF][NK];
   auto load_x = [&](int p) {
     if (dbg & 16) return;
+    const Pos q = pos_of(p);
 #pragma unroll
-    for (int q = 0; q < NF; ++q) {
-      const int f = wave + 4 * q;
-      const long g = f < NFR ? grow_of(p, f * 16 + fr) : -1L;
+    for (int i = 0; i < NF; ++i) {
+      const int f = wave + NW * i;
+      const long g = f < NFR ? grow_of(q, f * 16 + fr) : -1L;
       const bf16* src = x + (g < 0 ? 0L : g) * ldx + fg * 8;   // clamped: always a valid address
 #pragma unroll
       for (int kt = 0; kt < NK; ++kt) {
         const bf16x8 v = (kt * 32 + fg * 8 < C) ? *reinterpret_cast<const bf16x8*>(src + kt * 32) : bf16x8{};
-        xf[q][kt] = g < 0 ? bf16x8{} : v;
+        xf[i][kt] = g < 0 ? bf16x8{} : v;
       }
     }
   };
   if (rg < t.npanels) load_x(rg);   // the first panel's x in flight while the weights are staged
-  // weight slice of this head: slab row n < HD <- Wc[head*HD + n] (v), HD <= n < HD + 9 <-
-  // Wc[C + 9 head + n - HD] (logits), zero rows above; columns >= C zero
-  // (every load of the slice issued before the first conversion: one memory round trip)
-  constexpr int WPT = (NCOL * (KP / 4) + 255) / 256;
+  // weight slice of this unit: slab row n < 32 <- Wc[vc0 + n] (v), 32 <= n < 41 <- Wc[C + 9 head + n - 32]
+  // (logits), zero rows above; columns >= C zero (every load issued before the first conversion)
+  constexpr int WPT = (NCOL * (KP / 4) + NT - 1) / NT;
+  auto wrow = [&](int n) { return n < UD ? vc0 + n : (n < UD + 9 ? C + 9 * head + n - UD : -1); };
   float4 wv[WPT];
 #pragma unroll
-  for (int u = 0; u < WPT; ++u) {
-    const int idx = tid + u * 256;
+  for (int k4 = 0; k4 < WPT; ++k4) {
+    const int idx = tid + k4 * NT;
     const int n = idx / (KP / 4), k = (idx - n * (KP / 4)) * 4;
-    const int row = n < HD ? head * HD + n : (n < HD + 9 ? C + 9 * head + n - HD : -1);
+    const int row = wrow(n);
     const bool ok = idx < NCOL * (KP / 4) && row >= 0 && k < C;
     const float4 w4 = *reinterpret_cast<const float4*>(Wc + (ok ? (long)row * C + k : 0L));   // clamped address
-    wv[u] = ok ? w4 : float4{0.f, 0.f, 0.f, 0.f};
+    wv[k4] = ok ? w4 : float4{0.f, 0.f, 0.f, 0.f};
   }
 #pragma unroll
-  for (int u = 0; u < WPT; ++u) {
-    const int idx = tid + u * 256;
+  for (int k4 = 0; k4 < WPT; ++k4) {
+    const int idx = tid + k4 * NT;
     if (idx >= NCOL * (KP / 4)) break;
     const int n = idx / (KP / 4), k = (idx - n * (KP / 4)) * 4;
-    const float4 w4 = wv[u];
+    const float4 w4 = wv[k4];
     const bf16x4 h = {(bf16)w4.x, (bf16)w4.y, (bf16)w4.z, (bf16)w4.w};
     *reinterpret_cast<bf16x4*>(ws + n * WP + k) = h;
     if constexpr (SW) {
@@ -2008,17 +2079,26 @@ __global__ __launch_bounds__(256, 2) void outlook_vproj_head_fwd_kernel(
       *reinterpret_cast<bf16x4*>(ws + (NCOL + n) * WP + k) = l;
     }
   }
-  for (int n = tid; n < NCOL; n += 256) {
-    const int row = n < HD ? head * HD + n : (n < HD + 9 ? C + 9 * head + n - HD : -1);
+  for (int n = tid; n < NCOL; n += NT) {
+    const int row = wrow(n);
     bs[n] = (bias && row >= 0) ? bias[row] : 0.f;
   }
+  // interior output o of a halo panel -> its halo-tile row and global row (or -1: past a ragged edge)
+  auto out_of = [&](const Pos& q, int o, int& r) -> long {
+    const int oy = fdiv(o, t.fTW), ox = o - oy * t.TW;
+    r = (oy + 1) * t.HWD + ox + 1;
+    const int gy = q.y0 + 1 + oy, gx = q.x0 + 1 + ox;
+    return (gy < H && gx < W) ? q.img * HW + gy * W + gx : -1L;
+  };
+  const int NOUT = HALO ? t.NOUT : R;   // rows that produce output (halo: the tile's interior)
   for (int p = rg; p < t.npanels; p += t.RG) {
-    // 1. [v_h | logits_h] of the panel's rows on MFMA
+    const Pos q = pos_of(p);
+    // 1. [v_u | logits_h] of the panel's rows on MFMA
     f32x4 acc[NF][NJ];
 #pragma unroll
-    for (int q = 0; q < NF; ++q)
+    for (int i = 0; i < NF; ++i)
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) acc[q][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     __syncthreads();   // weights staged (first panel) / the previous panel's gather is done with rs and P
 #pragma unroll
     for (int kt = 0; kt < ((dbg & 8) ? 0 : NK); ++kt)
@@ -2026,58 +2106,72 @@ __global__ __launch_bounds__(256, 2) void outlook_vproj_head_fwd_kernel(
       for (int j = 0; j < NJ; ++j) {
         const bf16x8 wh = *reinterpret_cast<const bf16x8*>(ws + (j * 16 + fr) * WP + kt * 32 + fg * 8);
 #pragma unroll
-        for (int q = 0; q < NF; ++q) acc[q][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, xf[q][kt], acc[q][j], 0, 0, 0);
+        for (int i = 0; i < NF; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, xf[i][kt], acc[i][j], 0, 0, 0);
         if constexpr (SW) {
           const bf16x8 wl = *reinterpret_cast<const bf16x8*>(ws + (NCOL + j * 16 + fr) * WP + kt * 32 + fg * 8);
 #pragma unroll
-          for (int q = 0; q < NF; ++q) acc[q][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl, xf[q][kt], acc[q][j], 0, 0, 0);
+          for (int i = 0; i < NF; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl, xf[i][kt], acc[i][j], 0, 0, 0);
         }
       }
     if (p + t.RG < t.npanels) load_x(p + t.RG);   // in flight during the epilogue, softmax and gather
     // lane: row f * 16 + fr, columns 16 j + 4 fg .. + 3 (+ bias, rounded to bf16 as the GEMM output)
 #pragma unroll
-    for (int q = 0; q < NF; ++q) {
-      const int f = wave + 4 * q;
+    for (int i = 0; i < NF; ++i) {
+      const int f = wave + NW * i;
       if (f >= NFR) continue;
       const int m = f * 16 + fr;
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const int n = j * 16 + 4 * fg;
         const float4 b4 = *reinterpret_cast<const float4*>(bs + n);
-        const bf16x4 o = {(bf16)(acc[q][j][0] + b4.x), (bf16)(acc[q][j][1] + b4.y), (bf16)(acc[q][j][2] + b4.z),
-                          (bf16)(acc[q][j][3] + b4.w)};
+        if (L32 && j == NJ - 1) {   // the logit columns 32 .. 40: fp32 at slots 32 + 2 (n - 32) (44 .. 47: pad, dropped)
+          if (fg < 3)
+            *reinterpret_cast<float4*>(rs + m * RP + UD + 8 * fg) =
+                float4{acc[i][j][0] + b4.x, acc[i][j][1] + b4.y, acc[i][j][2] + b4.z, acc[i][j][3] + b4.w};
+          continue;
+        }
+        const bf16x4 o = {(bf16)(acc[i][j][0] + b4.x), (bf16)(acc[i][j][1] + b4.y), (bf16)(acc[i][j][2] + b4.z),
+                          (bf16)(acc[i][j][3] + b4.w)};
         *reinterpret_cast<bf16x4*>(rs + m * RP + n) = o;
       }
     }
     __syncthreads();
-    // 2a. the head's columns of cat (training): v_h as 16-B rows, the 9 logits as bf16 elements
+    // 2a. the unit's columns of cat (training): v_u as 16-B rows, the head's 9 logits (first unit) as bf16 elements
     if (cat) {
-      for (int idx = tid; idx < ((dbg & 2) ? 0 : R * HD8); idx += 256) {
-        const int r = idx / HD8, c8 = idx - r * HD8;
-        const long g = grow_of(p, r);
+      for (int idx = tid; idx < ((dbg & 2) ? 0 : NOUT * UD8); idx += NT) {
+        const int o = idx >> 2, c8 = idx & 3;
+        int r = o;
+        const long g = HALO ? out_of(q, o, r) : grow_of(q, o);
         if (g >= 0)
-          *reinterpret_cast<uint4*>(cat + g * ldc + head * HD + c8 * 8) = *reinterpret_cast<const uint4*>(rs + r * RP + c8 * 8);
+          *reinterpret_cast<uint4*>(cat + g * ldc + vc0 + c8 * 8) = *reinterpret_cast<const uint4*>(rs + r * RP + c8 * 8);
       }
-      for (int idx = tid; idx < ((dbg & 1) ? 0 : R * 9); idx += 256) {
-        const int r = idx / 9, jj = idx - r * 9;
-        const long g = grow_of(p, r);
-        if (g >= 0) cat[g * ldc + C + 9 * head + jj] = rs[r * RP + HD + jj];
-      }
-      const int pad = ldc - C - 9 * heads;   // the zero columns of [v | logits | 0] (the last head's)
-      if (head == heads - 1)
-        for (int idx = tid; idx < R * pad; idx += 256) {
-          const int r = idx / pad, jj = idx - r * pad;
-          const long g = grow_of(p, r);
+      if (sub == 0)
+        for (int idx = tid; idx < ((dbg & 1) ? 0 : NOUT * 9); idx += NT) {
+          const int o = idx / 9, jj = idx - o * 9;
+          int r = o;
+          const long g = HALO ? out_of(q, o, r) : grow_of(q, o);
+          if (g < 0) continue;
+          if constexpr (L32) lg[g * ldl + 9 * head + jj] = reinterpret_cast<const float*>(rs + r * RP + UD)[jj];
+          else cat[g * ldc + C + 9 * head + jj] = rs[r * RP + UD + jj];
+        }
+      const int pad = ldc - C - 9 * heads;   // the zero columns of [v | logits | 0] (the last unit's)
+      if (!L32 && u == t.units - 1)
+        for (int idx = tid; idx < NOUT * pad; idx += NT) {
+          const int o = idx / pad, jj = idx - o * pad;
+          int r = o;
+          const long g = HALO ? out_of(q, o, r) : grow_of(q, o);
           if (g >= 0) cat[g * ldc + C + 9 * heads + jj] = (bf16)0.f;
         }
     }
-    // 2b. softmax over the 9 (bf16-rounded) logits of every panel pixel
-    for (int r = tid; r < R; r += 256) {
-      const bf16* l = rs + r * RP + HD;
+    // 2b. softmax over the 9 (bf16-rounded) logits of every output pixel of the panel
+    for (int o = tid; o < NOUT; o += NT) {
+      int r = o;
+      if constexpr (HALO) out_of(q, o, r);
+      const bf16* l = rs + r * RP + UD;
       float a[9], mx = -INFINITY;
 #pragma unroll
       for (int jj = 0; jj < 9; ++jj) {
-        a[jj] = (float)l[jj];
+        a[jj] = L32 ? reinterpret_cast<const float*>(l)[jj] : (float)l[jj];
         mx = fmaxf(mx, a[jj]);
       }
       float sm = 0.f;
@@ -2088,16 +2182,29 @@ __global__ __launch_bounds__(256, 2) void outlook_vproj_head_fwd_kernel(
       }
       const float inv = 1.0f / sm;
 #pragma unroll
-      for (int jj = 0; jj < 9; ++jj) P[r * 9 + jj] = a[jj] * inv;
+      for (int jj = 0; jj < 9; ++jj) P[o * 9 + jj] = a[jj] * inv;
     }
     __syncthreads();
-    // 3. y[:, head] = 3 x 3 gather of v_h weighted by the softmax (out-of-image neighbours: v = 0)
-    for (int idx = tid; idx < ((dbg & 4) ? 0 : R * HD8); idx += 256) {
-      const int r = idx / HD8, cc = idx - r * HD8;
-      const long g = grow_of(p, r);
+    // 3. y[:, unit] = 3 x 3 gather of v_u weighted by the softmax (out-of-image neighbours: v = 0)
+    for (int idx = tid; idx < ((dbg & 4) ? 0 : NOUT * UD8); idx += NT) {
+      const int o = idx >> 2, cc = idx & 3;
+      int r = o;
+      const long g = HALO ? out_of(q, o, r) : grow_of(q, o);
       if (g < 0) continue;
-      const int i = fdiv(r, t.fRI), pix = r - i * t.RI;
-      const int yy = fdiv(pix, t.fW), xx = pix - yy * W;
+      int yy, xx, rbase, rstride;   // global pixel; the halo-tile row of the (-1, -1) neighbour and the row stride
+      if constexpr (HALO) {
+        const int oy = fdiv(o, t.fTW), ox = o - oy * t.TW;
+        yy = q.y0 + 1 + oy;
+        xx = q.x0 + 1 + ox;
+        rbase = oy * t.HWD + ox;
+        rstride = t.HWD;
+      } else {
+        const int i = fdiv(o, t.fRI), pix = o - i * t.RI;
+        yy = fdiv(pix, t.fW);
+        xx = pix - yy * W;
+        rbase = i * t.RI + (yy - 1) * W + (xx - 1);
+        rstride = W;
+      }
       float accy[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) accy[e] = 0.f;
@@ -2107,23 +2214,23 @@ __global__ __launch_bounds__(256, 2) void outlook_vproj_head_fwd_kernel(
         for (int kj = 0; kj < 3; ++kj) {
           const int ny = yy + ki - 1, nx = xx + kj - 1;
           if (ny < 0 || ny >= H || nx < 0 || nx >= W) continue;
-          const float w = P[r * 9 + ki * 3 + kj];
-          const uint4 raw = *reinterpret_cast<const uint4*>(rs + (i * t.RI + ny * W + nx) * RP + cc * 8);
+          const float w = P[o * 9 + ki * 3 + kj];
+          const uint4 raw = *reinterpret_cast<const uint4*>(rs + (rbase + ki * rstride + kj) * RP + cc * 8);
           const bf16* e8 = reinterpret_cast<const bf16*>(&raw);
 #pragma unroll
           for (int e = 0; e < 8; ++e) accy[e] = fmaf(w, (float)e8[e], accy[e]);
         }
-      store_vec<bf16, 8>(y + g * C + head * HD + cc * 8, accy);
+      store_vec<bf16, 8>(y + g * C + vc0 + cc * 8, accy);
     }
   }
 }
 
-// knob "vp_head" (default 1): the per-head whole-image kernel above for the wide stages it plans;
-// "vph_rows": target rows per panel (a panel is whole images, <= 128 rows)
-// (2: also head_dim 64 -- 14M / 22M stage 3 -- whose 125 KB weight slice leaves one workgroup per CU:
-// measured slower than the unfused pair there, 86 vs 48 us at 14M stage 3, profiles/r05b_vph.log)
+// knob "vp_head" (default 1): the per-head kernel above for the wide stages it plans (whole-image panels for
+// images of <= 128 pixels, halo tiles above); 2: also head_dim 64 (two 32-column units per head; the round-5
+// form with one 80-row slab per head measured slower than the unfused pair, 86 vs 48 us at 14M stage 3,
+// profiles/r05b_vph.log); 0: off.  "vph_rows": target rows per whole-image panel (<= 128)
 static int g_vp_head = 1;
-void set_vp_head(int v) { g_vp_head = v < 0 ? 0 : (v > 2 ? 2 : v); }
+void set_vp_head(int v) { g_vp_head = v < 0 ? 0 : (v > 3 ? 3 : v); }
 // (0 = auto: 128 for images of <= 32 pixels, 64 otherwise -- measured, tools/bench_vproj.py cold L2,
 // profiles/r05c_vph.log: 7M stage 3 (4 x 4) 21.2 -> 19.4 us at 128 rows, stage 2 (8 x 8) 34.6 vs 41.9 us at 64)
 static int g_vph_rows = 0;
@@ -2134,49 +2241,123 @@ static int g_vph_wgs = 3;
 void set_vph_wgs(int v) { g_vph_wgs = v < 1 ? 1 : (v > 8 ? 8 : v); }
 static int g_vph_dbg = 0;
 void set_vph_dbg(int v) { g_vph_dbg = v; }
+// "vph_halo": the halo-tile form -- 0 (default) off (images > 128 pixels keep the unfused pair); 1 where a pixel's
+// x is re-read by at most 4 units (C = 128: 14M / 22M stage 1); 2 every wide shape; 3 every wide shape with 8-wave
+// workgroups (tiles of <= 384 computed rows instead of 192).  Measured (tools/bench_vproj.py, cold L2,
+// profiles/r06b_vproj_halo.log, fused_train vs the unfused GEMM + aggregation): 4 units 137.5 vs 139.6 us (14M
+// stage 1), 786 vs 840 us (22M stage 1); 8 units 111 vs 87 us (14M stage 2), 631 vs 444 us (22M stage 2); 12 units
+// (head_dim 64 as two units) 92 vs 48 us, 608 (438 with 8 waves) vs 188 us.  Phase what-ifs at 22M stage 2
+// (vph_dbg, r06c): no x loads and no MFMAs 296 us -- the per-panel phases (cat / y stores, softmax, gather, three
+// barriers) alone take 2/3 of the unfused pair's time once every pixel is visited by 8 workgroups.
+// "vph_tile" (TH * 100 + TW, 0 = auto): force a halo tile
+// Default 0: at the step level the 4-unit form measured no gain (14M 43.31 / 43.46 ms off vs 43.60 / 43.55 on,
+// 22M 340.5 / 338.8 vs 339.5 / 339.5 ms, profiles/r06d_halo_step.log), so it stays opt-in.
+static int g_vph_halo = 0;
+void set_vph_halo(int v) { g_vph_halo = v < 0 ? 0 : (v > 3 ? 3 : v); }
+static int g_vph_tile = 0;
+void set_vph_tile(int v) { g_vph_tile = v < 0 ? 0 : v; }
 
-static bool vhead_plan(int B, int H, int W, int C, int heads, int k, int ldc, ogv_dtype dt, VHead& t) {
+// the halo tile with the fewest computed rows per output pixel (ragged edge tiles counted whole), R <= rmax
+static bool vhead_halo_tile(int H, int W, int rmax, int& TH, int& TW) {
+  if (g_vph_tile) {
+    TH = g_vph_tile / 100;
+    TW = g_vph_tile % 100;
+    return TH >= 1 && TW >= 1 && ((TH + 2) * (TW + 2) + 15) / 16 * 16 <= rmax;
+  }
+  double best = 1e30;
+  TH = TW = 0;
+  for (int tw = 4; tw <= 62 && tw <= W + 2; tw += 2)
+    for (int th = 1; th <= 32; ++th) {
+      const int rr = ((th + 2) * (tw + 2) + 15) / 16 * 16;
+      if (rr > rmax) break;
+      const double tiles = (double)((H + th - 1) / th) * ((W + tw - 1) / tw);
+      const double cost = tiles * rr / ((double)H * W) + 1e-3 * tiles;   // rows computed per pixel, then fewer tiles
+      if (cost < best) { best = cost; TH = th; TW = tw; }
+    }
+  return TH > 0;
+}
+
+static bool vhead_plan(int B, int H, int W, int C, int heads, int k, int ldc, ogv_dtype dt, VHead& t, int& nw) {
   if (!g_outlook_vproj || !g_vp_head) return false;
   if (dt != OGV_BF16 || k != 3 || B <= 0 || H <= 0 || W <= 0 || heads <= 0) return false;
   if (C % 32 != 0 || !vbig_cj(C / 32) || C % heads != 0) return false;   // C in {128, 192, 256, 384}
   const int hd = C / heads;
-  if (hd != 32 && !(hd == 64 && g_vp_head == 2)) return false;
+  if (hd != 32 && !(hd == 64 && g_vp_head >= 2)) return false;
   if (ldc != (C + heads * 9 + 7) / 8 * 8) return false;
   const int HW = H * W;
   t = VHead{};
+  t.S = hd / 32;
+  t.units = heads * t.S;
   t.RI = (HW + 15) / 16 * 16;
-  if (t.RI > 128) return false;
-  const int rows = g_vph_rows ? g_vph_rows : (t.RI <= 32 ? 128 : 64);
-  t.IPP = rows / t.RI < 1 ? 1 : rows / t.RI;
-  t.R = t.IPP * t.RI;
-  t.npanels = (B + t.IPP - 1) / t.IPP;
-  const int NCOL = hd + 16, KP = C;
-  t.WP = KP + 8;      // (KP + 8) / 2 dwords per row: 16 fragment rows on distinct bank quads
-  t.RP = NCOL + 8;
-  const size_t lds = (hd == 32 ? vhead_lds<2, 4> : vhead_lds<4, 4>)(t, true);
+  nw = 4;
+  if (t.RI <= 128) {
+    const int rows = g_vph_rows ? g_vph_rows : (t.RI <= 32 ? 128 : 64);
+    t.IPP = rows / t.RI < 1 ? 1 : rows / t.RI;
+    t.R = t.IPP * t.RI;
+    t.npanels = (B + t.IPP - 1) / t.IPP;
+  } else {
+    if (!g_vph_halo || (g_vph_halo == 1 && t.units > 4)) return false;
+    nw = g_vph_halo == 3 ? 8 : 4;
+    int TH, TW;
+    if (!vhead_halo_tile(H, W, 48 * nw, TH, TW)) return false;
+    t.halo = 1;
+    t.TH = TH;
+    t.TW = TW;
+    t.HWD = TW + 2;
+    t.TX = (W + TW - 1) / TW;
+    t.TPI = t.TX * ((H + TH - 1) / TH);
+    t.NOUT = TH * TW;
+    t.R = ((TH + 2) * t.HWD + 15) / 16 * 16;
+    if ((long)B * t.TPI >= (1L << 22)) return false;
+    t.npanels = B * t.TPI;
+    t.fHWD = fdiv_make(t.HWD);
+    t.fTX = fdiv_make(t.TX);
+    t.fTPI = fdiv_make(t.TPI);
+    t.fTW = fdiv_make(TW);
+  }
+  t.WP = C + 8;      // (C + 8) / 2 dwords per row: 16 fragment rows on distinct bank quads
+  t.RP = 48 + 8;
+  const size_t lds = vhead_lds(t, true);
   if (lds > 160 * 1024) return false;
   const int fit = (int)((160 * 1024) / lds);
-  const int per_cu = g_vph_wgs < fit ? g_vph_wgs : fit;
-  int rg = (256 * per_cu / heads) / 8 * 8;
+  const int want = nw == 8 ? (g_vph_wgs + 1) / 2 : g_vph_wgs;
+  const int per_cu = want < fit ? want : fit;
+  int rg = (256 * per_cu / t.units) / 8 * 8;
   const int np8 = (t.npanels + 7) / 8 * 8;
   t.RG = rg < 8 ? 8 : (rg > np8 ? np8 : rg);
-  if ((long)t.RG * heads >= (1L << 24)) return false;
+  if ((long)t.RG * t.units >= (1L << 24)) return false;
   t.fRI = fdiv_make(t.RI);
   t.fW = fdiv_make(W);
   return true;
 }
 
-template <int NJV, int NK, int NF>
+template <int NK, int NF, bool HALO, int NW>
 static int vhead_run(const bf16* x, int ldx, const float* Wc, const float* bias, bf16* cat, int ldc, bf16* y, int B,
-                      int H, int W, int C, int heads, const VHead& t, bool sw, hipStream_t s) {
-  const size_t lds = vhead_lds<NJV, NK>(t, sw);
-  auto kern = sw ? outlook_vproj_head_fwd_kernel<NJV, NK, NF, true> : outlook_vproj_head_fwd_kernel<NJV, NK, NF, false>;
+                      int H, int W, int C, int heads, const VHead& t, bool sw, hipStream_t s, float* lg, int ldl,
+                      bool l32) {
+  const size_t lds = vhead_lds(t, sw);
+  auto kern = l32 ? (sw ? outlook_vproj_head_fwd_kernel<NK, NF, true, HALO, NW, true>
+                        : outlook_vproj_head_fwd_kernel<NK, NF, false, HALO, NW, true>)
+                  : (sw ? outlook_vproj_head_fwd_kernel<NK, NF, true, HALO, NW, false>
+                        : outlook_vproj_head_fwd_kernel<NK, NF, false, HALO, NW, false>);
   if (!lds_grant(reinterpret_cast<const void*>(kern), lds)) {
     set_error("%s: dynamic LDS grant of %zu bytes refused", "ogv_outlook_vproj_fwd", lds);
     return OGV_ERR_LAUNCH;
   }
-  kern<<<(unsigned)(t.RG * heads), 256, lds, s>>>(x, ldx, Wc, bias, cat, ldc, y, B, H, W, C, heads, t, g_vph_dbg);
+  kern<<<(unsigned)(t.RG * t.units), NW * 64, lds, s>>>(x, ldx, Wc, bias, cat, ldc, y, B, H, W, C, heads, t, g_vph_dbg,
+                                                          lg, ldl);
   return OGV_OK;
+}
+
+template <int NK>
+static int vhead_dispatch(const bf16* x, int ldx, const float* Wc, const float* bias, bf16* cat, int ldc, bf16* y,
+                          int B, int H, int W, int C, int heads, const VHead& t, int nw, bool sw, hipStream_t s,
+                          float* lg, int ldl, bool l32) {
+  if (t.halo)
+    return nw == 8 ? vhead_run<NK, 3, true, 8>(x, ldx, Wc, bias, cat, ldc, y, B, H, W, C, heads, t, sw, s, lg, ldl, l32)
+                   : vhead_run<NK, 3, true, 4>(x, ldx, Wc, bias, cat, ldc, y, B, H, W, C, heads, t, sw, s, lg, ldl, l32);
+  return t.R > 64 ? vhead_run<NK, 2, false, 4>(x, ldx, Wc, bias, cat, ldc, y, B, H, W, C, heads, t, sw, s, lg, ldl, l32)
+                  : vhead_run<NK, 1, false, 4>(x, ldx, Wc, bias, cat, ldc, y, B, H, W, C, heads, t, sw, s, lg, ldl, l32);
 }
 
 static bool vproj_bwd_plan(int B, int H, int W, int C, int heads, int k, int ldc, ogv_dtype dt, VTile& t, int& nw) {
@@ -2210,7 +2391,8 @@ extern "C" int ogv_outlook_vproj_supported(int B, int H, int W, int C, int heads
   if (g_outlook_vproj < (train ? 2 : 1) || !lds_160k()) return 0;   // every fused variant may need > 64 KB
   int nw = 0;
   VHead th;
-  if (vhead_plan(B, H, W, C, heads, k, ldc, dt, th)) return 1;   // wide stages, small images: per-head kernel
+  int thw = 4;
+  if (vhead_plan(B, H, W, C, heads, k, ldc, dt, th, thw)) return 1;   // wide stages: the per-head kernel
   if (vbig_plan(B, H, W, C, heads, k, ldc, dt, t)) return 1;   // wide stages: forward with cat, tiled backward
   if (!vproj_plan(B, H, W, C, heads, k, ldc, dt, t, nw)) return 0;
   if (!train || g_outlook_vproj < 3) return 1;
@@ -2258,36 +2440,43 @@ extern "C" int ogv_outlook_vproj_bwd(const void* x, int ldx, const float* w, con
   return OGV_ERR_ARG;
 }
 
-extern "C" int ogv_outlook_vproj_fwd(const void* x, int ldx, const float* w, const float* bias, void* cat, int ldc,
-                                     void* y, int B, int H, int W, int C, int heads, int k, ogv_dtype dt,
-                                     void* stream) {
+// l32: the fp32-logits form -- `cat` receives v only ([M, ldc] bf16 rows), `lg` the logits ([M, ldl] fp32);
+// the weight has wrows = C + 9 heads rounded up to 8 rows either way
+static int vproj_fwd_impl(const void* x, int ldx, const float* w, const float* bias, void* cat, int ldc, float* lg,
+                          int ldl, bool l32, void* y, int B, int H, int W, int C, int heads, int k, ogv_dtype dt,
+                          void* stream) {
   OGV_REQUIRE(x && w && y, "ogv_outlook_vproj_fwd: null pointer");
   int rc = check_args(B, H, W, C, heads, k, heads * k * k, C, dt, "ogv_outlook_vproj_fwd");
   if (rc) return rc;
+  const int wrows = (C + heads * k * k + 7) / 8 * 8;
+  if (l32) {
+    OGV_REQUIRE(!cat == !lg, "ogv_outlook_vproj_fwd_l32: v and logits are written together (both or neither)");
+    OGV_REQUIRE(!cat || (ldc >= C && ldc % 8 == 0 && ldl >= (heads * 9 + 3) / 4 * 4 && ldl % 4 == 0 && al16p(lg)),
+                "ogv_outlook_vproj_fwd_l32: ld_v %d (>= C, 8 | ld_v) / ld_logits %d (>= 9 heads rounded to 4, 16-B rows)",
+                ldc, ldl);
+  }
   VTile t;
   int nw = 0;
   VHead th;
-  if (vhead_plan(B, H, W, C, heads, k, ldc, dt, th)) {
+  int thw = 4;
+  if (vhead_plan(B, H, W, C, heads, k, wrows, dt, th, thw)) {
     OGV_REQUIRE(ldx >= C && ldx % 8 == 0 && al16p(x) && al16p(y) && (!cat || al16p(cat)) && al16p(w),
                 "ogv_outlook_vproj_fwd: rows must be 16-B aligned (ldx %d)", ldx);
     const bool sw = (split_w() & 1) != 0;
     hipStream_t s = as_stream(stream);
     const bf16* xb = (const bf16*)x;
     bf16 *cb = (bf16*)cat, *yb = (bf16*)y;
-    const int nf = th.R > 64 ? 2 : 1;
-#define OGV_VHEAD(njv, nk)                                                                                  \
-  if (C / heads == njv * 16 && C / 32 == nk) {                                                              \
-    const int e = nf == 1 ? vhead_run<njv, nk, 1>(xb, ldx, w, bias, cb, ldc, yb, B, H, W, C, heads, th, sw, s) \
-                          : vhead_run<njv, nk, 2>(xb, ldx, w, bias, cb, ldc, yb, B, H, W, C, heads, th, sw, s); \
-    return e ? e : check_launch("ogv_outlook_vproj_fwd");                                                  \
+    int e;
+    switch (C / 32) {
+      case 4: e = vhead_dispatch<4>(xb, ldx, w, bias, cb, ldc, yb, B, H, W, C, heads, th, thw, sw, s, lg, ldl, l32); break;
+      case 6: e = vhead_dispatch<6>(xb, ldx, w, bias, cb, ldc, yb, B, H, W, C, heads, th, thw, sw, s, lg, ldl, l32); break;
+      case 8: e = vhead_dispatch<8>(xb, ldx, w, bias, cb, ldc, yb, B, H, W, C, heads, th, thw, sw, s, lg, ldl, l32); break;
+      default: e = vhead_dispatch<12>(xb, ldx, w, bias, cb, ldc, yb, B, H, W, C, heads, th, thw, sw, s, lg, ldl, l32); break;
+    }
+    return e ? e : check_launch("ogv_outlook_vproj_fwd");
   }
-    OGV_VHEAD(2, 4) OGV_VHEAD(2, 6) OGV_VHEAD(2, 8) OGV_VHEAD(2, 12)
-    OGV_VHEAD(4, 4) OGV_VHEAD(4, 6) OGV_VHEAD(4, 8) OGV_VHEAD(4, 12)
-#undef OGV_VHEAD
-    OGV_REQUIRE(false, "ogv_outlook_vproj_fwd: no per-head instantiation for C %d / %d heads", C, heads);
-  }
-  const bool big = vbig_plan(B, H, W, C, heads, k, ldc, dt, t);
-  OGV_REQUIRE(big || vproj_plan(B, H, W, C, heads, k, ldc, dt, t, nw),
+  const bool big = !l32 && vbig_plan(B, H, W, C, heads, k, wrows, dt, t);
+  OGV_REQUIRE(big || vproj_plan(B, H, W, C, heads, k, wrows, dt, t, nw, l32),
               "ogv_outlook_vproj_fwd: unsupported shape (needs bf16, k=3, 8 | head_dim, 16 | C <= 96 or "
               "C in {128, 192, 256, 384} with head_dim <= 64, ldc = C + 9*heads rounded up to 8; see "
               "ogv_outlook_vproj_supported)");
@@ -2300,10 +2489,10 @@ extern "C" int ogv_outlook_vproj_fwd(const void* x, int ldx, const float* w, con
     bf16 *cb = (bf16*)cat, *yb = (bf16*)y;
     int e;
     switch (C / 32) {
-      case 4: e = vbig_run<4>(xb, ldx, w, ldc, bias, cb, ldc, yb, H, W, C, heads, t, sw, s); break;
-      case 6: e = vbig_run<6>(xb, ldx, w, ldc, bias, cb, ldc, yb, H, W, C, heads, t, sw, s); break;
-      case 8: e = vbig_run<8>(xb, ldx, w, ldc, bias, cb, ldc, yb, H, W, C, heads, t, sw, s); break;
-      default: e = vbig_run<12>(xb, ldx, w, ldc, bias, cb, ldc, yb, H, W, C, heads, t, sw, s); break;
+      case 4: e = vbig_run<4>(xb, ldx, w, wrows, bias, cb, ldc, yb, H, W, C, heads, t, sw, s); break;
+      case 6: e = vbig_run<6>(xb, ldx, w, wrows, bias, cb, ldc, yb, H, W, C, heads, t, sw, s); break;
+      case 8: e = vbig_run<8>(xb, ldx, w, wrows, bias, cb, ldc, yb, H, W, C, heads, t, sw, s); break;
+      default: e = vbig_run<12>(xb, ldx, w, wrows, bias, cb, ldc, yb, H, W, C, heads, t, sw, s); break;
     }
     return e ? e : check_launch("ogv_outlook_vproj_fwd");
   }
@@ -2314,8 +2503,8 @@ extern "C" int ogv_outlook_vproj_fwd(const void* x, int ldx, const float* w, con
   bf16 *cb = (bf16*)cat, *yb = (bf16*)y;
 #define OGV_VPROJ(nj, nk)                                                                      \
   if (NJ == nj && NK == nk) {                                                                  \
-    const int e = nw == 4 ? vproj_run<nj, nk, 4>(xb, ldx, w, ldc, bias, cb, ldc, yb, H, W, C, heads, t, sw, s) \
-                          : vproj_run<nj, nk, 8>(xb, ldx, w, ldc, bias, cb, ldc, yb, H, W, C, heads, t, sw, s); \
+    const int e = nw == 4 ? vproj_run<nj, nk, 4>(xb, ldx, w, wrows, bias, cb, ldc, yb, H, W, C, heads, t, sw, s, lg, ldl) \
+                          : vproj_run<nj, nk, 8>(xb, ldx, w, wrows, bias, cb, ldc, yb, H, W, C, heads, t, sw, s, lg, ldl); \
     return e ? e : check_launch("ogv_outlook_vproj_fwd");                                      \
   }
   // (NJ, NK) pairs the plan admits: 16 | C <= 96, 8 | head_dim, ncol = C + 9 heads rounded to 16 <= 128
@@ -2325,6 +2514,39 @@ extern "C" int ogv_outlook_vproj_fwd(const void* x, int ldx, const float* w, con
 #undef OGV_VPROJ
   OGV_REQUIRE(false, "ogv_outlook_vproj_fwd: no instantiation for %d column / %d k blocks", NJ, NK);
   return OGV_ERR_ARG;
+}
+
+extern "C" int ogv_outlook_vproj_fwd(const void* x, int ldx, const float* w, const float* bias, void* cat, int ldc,
+                                     void* y, int B, int H, int W, int C, int heads, int k, ogv_dtype dt,
+                                     void* stream) {
+  if (k > 0 && heads > 0)
+    OGV_REQUIRE(ldc == (C + heads * k * k + 7) / 8 * 8, "ogv_outlook_vproj_fwd: ldc %d must be C + heads*k*k rounded up to 8",
+                ldc);
+  return vproj_fwd_impl(x, ldx, w, bias, cat, ldc, nullptr, 0, false, y, B, H, W, C, heads, k, dt, stream);
+}
+
+// knob "vp_l32" (default 1): the fused Outlooker keeps the logits in fp32 (ogv_outlook_vproj_fwd_l32 +
+// ogv_outlook_agg_bwd_l32) wherever its per-head or tile kernel runs; 0: the round-5 bf16 cat
+static int g_vp_l32 = 1;
+namespace ogv {
+void set_vp_l32(int v) { g_vp_l32 = v ? 1 : 0; }
+}  // namespace ogv
+
+extern "C" int ogv_outlook_vproj_l32_supported(int B, int H, int W, int C, int heads, int k, int train, ogv_dtype dt) {
+  if (!g_vp_l32 || g_outlook_vproj < (train ? 2 : 1) || !lds_160k() || heads <= 0 || k != 3) return 0;
+  const int wrows = (C + heads * k * k + 7) / 8 * 8;
+  VTile t;
+  VHead th;
+  int nw = 0;
+  if (vhead_plan(B, H, W, C, heads, k, wrows, dt, th, nw)) return 1;
+  if (g_vp_big && vbig_plan(B, H, W, C, heads, k, wrows, dt, t)) return 0;   // the streaming kernel: bf16 cat only
+  return vproj_plan(B, H, W, C, heads, k, wrows, dt, t, nw, true) ? 1 : 0;
+}
+
+extern "C" int ogv_outlook_vproj_fwd_l32(const void* x, int ldx, const float* w, const float* bias, void* v, int ldv,
+                                         float* logits, int ldl, void* y, int B, int H, int W, int C, int heads, int k,
+                                         ogv_dtype dt, void* stream) {
+  return vproj_fwd_impl(x, ldx, w, bias, v, ldv, logits, ldl, true, y, B, H, W, C, heads, k, dt, stream);
 }
 
 extern "C" int ogv_outlook_agg_fwd(const void* v, const void* logits, void* y, int B, int H, int W, int C, int heads,
@@ -2375,4 +2597,24 @@ extern "C" int ogv_outlook_agg_bwd(const void* dy, const void* v, const void* lo
   OGV_OUTLOOK_DISPATCH(launch_bwd, dy, v, logits, dv, dlogits, probs_ws, B, H, W, C, heads, ldl, ldv, lddv, lddl,
                        dl_cols, as_stream(stream));
   return check_launch("ogv_outlook_agg_bwd");
+}
+
+extern "C" int ogv_outlook_agg_bwd_l32(const void* dy, const void* v, const float* logits, void* dv, void* dlogits,
+                                       int B, int H, int W, int C, int heads, int k, int ldl, int ldv, int lddv,
+                                       int lddl, int dl_cols, ogv_dtype dt, void* stream) {
+  if (skip_mask() & 64) return OGV_OK;
+  OGV_REQUIRE(dy && v && logits && dv && dlogits, "ogv_outlook_agg_bwd_l32: null pointer");
+  int rc = check_args(B, H, W, C, heads, k, ldl, ldv, dt, "ogv_outlook_agg_bwd_l32");
+  if (rc) return rc;
+  OGV_REQUIRE(lddv >= C && lddl >= heads * k * k && dl_cols >= heads * k * k && dl_cols <= lddl,
+              "ogv_outlook_agg_bwd_l32: ld_dv %d / ld_dlogits %d / dl_cols %d too small", lddv, lddl, dl_cols);
+  const int hd = C / heads;
+  OGV_REQUIRE(use_tile(2, dt, k, hd, {dy, v, dv}, {ldv, lddv, C}),
+              "ogv_outlook_agg_bwd_l32: needs the LDS-tiled backward (bf16, k = 3, 8 | head_dim <= 64, 16-B rows, "
+              "knob outlook_tile bit 2)");
+  const OTile t = otile_plan(B, H, W, heads, hd, true);
+  OGV_REQUIRE(t.ntiles < (1L << 22), "ogv_outlook_agg: %ld tiles exceed the tile kernels' index range", t.ntiles);
+  OGV_OTILE_HD(otile_bwd_run, hd, (const bf16*)dy, C, (const bf16*)v, ldv, logits, ldl, (bf16*)dv, lddv,
+               (bf16*)dlogits, lddl, dl_cols, H, W, heads, t, as_stream(stream));
+  return check_launch("ogv_outlook_agg_bwd_l32");
 }

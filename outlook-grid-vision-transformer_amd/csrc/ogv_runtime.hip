@@ -312,6 +312,18 @@ extern "C" int ogv_set_option(const char* name, int value) {
     set_vph_wgs(value);
     return OGV_OK;
   }
+  if (!strcmp(name, "vp_l32")) {
+    set_vp_l32(value);
+    return OGV_OK;
+  }
+  if (!strcmp(name, "vph_halo")) {
+    set_vph_halo(value);
+    return OGV_OK;
+  }
+  if (!strcmp(name, "vph_tile")) {
+    set_vph_tile(value);
+    return OGV_OK;
+  }
   if (!strcmp(name, "vph_dbg")) {
     set_vph_dbg(value);
     return OGV_OK;

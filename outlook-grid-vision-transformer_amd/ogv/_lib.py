@@ -82,6 +82,9 @@ SIGNATURES = {
     "ogv_outlook_vproj_supported": (_i, [_i, _i, _i, _i, _i, _i, _i, _i, _i]),
     "ogv_outlook_vproj_bwd_supported": (_i, [_i, _i, _i, _i, _i, _i, _i, _i]),
     "ogv_outlook_vproj_fwd": (_i, [_p, _i, _p, _p, _p, _i, _p, _i, _i, _i, _i, _i, _i, _i, _p]),
+    "ogv_outlook_vproj_l32_supported": (_i, [_i, _i, _i, _i, _i, _i, _i, _i]),
+    "ogv_outlook_vproj_fwd_l32": (_i, [_p, _i, _p, _p, _p, _i, _p, _i, _p, _i, _i, _i, _i, _i, _i, _i, _p]),
+    "ogv_outlook_agg_bwd_l32": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _p]),
     "ogv_outlook_vproj_bwd": (_i, [_p, _i, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _p]),
     "ogv_outlook_agg_bwd": (_i, [_p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _p]),
     "ogv_grid_attn_fwd": (_i, [_p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _f, _i, _p]),

@@ -160,14 +160,19 @@ def probe_bytes(name: str, u: dict) -> int:
     e = u["elem"]
     if name == "outlook_fwd":   # read v [M,C] + logits [M,k*k*h], write y [M,C]
         return e * u["M"] * (2 * u["C"] + u["k"] * u["k"] * u["heads"])
-    if name == "outlook_vproj":  # read x [M,C] + fp32 W [ld,C] (+ bias), write y [M,C] (+ cat [M,ld] in training)
+    if name == "outlook_vproj":  # read x [M,C] + fp32 W [ld,C] (+ bias), write y [M,C] (+ cat [M,ld] in training;
+        # the fp32-logits form: v [M,C] + fp32 logits [M, 9h rounded to 4])
+        if u.get("l32"):
+            saved = (e * u["C"] + 4 * _l32_ld(u["heads"], u["k"])) if u["cat"] else 0
+            return e * u["M"] * 2 * u["C"] + u["M"] * saved + 4 * u["ld"] * (u["C"] + 1)
         return e * u["M"] * (2 * u["C"] + (u["ld"] if u["cat"] else 0)) + 4 * u["ld"] * (u["C"] + 1)
     if name == "outlook_vproj_bwd":  # read x [M,C], dy [M,C] + fp32 W [ld,C] (+ bias), write dcat [M,ld]
         return e * u["M"] * (2 * u["C"] + u["ld"]) + 4 * u["ld"] * (u["C"] + 1)
     if name == "grid_fwd":     # read qkv [M,3C], write out [M,C] + fp32 lse [M,h]
         return e * u["M"] * 4 * u["C"] + 4 * u["M"] * u["heads"]
-    if name == "outlook_bwd":   # read dy, v, logits; write dv, dlogits
-        return e * u["M"] * (3 * u["C"] + 2 * u["k"] * u["k"] * u["heads"])
+    if name == "outlook_bwd":   # read dy, v, logits; write dv, dlogits (the fp32-logits form reads fp32 logits)
+        nl = u["k"] * u["k"] * u["heads"]
+        return e * u["M"] * (3 * u["C"] + nl) + (4 if u.get("l32") else e) * u["M"] * nl
     if name == "wgrad":         # read G [M,N], X [M,K]; write fp32 dW [N,K] (+ dbias)
         return e * u["M"] * (u["N"] + u["K"]) + 4 * u["N"] * u["K"] + (4 * u["N"] if u["bias"] else 0)
     if name in ("gemm_fwd", "sgemm", "gemm_tiled", "gemm_panel") and u.get("kind", "fwd") == "fwd":
@@ -836,32 +841,49 @@ class _OutlookAggCat(torch.autograd.Function):
         return dcat, None, None, None, None, None, None
 
 
+def _l32_ld(heads, k):
+    return (heads * k * k + 3) // 4 * 4
+
+
 class _OutlookVProj(torch.autograd.Function):
     """Outlooker forward fused with its v / attn 1x1 projections (ogv_outlook_vproj_fwd): x [M, C]
     -> y [M, C].  mode 0: inference (nothing saved); 1: training with the fused backward
     (ogv_outlook_vproj_bwd recomputes [v | logits] from x in LDS, so the forward writes only y);
     2: training that saves cat = [v | logits | 0] [M, ld] for the LDS-tiled aggregation backward.
-    Either backward yields ONE dcat = [dv | dlogits | 0], then ONE dgrad + ONE wgrad of the
-    concatenated weight (as _OutlookAggCat + _Linear)."""
+    l32 (the default where ogv_outlook_vproj_l32_supported): the fp32-logits form -- the forward's softmax
+    reads the logits unrounded, mode 2 saves v [M, C] bf16 and the logits [M, 9 heads rounded to 4] fp32
+    (ogv_outlook_vproj_fwd_l32), and the tiled backward recomputes the softmax from them
+    (ogv_outlook_agg_bwd_l32).  Either backward yields ONE dcat = [dv | dlogits | 0], then ONE dgrad +
+    ONE wgrad of the concatenated weight (as _OutlookAggCat + _Linear)."""
 
     @staticmethod
-    def forward(ctx, x2d, w, b, C, B, H, W, heads, k, mode):
+    def forward(ctx, x2d, w, b, C, B, H, W, heads, k, mode, l32):
         lib = _lib.load()
         M = x2d.shape[0]
         ld = w.shape[0]
         y = torch.empty((M, C), dtype=x2d.dtype, device=x2d.device)
-        cat = torch.empty((M, ld), dtype=x2d.dtype, device=x2d.device) if mode == 2 else None
-        ou = dict(M=M, C=C, ld=ld, heads=heads, k=k, cat=mode == 2, elem=x2d.element_size())
-        with _probe("outlook_vproj", ou), _census("outlook_vproj", ou):
-            check(lib.ogv_outlook_vproj_fwd(_ptr(x2d), x2d.stride(0), _ptr(w), _ptr(b), _ptr(cat), ld, _ptr(y), B, H, W,
-                                            C, heads, k, _dt(x2d), _stream()), "ogv_outlook_vproj_fwd")
-        ctx.save_for_backward(x2d, w, b, cat)
+        ou = dict(M=M, C=C, ld=ld, heads=heads, k=k, cat=mode == 2, elem=x2d.element_size(), l32=l32)
+        lg = None
+        if l32:
+            lld = _l32_ld(heads, k)
+            cat = torch.empty((M, C), dtype=x2d.dtype, device=x2d.device) if mode == 2 else None
+            lg = torch.empty((M, lld), dtype=torch.float32, device=x2d.device) if mode == 2 else None
+            with _probe("outlook_vproj", ou), _census("outlook_vproj", ou):
+                check(lib.ogv_outlook_vproj_fwd_l32(_ptr(x2d), x2d.stride(0), _ptr(w), _ptr(b), _ptr(cat), C, _ptr(lg),
+                                                    lld, _ptr(y), B, H, W, C, heads, k, _dt(x2d), _stream()),
+                      "ogv_outlook_vproj_fwd_l32")
+        else:
+            cat = torch.empty((M, ld), dtype=x2d.dtype, device=x2d.device) if mode == 2 else None
+            with _probe("outlook_vproj", ou), _census("outlook_vproj", ou):
+                check(lib.ogv_outlook_vproj_fwd(_ptr(x2d), x2d.stride(0), _ptr(w), _ptr(b), _ptr(cat), ld, _ptr(y), B, H,
+                                                W, C, heads, k, _dt(x2d), _stream()), "ogv_outlook_vproj_fwd")
+        ctx.save_for_backward(x2d, w, b, cat, lg)
         ctx.meta = (B, H, W, C, heads, k, b is not None, mode)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x2d, w, b, cat = ctx.saved_tensors
+        x2d, w, b, cat, lg = ctx.saved_tensors
         B, H, W, C, heads, k, has_bias, mode = ctx.meta
         M, ld = x2d.shape[0], w.shape[0]
         dy = dy.to(x2d.dtype).contiguous()
@@ -872,13 +894,21 @@ class _OutlookVProj(torch.autograd.Function):
                 check(_lib.load().ogv_outlook_vproj_bwd(_ptr(x2d), x2d.stride(0), _ptr(w), _ptr(b), _ptr(dy), _ptr(dcat),
                                                         ld, B, H, W, C, heads, k, _dt(x2d), _stream()),
                       "ogv_outlook_vproj_bwd")
+        elif lg is not None:
+            es = dcat.element_size()
+            ou = dict(M=M, C=C, heads=heads, k=k, elem=es, l32=True)
+            with _probe("outlook_bwd", ou), _census("outlook_bwd", ou):
+                check(_lib.load().ogv_outlook_agg_bwd_l32(_ptr(dy), _ptr(cat), _ptr(lg), _ptr(dcat),
+                                                          _vp(dcat.data_ptr() + C * es), B, H, W, C, heads, k,
+                                                          lg.stride(0), cat.stride(0), ld, ld, ld - C, _dt(dy), _stream()),
+                      "ogv_outlook_agg_bwd_l32")
         else:
             es = cat.element_size()
             _outlook_bwd(dy, cat.data_ptr(), ld, cat.data_ptr() + C * es, ld, dcat.data_ptr(), ld,
                          dcat.data_ptr() + C * es, ld, ld - C, B, H, W, C, heads, k)
         want_dw = ctx.needs_input_grad[1] or (has_bias and ctx.needs_input_grad[2])
         dx, dw, db = _linear_bwd(dcat, x2d, w, None, 1, 0, has_bias, ctx.needs_input_grad[0], want_dw)
-        return dx, dw, db, None, None, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None, None, None
 
 
 class _AliasedConcat(torch.autograd.Function):
@@ -927,8 +957,11 @@ def outlook_vproj(x2d, w, b, C, B, H, W, heads, k, save_cat=None):
             int(B), int(H), int(W), int(C), int(heads), int(k), int(w.shape[0]), OGV_BF16):
         raise ValueError(f"ogv.outlook_vproj: no recompute backward at C={C} (wide stages save cat)")
     mode = 0 if not train else (2 if save_cat else 1)
+    # the fp32-logits form wherever it applies (not with the recompute backward, mode 1)
+    l32 = mode != 1 and bool(_lib.load().ogv_outlook_vproj_l32_supported(int(B), int(H), int(W), int(C), int(heads),
+                                                                          int(k), int(train), OGV_BF16))
     return _OutlookVProj.apply(x2d, w.contiguous(), None if b is None else b.contiguous(), int(C), int(B), int(H),
-                               int(W), int(heads), int(k), mode)
+                               int(W), int(heads), int(k), mode, l32)
 
 
 def outlook_aggregate_rows(v2d, logits2d, B, H, W, heads, k):

@@ -287,7 +287,12 @@ def test_model_logits(name, dtype):
         # stages.2.1) -- and which of two bf16 realisations is further off on one parameter is a coin
         # flip (tools/diag_attn_bias.py: the same error with the Outlooker in fp32 torch ops).  So the
         # bar is the error DISTRIBUTION: RMS of the relative deviations <= max(3e-2, 1.5x the
-        # reference's own RMS), and the worst one <= max(0.1, 2x the reference's own worst).
+        # reference's own RMS), and the worst one <= 2x the reference's own worst (no absolute floor: round 6).
+        # Measured (profiles/r06_parity.jsonl): with the fused Outlooker's logits kept in fp32 Model B's
+        # worst fell 0.087 -> 0.063 (reference 0.044) and its RMS 0.0086 -> 0.0071 (reference 0.0100); an fp32
+        # emulation of bf16 storage of every activation (tools/bf16_storage_gradnorms.py) puts any bf16-storage
+        # implementation's worst at 0.06 on this fixture, the reference's autocast keeping its residual sums and
+        # normalisation outputs in fp32.
         floor = 1e-3 * np.abs(ref_gn).max()
         rel = np.abs(gn - ref_gn) / (np.abs(ref_gn) + floor)
         rel_ref = np.abs(arr["grad_norms_cpu_bf16_autocast"] - ref_gn) / (np.abs(ref_gn) + floor)
@@ -297,9 +302,9 @@ def test_model_logits(name, dtype):
               f"({names[w]}; reference bf16 worst {rel_ref.max():.4f})")
         fx.record("model_grad_norms_bf16", fixture=name, rms=rms, rms_reference_bf16=rms_ref, worst=float(rel[w]),
                   worst_param=names[w], worst_reference_bf16=float(rel_ref.max()),
-                  rms_bar=max(BF16_GRAD, 1.5 * rms_ref), worst_bar=max(0.1, 2.0 * rel_ref.max()))
+                  rms_bar=max(BF16_GRAD, 1.5 * rms_ref), worst_bar=2.0 * rel_ref.max())
         assert rms <= max(BF16_GRAD, 1.5 * rms_ref), (name, rms, rms_ref)
-        assert rel.max() <= max(0.1, 2.0 * rel_ref.max()), (name, names[w], rel[w], rel_ref.max())
+        assert rel.max() <= 2.0 * rel_ref.max(), (name, names[w], rel[w], rel_ref.max())
     else:
         ratio = np.abs(gn - ref_gn) / (atol + rtol * np.abs(ref_gn))
         w = int(np.argmax(ratio))
@@ -425,27 +430,38 @@ VPROJ_CASES = [  # B, C, heads, H, W: 7M stage 0 / 1, 14M / 22M stage 0 (C = 64)
     # the per-head kernel's panel edges: a last panel with fewer images than IPP, 6-pixel images (4 per
     # 64-row panel), 7 x 7 images (49 of 64 rows used), 128-row panels (two row fragments per wave)
     (5, 256, 8, 4, 4), (3, 192, 6, 2, 3), (3, 384, 6, 7, 7), (3, 128, 4, 8, 16),
+    # its halo-tile form (images of > 128 pixels): 22M stages 1-3 at 112 / 56 / 28 px, ragged tiles both ways,
+    # a single-row image, images just over 128 pixels
+    (1, 128, 4, 112, 112), (1, 256, 8, 56, 56), (1, 384, 6, 28, 28), (2, 128, 4, 23, 37), (1, 192, 6, 1, 200),
+    (3, 256, 8, 9, 15),
 ]
+VPROJ_HALO_CASES = VPROJ_CASES[-6:]
 
 
-@pytest.fixture(params=["head", "streaming"])
+@pytest.fixture(params=["head", "head64", "halo8", "streaming"])
 def vp_big(request):
-    """The wide-stage fused Outlookers (C > 96): "head" = the per-head whole-image kernel
-    (knob vp_head, default on) where it plans (images of <= 128 pixels), else the weight-streaming kernel;
-    "streaming" = the weight-streaming kernel only (opt-in knob vp_big).  Both on for the test."""
+    """The wide-stage fused Outlookers (C > 96): "head" = the per-head kernel (knob vp_head,
+    default on: whole-image panels for images of <= 128 pixels; 4-wave halo tiles above, knob vph_halo = 1,
+    opt-in) where it plans
+    (head_dim 32), else the weight-streaming kernel; "head64" = also head_dim 64 as two 32-column units
+    and the halo-tile form at every wide shape (vp_head = 2, vph_halo = 2); "halo8" = that with 8-wave halo-tile
+    workgroups (vph_halo = 3); "streaming" = the
+    weight-streaming kernel only (opt-in knob vp_big).  The streaming kernel is on in every variant."""
     from ogv._lib import load
     lib = load()
     assert lib.ogv_set_option(b"vp_big", 1) == 0
-    assert lib.ogv_set_option(b"vp_head", 1 if request.param == "head" else 0) == 0
+    assert lib.ogv_set_option(b"vp_head", {"head": 1, "head64": 2, "halo8": 2, "streaming": 0}[request.param]) == 0
+    assert lib.ogv_set_option(b"vph_halo", {"head": 1, "head64": 2, "halo8": 3, "streaming": 1}[request.param]) == 0
     yield request.param
     assert lib.ogv_set_option(b"vp_big", 0) == 0
     assert lib.ogv_set_option(b"vp_head", 1) == 0
+    assert lib.ogv_set_option(b"vph_halo", 0) == 0
 
 
-def _vproj_autocast_dx_error(x, w, b, dy, dx_ref, dw_ref, db_ref, C, nl, h, B, H, W):
+def _vproj_autocast_dx_error(x, w, b, dy, dx_ref, dw_ref, db_ref, C, nl, h, B, H, W, y_ref=None):
     """(max, RMS) of dx - dx_ref, max|dW - dW_ref|, max|db - db_ref| for the oracle's Outlooker (projection +
     outlook_aggregate, the reference's ops) run on this GPU under torch.autocast(bf16): the reference's own
-    bf16 error on the case (tests only)."""
+    bf16 error on the case (tests only); last: max|y - y_ref| of that forward (its y when y_ref is None)."""
     xa = x.to(DEV).requires_grad_()
     wa, ba = w.to(DEV).requires_grad_(), b.to(DEV).requires_grad_()
     with torch.autocast("cuda", dtype=torch.bfloat16):
@@ -455,7 +471,8 @@ def _vproj_autocast_dx_error(x, w, b, dy, dx_ref, dw_ref, db_ref, C, nl, h, B, H
         y = y.permute(0, 2, 3, 1).reshape(-1, C)
     y.float().backward(dy.to(DEV))
     e = xa.grad.double().cpu() - dx_ref.cpu()
-    return (e.abs().max().item(), e.pow(2).mean().sqrt().item(), fx.maxabs(wa.grad, dw_ref), fx.maxabs(ba.grad, db_ref))
+    out = (e.abs().max().item(), e.pow(2).mean().sqrt().item(), fx.maxabs(wa.grad, dw_ref), fx.maxabs(ba.grad, db_ref))
+    return out + ((y.detach().double().cpu() if y_ref is None else fx.maxabs(y.detach(), y_ref)),)
 
 
 @pytest.mark.parametrize("case", VPROJ_CASES)
@@ -465,6 +482,10 @@ def test_outlook_vproj_vs_oracle(case, vp_big):
     gradients of x, W and b through the fused op's backward, within 1e-2 * max(1, |ref|)."""
     from ogv import functional as OF
     B, C, h, H, W = case
+    if vp_big == "head" and C > 96 and C // h == 64:
+        pytest.skip("head_dim 64 without vp_head = 2 runs the streaming kernel: the 'streaming' variant")
+    if vp_big == "streaming" and case in VPROJ_HALO_CASES:
+        pytest.skip("the halo-tile cases are for the per-head kernel")
     nl = 9 * h
     ld = (C + nl + 7) // 8 * 8
     assert OF.outlook_vproj_supported(B, H, W, C, h, 3, ld, torch.bfloat16, False), case
@@ -488,7 +509,15 @@ def test_outlook_vproj_vs_oracle(case, vp_big):
     y = OF.outlook_vproj(xd, wd, bd, C, B, H, W, h, 3)
     y.backward(dy.to(DEV, torch.bfloat16))
     tol = lambda r: 1e-2 * max(1.0, r.abs().max().item())
-    assert fx.maxabs(y.float(), yr.detach()) <= tol(yr), "y"
+    a_max, a_rms, a_dw, a_db, a_y = _vproj_autocast_dx_error(x, w, b, dy, xr.grad, wr.grad, br.grad, C, nl, h, B, H, W,
+                                                             y_ref=yr.detach())
+    # y: the plain bound, or the reference's own bf16 forward error (the logits are O(6) by construction and cat is
+    # rounded to bf16 in every implementation -- the unfused GEMM's output, the reference's autocast conv -- so at
+    # the largest cases one rounded logit can move a softmax weight past 1e-2 of |y|: every fused kernel measures
+    # the same 0.042 at (1, 384, 6, 28, 28))
+    e_y = fx.maxabs(y.float(), yr.detach())
+    fx.record("outlook_vproj_y", case=list(case), kernel=vp_big, ours=e_y, plain_bound=tol(yr), oracle_gpu_autocast=a_y)
+    assert e_y <= max(tol(yr), a_y), ("y", e_y, tol(yr), a_y)
     # dx = dcat . W: its error is set by four bf16 rounding points -- cat (the logits above all: a rounded
     # logit of O(6) moves the softmax), dcat, the dgrad's bf16 weight and dx itself; an fp64 CPU emulation
     # of exactly those roundings reproduces this kernel's dx error to the last bit (0.0978587960935231 at
@@ -500,9 +529,13 @@ def test_outlook_vproj_vs_oracle(case, vp_big):
     # 0.0061 / max 0.051 -- the maximum sits on one outlier logit).
     ex = (xd.grad.double().cpu() - xr.grad.cpu())
     e_dx, r_dx = ex.abs().max().item(), ex.pow(2).mean().sqrt().item()
-    a_max, a_rms, a_dw, a_db = _vproj_autocast_dx_error(x, w, b, dy, xr.grad, wr.grad, br.grad, C, nl, h, B, H, W)
-    fx.record("outlook_vproj_dx", case=list(case), kernel=vp_big, ours_max=e_dx, ours_rms=r_dx, plain_bound=tol(xr.grad),
-              oracle_gpu_autocast_max=a_max, oracle_gpu_autocast_rms=a_rms)
+    from ogv._lib import load
+    l32 = bool(load().ogv_outlook_vproj_l32_supported(B, H, W, C, h, 3, 1, OF.OGV_BF16))
+    fx.record("outlook_vproj_dx", case=list(case), kernel=vp_big, l32=l32, ours_max=e_dx, ours_rms=r_dx,
+              plain_bound=tol(xr.grad), oracle_gpu_autocast_max=a_max, oracle_gpu_autocast_rms=a_rms)
+    if l32:   # the fp32-logits form (the default wherever it plans): the logit rounding point is gone -> the plain bar
+        assert e_dx <= tol(xr.grad), ("dx (fp32 logits)", e_dx, tol(xr.grad))
+        assert e_y <= tol(yr), ("y (fp32 logits)", e_y, tol(yr))
     assert e_dx <= tol(xr.grad) or (r_dx <= a_rms and e_dx <= 2.0 * a_max), ("dx", e_dx, r_dx, tol(xr.grad), a_max, a_rms)
     # dW / db: the plain bound, or the reference's own bf16 error (its autocast weight gradient is
     # rounded to bf16 as well; an fp64 emulation of the rounding points puts ours at 0.43-0.72 of its error)
@@ -533,13 +566,16 @@ def test_outlook_vproj_matches_unfused(case, vp_big):
     dy = torch.randn(B, C, H, W, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     outs = []
     try:
-        for knob in (2, 3, 0):
+        # the default (fp32 logits where planned), the bf16-cat form (vp_l32 = 0), the recompute backward, unfused
+        for knob, l32 in ((2, 1), (2, 0), (3, 1), (0, 1)):
             assert lib.ogv_set_option(b"outlook_vproj", knob) == 0
+            assert lib.ogv_set_option(b"vp_l32", l32) == 0
             m.zero_grad()
             xx = x.clone().requires_grad_()
             y = m(xx)
             y.backward(dy)
             outs.append([y.float(), xx.grad.float()] + [p.grad.clone() for p in m.parameters()])
+        assert lib.ogv_set_option(b"vp_l32", 1) == 0
         inf = []
         for knob in (1, 0):
             assert lib.ogv_set_option(b"outlook_vproj", knob) == 0
@@ -547,11 +583,13 @@ def test_outlook_vproj_matches_unfused(case, vp_big):
                 inf.append(m.eval()(x).float())
     finally:
         assert lib.ogv_set_option(b"outlook_vproj", 2) == 0
-    for o in outs[:2]:
-        for a, b in zip(o, outs[2]):
+        assert lib.ogv_set_option(b"vp_l32", 1) == 0
+    for o in outs[:3]:
+        for a, b in zip(o, outs[3]):
             assert fx.maxabs(a, b) <= 1e-2 * max(1.0, b.abs().max().item())
-    for a, b in zip(outs[0], outs[1]):     # saved cat vs recompute: the same function, bit for bit
-        assert torch.equal(a, b)
+    if C <= 96:   # saved bf16 cat vs recompute (the tile kernels): the same function, bit for bit
+        for a, b in zip(outs[1], outs[2]):
+            assert torch.equal(a, b)
     assert fx.maxabs(inf[0], inf[1]) <= 1e-2 * max(1.0, inf[1].abs().max().item())
     # the default no_grad forward IS the fused kernel: bit-identical to a direct call
     from ogv import functional as OF
@@ -983,10 +1021,48 @@ def test_outlook_vproj_full_size_matches_unfused(shape, vp_big):
     wq, bq = w.clone().requires_grad_(), b.clone().requires_grad_()
     y = OF.outlook_vproj(x, wq, bq, C, B, H, W, h, 3, save_cat=True)     # writes cat as well
     tol = 1e-2 * max(1.0, y_ref.float().abs().max().item())
-    assert fx.maxabs(y.detach().float(), y_ref.float()) <= tol
-    cat_f = y.grad_fn.saved_tensors[3]
-    assert fx.maxabs(cat_f.float(), cat.float()) <= 1e-2 * max(1.0, cat.float().abs().max().item())
-    assert torch.equal(cat_f[:, C + 9 * h:], torch.zeros_like(cat_f[:, C + 9 * h:]))
+    if y.grad_fn.saved_tensors[4] is not None:   # fp32 logits: against fp64, no less accurate than the unfused pair
+        with torch.no_grad():
+            xr, wr, br = x.double(), w.double(), b.double()
+            c64 = xr @ wr.t() + br
+            to_nchw = lambda t, c: t.reshape(B, H, W, c).permute(0, 3, 1, 2)  # noqa: E731
+            y64 = orc.outlook_aggregate(to_nchw(c64[:, :C], C), to_nchw(c64[:, C:C + 9 * h], 9 * h), h, 3)
+            y64 = y64.permute(0, 2, 3, 1).reshape(-1, C)
+        e_f, e_u = fx.maxabs(y.detach(), y64), fx.maxabs(y_ref, y64)
+        assert e_f <= max(tol, 1.1 * e_u), (e_f, e_u, tol)
+    else:
+        assert fx.maxabs(y.detach().float(), y_ref.float()) <= tol
+    cat_f, lg_f = y.grad_fn.saved_tensors[3], y.grad_fn.saved_tensors[4]
+    if lg_f is not None:   # the fp32-logits form: v [M, C] bf16 + logits [M, 9h rounded to 4] fp32
+        assert cat_f.shape[1] == C and lg_f.dtype == torch.float32
+        assert fx.maxabs(cat_f.float(), cat[:, :C].float()) <= 1e-2 * max(1.0, cat[:, :C].float().abs().max().item())
+        lr = cat[:, C:C + 9 * h].float()
+        assert fx.maxabs(lg_f[:, :9 * h], lr) <= 1e-2 * max(1.0, lr.abs().max().item())
+    else:
+        assert fx.maxabs(cat_f.float(), cat.float()) <= 1e-2 * max(1.0, cat.float().abs().max().item())
+        assert torch.equal(cat_f[:, C + 9 * h:], torch.zeros_like(cat_f[:, C + 9 * h:]))
+
+
+def _vproj_fp64(x, w, b, dy, C, B, H, W, h):
+    """fp64 reference on the device: projection + the oracle's outlook_aggregate (the reference's ops) with
+    autograd -> (y, dx, dW, db)."""
+    xr, wr, br = (t.double().clone().requires_grad_() for t in (x, w, b))
+    cat = xr @ wr.t() + br
+    to_nchw = lambda t, c: t.reshape(B, H, W, c).permute(0, 3, 1, 2)  # noqa: E731
+    y = orc.outlook_aggregate(to_nchw(cat[:, :C], C), to_nchw(cat[:, C:C + 9 * h], 9 * h), h, 3)
+    y = y.permute(0, 2, 3, 1).reshape(-1, C)
+    y.backward(dy.double())
+    return y.detach(), xr.grad, wr.grad, br.grad
+
+
+def _no_less_accurate(outs_fused, outs_unfused, ref, what):
+    """Each fused output within 1e-2 * max(1, |ref|) of the fp64 reference (3x for the weight gradients: bf16
+    dcat summed over M rows), or no further from it than the unfused GEMM + aggregation pair (+10%): the
+    fp32-logits form is compared with the truth, not with the bf16-logit pair it is more accurate than."""
+    for i, (a, u, r) in enumerate(zip(outs_fused, outs_unfused, ref)):
+        e_f, e_u = fx.maxabs(a, r), fx.maxabs(u, r)
+        tol = (3 if i >= 2 else 1) * 1e-2 * max(1.0, r.abs().max().item())
+        assert e_f <= max(tol, 1.1 * e_u), (what, ("y", "dx", "dW", "db")[i], e_f, e_u, tol)
 
 
 def _vproj_problem(B, C, h, H, W, seed):
@@ -1017,8 +1093,13 @@ def test_outlook_vproj_bwd_bitwise(case):
     x, w, b, dy, ld = _vproj_problem(B, C, h, H, W, seed=B * 7 + C + H)
     M = B * H * W
     wq, bq = w.clone().requires_grad_(), b.clone().requires_grad_()
-    y = OF.outlook_vproj(x, wq, bq, C, B, H, W, h, 3, save_cat=True)
+    assert lib.ogv_set_option(b"vp_l32", 0) == 0      # the bf16 cat the recompute backward reproduces
+    try:
+        y = OF.outlook_vproj(x, wq, bq, C, B, H, W, h, 3, save_cat=True)
+    finally:
+        assert lib.ogv_set_option(b"vp_l32", 1) == 0
     cat = y.grad_fn.saved_tensors[3]
+    assert cat.shape[1] == ld
     dcat_ref = torch.empty_like(cat)
     es = cat.element_size()
     OF._outlook_bwd(dy, cat.data_ptr(), ld, cat.data_ptr() + C * es, ld, dcat_ref.data_ptr(), ld,
@@ -1092,7 +1173,10 @@ def test_attn_drop_materialising_path(which):
         assert torch.equal(drop.eval()(x), ref.eval()(x))
 
 
-@pytest.mark.parametrize("shape", [(512, 192, 6, 8, 8), (512, 256, 8, 4, 4), (64, 384, 6, 14, 14)])
+@pytest.mark.parametrize("shape", [(512, 192, 6, 8, 8), (512, 256, 8, 4, 4), (64, 384, 6, 14, 14),
+                                   # 14M stages 1-3 at bs 256, 22M stages 1-3 at bs 128 (the halo-tile form)
+                                   (256, 128, 4, 32, 32), (256, 256, 8, 16, 16), (256, 384, 6, 8, 8),
+                                   (128, 128, 4, 112, 112), (128, 256, 8, 56, 56), (128, 384, 6, 28, 28)])
 def test_outlook_vproj_wide_train_grads_full_size_match_unfused(shape, vp_big):
     """Full size, wide stages (the weight-streaming fused forward writing cat, then the LDS-tiled
     aggregation backward): y, x / W / b gradients vs the unfused GEMM -> cat -> aggregation pair within
@@ -1102,17 +1186,22 @@ def test_outlook_vproj_wide_train_grads_full_size_match_unfused(shape, vp_big):
     B, C, h, H, W = shape
     x, w, b, dy, ld = _vproj_problem(B, C, h, H, W, seed=B + H + 3)
     outs = []
+    l32 = False
     for fused in (True, False):
         xx, wq, bq = x.clone().requires_grad_(), w.clone().requires_grad_(), b.clone().requires_grad_()
         if fused:
             y = OF.outlook_vproj(xx, wq, bq, C, B, H, W, h, 3)
             assert y.grad_fn.saved_tensors[3] is not None
+            l32 = y.grad_fn.saved_tensors[4] is not None
         else:
             y = OF.outlook_aggregate_cat(OF.linear_rows(xx, wq, bq), C, B, H, W, h, 3)
         y.backward(dy)
         outs.append((y.detach().float(), xx.grad.float(), wq.grad, bq.grad))
-    for i, (a, r) in enumerate(zip(*outs)):
-        assert fx.maxabs(a, r) <= (3 if i >= 2 else 1) * 1e-2 * max(1.0, r.abs().max().item()), (shape, i)
+    if l32:   # the fp32-logits form: against fp64 (on the device), no less accurate than the unfused pair
+        _no_less_accurate(outs[0], outs[1], _vproj_fp64(x, w, b, dy, C, B, H, W, h), shape)
+    else:
+        for i, (a, r) in enumerate(zip(*outs)):
+            assert fx.maxabs(a, r) <= (3 if i >= 2 else 1) * 1e-2 * max(1.0, r.abs().max().item()), (shape, i)
     with pytest.raises(ValueError):
         OF.outlook_vproj(x.clone().requires_grad_(), w, b, C, B, H, W, h, 3, save_cat=False)
 

@@ -2520,7 +2520,7 @@ extern "C" int ogv_outlook_vproj_fwd(const void* x, int ldx, const float* w, con
                                      void* y, int B, int H, int W, int C, int heads, int k, ogv_dtype dt,
                                      void* stream) {
   if (k > 0 && heads > 0)
-    OGV_REQUIRE(ldc == (C + heads * k * k + 7) / 8 * 8, "ogv_outlook_vproj_fwd: ldc %d must be C + heads*k*k rounded up to 8",
+    OGV_REQUIRE(ldc == (C + heads * k * k + 7) / 8 * 8, "ogv_outlook_vproj_fwd: unsupported shape (ldc %d must be C + heads*k*k rounded up to 8)",
                 ldc);
   return vproj_fwd_impl(x, ldx, w, bias, cat, ldc, nullptr, 0, false, y, B, H, W, C, heads, k, dt, stream);
 }

@@ -68,7 +68,7 @@ const char* ogv_last_error(void);
  *   at most 512 MB else 1 (resolved per shape by ogv_mbconv_a3_mode; a desc with a3 >= 0 ignores the knob);
  *   "vp_head" 0 / 1 (default) / 2: the per-head fused Outlooker forward for the wide stages off / on / also
  *   head_dim 64 (two 32-column units per head); "vph_halo" 0 (default) / 1 / 2 / 3: its halo-tile form for images of
- *   more than 128 pixels off / where <= 4 units share a pixel (C = 128) / every wide shape / with 8-wave workgroups; "vph_tile" (TH * 100 + TW, 0 = auto): force its tile; "vp_l32" 1 (default) / 0: the fused Outlooker's fp32-logits form
+ *   more than 128 pixels off / where <= 4 units share a pixel (C = 128) / every wide shape / with 8-wave workgroups; "vph_tile" (TH * 100 + TW, 0 = auto): force its tile; "pg_tconv1" 1 (default) / 0: a stride-2 transposed conv's four parity classes as one launch / four; "vp_l32" 1 (default) / 0: the fused Outlooker's fp32-logits form
  *   (ogv_outlook_vproj_l32_supported answers 0 with 0); "vph_rows" (0 = auto): target rows per panel of that kernel; "vph_wgs" (default 3):
  *   workgroups per CU its grid is sized for; "vph_dbg": phase-skipping timing experiments (wrong results);
  *   "dw_tw" 8 / 16 / 32 (default): column strip width of the depthwise kernels; "ln_rpi" 2 (default) / 4:

@@ -90,7 +90,16 @@ struct ConvG {
   // them (tap[0..ntap), tap-major columns k = t * Cs + c)
   int par = -1, ntap = 9;
   int tap[4] = {0, 0, 0, 0};
+  // par == 4: ALL four parity classes in one launch (panel kernel): workgroups [c G4, (c + 1) G4) run class c
+  // (G4 a multiple of 8, so a workgroup keeps its XCD); each class's taps follow from its parity
+  int cls_G = 0;
 };
+// the taps of parity class c of a stride-2 transposed 3x3 conv: output pixel parity (y & 1, x & 1) = (c >> 1, c & 1)
+// receives ky = 1 (even y) or {0, 2} (odd y), kx likewise
+__host__ __device__ constexpr int tconv_ntap(int c) { return c == 0 ? 1 : (c == 3 ? 4 : 2); }
+__host__ __device__ constexpr int tconv_tap(int c, int t) {
+  return c == 0 ? 4 : c == 1 ? (t == 0 ? 3 : 5) : c == 2 ? (t == 0 ? 1 : 7) : (t == 0 ? 0 : t == 1 ? 2 : t == 2 ? 6 : 8);
+}
 // tap[t] of a parity class through selects on the (uniform) kernel-argument values: a dynamic index
 // into the by-value argument struct makes the compiler re-load it from the kernarg segment and wait
 // for that load at every use
@@ -265,6 +274,7 @@ bool stem_wgrad_try(const void* x, const ConvG& cv, const void* dy, float* dw, f
 size_t stem_wgrad_ws_bytes(long M, int N, int Cin);
 void set_swg_min_m(int v);
 void set_pg_split(int v);
+void set_pg_tconv1(int v);
 int split_w();
 int skip_mask();
 void set_skip(int v);

@@ -68,6 +68,21 @@ __global__ __launch_bounds__(PG_NW * 64, 2) void pgemm_bf16_kernel(const bf16* _
                                                                 const float* __restrict__ W, int ldw, Epi epi,
                                                                 bf16* __restrict__ out, int ldo, int M, int N, int K,
                                                                 int nMt, int nNt, int dbg, ConvG cv) {
+  // the merged transposed-conv launch (cv.par == 4): this workgroup's parity class, its index within the
+  // class's workgroups and the class's taps / reduction length
+  int bid = blockIdx.x, G = gridDim.x;
+  if constexpr (CV) {
+    if (cv.par == 4) {
+      const int c = blockIdx.x / cv.cls_G;
+      bid = blockIdx.x - c * cv.cls_G;
+      G = cv.cls_G;
+      cv.par = c;
+      cv.ntap = tconv_ntap(c);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) cv.tap[t] = tconv_tap(c, t);
+      K = cv.ntap * cv.Cs;
+    }
+  }
   constexpr int BN = TN * 16;
   constexpr int BM = PG_NW * 16 * RS;
   constexpr int SLAB = pg_slab_elems<TN, BT>();
@@ -83,10 +98,10 @@ __global__ __launch_bounds__(PG_NW * 64, 2) void pgemm_bf16_kernel(const bf16* _
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fg = lane >> 4;
-  const int G = gridDim.x, xcd = blockIdx.x & 7;
-  // tiles of this workgroup: vb = blockIdx.x + G * j; M-panel index is non-decreasing in j
-  auto tile_mt = [&](int j) { return (((blockIdx.x + G * j) >> 3) / nNt) * 8 + xcd; };
-  auto tile_nt = [&](int j) { return ((blockIdx.x + G * j) >> 3) % nNt; };
+  const int xcd = bid & 7;
+  // tiles of this workgroup: vb = bid + G * j; M-panel index is non-decreasing in j
+  auto tile_mt = [&](int j) { return (((bid + G * j) >> 3) / nNt) * 8 + xcd; };
+  auto tile_nt = [&](int j) { return ((bid + G * j) >> 3) % nNt; };
   int ntiles = 0;
   while (tile_mt(ntiles) < nMt) ++ntiles;
   if (ntiles == 0) return;
@@ -659,15 +674,20 @@ static PgPlan pg_plan(int M, int N, int K, bool stats, bool sw, bool bt, bool pa
   return p;
 }
 
+// persistent: at most pg_per_cu workgroups per CU (shared by `parts` class groups), a multiple of 8 (keeps
+// each one's XCD)
+static unsigned pg_grid(const PgPlan& p, int parts = 1) {
+  const long vb = (long)((p.nMt + 7) / 8) * 8 * p.nNt;
+  return (unsigned)std::max<long>(8, std::min<long>(vb, (long)pg_cus() * g_pg_per_cu / parts / 8 * 8));
+}
 template <int RS, int TN, int PA, bool GT, int ZA, bool STATS, bool BT, bool SW, bool CV>
 static void pg_launch(const PgPlan& p, const bf16* A, int lda, const Pro& pro, const float* W, int ldw,
                       const Epi& epi, bf16* out, int ldo, int M, int N, int K, const ConvG& cv, hipStream_t s) {
   if (skip_mask() & 1) return;
   auto kern = pgemm_bf16_kernel<RS, TN, PA, GT, ZA, STATS, BT, SW, CV>;
   if (!lds_ok(reinterpret_cast<const void*>(kern), p.lds, "pgemm_bf16_kernel")) return;
-  // persistent: at most pg_per_cu workgroups per CU, a multiple of 8 (keeps each one's XCD)
-  const long vb = (long)((p.nMt + 7) / 8) * 8 * p.nNt;
-  const unsigned grid = (unsigned)std::min<long>(vb, (long)pg_cus() * g_pg_per_cu / 8 * 8);
+  // the merged transposed-conv launch: four class groups of cv.cls_G workgroups
+  const unsigned grid = (CV && cv.par == 4) ? (unsigned)(4 * cv.cls_G) : pg_grid(p);
   kern<<<grid, PG_NW * 64, p.lds, s>>>(A, lda, pro, W, ldw, epi, out, ldo, M, N, K, p.nMt, p.nNt, g_pg_dbg, cv);
 }
 
@@ -757,6 +777,9 @@ bool pgemm_dgrad_try(const void* dout, int ldd, const float* W, void* dA, int ld
 // (y, x) only receives taps with ky = y + 1 (mod 2), kx = x + 1 (mod 2), i.e. 1, 2, 2 or 4 of the 9
 // (K / 2.25 on average, no zero taps staged or multiplied).  Returns false (nothing launched) when
 // a class does not fit the panel kernel.
+// knob "pg_tconv1" 1 (default) / 0: the four parity classes as ONE launch (workgroup groups per class) / four
+static int g_pg_tconv1 = 1;
+void set_pg_tconv1(int v) { g_pg_tconv1 = v ? 1 : 0; }
 bool pgemm_tconv_try(const void* A, const ConvG& cv, const float* Wt, void* out, int M, int N, hipStream_t s) {
   if (!g_pgemm || !(g_pg_split & 4) || !cv.transposed || cv.stride != 2 || (cv.Hr & 1) || (cv.Wr & 1) || (cv.Cs & 7) ||
       !al16p(A) || !al16p(out) || !al16p(Wt) || M % (cv.Hr * cv.Wr))
@@ -781,6 +804,18 @@ bool pgemm_tconv_try(const void* A, const ConvG& cv, const float* Wt, void* out,
   }
   const bf16* a = static_cast<const bf16*>(A);
   bf16* o = static_cast<bf16*>(out);
+  if (g_pg_tconv1 && p[0].RS == p[3].RS && p[0].TN == p[3].TN) {
+    // one launch for the four classes (same tile plan: the plan depends on the rows and columns only)
+    ConvG g4 = cv;
+    g4.par = 4;
+    g4.cls_G = (int)pg_grid(p[3], 4);
+    PgPlan p4 = p[3];
+    for (int par = 0; par < 4; ++par) p4.lds = std::max(p4.lds, p[par].lds);
+    const int K4 = 4 * cv.Cs;   // (each class group uses its own K)
+    if (sw) pg_tiles<-1, false, 0, false, false, true, true>(p4, a, 0, Pro(), Wt, 9 * cv.Cs, Epi(), o, N, Mc, N, K4, s, g4);
+    else pg_tiles<-1, false, 0, false, false, false, true>(p4, a, 0, Pro(), Wt, 9 * cv.Cs, Epi(), o, N, Mc, N, K4, s, g4);
+    return true;
+  }
   for (int par = 0; par < 4; ++par) {
     const int K = g[par].ntap * cv.Cs;
     if (sw) pg_tiles<-1, false, 0, false, false, true, true>(p[par], a, 0, Pro(), Wt, 9 * cv.Cs, Epi(), o, N, Mc, N, K, s, g[par]);

@@ -806,14 +806,26 @@ class Trainer:
         """This call's update runs eagerly on a side stream (allocator / library warm-up, as graph
         capture requires); then the step is recorded on trainer-owned copies of the batch --
         recording executes nothing."""
+        # the warm-up step below allocates on a side stream, which cannot reuse blocks cached for the current one:
+        # hand those back first (and the side stream's before recording, below), so at most one step's activations
+        # are reserved at any time
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
             loss = self._eager(x, y)
         torch.cuda.current_stream().wait_stream(side)
         loss = loss.clone()
-        warm_grads = [p.grad for p in self.params]
+        # (the layout of each gradient the backward produced, checked below before recording the DP overlap)
+        bad_layout = [i for i, p in enumerate(self.params) if p.grad is not None and not _dense_like(p.grad, p)]
+        strides = {i: (tuple(self.params[i].grad.stride()), tuple(self.params[i].stride())) for i in bad_layout[:1]}
         self.opt.zero_grad(set_to_none=True)
+        # the graph records into a private memory pool: hand the eager steps' cached blocks back first, so the
+        # step's activations are not reserved twice (Model-A-22M at 224^2, bs 128: 286 of 288 GB reserved with the
+        # eager pool kept, round 5)
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
         self._x = x.detach().clone(memory_format=torch.preserve_format)
         self._y = y.detach().clone()
         if self.capture_hook is not None:
@@ -828,10 +840,10 @@ class Trainer:
             # every gradient must be laid out like its parameter for the in-place reduced views: checked on the
             # warm-up step's gradients before recording (a layout error raised mid-capture would leave earlier
             # buckets' collectives recorded on this rank only)
-            for i, (p, g) in enumerate(zip(self.params, warm_grads)):
-                if g is not None and not _dense_like(g, p):
-                    raise RuntimeError(f"Trainer(dp_overlap): gradient of parameter {i} is not laid out like the "
-                                       f"parameter (strides {tuple(g.stride())} vs {tuple(p.stride())})")
+            if bad_layout:
+                i = bad_layout[0]
+                raise RuntimeError(f"Trainer(dp_overlap): gradient of parameter {i} is not laid out like the "
+                                   f"parameter (strides {strides[i][0]} vs {strides[i][1]})")
             status, err = 0, None
             try:
                 with torch.cuda.graph(self._g, pool=pool, capture_error_mode=mode):

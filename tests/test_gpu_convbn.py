@@ -127,6 +127,37 @@ def test_conv_bn_act(case, dtype, wcl):
         assert e <= bound, f"{name}: max|d|={e:.3e} bound={bound:.3e} scale={scale:.3e} ({dtype}, {case})"
 
 
+@pytest.mark.parametrize("case", [(512, 48, 96, 32, 32), (512, 96, 192, 16, 16), (512, 192, 256, 8, 8),
+                                  (3, 16, 24, 10, 6), (2, 8, 16, 2, 2)])
+def test_transposed_conv_merged_launch_bitwise(case):
+    """The stride-2 conv's data gradient (a transposed conv) runs its four parity classes as ONE launch of the
+    panel kernel (knob pg_tconv1, default; workgroup groups per class) -- the same tiles and arithmetic as the
+    four launches it replaces, so dx (and every other gradient) is bit-identical to pg_tconv1 = 0; the 7M
+    downsample shapes at bs 512 included."""
+    from ogv import functional as OF
+    from ogv._lib import load
+    lib = load()
+    B, Cin, Cout, H, W = case
+    conv, bn = _modules(Cin, Cout, 2, True, "silu", seed=Cin + Cout)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    x = torch.randn(B, Cin, H, W, device="cuda", generator=g).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    outs = []
+    try:
+        for merged in (1, 0):
+            assert lib.ogv_set_option(b"pg_tconv1", merged) == 0
+            c, b = copy.deepcopy(conv).cuda().to(memory_format=torch.channels_last), copy.deepcopy(bn).cuda().train()
+            xd = x.clone().requires_grad_(True)
+            y = OF.conv3x3_bn_act(xd, c, b, "silu")
+            y.backward(torch.ones_like(y))
+            torch.cuda.synchronize()
+            outs.append([y.detach(), xd.grad, c.weight.grad, b.weight.grad, b.bias.grad])
+    finally:
+        assert lib.ogv_set_option(b"pg_tconv1", 1) == 0
+    for a, r in zip(*outs):
+        assert torch.equal(a, r)
+
+
 def test_stem_input_needs_no_grad():
     """The stem's input image has no gradient: the data-gradient GEMM is skipped."""
     from ogv import functional as OF

@@ -68,7 +68,8 @@ const char* ogv_last_error(void);
  *   at most 512 MB else 1 (resolved per shape by ogv_mbconv_a3_mode; a desc with a3 >= 0 ignores the knob);
  *   "vp_head" 0 / 1 (default) / 2: the per-head fused Outlooker forward for the wide stages off / on / also
  *   head_dim 64 (two 32-column units per head); "vph_halo" 0 (default) / 1 / 2 / 3: its halo-tile form for images of
- *   more than 128 pixels off / where <= 4 units share a pixel (C = 128) / every wide shape / with 8-wave workgroups; "vph_tile" (TH * 100 + TW, 0 = auto): force its tile; "pg_tconv1" 1 (default) / 0: a stride-2 transposed conv's four parity classes as one launch / four; "vp_l32" 1 (default) / 0: the fused Outlooker's fp32-logits form
+ *   more than 128 pixels off / where <= 4 units share a pixel (C = 128) / every wide shape / with 8-wave workgroups; "vph_tile" (TH * 100 + TW, 0 = auto): force its tile; "ln_epi" 0 / 1 (default) / 2: ogv_gemm_fwd_ln never / below
+ *   sgemm_min_m rows / at every M; "pg_tconv1" 1 (default) / 0: a stride-2 transposed conv's four parity classes as one launch / four; "vp_l32" 1 (default) / 0: the fused Outlooker's fp32-logits form
  *   (ogv_outlook_vproj_l32_supported answers 0 with 0); "vph_rows" (0 = auto): target rows per panel of that kernel; "vph_wgs" (default 3):
  *   workgroups per CU its grid is sized for; "vph_dbg": phase-skipping timing experiments (wrong results);
  *   "dw_tw" 8 / 16 / 32 (default): column strip width of the depthwise kernels; "ln_rpi" 2 (default) / 4:
@@ -216,6 +217,16 @@ int ogv_gemm_fwd(const void* A, int lda, const float* W, const float* bias, cons
 /* Forward with a second output (no reference counterpart; fuses the activation module between two
  * Linear layers, src/model/Out_Grid_Block.py MLP fc1 -> act -> fc2): out = A . W^T + bias and
  * aout = act_out(out) of the stored bf16 values, both [M, N] bf16.  bf16 only. */
+/* fwd fused with the residual stream's next LayerNorm (no reference counterpart: the producing Linear of a
+ * pre-norm block -- Outlook_Block.py:58-60, Out_Grid_Block.py:100-102 -- hands LN its rows in registers):
+ * out as ogv_gemm_fwd with act_in = NONE, and ln_out[m, :] = (out[m, :] - mean[m]) * rstd[m] * gamma + beta
+ * (row stride ldo; mean / rstd fp32 [M], rstd = 1 / sqrt(var + eps), the biased variance of the stored bf16
+ * row) -- what ogv_layernorm_fwd would compute from out.  bf16, N <= 192 (one column tile holds whole rows),
+ * knob "ln_epi"; returns OGV_ERR_UNSUPPORTED with nothing launched otherwise (the caller runs ogv_gemm_fwd +
+ * ogv_layernorm_fwd). */
+int ogv_gemm_fwd_ln(const void* A, int lda, const float* W, const float* bias, const void* res, const float* rs,
+                    int rps, void* out, int ldo, void* ln_out, const float* gamma, const float* beta, float eps,
+                    float* mean, float* rstd, int M, int N, int K, ogv_dtype dt, void* stream);
 int ogv_gemm_fwd_act(const void* A, int lda, const float* W, const float* bias, void* out, int ldo,
                      void* aout, int ldao, int M, int N, int K, ogv_act act_out, ogv_dtype dt, void* stream);
 size_t ogv_gemm_dgrad_ws_bytes(int N, int K);

@@ -73,6 +73,12 @@ struct Epi {
   // e.g. GELU(fc1) materialised for the next GEMM and its weight gradient (ogv_gemm_fwd_act)
   void* aout = nullptr;
   int ldao = 0, aact = 0;
+  // LayerNorm of the stored output rows (panel kernel, one column tile holding whole rows; ogv_gemm_fwd_ln):
+  // ln_out[m, :] = (out[m, :] - mean) * rstd * ln_g + ln_b, ln_mean / ln_rstd [M] for the LN backward
+  void* ln_out = nullptr;
+  const float *ln_g = nullptr, *ln_b = nullptr;
+  float *ln_mean = nullptr, *ln_rstd = nullptr;
+  float ln_eps = 0.f;
 };
 
 // Implicit-GEMM gather for 3x3 / pad-1 convolutions.  The A operand (or the wgrad X operand) is
@@ -186,6 +192,9 @@ bool sgemm_dgrad_try(const void* dout, int ldd, const float* W, void* dA, int ld
 // Pipelined panel GEMM (ogv_pgemm.hip) for small-M bf16 shapes; 0 / false = not handled.
 int pgemm_fwd_try(const void* A, int lda, const Pro& pro, const float* W, int ldw, void* out, int ldo, int M,
                   int N, int K, const Epi& epi, hipStream_t s);
+bool pgemm_fwd_ln_try(const void* A, int lda, const float* W, int ldw, void* out, int ldo, int M, int N, int K,
+                      const Epi& epi, hipStream_t s);
+void set_ln_epi(int v);
 bool pgemm_dgrad_try(const void* dout, int ldd, const float* W, void* dA, int lda, int M, int Nf, int Kf,
                      const Epi& epi, hipStream_t s);
 bool pgemm_route(int kind, int M, int N, int K, int act);

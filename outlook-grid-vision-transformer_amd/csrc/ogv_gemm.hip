@@ -1521,6 +1521,48 @@ extern "C" int ogv_gemm_fwd(const void* A, int lda, const float* W, const float*
   return check_launch("ogv_gemm_fwd");
 }
 
+// knob "ln_epi": the next LayerNorm in the producing GEMM's epilogue (ogv_gemm_fwd_ln) -- 0 never; 1 (default)
+// where the panel kernel is the route anyway (M below sgemm_min_m); 2 at every M (the panel kernel then replaces
+// the streaming one)
+static int g_ln_epi = 1;
+namespace ogv {
+void set_ln_epi(int v) { g_ln_epi = v < 0 ? 0 : (v > 2 ? 2 : v); }
+}  // namespace ogv
+
+// out = res + rs * (A . W^T + bias) (bf16, stored rounded) and the next LayerNorm of those rows, one launch:
+// ln_out = (out - mean) * rstd * gamma + beta (row stride ldo), mean / rstd [M] for the LN backward.
+// OGV_ERR_UNSUPPORTED, with nothing launched, where the panel kernel does not take it.
+extern "C" int ogv_gemm_fwd_ln(const void* A, int lda, const float* W, const float* bias, const void* res,
+                               const float* rs, int rps, void* out, int ldo, void* ln_out, const float* gamma,
+                               const float* beta, float eps, float* mean, float* rstd, int M, int N, int K,
+                               ogv_dtype dt, void* stream) {
+  int rc = check_common(M, N, K, OGV_ACT_NONE, dt, "ogv_gemm_fwd_ln");
+  if (rc) return rc;
+  OGV_REQUIRE(A && W && out && ln_out && gamma && beta && mean && rstd, "ogv_gemm_fwd_ln: null pointer");
+  OGV_REQUIRE(lda >= K && ldo >= N, "ogv_gemm_fwd_ln: lda %d / ldo %d too small", lda, ldo);
+  OGV_REQUIRE(!rs || rps > 0, "ogv_gemm_fwd_ln: rows-per-sample must be > 0 with a row scale");
+  if (dt != OGV_BF16 || !g_ln_epi || (g_ln_epi == 1 && M >= sgemm_min_m())) {
+    set_error("ogv_gemm_fwd_ln: unsupported here (bf16 panel-kernel shapes only, knob ln_epi)");
+    return OGV_ERR_UNSUPPORTED;
+  }
+  Epi epi;
+  epi.bias = bias;
+  epi.res = res;
+  epi.rs = rs;
+  epi.rps = rps > 0 ? rps : 1;
+  epi.ln_out = ln_out;
+  epi.ln_g = gamma;
+  epi.ln_b = beta;
+  epi.ln_mean = mean;
+  epi.ln_rstd = rstd;
+  epi.ln_eps = eps;
+  if (!pgemm_fwd_ln_try(A, lda, W, K, out, ldo, M, N, K, epi, as_stream(stream))) {
+    set_error("ogv_gemm_fwd_ln: unsupported shape (N <= 192, 8 | N, 8 | K, 16-B aligned rows)");
+    return OGV_ERR_UNSUPPORTED;
+  }
+  return check_launch("ogv_gemm_fwd_ln");
+}
+
 // out = A . W^T + bias (bf16, stored rounded) and aout = act(out) of the stored values, one launch:
 // the pre-activation for the next layer's data gradient (act'(Z)) and the activation for its
 // forward and weight gradient, so neither recomputes the activation per element.

@@ -63,7 +63,11 @@ __device__ __forceinline__ int pg_slot_col(int r) {
 // CV: implicit-GEMM 3x3 convolution (stem / downsample convs, their data gradients as transposed
 // convs): row m = output pixel, column k = tap * Cs + channel (tap-major weight), A fragments
 // gathered from the NHWC source (cv, conv_src; zero outside the image); lda unused.
-template <int RS, int TN, int PA, bool GT, int ZA, bool STATS, bool BT, bool SW, bool CV = false>
+// LNO: the residual stream's next LayerNorm in the epilogue (Epi::ln_*): the tile holds whole rows (one column
+// tile), so each row's mean / variance of the stored (rounded) outputs is a register sum over the lane's 8 * TN / 2
+// columns plus two xor shuffles across the four lanes sharing the row -- the LayerNorm kernel's read of the row and
+// its launch are gone
+template <int RS, int TN, int PA, bool GT, int ZA, bool STATS, bool BT, bool SW, bool CV = false, bool LNO = false>
 __global__ __launch_bounds__(PG_NW * 64, 2) void pgemm_bf16_kernel(const bf16* __restrict__ A, int lda, Pro pro,
                                                                 const float* __restrict__ W, int ldw, Epi epi,
                                                                 bf16* __restrict__ out, int ldo, int M, int N, int K,
@@ -337,7 +341,78 @@ __global__ __launch_bounds__(PG_NW * 64, 2) void pgemm_bf16_kernel(const bf16* _
   auto epilogue = [&](int j) {
     const int mt = tile_mt(j), n0 = tile_nt(j) * BN, mw = mt * BM + wave * 16 * RS;
     const float* cv = cvec + (j & 1) * 2 * BN;
-    if constexpr (!BT || PG_BT16) {
+    if constexpr (LNO) {   // (n0 = 0: the plan has one column tile)
+      bf16* lno = static_cast<bf16*>(epi.ln_out);
+      const float invN = 1.f / (float)N;
+#pragma unroll
+      for (int i = 0; i < RS; ++i) {
+        const int m = mw + i * 16 + fr;
+        const bool mok = m < M;
+        const long mc = mok ? m : M - 1;
+        const float rsc = epi.rs ? epi.rs[mc / epi.rps] : 1.f;
+        uint4 rv[TN / 2];
+#pragma unroll
+        for (int q = 0; q < TN / 2; ++q) {
+          rv[q] = uint4{0u, 0u, 0u, 0u};
+          if (res) rv[q] = *reinterpret_cast<const uint4*>(res + mc * ldo + min(32 * q + 8 * fg, N - 8));
+        }
+        // the stored (rounded) row values replace the accumulators (dead after the epilogue): no extra registers
+        float s = 0.f;
+#pragma unroll
+        for (int q = 0; q < TN / 2; ++q) {
+          const int n = 32 * q + 8 * fg;
+          const bool ok = mok && n < N;
+          const float4 b0 = *reinterpret_cast<const float4*>(cv + n);
+          const float4 b1 = *reinterpret_cast<const float4*>(cv + n + 4);
+          const float bias[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+          const bf16* rb = reinterpret_cast<const bf16*>(&rv[q]);
+          uint4 ov;
+          bf16* ob = reinterpret_cast<bf16*>(&ov);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            ob[e] = (bf16)((acc[i][2 * q + (e >> 2)][e & 3] + bias[e]) * rsc + (float)rb[e]);
+            const float vr = n < N ? (float)ob[e] : 0.f;
+            acc[i][2 * q + (e >> 2)][e & 3] = vr;
+            s += vr;
+          }
+          if (ok && !(dbg & 4)) *reinterpret_cast<uint4*>(out + (long)m * ldo + n) = ov;
+        }
+        s += __shfl_xor(s, 16, 64);
+        s += __shfl_xor(s, 32, 64);
+        const float mu = s * invN;
+        float ss = 0.f;
+#pragma unroll
+        for (int q = 0; q < TN / 2; ++q) {
+          const bool nok = 32 * q + 8 * fg < N;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float d = nok ? acc[i][2 * q + (e >> 2)][e & 3] - mu : 0.f;
+            ss = fmaf(d, d, ss);
+          }
+        }
+        ss += __shfl_xor(ss, 16, 64);
+        ss += __shfl_xor(ss, 32, 64);
+        const float rstd = rsqrtf(ss * invN + epi.ln_eps);
+#pragma unroll
+        for (int q = 0; q < TN / 2; ++q) {
+          const int n = 32 * q + 8 * fg, nc = min(n, N - 8);
+          const float4 g0 = *reinterpret_cast<const float4*>(epi.ln_g + nc);
+          const float4 g1 = *reinterpret_cast<const float4*>(epi.ln_g + nc + 4);
+          const float4 h0 = *reinterpret_cast<const float4*>(epi.ln_b + nc);
+          const float4 h1 = *reinterpret_cast<const float4*>(epi.ln_b + nc + 4);
+          const float gw[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+          const float bw[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+          float o[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = (acc[i][2 * q + (e >> 2)][e & 3] - mu) * rstd * gw[e] + bw[e];
+          if (mok && n < N) store_vec<bf16, 8>(lno + (long)m * ldo + n, o);
+        }
+        if (fg == 0 && mok) {
+          epi.ln_mean[m] = mu;
+          epi.ln_rstd[m] = rstd;
+        }
+      }
+    } else if constexpr (!BT || PG_BT16) {
       // lane: row m, columns 32 q + 8 fg .. + 7 of every fragment pair q (pg_col_slot)
 #pragma unroll
       for (int i = 0; i < RS; ++i) {
@@ -680,11 +755,11 @@ static unsigned pg_grid(const PgPlan& p, int parts = 1) {
   const long vb = (long)((p.nMt + 7) / 8) * 8 * p.nNt;
   return (unsigned)std::max<long>(8, std::min<long>(vb, (long)pg_cus() * g_pg_per_cu / parts / 8 * 8));
 }
-template <int RS, int TN, int PA, bool GT, int ZA, bool STATS, bool BT, bool SW, bool CV>
+template <int RS, int TN, int PA, bool GT, int ZA, bool STATS, bool BT, bool SW, bool CV, bool LNO = false>
 static void pg_launch(const PgPlan& p, const bf16* A, int lda, const Pro& pro, const float* W, int ldw,
                       const Epi& epi, bf16* out, int ldo, int M, int N, int K, const ConvG& cv, hipStream_t s) {
   if (skip_mask() & 1) return;
-  auto kern = pgemm_bf16_kernel<RS, TN, PA, GT, ZA, STATS, BT, SW, CV>;
+  auto kern = pgemm_bf16_kernel<RS, TN, PA, GT, ZA, STATS, BT, SW, CV, LNO>;
   if (!lds_ok(reinterpret_cast<const void*>(kern), p.lds, "pgemm_bf16_kernel")) return;
   // the merged transposed-conv launch: four class groups of cv.cls_G workgroups
   const unsigned grid = (CV && cv.par == 4) ? (unsigned)(4 * cv.cls_G) : pg_grid(p);
@@ -746,6 +821,40 @@ int pgemm_fwd_try(const void* A, int lda, const Pro& pro, const float* W, int ld
   }
 #undef OGV_PGF
   return st ? p.nMt : 1;
+}
+
+// out = epi(A . W^T) with the next LayerNorm in the epilogue (epi.ln_*): the panel kernel with ONE column tile of
+// 64 / 128 / 192 columns holding whole rows (N <= 192), no A prologue, no statistics.  Returns false (nothing
+// launched) for a shape it does not take.
+bool pgemm_fwd_ln_try(const void* A, int lda, const float* W, int ldw, void* out, int ldo, int M, int N, int K,
+                      const Epi& epi, hipStream_t s) {
+  if (!g_pgemm || M <= 0 || N > 192 || (N & 7) || (K & 7) || epi.zact || epi.stat || epi.aout || !epi.ln_out ||
+      !epi.ln_g || !epi.ln_b || !epi.ln_mean || !epi.ln_rstd)
+    return false;
+  if (!al16p(A) || (lda & 7) || !al16p(out) || (ldo & 7) || (ldw & 3) || !al16p(W) || !al16p(epi.ln_out) ||
+      !al16p(epi.ln_g) || !al16p(epi.ln_b) || (epi.res && !al16p(epi.res)))
+    return false;
+  const bool sw = (split_w() & 1) != 0 && (g_pg_split & 1);
+  PgPlan p;
+  p.TN = N <= 64 ? 4 : (N <= 128 ? 8 : 12);
+  p.nNt = 1;
+  p.RS = (p.TN == 12 || (long)((M + 127) / 128) < 512) ? 1 : 2;
+  p.nMt = (M + 64 * p.RS - 1) / (64 * p.RS);
+  p.lds = pg_lds(p.TN, false, sw, K, false, false);
+  if (p.lds > (size_t)g_pg_lds_kb * 1024) return false;
+  p.ok = 1;
+  const bf16* a = static_cast<const bf16*>(A);
+  bf16* o = static_cast<bf16*>(out);
+#define OGV_PGL(RS_, TN_)                                                                                          \
+  do {                                                                                                             \
+    if (sw) pg_launch<RS_, TN_, -1, false, 0, false, false, true, false, true>(p, a, lda, Pro(), W, ldw, epi, o, ldo, M, N, K, ConvG(), s); \
+    else pg_launch<RS_, TN_, -1, false, 0, false, false, false, false, true>(p, a, lda, Pro(), W, ldw, epi, o, ldo, M, N, K, ConvG(), s); \
+  } while (0)
+  if (p.TN == 12) OGV_PGL(1, 12);
+  else if (p.TN == 8) { if (p.RS == 2) OGV_PGL(2, 8); else OGV_PGL(1, 8); }
+  else { if (p.RS == 2) OGV_PGL(2, 4); else OGV_PGL(1, 4); }
+#undef OGV_PGL
+  return true;
 }
 
 // dA[M, Kf] = epi(dOut[M, Nf] . W[Nf, Kf]): reduction Nf, output columns Kf.

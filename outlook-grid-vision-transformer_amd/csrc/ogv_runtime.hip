@@ -312,6 +312,10 @@ extern "C" int ogv_set_option(const char* name, int value) {
     set_vph_wgs(value);
     return OGV_OK;
   }
+  if (!strcmp(name, "ln_epi")) {
+    set_ln_epi(value);
+    return OGV_OK;
+  }
   if (!strcmp(name, "pg_tconv1")) {
     set_pg_tconv1(value);
     return OGV_OK;

@@ -82,6 +82,7 @@ SIGNATURES = {
     "ogv_outlook_vproj_supported": (_i, [_i, _i, _i, _i, _i, _i, _i, _i, _i]),
     "ogv_outlook_vproj_bwd_supported": (_i, [_i, _i, _i, _i, _i, _i, _i, _i]),
     "ogv_outlook_vproj_fwd": (_i, [_p, _i, _p, _p, _p, _i, _p, _i, _i, _i, _i, _i, _i, _i, _p]),
+    "ogv_gemm_fwd_ln": (_i, [_p, _i, _p, _p, _p, _p, _i, _p, _i, _p, _p, _p, _f, _p, _p, _i, _i, _i, _i, _p]),
     "ogv_outlook_vproj_l32_supported": (_i, [_i, _i, _i, _i, _i, _i, _i, _i]),
     "ogv_outlook_vproj_fwd_l32": (_i, [_p, _i, _p, _p, _p, _i, _p, _i, _p, _i, _i, _i, _i, _i, _i, _i, _p]),
     "ogv_outlook_agg_bwd_l32": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _p]),
@@ -130,6 +131,7 @@ SIGNATURES = {
 }
 
 OGV_F32, OGV_BF16 = 0, 1
+OGV_OK, OGV_ERR_ARG, OGV_ERR_UNSUPPORTED, OGV_ERR_LAUNCH = 0, 1, 2, 3   # include/ogv.h status codes
 ACT = {None: 0, "none": 0, "gelu": 1, "silu": 2, "relu": 3}
 
 _lib = None

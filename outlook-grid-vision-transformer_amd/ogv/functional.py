@@ -176,9 +176,11 @@ def probe_bytes(name: str, u: dict) -> int:
     if name == "wgrad":         # read G [M,N], X [M,K]; write fp32 dW [N,K] (+ dbias)
         return e * u["M"] * (u["N"] + u["K"]) + 4 * u["N"] * u["K"] + (4 * u["N"] if u["bias"] else 0)
     if name in ("gemm_fwd", "sgemm", "gemm_tiled", "gemm_panel") and u.get("kind", "fwd") == "fwd":
-        # read A [M,K] (+ residual [M,N]) + fp32 W [N,K] (+ bias), write out [M,N] (+ act(out) [M,N])
+        # read A [M,K] (+ residual [M,N]) + fp32 W [N,K] (+ bias), write out [M,N] (+ act(out) [M,N]; + the next
+        # LayerNorm's output [M,N], its fp32 mean / rstd and the fp32 gamma / beta with ogv_gemm_fwd_ln)
         return (e * u["M"] * (u["K"] + u["N"] * (2 if u["res"] else 1) + (u["N"] if u.get("aout") else 0))
-                + 4 * u["N"] * u["K"] + (4 * u["N"] if u["bias"] else 0))
+                + 4 * u["N"] * u["K"] + (4 * u["N"] if u["bias"] else 0)
+                + ((e * u["M"] * u["N"] + 8 * u["M"] + 8 * u["N"]) if u.get("ln") else 0))
     if name in ("sgemm", "gemm_tiled", "gemm_panel"):   # dgrad: read dOut [M,N] (+ Z [M,K]) + fp32 W [N,K], write dA [M,K]
         return e * u["M"] * (u["N"] + u["K"] * (2 if u["z"] else 1)) + 4 * u["N"] * u["K"]
     raise KeyError(name)
@@ -582,6 +584,110 @@ def _linear_bwd(dout, x2d, w2d, rs, rps, act, has_bias, want_dx, want_dw, x_act=
                                          _ptr(rs), rps, _ptr(dx), K, M, N, K, act, _ptr(ws_d), dt, _stream()),
                       "ogv_gemm_dgrad")
     return dx, dw, db
+
+
+class _LinearLNPair(torch.autograd.Function):
+    """(LN(out), out) with out = residual + rs * (x2d @ W^T + b): a pre-norm block's producing Linear and the
+    residual stream's next LayerNorm (Outlook_Block.py:58-60, Out_Grid_Block.py:100-102) in ONE launch
+    (ogv_gemm_fwd_ln: the LN in the GEMM epilogue; where the kernel declines, ogv_gemm_fwd + ogv_layernorm_fwd).
+    out is the next block's residual (its gradient arrives here and is summed inside the LN backward, as
+    _LayerNormPair does); the backward is the LN backward then the Linear's."""
+
+    @staticmethod
+    def forward(ctx, x2d, w2d, bias, residual, row_scale, rps, gamma, beta, eps):
+        lib = _lib.load()
+        M, K = x2d.shape
+        N = w2d.shape[0]
+        dt = _dt(x2d)
+        out = torch.empty((M, N), dtype=x2d.dtype, device=x2d.device)
+        y = torch.empty((M, N), dtype=x2d.dtype, device=x2d.device)
+        mean = torch.empty((M,), dtype=torch.float32, device=x2d.device)
+        rstd = torch.empty((M,), dtype=torch.float32, device=x2d.device)
+        units = dict(M=M, N=N, K=K, elem=x2d.element_size(), res=residual is not None, bias=bias is not None, ln=True)
+        with _census("gemm_fwd", units):
+            rc = lib.ogv_gemm_fwd_ln(_ptr(x2d), x2d.stride(0), _ptr(w2d), _ptr(bias), _ptr(residual), _ptr(row_scale),
+                                     int(rps), _ptr(out), N, _ptr(y), _ptr(gamma), _ptr(beta), float(eps), _ptr(mean),
+                                     _ptr(rstd), M, N, K, dt, _stream())
+        if rc == _lib.OGV_ERR_UNSUPPORTED:    # nothing launched: the two ops
+            units["ln"] = False
+            with _census("gemm_fwd", units):
+                check(lib.ogv_gemm_fwd(_ptr(x2d), x2d.stride(0), _ptr(w2d), _ptr(bias), _ptr(residual), _ptr(row_scale),
+                                       int(rps), _ptr(out), N, M, N, K, ACT[None], dt, _stream()), "ogv_gemm_fwd")
+            with _census("layernorm_fwd", dict(M=M, C=N, elem=x2d.element_size())):
+                check(lib.ogv_layernorm_fwd(_ptr(out), _ptr(gamma), _ptr(beta), _ptr(y), _ptr(mean), _ptr(rstd), M, N,
+                                            float(eps), dt, _stream()), "ogv_layernorm_fwd")
+        else:
+            check(rc, "ogv_gemm_fwd_ln")
+        ctx.save_for_backward(x2d, w2d, row_scale, out, gamma, mean, rstd)
+        ctx.meta = (int(rps), bias is not None, residual is not None, beta is not None)
+        return y, out
+
+    @staticmethod
+    def backward(ctx, dy, dres):
+        lib = _lib.load()
+        x2d, w2d, rs, out, gamma, mean, rstd = ctx.saved_tensors
+        rps, has_bias, has_res, has_beta = ctx.meta
+        M, N = out.shape
+        dgamma = dbeta = None
+        if dy is None:
+            dtot = dres.to(x2d.dtype).contiguous()
+        else:
+            dy = dy.to(x2d.dtype).contiguous()
+            if dres is not None:
+                dres = dres.to(x2d.dtype).contiguous()
+            dtot = torch.empty_like(out)
+            dgamma = torch.empty((N,), dtype=torch.float32, device=x2d.device)
+            dbeta = torch.empty((N,), dtype=torch.float32, device=x2d.device) if has_beta else None
+            ws = _ws(lib.ogv_layernorm_bwd_ws_bytes(M, N), x2d.device, deferrable=True)
+            with _census("layernorm_bwd", dict(M=M, C=N, elem=x2d.element_size(), dres=dres is not None)):
+                check(lib.ogv_layernorm_bwd(_ptr(dy), _ptr(out), _ptr(gamma), _ptr(mean), _ptr(rstd), _ptr(dres),
+                                            _ptr(dtot), _ptr(dgamma), _ptr(dbeta), _ptr(ws), M, N, _dt(x2d), _stream()),
+                      "ogv_layernorm_bwd")
+        want_dx = ctx.needs_input_grad[0]
+        want_dw = ctx.needs_input_grad[1] or (has_bias and ctx.needs_input_grad[2])
+        dx, dw, db = _linear_bwd(dtot, x2d, w2d, rs, rps, 0, has_bias, want_dx, want_dw)
+        dresid = dtot if has_res and ctx.needs_input_grad[3] else None
+        return dx, dw, db, dresid, None, None, dgamma, dbeta, None
+
+
+def linear_rows_ln(x2d, weight, bias, residual, row_scale, rps, gamma, beta, eps):
+    """(LN(out), out), out = residual + rs * (x2d @ W^T + b): see _LinearLNPair.  x2d [M, K] bf16 / fp32 rows,
+    weight [N, K] (or [N, K, 1, 1]), gamma / beta [N] (the LayerNorm's affine, beta may be None)."""
+    require_device(x2d, weight, bias, residual, row_scale, gamma, beta, what="ogv.linear_ln")
+    x2d = _rows_contig(x2d)
+    w2d = f32(weight).reshape(weight.shape[0], -1)
+    if w2d.shape[1] != x2d.shape[1]:
+        raise ValueError(f"ogv.linear_ln: weight in_features {w2d.shape[1]} != input features {x2d.shape[1]}")
+    if residual is not None:
+        residual = residual.to(x2d.dtype).contiguous()
+        if residual.shape != (x2d.shape[0], w2d.shape[0]):
+            raise ValueError("ogv.linear_ln: residual shape mismatch")
+    if row_scale is not None:
+        row_scale = row_scale.float().contiguous()
+    g = f32(gamma).contiguous()
+    b = f32(beta).contiguous() if beta is not None else torch.zeros_like(g)
+    return _LinearLNPair.apply(x2d, w2d, f32(bias), residual, row_scale, int(rps), g, b, float(eps))
+
+
+# knob: OGV_LN_EPI=1 runs the residual stream's next LayerNorm in the producing Linear's epilogue where the
+# kernel takes the shape (opt-in: no step-time gain measured at 7M, profiles/r06k_ln_epi_ab.log; default off
+# keeps every LayerNorm a launch of its own)
+_LN_EPI = os.environ.get("OGV_LN_EPI", "0") == "1"
+
+
+def ln_epilogue_params(norm, *mods):
+    """(gamma, beta, eps) when `norm` -- the residual stream's next LayerNorm (ogv.layers.LayerNorm or
+    LayerNorm2d) -- can run in the producing Linear's epilogue: no hooks on it or on the producing modules,
+    a 1-D affine normalisation.  None otherwise (the caller runs the Linear, then norm.forward_pair)."""
+    if not _LN_EPI or norm is None:
+        return None
+    ln = getattr(norm, "ln", norm)       # LayerNorm2d wraps an nn.LayerNorm as .ln
+    for m in (norm, ln) + mods:
+        if m._forward_hooks or m._forward_pre_hooks:
+            return None
+    if not isinstance(ln, torch.nn.LayerNorm) or len(ln.normalized_shape) != 1 or ln.weight is None:
+        return None
+    return ln.weight, ln.bias, ln.eps
 
 
 # knob: OGV_MAT_ACT=0 keeps the activation between two Linears as the second GEMM's prologue

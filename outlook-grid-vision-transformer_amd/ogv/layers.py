@@ -33,9 +33,11 @@ class Conv1x1(nn.Conv2d):
     def __init__(self, in_channels: int, out_channels: int, bias: bool = True):
         super().__init__(in_channels, out_channels, kernel_size=1, bias=bias)
 
-    def forward(self, x, residual=None, row_scale=None, act_in=None, x_act=None, emit_act=None):
+    def forward(self, x, residual=None, row_scale=None, act_in=None, x_act=None, emit_act=None, then_norm=None):
         """emit_act: return (y, emit_act(y)) from one launch (bf16); x_act: act_in(x) as emitted by
-        the previous layer (the product and the weight gradient read it, x feeds act'(x))."""
+        the previous layer (the product and the weight gradient read it, x feeds act'(x)).
+        then_norm: the residual stream's next LayerNorm2d -- returns (then_norm(y), y as the residual), the
+        normalisation in this GEMM's epilogue where it can run there (OF.linear_rows_ln)."""
         B, C, H, W = x.shape
         dt = OF.compute_dtype(x)
         x2d = OF.nchw_to_rows(x.to(dt))
@@ -43,6 +45,12 @@ class Conv1x1(nn.Conv2d):
             y, a = OF.linear_rows_act(x2d, self.weight, self.bias, emit_act)
             return OF.rows_to_nchw(y, B, H, W), OF.rows_to_nchw(a, B, H, W)
         r2d = OF.nchw_to_rows(residual.to(dt)) if residual is not None else None
+        if then_norm is not None:
+            lnp = OF.ln_epilogue_params(then_norm, self) if act_in is None and x_act is None else None
+            if lnp is not None:
+                yn, y = OF.linear_rows_ln(x2d, self.weight, self.bias, r2d, row_scale, H * W, *lnp)
+                return OF.rows_to_nchw(yn, B, H, W), OF.rows_to_nchw(y, B, H, W)
+            return then_norm.forward_pair(self(x, residual, row_scale, act_in, x_act))
         xa2d = OF.nchw_to_rows(x_act) if x_act is not None else None
         y = OF.linear_rows(x2d, self.weight, self.bias, r2d, row_scale, H * W, act_in, xa2d)
         return OF.rows_to_nchw(y, B, H, W)
@@ -62,8 +70,9 @@ class Linear(nn.Linear):
     """nn.Linear over the last dim of a contiguous [..., in] tensor (BHWC or [B, N, C]).
     ``rps`` = rows per sample for the DropPath row scale."""
 
-    def forward(self, x, residual=None, row_scale=None, rps=None, act_in=None, x_act=None, emit_act=None):
-        """emit_act / x_act: as Conv1x1.forward."""
+    def forward(self, x, residual=None, row_scale=None, rps=None, act_in=None, x_act=None, emit_act=None,
+                then_norm=None):
+        """emit_act / x_act / then_norm: as Conv1x1.forward (then_norm: the next ogv LayerNorm)."""
         lead = x.shape[:-1]
         dt = OF.compute_dtype(x)
         x2d = x.to(dt).reshape(-1, x.shape[-1])
@@ -73,6 +82,12 @@ class Linear(nn.Linear):
         r2d = residual.to(dt).reshape(-1, self.out_features) if residual is not None else None
         if rps is None:
             rps = max(1, x2d.shape[0] // max(1, lead[0] if len(lead) else 1))
+        if then_norm is not None:
+            lnp = OF.ln_epilogue_params(then_norm, self) if act_in is None and x_act is None else None
+            if lnp is not None:
+                yn, y = OF.linear_rows_ln(x2d, self.weight, self.bias, r2d, row_scale, rps, *lnp)
+                return yn.view(*lead, self.out_features), y.view(*lead, self.out_features)
+            return then_norm.forward_pair(self(x, residual, row_scale, rps, act_in, x_act))
         xa2d = x_act.reshape(-1, x.shape[-1]) if x_act is not None else None
         y = OF.linear_rows(x2d, self.weight, self.bias, r2d, row_scale, rps, act_in, xa2d)
         return y.view(*lead, self.out_features)

@@ -85,7 +85,10 @@ def grid_tail(blk, x):
     if not xb.is_contiguous():
         xb = xb.contiguous()
     xn, xr = blk.norm2.forward_pair(xb)
-    xb = blk.grid_attn(xn, residual=xr, row_scale=drop_path_scale(blk.dp2, xb))
-    xn, xr = blk.norm3.forward_pair(xb)
+    if blk.grid_attn._forward_hooks or blk.grid_attn._forward_pre_hooks:   # hooks see the reference's output
+        xb = blk.grid_attn(xn, residual=xr, row_scale=drop_path_scale(blk.dp2, xb))
+        xn, xr = blk.norm3.forward_pair(xb)
+    else:   # the grid proj GEMM's epilogue also applies norm3 to the rows it stores (ogv_gemm_fwd_ln)
+        xn, xr = blk.grid_attn(xn, residual=xr, row_scale=drop_path_scale(blk.dp2, xb), then_norm=blk.norm3)
     xb = blk.mlp(xn, residual=xr, row_scale=drop_path_scale(blk.dp3, xb))
     return xb.permute(0, 3, 1, 2)                                  # NCHW (channels_last) view

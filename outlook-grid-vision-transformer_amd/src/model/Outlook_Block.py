@@ -49,8 +49,11 @@ class OutlookerBlock2d(nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         x = x.to(OF.compute_dtype(x))
         xn, xr = self.norm1.forward_pair(x)
-        x = self.attn(xn, residual=xr, row_scale=drop_path_scale(self.dp1, x))
-        xn, xr = self.norm2.forward_pair(x)
+        if self.attn._forward_hooks or self.attn._forward_pre_hooks:   # hooks see the reference's single output
+            x = self.attn(xn, residual=xr, row_scale=drop_path_scale(self.dp1, x))
+            xn, xr = self.norm2.forward_pair(x)
+        else:   # the proj GEMM's epilogue also applies norm2 to the rows it stores (ogv_gemm_fwd_ln)
+            xn, xr = self.attn(xn, residual=xr, row_scale=drop_path_scale(self.dp1, x), then_norm=self.norm2)
         x = self.mlp(xn, residual=xr, row_scale=drop_path_scale(self.dp2, x))
         return x
 

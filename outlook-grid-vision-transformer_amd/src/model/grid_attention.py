@@ -78,8 +78,9 @@ class MultiHeadSelfAttention(nn.Module):
         out = (attn @ v).to(qkv.dtype)                                   # [B g g, h, N, hd]
         return out.view(B, g, g, h, H // g, W // g, hd).permute(0, 4, 1, 5, 2, 3, 6).reshape(B * H * W, self.dim)
 
-    def attend_rows(self, x2d, B, H, W, g, residual=None, row_scale=None):
-        """Rows of a [B, H, W, C] image (or [B, 1, N, C] token set) -> attended rows (+ residual)."""
+    def attend_rows(self, x2d, B, H, W, g, residual=None, row_scale=None, then_norm=None):
+        """Rows of a [B, H, W, C] image (or [B, 1, N, C] token set) -> attended rows (+ residual); with
+        then_norm (the residual stream's next LayerNorm): (then_norm(rows), rows as the residual)."""
         capture = bool(getattr(self, "capture_attn", False))
         qkv = self.qkv(x2d, rps=H * W)
         if self.training and self.attn_drop.p > 0:
@@ -91,12 +92,12 @@ class MultiHeadSelfAttention(nn.Module):
                 self.last_attn_postdrop = self.last_attn
         if self.training and self.proj_drop.p > 0:
             y = self.proj_drop(self.proj(out, rps=H * W))
-            if residual is None:
-                return y
-            if row_scale is not None:
-                y = y * row_scale.repeat_interleave(H * W).view(-1, 1).to(y.dtype)
-            return residual + y
-        return self.proj(out, residual=residual, row_scale=row_scale, rps=H * W)
+            if residual is not None:
+                if row_scale is not None:
+                    y = y * row_scale.repeat_interleave(H * W).view(-1, 1).to(y.dtype)
+                y = residual + y
+            return then_norm.forward_pair(y) if then_norm is not None else y
+        return self.proj(out, residual=residual, row_scale=row_scale, rps=H * W, then_norm=then_norm)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if x.ndim != 3:
@@ -120,7 +121,8 @@ class GridAttention2D(nn.Module):
                                                            qkv_bias=cfg.qkv_bias, attn_drop=cfg.attn_drop,
                                                            proj_drop=cfg.proj_drop))
 
-    def forward(self, x: torch.Tensor, residual=None, row_scale=None) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, residual=None, row_scale=None, then_norm=None):
+        """then_norm: the residual stream's next LayerNorm -> (then_norm(out), out as the residual), BHWC."""
         if x.ndim != 4:
             raise ValueError(f"Expected x.ndim==4 (BHWC). Got {tuple(x.shape)}")
         B, H, W, C = x.shape
@@ -137,7 +139,10 @@ class GridAttention2D(nn.Module):
         dt = OF.compute_dtype(x)
         x2d = x.to(dt).reshape(B * H * W, C)
         r2d = residual.to(dt).reshape(B * H * W, C) if residual is not None else None
-        return self.mhsa.attend_rows(x2d, B, H, W, g, residual=r2d, row_scale=row_scale).view(B, H, W, C)
+        out = self.mhsa.attend_rows(x2d, B, H, W, g, residual=r2d, row_scale=row_scale, then_norm=then_norm)
+        if then_norm is not None:
+            return out[0].view(B, H, W, C), out[1].view(B, H, W, C)
+        return out.view(B, H, W, C)
 
 
 LocalAttention2D = GridAttention2D  # older name used by the reference notebooks

@@ -210,7 +210,8 @@ class OutlookAttention2d(nn.Module):
                                 torch.zeros(max(rows, 0), device=device))
         return z
 
-    def forward(self, x: torch.Tensor, residual=None, row_scale=None) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, residual=None, row_scale=None, then_norm=None):
+        """then_norm: the residual stream's next LayerNorm2d -> (then_norm(out), out as the residual)."""
         B, C, H, W = x.shape
         if self.stride != 1 or (self.training and self.attn_drop.p > 0):
             y = self._forward_materialised(x)
@@ -234,9 +235,9 @@ class OutlookAttention2d(nn.Module):
             y = OF.rows_to_nchw(y, B, H, W)
         if self.training and self.proj_drop.p > 0:
             y = self.proj_drop(self.proj(y))
-            if residual is None:
-                return y
-            if row_scale is not None:
-                y = y * row_scale.view(-1, 1, 1, 1).to(y.dtype)
-            return residual + y
-        return self.proj(y, residual=residual, row_scale=row_scale)
+            if residual is not None:
+                if row_scale is not None:
+                    y = y * row_scale.view(-1, 1, 1, 1).to(y.dtype)
+                y = residual + y
+            return then_norm.forward_pair(y) if then_norm is not None else y
+        return self.proj(y, residual=residual, row_scale=row_scale, then_norm=then_norm)

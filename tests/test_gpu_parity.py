@@ -175,6 +175,15 @@ def test_golden_bf16(name):
     assert fx.compare_grads(grads, arr, BF16_GRAD, 1e-4, name + " bf16", floor_tag="bf16", floor_scale=2.0) > 0
 
 
+@pytest.mark.parametrize("name", fx.fixture_names("outgrid_block_") + ["outlooker_block_s1"])
+def test_golden_bf16_ln_epilogue(name, monkeypatch):
+    """test_golden_bf16's bars with the opt-in LayerNorm-in-the-producing-GEMM form on (OGV_LN_EPI=1: proj ->
+    norm2 / norm3 as ogv_gemm_fwd_ln where the panel kernel takes the shape, _LinearLNPair's backward)."""
+    from ogv import functional as OF
+    monkeypatch.setattr(OF, "_LN_EPI", True)
+    test_golden_bf16(name)
+
+
 def test_capture_attn_hook():
     meta, arr = fx.load("grid_attn_capture_s1")
     mod = _module(meta)
@@ -1276,3 +1285,67 @@ def test_mbconv_a3_knob_change_between_fwd_and_bwd(first, then):
         assert lib.ogv_set_option(b"mb_a3", 3) == 0
     for k, (a, b) in enumerate(zip(*res)):
         assert torch.equal(a, b), (k, fx.maxabs(b, a))
+
+
+@pytest.mark.parametrize("M,N,K,res,rs", [(32768, 128, 192, True, True), (131072, 96, 96, True, False),
+                                          (8192, 128, 768, True, True), (1000, 48, 96, True, False),
+                                          (4104, 64, 256, False, False), (2048, 128, 384, True, True),
+                                          (32768, 96, 384, True, False)])
+def test_gemm_fwd_ln_matches_gemm_then_layernorm(M, N, K, res, rs):
+    """ogv_gemm_fwd_ln (the producing Linear of a pre-norm block with the residual stream's next LayerNorm in its
+    epilogue) against ogv_gemm_fwd followed by ogv_layernorm_fwd on the same inputs: the stored rows bit-identical
+    (same epilogue arithmetic), the LayerNorm output within one bf16 rounding of |ref| (fp32 row statistics summed
+    in another order), mean / rstd to fp32 rounding; then the fused op's gradients (OF.linear_rows_ln) against
+    the two separate ops' (linear_rows + layer_norm_rows_pair) within 1e-2 * max(1, |ref|)."""
+    from ogv import functional as OF
+    from ogv._lib import load
+    lib = load()
+    g = torch.Generator(device=DEV).manual_seed(M + N + K)
+    x = torch.randn(M, K, device=DEV, generator=g).to(torch.bfloat16)
+    w = torch.randn(N, K, device=DEV, generator=g) / K ** 0.5
+    b = 0.1 * torch.randn(N, device=DEV, generator=g)
+    r = torch.randn(M, N, device=DEV, generator=g).to(torch.bfloat16) if res else None
+    B = 4 if M % 4 == 0 else 1
+    scale = (torch.rand(B, device=DEV, generator=g) + 0.5) if rs else None
+    gam = 1.0 + 0.1 * torch.randn(N, device=DEV, generator=g)
+    bet = 0.1 * torch.randn(N, device=DEV, generator=g)
+    rps = M // B
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    y = torch.empty_like(out)
+    mean = torch.empty(M, device=DEV)
+    rstd = torch.empty(M, device=DEV)
+    p = OF._ptr
+    rc = lib.ogv_gemm_fwd_ln(p(x), K, p(w), p(b), p(r), p(scale), rps, p(out), N, p(y), p(gam), p(bet), 1e-5, p(mean),
+                             p(rstd), M, N, K, OF.OGV_BF16, OF._stream())
+    assert rc == 0, load().ogv_last_error()
+    # (N = 192 needs a 192-column tile whose split-weight slab passes the two-workgroups-per-CU LDS cap: declined,
+    # nothing launched -- the op then runs the GEMM and the LayerNorm separately, as before)
+    assert lib.ogv_gemm_fwd_ln(p(x), K, p(torch.zeros(192, K, device=DEV)), None, None, None, 1, p(out), 192, p(y), p(gam),
+                               p(bet), 1e-5, p(mean), p(rstd), M, 192, K, OF.OGV_BF16, OF._stream()) == 2 if N <= 128 and \
+        M < 262144 and M * 192 <= out.numel() else True
+    ref = OF.linear_rows(x, w, b, r, scale, rps)
+    yr, _ = OF.layer_norm_rows_pair(ref, gam, bet, 1e-5)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    assert fx.maxabs(y.float(), yr.float()) <= 8e-3 * max(1.0, yr.float().abs().max().item())
+    xd = ref.float()
+    mu = xd.mean(1)
+    assert fx.maxabs(mean, mu) <= 1e-5 * max(1.0, mu.abs().max().item())
+    assert fx.maxabs(rstd, 1.0 / torch.sqrt(xd.var(1, unbiased=False) + 1e-5)) <= 1e-4 * rstd.abs().max().item()
+    # autograd: the fused op vs the two ops
+    dy = torch.randn(M, N, device=DEV, generator=g).to(torch.bfloat16)
+    dres = torch.randn(M, N, device=DEV, generator=g).to(torch.bfloat16)
+    grads = []
+    for fused in (True, False):
+        leaves = [t.clone().requires_grad_() for t in (x, w, b, gam, bet)] + ([r.clone().requires_grad_()] if res else [])
+        xx, ww, bb, gg, be = leaves[:5]
+        rr = leaves[5] if res else None
+        if fused:
+            yn, o = OF.linear_rows_ln(xx, ww, bb, rr, scale, rps, gg, be, 1e-5)
+        else:
+            o = OF.linear_rows(xx, ww, bb, rr, scale, rps)
+            yn, o = OF.layer_norm_rows_pair(o, gg, be, 1e-5)
+        torch.autograd.backward([yn, o], [dy, dres])
+        grads.append([t.grad.float() for t in leaves])
+    for a, rf in zip(*grads):
+        assert fx.maxabs(a, rf) <= 1e-2 * max(1.0, rf.abs().max().item())

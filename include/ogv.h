@@ -73,7 +73,8 @@ const char* ogv_last_error(void);
  *   (ogv_outlook_vproj_l32_supported answers 0 with 0); "vph_rows" (0 = auto): target rows per panel of that kernel; "vph_wgs" (default 3):
  *   workgroups per CU its grid is sized for; "vph_dbg": phase-skipping timing experiments (wrong results);
  *   "dw_tw" 8 / 16 / 32 (default): column strip width of the depthwise kernels; "ln_rpi" 2 (default) / 4:
- *   rows per iteration of the LayerNorm kernels.
+ *   rows per iteration of the LayerNorm kernels; "wg2_pbeta" (percent, 0 = off): cap the split-M weight gradient's slab
+ *   count so its fp32 partials stay below that fraction of the launch's operand bytes (at least one workgroup per CU).
  * Options pick kernel plans, and every *_ws_bytes query sizes the workspace for the plans in force
  * when it is called: set options first, then size workspaces (a workspace sized under other option
  * values can be too small -- e.g. wg_blocks / wg_tile / swg_min_m change the split-M partial count).
@@ -353,6 +354,26 @@ int ogv_bn_act_fwd(const void* x, void* out, float* saved, void* ws, const float
 int ogv_bn_act_bwd(const void* dout, const void* x, const float* saved, void* dx, float* dbn_w, float* dbn_b,
                    void* ws, const float* bn_w, int M, int C, int train, int act, ogv_dtype dt,
                    void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * The classifier head's BatchNorm2d + global average pool as ONE op (src/Model_A_OutGridNet.py:64-66,
+ * src/Model_B_OutGridNet.py head): BatchNorm is a per-channel affine map, so mean_p(BN(x)) = BN(mean_p(x));
+ * pooled[b, c] = sc[c] * (sum_p x[b, p, c] / HW) + sh[c] with the batch statistics (train, running-stat
+ * update, shift = running mean as ogv_bn_act_fwd) or the running ones (eval), from ONE read of x [B*HW, C]
+ * (image-major NHWC rows).  pooled_raw (fp32 [B, C], the plain means) and saved (>= ogv_bn_act_saved_bytes(C))
+ * are kept for the backward, which writes dx from one read of x:
+ *   dx[b, p, c] = gamma*invstd * (dpooled[b, c]/HW - sum_b dpooled/N - xhat[b, p, c] * sum_b dpooled*xhat_b/N)
+ * (eval: gamma*invstd * dpooled/HW), xhat_b = (pooled_raw - mean)*invstd, N = B*HW; dgamma = sum_b dpooled*xhat_b,
+ * dbeta = sum_b dpooled.  Replaces ogv_bn_act_fwd/bwd + the pool and its broadcast gradient (7 launches -> 6,
+ * 10 passes over [B*HW, C] -> 2).
+ * ------------------------------------------------------------------------------------------- */
+size_t ogv_head_bn_pool_ws_bytes(int B, int C);
+int ogv_head_bn_pool_fwd(const void* x, float* pooled_raw, float* pooled, float* saved, void* ws, const float* bn_w,
+                         const float* bn_b, float* running_mean, float* running_var, int B, int HW, int C, int train,
+                         float eps, float momentum, ogv_dtype dt, void* stream);
+int ogv_head_bn_pool_bwd(const float* dpooled, const void* x, const float* pooled_raw, const float* saved, void* dx,
+                         float* dbn_w, float* dbn_b, void* ws, const float* bn_w, int B, int HW, int C, int train,
+                         ogv_dtype dt, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Batch mixing (training-loop input side).  Replaces apply_mixup_cutmix's tensor work

@@ -196,6 +196,28 @@ __device__ __forceinline__ float act_grad(int act, float x) {
     default: return 1.f;
   }
 }
+// act(x) and act'(x) with their shared transcendental evaluated once (bit-identical to act_fwd / act_grad:
+// the same expressions on the same values; the compiler does not always merge the two when registers are tight)
+__device__ __forceinline__ void act_both(int act, float x, float& f, float& g) {
+  switch (act) {
+    case OGV_ACT_GELU: {
+      float e;
+      const float cdf = gelu_cdf(x, e);
+      f = x * cdf;
+      g = fmaf(x * 0.39894228040143268f, e, cdf);
+      return;
+    }
+    case OGV_ACT_SILU: {
+      const float s = fast_sigmoid(x);
+      f = x * s;
+      g = s * (1.0f + x * (1.0f - s));
+      return;
+    }
+    default:
+      f = act_fwd(act, x);
+      g = act_grad(act, x);
+  }
+}
 
 // ---------------------------------------------------------------- wave reductions (wave64)
 // Exchanges inside a row of 16 lanes go through DPP (an operand modifier of a VALU instruction);

@@ -519,3 +519,165 @@ extern "C" int ogv_bn_act_bwd(const void* dout, const void* x, const float* save
   OGV_CB_DISPATCH(dt, V, bn_bwd_apply_run, dout, x, b.sc, b.sh, act, b.mean, b.invstd, coef, dx, (long)M, C, s);
   return check_launch("ogv_bn_act_bwd");
 }
+
+namespace ogv {
+
+// ------------------------------------------------------------------ head: BatchNorm2d + global average pool
+// Block = (one image, 4 channel chunks of V) x 64 row slots: fp64 sums of (x - shift), (x - shift)^2 (the
+// BatchNorm partial row of this image, the layout bn_reduce_finalize reads: [b][0..C) and [b][C..2C)) and of x
+// itself ([b][2C..3C): the pool).  One read of x.
+template <typename T, int V>
+__global__ __launch_bounds__(256) void head_pool_stats_kernel(const T* __restrict__ x, const float* __restrict__ shift,
+                                                              double* __restrict__ stat, int B, int HW, int C) {
+  __shared__ double lds[3 * 4 * 4 * 8];
+  const int gx = (C + 4 * V - 1) / (4 * V);
+  long lid;
+  if (!xcd_block((long)gx * B, lid)) return;
+  const int bx = (int)(lid % gx), b = (int)(lid / gx);
+  const int chunk = threadIdx.x & 3, slot = threadIdx.x >> 2;
+  const int c0 = (bx * 4 + chunk) * V;
+  double q[3][V];
+#pragma unroll
+  for (int i = 0; i < V; ++i) { q[0][i] = 0.0; q[1][i] = 0.0; q[2][i] = 0.0; }
+  if (c0 < C) {
+    float sf[V];
+    load_vec<float, V>(shift + c0, sf);
+#pragma unroll
+    for (int i = 0; i < V; ++i) sf[i] = bn_shift(sf[i]);
+    const T* xb = x + (long)b * HW * C + c0;
+    for (int r = slot; r < HW; r += 64) {
+      float v[V];
+      load_vec<T, V>(xb + (long)r * C, v);
+#pragma unroll
+      for (int i = 0; i < V; ++i) {
+        const double d = (double)v[i] - (double)sf[i];
+        q[0][i] += d;
+        q[1][i] = fma(d, d, q[1][i]);
+        q[2][i] += (double)v[i];
+      }
+    }
+  }
+  chunk_reduce_store<3, V, double>(q, lds, stat + (long)b * 3 * C, C, C, bx * 4 * V);
+}
+
+// pooled_raw = sum x / HW, pooled = pooled_raw * sc + sh   ([B, C], thread per element)
+__global__ void head_pool_apply_kernel(const double* __restrict__ stat, const float* __restrict__ sc,
+                                       const float* __restrict__ sh, float* __restrict__ raw, float* __restrict__ pooled,
+                                       int B, int HW, int C) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)B * C) return;
+  const int b = (int)(i / C), c = (int)(i - (long)b * C);
+  const float m = (float)(stat[(long)b * 3 * C + 2 * C + c] / (double)HW);
+  raw[i] = m;
+  pooled[i] = fmaf(m, sc[c], sh[c]);
+}
+
+// backward partial rows, one per image: [g, g * xhat_b] with xhat_b = (pooled_raw - mean) * invstd -- the
+// image's sum over its pixels of dz = g / HW and of dz * xhat
+__global__ void head_pool_bwd_stats_kernel(const float* __restrict__ g, const float* __restrict__ raw,
+                                           const float* __restrict__ mean, const float* __restrict__ invstd,
+                                           float* __restrict__ stat, int B, int C) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)B * C) return;
+  const int b = (int)(i / C), c = (int)(i - (long)b * C);
+  const float gv = g[i];
+  stat[(long)b * 2 * C + c] = gv;
+  stat[(long)b * 2 * C + C + c] = gv * ((raw[i] - mean[c]) * invstd[c]);
+}
+
+// dx = coef0 * (g[b] / HW - coef1 - (x - mean) * invstd * coef2)
+template <typename T, int V>
+__global__ __launch_bounds__(256) void head_pool_dx_kernel(const float* __restrict__ g, const T* __restrict__ x,
+                                                           const float* __restrict__ mean,
+                                                           const float* __restrict__ invstd,
+                                                           const float* __restrict__ coef, T* __restrict__ dx, int HW,
+                                                           long M, int C) {
+  const int nch = C / V;
+  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid >= M * nch) return;
+  const int c0 = (int)(tid % nch) * V;
+  const long m = tid / nch, b = m / HW;
+  const float ihw = 1.f / (float)HW;
+  float v[V], gv[V], mu[V], is[V], ca[V], cb[V], cc[V];
+  load_vec<T, V>(x + m * C + c0, v);
+  load_vec<float, V>(g + b * C + c0, gv);
+  load_vec<float, V>(mean + c0, mu);
+  load_vec<float, V>(invstd + c0, is);
+  load_vec<float, V>(coef + c0, ca);
+  load_vec<float, V>(coef + C + c0, cb);
+  load_vec<float, V>(coef + 2 * C + c0, cc);
+#pragma unroll
+  for (int i = 0; i < V; ++i) v[i] = ca[i] * (gv[i] * ihw - cb[i] - (v[i] - mu[i]) * is[i] * cc[i]);
+  store_vec<T, V>(dx + m * C + c0, v);
+}
+
+template <typename T, int V>
+static void head_stats_run(const void* x, const float* shift, double* stat, int B, int HW, int C, hipStream_t s) {
+  head_pool_stats_kernel<T, V><<<xcd_grid((long)cdiv(C, 4 * V) * B), 256, 0, s>>>((const T*)x, shift, stat, B, HW, C);
+}
+template <typename T, int V>
+static void head_dx_run(const float* g, const void* x, const float* mean, const float* invstd, const float* coef, void* dx,
+                        int HW, long M, int C, hipStream_t s) {
+  head_pool_dx_kernel<T, V><<<cdiv(M * (C / V), 256), 256, 0, s>>>(g, (const T*)x, mean, invstd, coef, (T*)dx, HW, M, C);
+}
+
+static int head_check(int B, int HW, int C, ogv_dtype dt, const char* fn) {
+  OGV_REQUIRE(B > 0 && HW > 0 && C > 0 && (long)B * HW <= INT32_MAX, "%s: bad shape B=%d HW=%d C=%d", fn, B, HW, C);
+  OGV_REQUIRE(dt == OGV_F32 || dt == OGV_BF16, "%s: bad dtype %d", fn, (int)dt);
+  return OGV_OK;
+}
+
+}  // namespace ogv
+
+using namespace ogv;
+
+extern "C" size_t ogv_head_bn_pool_ws_bytes(int B, int C) {
+  if (B <= 0 || C <= 0) return 0;
+  Carve c(nullptr);   // forward: fp64 [B][3C] + finalize scratch; backward: fp32 [B][2C] + coef [3C] (smaller)
+  c.take<double>((size_t)B * 3 * C);
+  c.take<double>(2 * (size_t)C);
+  c.take<float>(3 * (size_t)C);
+  return c.off;
+}
+
+extern "C" int ogv_head_bn_pool_fwd(const void* x, float* pooled_raw, float* pooled, float* saved, void* ws,
+                                    const float* bn_w, const float* bn_b, float* rm, float* rv, int B, int HW, int C,
+                                    int train, float eps, float momentum, ogv_dtype dt, void* stream) {
+  int rc = head_check(B, HW, C, dt, "ogv_head_bn_pool_fwd");
+  if (rc) return rc;
+  OGV_REQUIRE(x && pooled_raw && pooled && saved && ws && rm && rv, "ogv_head_bn_pool_fwd: null pointer");
+  hipStream_t s = as_stream(stream);
+  Carve cs(saved);
+  const BnSaved b = take_bn_saved(cs, C);
+  Carve cw(ws);
+  double* stat = cw.take<double>((size_t)B * 3 * C);
+  double* sums = cw.take<double>(2 * (size_t)C);
+  const int V = vec_width(C);
+  OGV_CB_DISPATCH(dt, V, head_stats_run, x, rm, stat, B, HW, C, s);
+  if (train)
+    bn_reduce_finalize_launch(stat, B, 3L * C, C, (double)B * HW, bn_w, bn_b, eps, momentum, rm, rv, b.mean, b.invstd,
+                              b.sc, b.sh, s);
+  else
+    bn_finalize_launch(sums, C, (double)B * HW, bn_w, bn_b, eps, momentum, rm, rv, b.mean, b.invstd, b.sc, b.sh, 0, s);
+  head_pool_apply_kernel<<<cdiv((long)B * C, 256), 256, 0, s>>>(stat, b.sc, b.sh, pooled_raw, pooled, B, HW, C);
+  return check_launch("ogv_head_bn_pool_fwd");
+}
+
+extern "C" int ogv_head_bn_pool_bwd(const float* dpooled, const void* x, const float* pooled_raw, const float* saved,
+                                    void* dx, float* dbn_w, float* dbn_b, void* ws, const float* bn_w, int B, int HW,
+                                    int C, int train, ogv_dtype dt, void* stream) {
+  int rc = head_check(B, HW, C, dt, "ogv_head_bn_pool_bwd");
+  if (rc) return rc;
+  OGV_REQUIRE(dpooled && x && pooled_raw && saved && ws && dx, "ogv_head_bn_pool_bwd: null pointer");
+  hipStream_t s = as_stream(stream);
+  Carve cs(const_cast<float*>(saved));
+  const BnSaved b = take_bn_saved(cs, C);
+  Carve cw(ws);
+  float* stat = cw.take<float>((size_t)B * 2 * C);
+  float* coef = cw.take<float>(3 * (size_t)C);
+  head_pool_bwd_stats_kernel<<<cdiv((long)B * C, 256), 256, 0, s>>>(dpooled, pooled_raw, b.mean, b.invstd, stat, B, C);
+  bn_reduce_coeffs_launch(stat, B, 2L * C, C, (float)((double)B * HW), bn_w, b.invstd, dbn_w, dbn_b, coef, train, s);
+  const int V = vec_width(C);
+  OGV_CB_DISPATCH(dt, V, head_dx_run, dpooled, x, b.mean, b.invstd, coef, dx, HW, (long)B * HW, C, s);
+  return check_launch("ogv_head_bn_pool_bwd");
+}

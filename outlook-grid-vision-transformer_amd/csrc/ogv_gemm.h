@@ -226,6 +226,7 @@ int wg2_mode();
 void set_wg2(int v);
 void set_wg2_blocks(int v);
 void set_wg2_tile(int v);
+void set_wg2_pbeta(int v);
 int sgemm_mode();
 void set_sgemm_mode(int v);
 int sgemm_min_m();

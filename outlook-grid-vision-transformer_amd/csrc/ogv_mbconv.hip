@@ -657,11 +657,13 @@ __global__ __launch_bounds__(256) void dw_dgrad_tile_kernel(const T* __restrict_
     const long off = ((b * t.H + y) * t.W + ti.x0 + px) * t.C + c;
     float ev[V];
     ce[r].unpack(ev);
-    float acc[V], av[V];
+    // act(BN1(e)) for the weight gradient and act'(BN1(e)) for the output from one transcendental pair
+    float acc[V], av[V], ag[V];
 #pragma unroll
     for (int i = 0; i < V; ++i) {
       acc[i] = 0.f;
-      if constexpr (WG) av[i] = act_fwd(ACT, fmaf(ev[i], s[i], h[i]));
+      if constexpr (WG) act_both(ACT, fmaf(ev[i], s[i], h[i]), av[i], ag[i]);
+      else ag[i] = act_grad(ACT, fmaf(ev[i], s[i], h[i]));
     }
 #pragma unroll
     for (int ki = 0; ki < 3; ++ki)
@@ -687,7 +689,7 @@ __global__ __launch_bounds__(256) void dw_dgrad_tile_kernel(const T* __restrict_
     float o2[V];
 #pragma unroll
     for (int i = 0; i < V; ++i) {
-      o2[i] = to_f(from_f<T>(acc[i] * act_grad(ACT, fmaf(ev[i], s[i], h[i]))));
+      o2[i] = to_f(from_f<T>(acc[i] * ag[i]));
       q[0][i] += o2[i];
       q[1][i] = fmaf(o2[i], (ev[i] - mu[i]) * is[i], q[1][i]);
     }

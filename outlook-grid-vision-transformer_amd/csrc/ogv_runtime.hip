@@ -232,6 +232,10 @@ extern "C" int ogv_set_option(const char* name, int value) {
     set_wg2_blocks(value);
     return OGV_OK;
   }
+  if (!strcmp(name, "wg2_pbeta")) {
+    set_wg2_pbeta(value);
+    return OGV_OK;
+  }
   if (!strcmp(name, "wg2_tile")) {
     set_wg2_tile(value);
     return OGV_OK;

@@ -382,6 +382,12 @@ int wg2_mode() { return g_wg2; }
 void set_wg2(int v) { g_wg2 = v < 0 ? 0 : (v > 2 ? 2 : v); }
 void set_wg2_blocks(int v) { g_wg2_blocks = v < 64 ? 64 : v; }
 void set_wg2_tile(int v) { g_wg2_tile = (v == 64 || v == 96 || v == 128 || v == 192) ? v : 0; }
+// knob "wg2_pbeta" (percent; 0 = off): cap the slab count so the fp32 slab partials (written here, read back
+// by the column reduction: S * (N*K + N) * 4 bytes each way) stay below beta x the launch's algorithmic
+// operand bytes M * (N + K) * 2 -- at small M and wide layers (7M stage 3: M = 8192, N = K = 384) the ~768-
+// workgroup target makes the partials 2x the operands; never below one workgroup per CU
+static int g_wg2_pbeta = 0;
+void set_wg2_pbeta(int v) { g_wg2_pbeta = v < 0 ? 0 : v; }
 
 struct W2Plan {
   int ok = 0, BN = 0, BK = 0, nNt = 0, nKt = 0, S = 0, mchunk = 0;
@@ -409,6 +415,11 @@ static W2Plan wgrad2_plan(int M, int N, int K, bool pro) {
   const long tiles = (long)p.nNt * p.nKt;
   long S = (g_wg2_blocks + tiles - 1) / tiles;
   S = std::min<long>(S, ((long)M + 4 * W2_MS - 1) / (4 * W2_MS));  // >= 4 steps per workgroup
+  if (g_wg2_pbeta > 0) {
+    const double cap = g_wg2_pbeta * 0.01 * (double)M * (N + K) * 2.0 / (4.0 * ((double)N * K + N));
+    const long floor_s = (256 + tiles - 1) / tiles;
+    S = std::min<long>(S, std::max<long>((long)cap, floor_s));
+  }
   S = std::max<long>(1, S);
   int mchunk = (int)((M + S - 1) / S);
   mchunk = (mchunk + W2_MS - 1) / W2_MS * W2_MS;

@@ -117,6 +117,9 @@ SIGNATURES = {
     "ogv_bn_act_ws_bytes": (_sz, [_i, _i]),
     "ogv_bn_act_fwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _f, _f, _i, _i, _p]),
     "ogv_bn_act_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p]),
+    "ogv_head_bn_pool_ws_bytes": (_sz, [_i, _i]),
+    "ogv_head_bn_pool_fwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _f, _f, _i, _p]),
+    "ogv_head_bn_pool_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p]),
     "ogv_mix_images": (_i, [_p, _p, _p, _i, _i, _i, _i, _i, _i, _f, _f, _i, _i, _i, _i, _i, _p]),
     "ogv_mix_targets": (_i, [_p, _p, _p, _i, _i, _f, _f, _p]),
     "ogv_cast": (_i, [_p, _i, _p, _i, _sz, _p]),

@@ -342,6 +342,9 @@ def op_cost(name: str, u: dict):
             return s * (Mi * Ci + 3 * Mo * Co) + 4 * 9 * Ci * Co, f
         # BN reduce (dout, y), BN apply (dout, y -> dy), wgrad (dy, x), dgrad (dy -> dx)
         return s * (7 * Mo * Co + 2 * Mi * Ci) + 8 * 9 * Ci * Co, 2 * f
+    if name in ("bn_act_fwd", "bn_act_bwd") and u.get("head"):   # the head's BN + pool: x once (+ dx)
+        return (s * M * C + 8 * (M // max(1, u.get("hw", 1))) * C, 4 * M * C) if name == "bn_act_fwd" else \
+            (2 * s * M * C, 6 * M * C)
     if name == "bn_act_fwd":         # (statistics pass over x when training) + apply
         return s * M * C * (3 if u.get("train") else 2), 4 * M * C
     if name == "bn_act_bwd":         # reduce (dout, x) + apply (dout, x -> dx)
@@ -1356,6 +1359,60 @@ class _BNAct(torch.autograd.Function):
             check(lib.ogv_bn_act_bwd(_ptr(dout), _ptr(x2d), _ptr(saved), _ptr(dx), _ptr(dg), _ptr(dbb), _ptr(ws),
                                      _ptr(bn_w), M, C, train, act, dt, _stream()), "ogv_bn_act_bwd")
         return dx, None, None, None, dg, dbb
+
+
+class _HeadBNPool(torch.autograd.Function):
+    """mean_p(BatchNorm2d(x)) as BN(mean_p(x)) from one read of x (ogv_head_bn_pool_fwd/bwd): the classifier
+    head of MaxOutNet / OutlookerFrontGridNet (Model_A_OutGridNet.py:64-66).  Returns fp32 [B, C]."""
+
+    @staticmethod
+    def forward(ctx, x2d, meta, rm, rv, bn_w, bn_b):
+        lib = _lib.load()
+        B, HW, train, eps, mom = meta
+        C = x2d.shape[1]
+        dt = _dt(x2d)
+        raw = torch.empty((B, C), dtype=torch.float32, device=x2d.device)
+        pooled = torch.empty((B, C), dtype=torch.float32, device=x2d.device)
+        saved = torch.empty(lib.ogv_bn_act_saved_bytes(C) // 4, dtype=torch.float32, device=x2d.device)
+        ws = _ws(lib.ogv_head_bn_pool_ws_bytes(B, C), x2d.device)
+        with _census("bn_act_fwd", dict(M=B * HW, C=C, train=train, elem=x2d.element_size(), head=True, hw=HW)):
+            check(lib.ogv_head_bn_pool_fwd(_ptr(x2d), _ptr(raw), _ptr(pooled), _ptr(saved), _ptr(ws), _ptr(bn_w),
+                                           _ptr(bn_b), _ptr(rm), _ptr(rv), B, HW, C, train, eps, mom, dt, _stream()),
+                  "ogv_head_bn_pool_fwd")
+        ctx.save_for_backward(x2d, raw, saved, bn_w)
+        ctx.meta = meta
+        return pooled
+
+    @staticmethod
+    def backward(ctx, dpooled):
+        lib = _lib.load()
+        x2d, raw, saved, bn_w = ctx.saved_tensors
+        B, HW, train, _, _ = ctx.meta
+        C = x2d.shape[1]
+        dpooled = dpooled.float().contiguous()
+        dx = torch.empty_like(x2d)
+        dg = torch.empty_like(bn_w) if bn_w is not None else None
+        dbb = torch.empty((C,), dtype=torch.float32, device=x2d.device) if ctx.needs_input_grad[5] else None
+        ws = _ws(lib.ogv_head_bn_pool_ws_bytes(B, C), x2d.device)
+        with _census("bn_act_bwd", dict(M=B * HW, C=C, elem=x2d.element_size(), head=True, hw=HW)):
+            check(lib.ogv_head_bn_pool_bwd(_ptr(dpooled), _ptr(x2d), _ptr(raw), _ptr(saved), _ptr(dx), _ptr(dg),
+                                           _ptr(dbb), _ptr(ws), _ptr(bn_w), B, HW, C, train, _dt(x2d), _stream()),
+                  "ogv_head_bn_pool_bwd")
+        return dx, None, None, None, dg, dbb
+
+
+def head_bn_pool(x, bn):
+    """BatchNorm2d(x).mean((2, 3)) in fp32 [B, C] (nn.BatchNorm2d semantics incl. the running-stat update),
+    computed as BN of the per-image channel means (BN is per-channel affine): one pass over x each way."""
+    require_device(x, what="ogv.head_bn_pool")
+    has_bn, train, eps, mom, rm, rv = _bn_args(bn)
+    B, C, H, W = x.shape
+    x2d = _rows_contig(nchw_to_rows(x.to(compute_dtype(x))))
+    y = _HeadBNPool.apply(x2d, (int(B), int(H * W), train, eps, mom), rm, rv,
+                          f32(bn.weight) if bn.affine else None, f32(bn.bias) if bn.affine else None)
+    if train and not getattr(bn, "_ogv_nbt_pooled", False):
+        bn.num_batches_tracked.add_(1)
+    return y
 
 
 def batchnorm_act_nchw(x, bn, act=None):

@@ -47,23 +47,41 @@ class MaxOutNet(nn.Module):
                 x = blk(x)
             if si < len(self.downs):
                 x = self.downs[si](x)
-        return classifier_head(self.head_norm(x), self.classifier)
+        return classifier_head(x, self.classifier, self.head_norm)
 
 
-def classifier_head(x, classifier: nn.Linear):
-    """GAP -> Linear (Model_A_OutGridNet.py:65-67) in fp32 even under bf16 autocast: the pooled
+def classifier_head(x, classifier: nn.Linear, norm=None):
+    """head_norm -> GAP -> Linear (Model_A_OutGridNet.py:64-67) in fp32 even under bf16 autocast: the pooled
     features are averaged in fp32 and the classifier keeps its fp32 weights, so the logits carry no
-    bf16 rounding of their own.  The Linear runs on the native fp32 GEMM (ogv_gemm_fwd: the
-    thread-group kernel for [B, K] outputs, its dgrad / weight gradient on the exact-f32 MFMA kernels)
-    -- the module itself is called instead whenever the call must be observable or is not a plain
-    Linear on the GPU: a subclass or wrapper (its own forward), module or global forward (pre-)hooks,
-    or CPU features (the native kernels take device pointers only)."""
-    pooled = x.mean(dim=(2, 3), dtype=torch.float32)
+    bf16 rounding of their own.  A plain ogv BatchNorm2d `norm` (no hooks) and the pool run as ONE op,
+    BN of the per-image channel means (BN is per-channel affine, so the two commute: ogv_head_bn_pool_*,
+    one pass over x forward and backward); otherwise norm(x) runs as its own module first.  The Linear
+    runs on the native fp32 GEMM (ogv_gemm_fwd: the thread-group kernel for [B, K] outputs, its dgrad /
+    weight gradient on the exact-f32 MFMA kernels) -- the module itself is called instead whenever the
+    call must be observable or is not a plain Linear on the GPU: a subclass or wrapper (its own forward),
+    module or global forward (pre-)hooks, or CPU features (the native kernels take device pointers only)."""
+    if norm is not None and _fused_head_norm_ok(norm, x):
+        from ogv import functional as OF
+        pooled = OF.head_bn_pool(x, norm)
+    else:
+        if norm is not None:
+            x = norm(x)
+        pooled = x.mean(dim=(2, 3), dtype=torch.float32)
     if not _native_classifier_ok(classifier, pooled):
         with torch.autocast(pooled.device.type, enabled=False):
             return classifier(pooled)
     from ogv import functional as OF
     return OF.linear_rows(pooled, classifier.weight, classifier.bias)
+
+
+def _fused_head_norm_ok(norm, x) -> bool:
+    """The head BatchNorm may fold into the pool: exactly the ogv BatchNorm2d (its forward is the native
+    kernel anyway), on the GPU, with no module or global forward hooks (its output would have to exist)."""
+    from torch.nn.modules import module as _m
+    from ogv.layers import BatchNorm2d
+    return (type(norm) is BatchNorm2d and x.is_cuda and x.dim() == 4 and norm.track_running_stats
+            and not (norm._forward_hooks or norm._forward_pre_hooks
+                     or _m._global_forward_hooks or _m._global_forward_pre_hooks))
 
 
 def _native_classifier_ok(classifier, pooled) -> bool:

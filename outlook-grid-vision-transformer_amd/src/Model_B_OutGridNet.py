@@ -58,4 +58,4 @@ class OutlookerFrontGridNet(nn.Module):
                 x = blk(x)
             if si < len(self.downs):
                 x = self.downs[si](x)
-        return classifier_head(self.head_norm(x), self.classifier)
+        return classifier_head(x, self.classifier, self.head_norm)

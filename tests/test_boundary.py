@@ -186,6 +186,33 @@ def test_classifier_head_native_path_only_for_plain_gpu_linear():
     assert _native_classifier_ok(lin, fake_cuda)
 
 
+def test_head_norm_folds_into_pool_only_when_unobservable():
+    """The head BatchNorm2d + pool run as one native op (BN of the per-image means) only for the ogv
+    BatchNorm2d itself on the GPU with no hooks; on CPU features the module runs and the result is the
+    reference's head_norm -> mean -> classifier."""
+    from torch import nn
+    from ogv.layers import BatchNorm2d
+    from src.Model_A_OutGridNet import _fused_head_norm_ok, classifier_head
+    bn, lin = BatchNorm2d(8).eval(), nn.Linear(8, 5)
+    x = torch.randn(3, 8, 2, 2)
+    fake = type("T", (), {"is_cuda": True, "dim": lambda self: 4})()
+    assert _fused_head_norm_ok(bn, fake)
+    assert not _fused_head_norm_ok(bn, x)                                 # CPU tensor
+    assert not _fused_head_norm_ok(nn.BatchNorm2d(8), fake)               # stock module: its own forward
+    h = bn.register_forward_hook(lambda m, i, o: None)
+    assert not _fused_head_norm_ok(bn, fake)
+    h.remove()
+    h = torch.nn.modules.module.register_module_forward_pre_hook(lambda m, i: None)
+    try:
+        assert not _fused_head_norm_ok(bn, fake)
+    finally:
+        h.remove()
+    ref = nn.BatchNorm2d(8).eval()
+    ref.load_state_dict(bn.state_dict())
+    with torch.no_grad():
+        torch.testing.assert_close(classifier_head(x, lin, ref), lin(ref(x).mean(dim=(2, 3))))
+
+
 def test_gemm_routing_table():
     """Host-side planner (no GPU): which kernel a bf16 projection runs on (ogv_gemm_stream_route:
     1 streaming, 2 panel, 0 LDS-tiled), on the Model-A-7M shapes and the edges of each route."""

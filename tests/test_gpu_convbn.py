@@ -198,6 +198,70 @@ def test_head_batchnorm(dtype, train):
         assert e <= tol * scale, f"{name}: {e:.3e} / {scale:.3e}"
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("train", [True, False])
+@pytest.mark.parametrize("shape", [(512, 384, 4, 4), (16, 256, 4, 4), (8, 96, 7, 7), (3, 20, 5, 3), (5, 12, 1, 1)])
+def test_head_bn_pool_matches_bn_then_mean(shape, dtype, train):
+    """The classifier head's BatchNorm2d -> mean((2, 3)) as ONE op (ogv_head_bn_pool_*: BN of the per-image
+    channel means) against the reference's order -- nn.BatchNorm2d then the mean -- in fp64 on the same (bf16-
+    rounded) input: pooled features, running statistics, input and BN-affine gradients.  The op reads x in its
+    storage type and computes in fp32 / fp64, so the bf16 bars are the fp32 ones except for dx (stored bf16)."""
+    from ogv import functional as OF
+    from ogv.layers import BatchNorm2d
+    B, C, H, W = shape
+    torch.manual_seed(B + C + H)
+    ref = nn.BatchNorm2d(C)
+    with torch.no_grad():
+        ref.weight.uniform_(0.5, 1.5)
+        ref.bias.uniform_(-0.3, 0.3)
+        ref.running_mean.uniform_(-0.2, 0.2)
+        ref.running_var.uniform_(0.5, 1.5)
+    mod = BatchNorm2d(C)
+    mod.load_state_dict(ref.state_dict())
+    ref = ref.double().train(train)
+    mod = mod.cuda().train(train)
+    x = (1.5 * torch.randn(B, C, H, W) + 0.7).to(dtype)      # a mean far from the running mean: shifted sums
+    xr = x.double().requires_grad_(True)
+    pr = ref(xr).mean(dim=(2, 3))
+    g = torch.randn(B, C)
+    pr.backward(g.double())
+    xd = x.cuda().contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    pd = OF.head_bn_pool(xd, mod)
+    assert pd.dtype == torch.float32 and pd.shape == (B, C)
+    pd.backward(g.cuda())
+    assert int(mod.num_batches_tracked) == int(ref.num_batches_tracked)
+    for name, got, want, tol in [("pooled", pd, pr, 1e-5), ("rm", mod.running_mean, ref.running_mean, 1e-6),
+                                 ("rv", mod.running_var, ref.running_var, 1e-6),
+                                 ("dgamma", mod.weight.grad, ref.weight.grad, 1e-5),
+                                 ("dbeta", mod.bias.grad, ref.bias.grad, 1e-5),
+                                 ("dx", xd.grad, xr.grad, 1e-5 if dtype == torch.float32 else 1e-2)]:
+        e, scale = _err(got, want)
+        assert e <= tol * scale, f"{name}: {e:.3e} / {scale:.3e}"
+
+
+def test_model_head_uses_fused_bn_pool_unless_hooked():
+    """MaxOutNet's head: head_norm + pool as ogv_head_bn_pool (the module's own forward never runs), the
+    same logits as BatchNorm2d -> mean -> Linear; with a forward hook on head_norm the module runs (its
+    output observable) and the logits agree."""
+    from ogv.layers import BatchNorm2d
+    from src.Model_A_OutGridNet import classifier_head
+    torch.manual_seed(3)
+    bn, lin = BatchNorm2d(64).cuda(), nn.Linear(64, 10).cuda()
+    x = torch.randn(6, 64, 4, 4, device="cuda").contiguous(memory_format=torch.channels_last)
+    calls = []
+    y_fused = classifier_head(x, lin, bn)
+    assert not calls
+    bn2 = copy.deepcopy(bn)
+    bn2.load_state_dict({**bn.state_dict(), "running_mean": torch.zeros(64), "running_var": torch.ones(64),
+                         "num_batches_tracked": torch.tensor(0)})
+    h = bn2.register_forward_hook(lambda m, i, o: calls.append(o.shape))
+    y_hooked = classifier_head(x, lin, bn2)
+    h.remove()
+    assert calls == [(6, 64, 4, 4)]
+    torch.testing.assert_close(y_fused, y_hooked, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(bn.running_mean, bn2.running_mean, rtol=1e-6, atol=1e-6)
+
+
 def test_convbn_full_size_stem_stats():
     """bs=512 stem (M = 524288 rows): BN batch statistics of the native path equal the
     mean/var of its own conv output recomputed by torch in fp64 (size-independent property)."""

@@ -19,13 +19,14 @@ python3 tools/probe_vs_trace.py "$OUT/prof/bench_kernel_trace.csv" "$OUT/prof.lo
 cat "$OUT/probe_vs_trace.txt"
 gzip -f "$OUT/prof/bench_kernel_trace.csv"
 if [ "${PMC:-1}" = 1 ]; then
-  cp profiles/pmc_traffic.json "$OUT/pmc_traffic.json" 2>/dev/null || true
+  # FRESH=1: start from an empty table (entries of kernels the step no longer launches are dropped)
+  if [ "${FRESH:-0}" = 1 ]; then echo '{}' > "$OUT/pmc_traffic.json"; else cp profiles/pmc_traffic.json "$OUT/pmc_traffic.json" 2>/dev/null || true; fi
   for PR in ${PMC_PROBES:-gemm_panel outlook_bwd sgemm}; do
     ARGS="--eager --steps 2 --warmup 1 --no-cpu-baseline --no-parity --step-roofline 0 --probe $PR $BA"
     timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch_$PR" -o run -- python3 bench.py $ARGS > "$OUT/fetch_$PR.log" 2>&1 || { echo "pmc fetch rc=$?"; exit 1; }
     timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write_$PR" -o run -- python3 bench.py $ARGS > "$OUT/write_$PR.log" 2>&1 || { echo "pmc write rc=$?"; exit 1; }
     python3 tools/pmc_traffic.py "$OUT/fetch_$PR" "$OUT/write_$PR" --probe "$PR" --out "$OUT/pmc_traffic.json" \
-      ${KEYPFX:+--key "$KEYPFX:$PR"}
+      ${KEYPFX:+--key "$KEYPFX:$PR"} ${TAG:+--tag "$TAG"}
     find "$OUT/fetch_$PR" "$OUT/write_$PR" -name "*counter_collection.csv" -exec gzip -f {} \;
     find "$OUT/fetch_$PR" "$OUT/write_$PR" -type f ! -name "*.gz" -delete
   done

@@ -62,6 +62,7 @@ def main():
                     "'<model>/bs<B>:<probe>' for workloads other than Model-A-7M bs=512)")
     ap.add_argument("--skip-steps", type=int, default=1, help="leading launches per probe treated as warmup: "
                     "steps to drop (the probe keeps the last step's launches)")
+    ap.add_argument("--tag", default="", help="measurement tag stored in the entry (e.g. the round and box run)")
     a = ap.parse_args()
     fetch = read_counter(a.fetch_dir, "FETCH_SIZE")
     write = read_counter(a.write_dir, "WRITE_SIZE")
@@ -89,6 +90,8 @@ def main():
                       "fetch_bytes_per_launch": sum(fb) / n, "write_bytes_per_launch": sum(wb) / n,
                       "hbm_bytes_per_launch": (sum(fb) + sum(wb)) / n,
                       "correction": "FETCH_SIZE(KB)*1024*2 (gfx950 half-count of wide reads) + WRITE_SIZE(KB)*1024"}
+        if a.tag:
+            out[key]["measured"] = a.tag
         print(key, json.dumps(out[key]))
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     with open(a.out, "w") as fo:

@@ -523,29 +523,47 @@ extern "C" int ogv_bn_act_bwd(const void* dout, const void* x, const float* save
 namespace ogv {
 
 // ------------------------------------------------------------------ head: BatchNorm2d + global average pool
-// Block = (one image, 4 channel chunks of V) x 64 row slots: fp64 sums of (x - shift), (x - shift)^2 (the
-// BatchNorm partial row of this image, the layout bn_reduce_finalize reads: [b][0..C) and [b][C..2C)) and of x
-// itself ([b][2C..3C): the pool).  One read of x.
+// Block = 4 channel chunks of V x 64 images: each thread walks its image's HW rows for its chunk (the image's
+// channel sums stay in the thread: pooled_raw = sum / HW is written directly), and the fp64 shifted BatchNorm
+// sums of the block's 64 images are reduced into one partial row ([blk][0..C) and [blk][C..2C), the layout
+// bn_reduce_finalize reads).  One read of x; ceil(B / 64) partial rows.
+constexpr int HP_IMG = 64;
 template <typename T, int V>
 __global__ __launch_bounds__(256) void head_pool_stats_kernel(const T* __restrict__ x, const float* __restrict__ shift,
-                                                              double* __restrict__ stat, int B, int HW, int C) {
-  __shared__ double lds[3 * 4 * 4 * 8];
+                                                              double* __restrict__ stat, float* __restrict__ raw, int B,
+                                                              int HW, int C) {
+  __shared__ double lds[2 * 4 * 4 * 8];
   const int gx = (C + 4 * V - 1) / (4 * V);
-  long lid;
-  if (!xcd_block((long)gx * B, lid)) return;
-  const int bx = (int)(lid % gx), b = (int)(lid / gx);
-  const int chunk = threadIdx.x & 3, slot = threadIdx.x >> 2;
+  const int bx = (int)(blockIdx.x % gx), by = (int)(blockIdx.x / gx);
+  const int chunk = threadIdx.x & 3, im = threadIdx.x >> 2;
   const int c0 = (bx * 4 + chunk) * V;
-  double q[3][V];
+  const int b = by * HP_IMG + im;
+  double q[2][V];
 #pragma unroll
-  for (int i = 0; i < V; ++i) { q[0][i] = 0.0; q[1][i] = 0.0; q[2][i] = 0.0; }
-  if (c0 < C) {
+  for (int i = 0; i < V; ++i) { q[0][i] = 0.0; q[1][i] = 0.0; }
+  if (c0 < C && b < B) {
     float sf[V];
     load_vec<float, V>(shift + c0, sf);
+    double sx[V];
 #pragma unroll
-    for (int i = 0; i < V; ++i) sf[i] = bn_shift(sf[i]);
+    for (int i = 0; i < V; ++i) { sf[i] = bn_shift(sf[i]); sx[i] = 0.0; }
     const T* xb = x + (long)b * HW * C + c0;
-    for (int r = slot; r < HW; r += 64) {
+    int r = 0;
+    for (; r + 4 <= HW; r += 4) {
+      float v[4][V];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) load_vec<T, V>(xb + (long)(r + u) * C, v[u]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+          const double d = (double)v[u][i] - (double)sf[i];
+          q[0][i] += d;
+          q[1][i] = fma(d, d, q[1][i]);
+          sx[i] += (double)v[u][i];
+        }
+    }
+    for (; r < HW; ++r) {
       float v[V];
       load_vec<T, V>(xb + (long)r * C, v);
 #pragma unroll
@@ -553,23 +571,24 @@ __global__ __launch_bounds__(256) void head_pool_stats_kernel(const T* __restric
         const double d = (double)v[i] - (double)sf[i];
         q[0][i] += d;
         q[1][i] = fma(d, d, q[1][i]);
-        q[2][i] += (double)v[i];
+        sx[i] += (double)v[i];
       }
     }
+    float m[V];
+#pragma unroll
+    for (int i = 0; i < V; ++i) m[i] = (float)(sx[i] / (double)HW);
+    store_vec<float, V>(raw + (long)b * C + c0, m);
   }
-  chunk_reduce_store<3, V, double>(q, lds, stat + (long)b * 3 * C, C, C, bx * 4 * V);
+  chunk_reduce_store<2, V, double>(q, lds, stat + (long)by * 2 * C, C, C, bx * 4 * V);
 }
 
-// pooled_raw = sum x / HW, pooled = pooled_raw * sc + sh   ([B, C], thread per element)
-__global__ void head_pool_apply_kernel(const double* __restrict__ stat, const float* __restrict__ sc,
-                                       const float* __restrict__ sh, float* __restrict__ raw, float* __restrict__ pooled,
-                                       int B, int HW, int C) {
+// pooled = pooled_raw * sc + sh   ([B, C], thread per element)
+__global__ void head_pool_apply_kernel(const float* __restrict__ raw, const float* __restrict__ sc,
+                                       const float* __restrict__ sh, float* __restrict__ pooled, int B, int C) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (long)B * C) return;
-  const int b = (int)(i / C), c = (int)(i - (long)b * C);
-  const float m = (float)(stat[(long)b * 3 * C + 2 * C + c] / (double)HW);
-  raw[i] = m;
-  pooled[i] = fmaf(m, sc[c], sh[c]);
+  const int c = (int)(i % C);
+  pooled[i] = fmaf(raw[i], sc[c], sh[c]);
 }
 
 // backward partial rows, one per image: [g, g * xhat_b] with xhat_b = (pooled_raw - mean) * invstd -- the
@@ -612,8 +631,9 @@ __global__ __launch_bounds__(256) void head_pool_dx_kernel(const float* __restri
 }
 
 template <typename T, int V>
-static void head_stats_run(const void* x, const float* shift, double* stat, int B, int HW, int C, hipStream_t s) {
-  head_pool_stats_kernel<T, V><<<xcd_grid((long)cdiv(C, 4 * V) * B), 256, 0, s>>>((const T*)x, shift, stat, B, HW, C);
+static void head_stats_run(const void* x, const float* shift, double* stat, float* raw, int B, int HW, int C,
+                           hipStream_t s) {
+  head_pool_stats_kernel<T, V><<<cdiv(C, 4 * V) * cdiv(B, HP_IMG), 256, 0, s>>>((const T*)x, shift, stat, raw, B, HW, C);
 }
 template <typename T, int V>
 static void head_dx_run(const float* g, const void* x, const float* mean, const float* invstd, const float* coef, void* dx,
@@ -633,10 +653,10 @@ using namespace ogv;
 
 extern "C" size_t ogv_head_bn_pool_ws_bytes(int B, int C) {
   if (B <= 0 || C <= 0) return 0;
-  Carve c(nullptr);   // forward: fp64 [B][3C] + finalize scratch; backward: fp32 [B][2C] + coef [3C] (smaller)
-  c.take<double>((size_t)B * 3 * C);
-  c.take<double>(2 * (size_t)C);
-  c.take<float>(3 * (size_t)C);
+  Carve c(nullptr);   // forward: fp64 [ceil(B / 64)][2C] + finalize scratch; backward: fp32 [B][2C] + coef [3C]
+  const size_t fwd = (size_t)cdiv(B, HP_IMG) * 2 * C * sizeof(double) + 2 * (size_t)C * sizeof(double);
+  const size_t bwd = ((size_t)B * 2 * C + 3 * (size_t)C) * sizeof(float);
+  c.take<char>((fwd > bwd ? fwd : bwd) + 256);
   return c.off;
 }
 
@@ -650,16 +670,17 @@ extern "C" int ogv_head_bn_pool_fwd(const void* x, float* pooled_raw, float* poo
   Carve cs(saved);
   const BnSaved b = take_bn_saved(cs, C);
   Carve cw(ws);
-  double* stat = cw.take<double>((size_t)B * 3 * C);
+  const int R = cdiv(B, HP_IMG);
+  double* stat = cw.take<double>((size_t)R * 2 * C);
   double* sums = cw.take<double>(2 * (size_t)C);
   const int V = vec_width(C);
-  OGV_CB_DISPATCH(dt, V, head_stats_run, x, rm, stat, B, HW, C, s);
+  OGV_CB_DISPATCH(dt, V, head_stats_run, x, rm, stat, pooled_raw, B, HW, C, s);
   if (train)
-    bn_reduce_finalize_launch(stat, B, 3L * C, C, (double)B * HW, bn_w, bn_b, eps, momentum, rm, rv, b.mean, b.invstd,
+    bn_reduce_finalize_launch(stat, R, 2L * C, C, (double)B * HW, bn_w, bn_b, eps, momentum, rm, rv, b.mean, b.invstd,
                               b.sc, b.sh, s);
   else
     bn_finalize_launch(sums, C, (double)B * HW, bn_w, bn_b, eps, momentum, rm, rv, b.mean, b.invstd, b.sc, b.sh, 0, s);
-  head_pool_apply_kernel<<<cdiv((long)B * C, 256), 256, 0, s>>>(stat, b.sc, b.sh, pooled_raw, pooled, B, HW, C);
+  head_pool_apply_kernel<<<cdiv((long)B * C, 256), 256, 0, s>>>(pooled_raw, b.sc, b.sh, pooled, B, C);
   return check_launch("ogv_head_bn_pool_fwd");
 }
 

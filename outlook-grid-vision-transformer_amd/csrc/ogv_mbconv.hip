@@ -453,12 +453,17 @@ __device__ __forceinline__ void dw_reduce_store(A (&q)[NQ][V], float* lds_raw, i
 }
 
 // The shared row walk over the block's virtual rows: ring <- rows -1, 0; regs <- rows 1..R; per
-// step: store regs (rows u+1..u+R), pre(u, px) issues the body's own per-pixel loads for output rows
-// u..u+R-1, then the prefetch of rows u+R+1..u+2R is issued (always: past the end it re-reads a
-// clamped row), then the output rows among u..u+R-1 (not seam rows) are computed through
-// body(r, u+r, image, y, px), one item (pixel, V channels) per thread and row.  Issue order = retire
-// order, so the body waits for its own loads only while the prefetch stays in flight.
-template <typename T, int V, int LDQ, bool TWO, int R, typename Stage, typename Pre, typename Body>
+// step: store regs (rows u+1..u+R), issue the prefetch of rows u+R+1..u+2R (always: past the end it
+// re-reads a clamped row), then pre(u+R, px, slot') issues the body's own per-pixel loads for the NEXT
+// step's output rows into the other buffer, then the output rows among u..u+R-1 (not seam rows) are
+// computed through body(r, u+r, image, y, px, slot), one item (pixel, V channels) per thread and row, from
+// the per-pixel data loaded one step earlier.  Issue order = retire order, so nothing the bodies read is
+// behind the prefetch in flight.
+template <int S>
+struct DwSlot {
+  static constexpr int v = S;
+};
+template <typename T, int V, int LDQ, bool TWO, int R, bool PRE = true, typename Stage, typename Pre, typename Body>
 __device__ __forceinline__ void dw_walk(float* ring, const T* __restrict__ src, const T* __restrict__ src2,
                                         const DwTile& t, const TileIdx& ti, int cc, int chunk, bool cok,
                                         Stage&& stage, Pre&& pre, Body&& body) {
@@ -471,18 +476,36 @@ __device__ __forceinline__ void dw_walk(float* ring, const T* __restrict__ src, 
   const bool item = cok && (int)threadIdx.x < nitems;
   const int px = min((int)threadIdx.x, nitems - 1) / t.chunks;
   const int nv = ti.nimg * (t.H + 1) - 1;  // virtual rows incl. the seams between images
-  for (p = vnext(t, p); p.u < nv; p = vadv<R>(t, p)) {
+  p = vnext(t, p);
+  pre(p, px, DwSlot<0>());   // the first step's per-pixel loads
+  // steps alternate between the two per-pixel buffers (unrolled in pairs: no register copy, so nothing
+  // waits for the stores of a step before the next one starts)
+  auto step = [&](auto slot) {
+    constexpr int S = decltype(slot)::v;
     rp.store(ring, t, ti, vnext(t, p), R, chunk, cok, stage);
     __syncthreads();
-    pre(p, px);
     rp.template load<R>(src, src2, t, ti, vadv<R + 1>(t, p), cc);
+    // the body's own per-pixel loads run one step ahead as well, issued right behind the prefetch: loads
+    // retire in issue order, and loaded in the same step (the compiler sank them below the prefetch) the
+    // first body waited for the whole prefetch (vmcnt(0)), exposing the next rows' latency every step
+    pre(vadv<R>(t, p), px, DwSlot<1 - S>());
     if (item) {
       VRow q = p;
 #pragma unroll
       for (int r = 0; r < R; ++r, q = vnext(t, q))
-        if (q.u < nv && q.y < t.H) body(r, q.u, ti.b0 + q.im, q.y, px);
+        if (q.u < nv && q.y < t.H) body(r, q.u, ti.b0 + q.im, q.y, px, DwSlot<S>());
     }
     __syncthreads();
+    p = vadv<R>(t, p);
+  };
+  if constexpr (PRE) {
+    while (p.u < nv) {
+      step(DwSlot<0>());
+      if (p.u >= nv) break;
+      step(DwSlot<1>());
+    }
+  } else {   // no per-pixel loads: one buffer, no unrolled pair (fewer registers)
+    while (p.u < nv) step(DwSlot<0>());
   }
 }
 // pre-load helper: V elements of src at this thread's pixel of virtual row u (clamped into the tensor)
@@ -524,8 +547,8 @@ __global__ __launch_bounds__(256) void dw_fwd_tile_kernel(const T* __restrict__ 
 #pragma unroll
     for (int k = 0; k < V; ++k) v[k] = act_fwd(ACT, fmaf(v[k], s[k], h[k]));
   };
-  dw_walk<T, V, LDQ, false, R>(ring, e, e, t, ti, cc, chunk, cok, stage, [&](VRow, int) {},
-                           [&](int, int u, long b, int y, int px) {
+  dw_walk<T, V, LDQ, false, R, false>(ring, e, e, t, ti, cc, chunk, cok, stage, [&](VRow, int, auto) {},
+                           [&](int, int u, long b, int y, int px, auto) {
     float acc[V];
 #pragma unroll
     for (int i = 0; i < V; ++i) acc[i] = 0.f;
@@ -628,10 +651,10 @@ __global__ __launch_bounds__(256) void dw_dgrad_tile_kernel(const T* __restrict_
 #pragma unroll
     for (int i = 0; i < V; ++i) q9[k][i] = 0.f;
   const int cc = cok ? c : 0;
-  RawVec<T, V> ce[R];  // e at this thread's output pixel of the current rows
-  auto pre = [&](VRow q, int px) {
+  RawVec<T, V> ce[2][R];  // e at this thread's output pixel of a step's rows (two steps in flight)
+  auto pre = [&](VRow q, int px, auto slot) {
 #pragma unroll
-    for (int r = 0; r < R; ++r, q = vnext(t, q)) dw_pixel_load(ce[r], e, t, ti, q, px, cc);
+    for (int r = 0; r < R; ++r, q = vnext(t, q)) dw_pixel_load(ce[decltype(slot)::v][r], e, t, ti, q, px, cc);
   };
   auto stage = [&](float (&v)[V], const float (&dv)[V], int im) {
     if constexpr (BN2) {
@@ -653,10 +676,11 @@ __global__ __launch_bounds__(256) void dw_dgrad_tile_kernel(const T* __restrict_
       }
     }
   };
-  dw_walk<T, V, LDQ, BN2, R>(ring, dd, b2.d, t, ti, cc, chunk, cok, stage, pre, [&](int r, int u, long b, int y, int px) {
+  dw_walk<T, V, LDQ, BN2, R>(ring, dd, b2.d, t, ti, cc, chunk, cok, stage, pre, [&](int r, int u, long b, int y, int px,
+                                                                                   auto slot) {
     const long off = ((b * t.H + y) * t.W + ti.x0 + px) * t.C + c;
     float ev[V];
-    ce[r].unpack(ev);
+    ce[decltype(slot)::v][r].unpack(ev);
     // act(BN1(e)) for the weight gradient and act'(BN1(e)) for the output from one transcendental pair
     float acc[V], av[V], ag[V];
 #pragma unroll
@@ -722,18 +746,19 @@ __global__ __launch_bounds__(256) void dw_wgrad_tile_kernel(const T* __restrict_
 #pragma unroll
     for (int i = 0; i < V; ++i) q[k][i] = 0.f;
   const int cc = cok ? c : 0;
-  RawVec<T, V> cg[DW_R];  // dd at this thread's output pixel of the current rows
-  auto pre = [&](VRow q, int px) {
+  RawVec<T, V> cg[2][DW_R];  // dd at this thread's output pixel of a step's rows (two steps in flight)
+  auto pre = [&](VRow q, int px, auto slot) {
 #pragma unroll
-    for (int r = 0; r < DW_R; ++r, q = vnext(t, q)) dw_pixel_load(cg[r], dd, t, ti, q, px, cc);
+    for (int r = 0; r < DW_R; ++r, q = vnext(t, q)) dw_pixel_load(cg[decltype(slot)::v][r], dd, t, ti, q, px, cc);
   };
   auto stage = [&](float (&v)[V], const float (&)[V], int) {
 #pragma unroll
     for (int k = 0; k < V; ++k) v[k] = act_fwd(ACT, fmaf(v[k], s[k], h[k]));
   };
-  dw_walk<T, V, LDQ, false, DW_R>(ring, e, e, t, ti, cc, chunk, cok, stage, pre, [&](int r, int u, long, int, int px) {
+  dw_walk<T, V, LDQ, false, DW_R>(ring, e, e, t, ti, cc, chunk, cok, stage, pre, [&](int r, int u, long, int, int px,
+                                                                                   auto slot) {
     float g[V];
-    cg[r].unpack(g);
+    cg[decltype(slot)::v][r].unpack(g);
 #pragma unroll
     for (int ki = 0; ki < 3; ++ki)
 #pragma unroll

@@ -1383,7 +1383,9 @@ void set_dw_fuse(int v) { g_dw_fuse = v; }
 // written to HBM: one [M, mid] write + read and the bn2_apply launch saved); needs dw_fuse
 static int g_dw_bn2 = 1;
 void set_dw_bn2(int v) { g_dw_bn2 = v; }
-static int g_dw_bwd_r = 4;
+// (default 2 since the per-pixel loads run a step ahead: 7M 14.42 / 14.38 ms with 4 rows per step, 14.35 / 14.35
+// with 2, profiles/r06t_knobs.log; fewer live registers, 228 vs 252 VGPRs)
+static int g_dw_bwd_r = 2;
 void set_dw_bwd_r(int v) { g_dw_bwd_r = v == 2 ? 2 : 4; }
 // dynamic LDS of dw_dgrad_tile_kernel: the staged tile (+ the 9-tap partials with part) and, BN2-staged
 // (b2), the per-image gate / dpool table

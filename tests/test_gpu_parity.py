@@ -979,6 +979,35 @@ def test_mbconv_bn2_staged_matches_materialised(C, H, B, dtype):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("C,H,B", [(48, 32, 4), (96, 16, 3), (192, 8, 2), (20, 6, 2), (64, 2, 9)])
+def test_mbconv_dw_bwd_rows_per_step_bitwise(C, H, B):
+    """The BN2-staged depthwise backward with 2 (default) or 4 output rows per pipeline step: every thread
+    accumulates its rows in the same order either way, so every gradient is bit-identical."""
+    from ogv._lib import load
+    from src.model.mbc_conv import MBConv, MBConvConfig
+    lib = load()
+    torch.manual_seed(C + 2 * H + B)
+    m = MBConv(C, C, 1, MBConvConfig()).to(DEV)
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    x = torch.randn(B, C, H, H, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    dy = torch.randn_like(x)
+    res = []
+    try:
+        for r in (4, 2):
+            assert lib.ogv_set_option(b"dw_bwd_r", r) == 0
+            m.load_state_dict(sd)
+            m.zero_grad(set_to_none=True)
+            xx = x.clone().requires_grad_()
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                y = m.train()(xx)
+            y.backward(dy)
+            res.append([xx.grad.clone()] + [p.grad.clone() for p in m.parameters()])
+    finally:
+        assert lib.ogv_set_option(b"dw_bwd_r", 2) == 0
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+
+
 def test_outgrid_block_with_dropouts():
     """proj_drop / ffn_drop > 0 (no reference config uses them; the modules then take torch Dropout on
     the HIP kernels' outputs with an explicit residual add): training forward + backward finite and

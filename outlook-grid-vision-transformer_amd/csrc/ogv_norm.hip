@@ -21,10 +21,13 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, co
   for (int v = 0; v < NV; ++v) {
     const int c = (v * G + lane_g) * VEC;
     valid[v] = c < C;
+    // unconditional loads at a clamped column (a lane without a column stores nothing): a per-lane guard
+    // put each of these loads in a branch of its own and the rows' loads waited behind all of them
+    const int cc = valid[v] ? c : 0;
 #pragma unroll
     for (int i = 0; i < VEC; ++i) {
-      gw[v * VEC + i] = valid[v] && gamma ? gamma[c + i] : 1.f;
-      bw[v * VEC + i] = valid[v] && beta ? beta[c + i] : 0.f;
+      gw[v * VEC + i] = gamma ? gamma[cc + i] : 1.f;
+      bw[v * VEC + i] = beta ? beta[cc + i] : 0.f;
     }
   }
   const float invC = 1.f / (float)C;
@@ -32,12 +35,20 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, co
   const long stride = (long)gridDim.x * rows_per_block;
   for (long row0 = blockIdx.x * rows_per_block + threadIdx.x / G; row0 < M; row0 += RPI * stride) {
     float xv[RPI][E];
+    // raw bits of every row first, converted once all are in flight (converting next to each load let the
+    // scheduler put the next row's load behind the first row's wait: one round trip per row)
+    RawVec<T, VEC> rx[RPI][NV];
 #pragma unroll
     for (int q = 0; q < RPI; ++q) {
       const long row = min(row0 + q * stride, M - 1);
 #pragma unroll
-      for (int v = 0; v < NV; ++v) load_vec<T, VEC>(x + row * C + min((v * G + lane_g) * VEC, C - VEC), xv[q] + v * VEC);
+      for (int v = 0; v < NV; ++v) rx[q][v].load(x + row * C + min((v * G + lane_g) * VEC, C - VEC));
     }
+    __builtin_amdgcn_sched_barrier(0);   // (the machine scheduler would otherwise still interleave them)
+#pragma unroll
+    for (int q = 0; q < RPI; ++q)
+#pragma unroll
+      for (int v = 0; v < NV; ++v) rx[q][v].unpack(xv[q] + v * VEC);
 #pragma unroll
     for (int q = 0; q < RPI; ++q) {
       const long row = row0 + q * stride;
@@ -92,9 +103,10 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
   for (int v = 0; v < NV; ++v) {
     const int c = (v * G + lane_g) * VEC;
     valid[v] = c < C;
+    const int cc = valid[v] ? c : 0;   // (clamped, unconditional: as in the forward; d = 0 on such lanes)
 #pragma unroll
     for (int i = 0; i < VEC; ++i) {
-      gw[v * VEC + i] = valid[v] && gamma ? gamma[c + i] : 1.f;
+      gw[v * VEC + i] = gamma ? gamma[cc + i] : 1.f;
       dgam[v * VEC + i] = 0.f;
       dbet[v * VEC + i] = 0.f;
     }

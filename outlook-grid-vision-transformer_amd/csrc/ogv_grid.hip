@@ -206,11 +206,13 @@ __global__ __launch_bounds__(256) void grid_bwd_delta_kernel(const T* __restrict
   delta[tid] = s;
 }
 
-// dQ_i = scale * sum_j P_ij (dP_ij - delta_i) K_j        (thread per (query, head))
+// dQ_i = scale * sum_j P_ij (dP_ij - delta_i) K_j        (thread per (query, head)).
+// delta_i = <dO_i, O_i> is formed here from the query's own rows (grid_bwd_delta_kernel's arithmetic, same
+// order) and written for the dK / dV kernel that follows: no separate delta launch
 template <typename T, int HDMAX, int V>
 __global__ __launch_bounds__(256) void grid_bwd_dq_kernel(const T* __restrict__ dout, const T* __restrict__ qkv,
-                                                          const float* __restrict__ lse,
-                                                          const float* __restrict__ delta, T* __restrict__ dqkv,
+                                                          const T* __restrict__ out, const float* __restrict__ lse,
+                                                          float* __restrict__ delta, T* __restrict__ dqkv,
                                                           GridGeom G, float scale) {
   const long total = (long)G.B * G.g * G.g * G.N * G.heads;
   const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -223,21 +225,29 @@ __global__ __launch_bounds__(256) void grid_bwd_dq_kernel(const T* __restrict__ 
   const long C3 = 3L * G.C;
   const long pq = G.pixel(grp, t);
 
-  float q[HDMAX], go[HDMAX], dq[HDMAX];
+  float q[HDMAX], go[HDMAX], dq[HDMAX], ov[HDMAX];
 #pragma unroll
   for (int d0 = 0; d0 < HDMAX; d0 += V) {
     if (d0 < hd) {
       load_vec<T, V>(qkv + pq * C3 + h * hd + d0, q + d0);
       load_vec<T, V>(dout + pq * G.C + h * hd + d0, go + d0);
+      load_vec<T, V>(out + pq * G.C + h * hd + d0, ov + d0);
     } else {
 #pragma unroll
-      for (int i = 0; i < V; ++i) { q[d0 + i] = 0.f; go[d0 + i] = 0.f; }
+      for (int i = 0; i < V; ++i) { q[d0 + i] = 0.f; go[d0 + i] = 0.f; ov[d0 + i] = 0.f; }
     }
   }
+  float dl = 0.f;
+#pragma unroll
+  for (int d0 = 0; d0 < HDMAX; d0 += V)
+    if (d0 < hd) {
+#pragma unroll
+      for (int i = 0; i < V; ++i) dl = fmaf(go[d0 + i], ov[d0 + i], dl);
+    }
+  delta[pq * G.heads + h] = dl;
 #pragma unroll
   for (int d = 0; d < HDMAX; ++d) { q[d] *= scale; dq[d] = 0.f; }
   const float lq = lse[pq * G.heads + h];
-  const float dl = delta[pq * G.heads + h];
   for (int u = 0; u < G.N; ++u) {
     const long pk = G.pixel(grp, u);
     const T* kp = qkv + pk * C3 + G.C + h * hd;
@@ -364,12 +374,9 @@ static void fwd_launch(const void* qkv, void* out, float* lse, float* probs, con
 template <typename T, int HDMAX, int V>
 static void bwd_launch(const void* dout, const void* qkv, const void* out, const float* lse, void* dqkv,
                        float* delta, const GridGeom& G, float scale, hipStream_t s) {
-  const long M = (long)G.B * G.H * G.W;
-  grid_bwd_delta_kernel<T, V><<<cdiv(M * G.heads, 256), 256, 0, s>>>((const T*)dout, (const T*)out, delta, M, G.C,
-                                                                      G.heads);
-  const long total = (long)G.B * G.g * G.g * G.N * G.heads;
-  grid_bwd_dq_kernel<T, HDMAX, V><<<cdiv(total, 256), 256, 0, s>>>((const T*)dout, (const T*)qkv, lse, delta,
-                                                                   (T*)dqkv, G, scale);
+  const long total = (long)G.B * G.g * G.g * G.N * G.heads;   // (the dQ kernel writes delta for dK / dV)
+  grid_bwd_dq_kernel<T, HDMAX, V><<<cdiv(total, 256), 256, 0, s>>>((const T*)dout, (const T*)qkv, (const T*)out, lse,
+                                                                   delta, (T*)dqkv, G, scale);
   grid_bwd_dkv_kernel<T, HDMAX, V><<<cdiv(total, 256), 256, 0, s>>>((const T*)dout, (const T*)qkv, lse, delta,
                                                                     (T*)dqkv, G, scale);
 }

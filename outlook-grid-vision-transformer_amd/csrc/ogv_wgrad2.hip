@@ -351,7 +351,7 @@ __global__ __launch_bounds__(W2_NT) void wgrad2_bf16_kernel(const bf16* __restri
 
 // ------------------------------------------------------------------------------------------------
 static int g_wg2 = 2;          // knob "wg2": 0 off, 1 = this kernel below the streaming-wgrad M, 2 = at every M (default: measured faster than both other kernels at every 7M shape but one, which ties)
-static int g_wg2_blocks = 768;   // knob "wg2_blocks": workgroups the split-M plan aims for (measured 7M step, 30 steps: 512 16.32, 768 16.29, 1024 16.36-16.37, 1536 16.41 ms)
+static int g_wg2_blocks = 512;   // knob "wg2_blocks": workgroups the split-M plan aims for (round 4, 7M step, 30 steps: 512 16.32, 768 16.29, 1024 16.36-16.37, 1536 16.41 ms; round-6 re-sweep at 14.36 ms, three paired rounds: 512 14.308-14.326, 768 14.358-14.365, 1024 14.416-14.459 ms — profiles/r06_sweep.txt)
 static int g_wg2_tile = 0;     // knob "wg2_tile": force the N edge (64 / 96 / 128 / 192; K edge 64 / 128)
 static int g_wg2_conv = 1;     // knob "wg2_conv": 3x3 conv weight gradients (8 | C_in) on this kernel (0: tiled kernel)
 void set_wg2_conv(int v) { g_wg2_conv = v ? 1 : 0; }

@@ -80,7 +80,7 @@ CASES = [  # M, N, K, prologue act, bias, rowscale
 ]
 MODES = [("default", {}), ("wg2=0", {"wg2": 0}), ("wg2=1", {"wg2": 1}),
          ("wg2_fuse=1", {"wg2_fuse": 1})]  # default = wg2 2, wg2_fuse 0
-DEFAULTS = {"wg2": 2, "wg2_blocks": 768, "wg2_tile": 0, "wg2_fuse": 0}
+DEFAULTS = {"wg2": 2, "wg2_blocks": 512, "wg2_tile": 0, "wg2_fuse": 0}
 
 
 def _inputs(M, N, K, rs, seed):
